@@ -1,0 +1,193 @@
+#!/usr/bin/env python
+"""bench.py -- BASELINE.json metric: Mrays/s + frames/s at 1080p, 32 candidates, 4 spatial neighbours.
+
+Workload (configs[1], C2): Cornell box with 1024 emissive quads (2048 emissive triangles), 1920x1080,
+A=32 area + B=1 BRDF candidates, spatial reuse k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20.
+A "step" is one frame of the hot path (SimpleGuiDX11::produceRestir, pg/simpleguidx11.cpp:359-487):
+G-buffer + initial RIS, spatial reuse, shade.  Scene + buffers are resident in HBM before timing.
+
+N=1: one GPU renders the whole frame.  N>1 (torchrun): the frame is split into N row bands
+(strong scaling, one process per GPU); reservoir halo rows are exchanged over RCCL before each
+spatial pass and the band framebuffers are gathered to rank 0 (restir_amd/distributed.py).
+
+Output: one JSON line (rank 0) with value = whole-job frames/s, plus mrays_per_s, roofline of the
+dominant kernel (k_gbuffer_initial, algorithmic bytes, HIP-event timed) and cpu_baseline (the oracle
+restatement on this host's cores, N=1 only).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "restir-embree_amd"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# algorithmic bytes per pixel of the dominant kernel k_gbuffer_initial: G-buffer record write
+# (5 x float4 = 80 B) + reservoir write (3 x float4 = 48 B); scene/BVH reads are cache-resident
+# shared data, not per-pixel traffic.  DESIGN.md "Roofline".
+DOMINANT_BYTES_PER_PX = 80 + 48
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--scene", default="C2", choices=["C1", "C2", "C3"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def cpu_baseline(sc, prm, W, H, threads):
+    """The oracle (CPU restatement, OpenMP) timed on this host: one full frame of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+
+    oracle_lib.build()
+    L = oracle_lib.lib()
+    n_threads = max(1, min(threads, os.cpu_count() or 1))
+    L.or_set_num_threads(n_threads)
+    osc = oracle_lib.OracleScene(sc)
+    rr = oracle_lib.OracleRenderer(W, H)
+    rr.render(osc, sc.camera, prm, 0)          # warm-up frame (page-in, caches)
+    t0 = time.perf_counter()
+    rr.render(osc, sc.camera, prm, 1)
+    dt = time.perf_counter() - t0
+    return {"value": round(1.0 / dt, 5), "unit": "frames/s", "cores": n_threads, "kind": "port",
+            "sample": f"1 full {W}x{H} frame of the same C2 workload after 1 warm-up frame "
+                      f"(oracle/restir_oracle.c, OpenMP, {n_threads} threads); s/frame={dt:.3f}; "
+                      f"Mrays/s={rr.rays / dt / 1e6:.2f}"}
+
+
+def main():
+    args = parse()
+    import torch
+    from restir_amd import Renderer, scenes
+    from restir_amd.params import metric_params, c3_params, default_params
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    W, H = args.width, args.height
+    if args.scene == "C1":
+        sc, prm = scenes.cornell_box(8), default_params()
+    elif args.scene == "C2":
+        sc, prm = scenes.cornell_many_lights(1024), metric_params()
+    else:
+        sc, prm = scenes.sponza_like(), c3_params()
+    stream = torch.cuda.current_stream().cuda_stream
+
+    if world == 1:
+        r = Renderer(W, H, device=local, stream=stream)
+        gs = r.load_scene(sc)
+        step = lambda f: r.produce_restir(gs, sc.camera, prm, f, copy_out=False, timed=True)
+        times = lambda: r.last_times
+    else:
+        from restir_amd.distributed import TiledRenderer
+        tr = TiledRenderer(W, H, rank, world, device=local, stream=stream)
+        gs = tr.load_scene(sc)
+        step = lambda f: tr.render(gs, sc.camera, prm, f, gather=True, timed=True)
+        times = lambda: tr.last_times
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for f in range(args.warmup):
+        step(f)
+    barrier()
+    torch.cuda.synchronize()
+    acc = {"gbuffer_initial_ms": 0.0, "spatial_ms": 0.0, "temporal_ms": 0.0, "shade_ms": 0.0, "total_ms": 0.0}
+    rays = 0
+    t0 = time.perf_counter()
+    for f in range(args.steps):
+        step(args.warmup + f)
+        t = times()
+        for k in acc:
+            acc[k] += getattr(t, k)
+        rays += int(t.rays)
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt, float(rays)], dtype=torch.float64, device="cuda")
+        dmax = tt.clone()
+        dist.all_reduce(dmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+        dt, rays = float(dmax[0]), int(tt[1])
+        acc_t = torch.tensor([acc[k] for k in acc], dtype=torch.float64, device="cuda")
+        dist.all_reduce(acc_t, op=dist.ReduceOp.MAX)
+        acc = {k: float(v) for k, v in zip(acc, acc_t.tolist())}
+    ms_per_step = dt / args.steps * 1e3
+    fps = args.steps / dt
+    mrays = rays / dt / 1e6
+    k_ms = acc["gbuffer_initial_ms"] / args.steps
+    px_band = W * math.ceil(H / world)
+    achieved = DOMINANT_BYTES_PER_PX * px_band / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf) and world == 1:
+        try:
+            with open(tf) as f:
+                pmc = json.load(f)
+            if pmc.get("config") == f"{args.scene}_{W}x{H}":
+                traffic = pmc.get("k_gbuffer_initial_bytes_per_launch")
+        except Exception:
+            traffic = None
+    if rank == 0:
+        out = {
+            "metric": "Mrays/s + frames/s at 1080p, 32 candidates, 4 spatial neighbours",
+            "value": round(fps, 4),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural scene, BASELINE.json configs[1])",
+            "config": {"workload": f"{args.scene}: Cornell box + 1024 emissive quads, {W}x{H}, A=32 B=1, "
+                                   f"spatial k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20",
+                       "width": W, "height": H, "parallelism": f"row-bands x{world}" if world > 1 else "1 GPU"},
+            "mrays_per_s": round(mrays, 2),
+            "rays_per_frame": rays // max(1, args.steps),
+            "pass_ms": {k: round(v / args.steps, 4) for k, v in acc.items()},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                         "kernel": "k_gbuffer_initial", "bytes_per_px": DOMINANT_BYTES_PER_PX,
+                         "kernel_ms": round(k_ms, 4)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(sc, prm, W, H, args.cpu_threads)
+            except Exception as e:  # the baseline is reported, never required for the GPU number
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,183 @@
+/*
+ * restir_c.h -- C ABI of the MI355X-native ReSTIR DI renderer (librestir_amd.so).
+ *
+ * Drop-in boundary for the reference's per-pixel hot path (Tonz24/restir-embree,
+ * pg/ = template/src/pg/pg1_embree/).  The reference's seam is three C++ members of one object
+ * (SURVEY.md §8b):
+ *   scene-load   Raytracer::LoadScene(file)            pg/raytracer.cpp:34-38
+ *                -> Scene::Scene(file, RTCDevice)        pg/Scene.cpp:8-16 (rtcCommitScene = BVH build :15)
+ *   render       SimpleGuiDX11::produceRestir(float t) pg/simpleguidx11.cpp:359-487
+ *   framebuffer  glm::vec3* frame_data                 pg/simpleguidx11.h:152 (linear HDR RGB f32,
+ *                                                       row-major y*W+x, y=0 = top row)
+ * and the Embree device lifecycle it wraps (rtcNewDevice/rtcReleaseDevice, pg/simpleguidx11.cpp:48,
+ * pg/raytracer.cpp:28-32).  Each entry point below cites the call it replaces.
+ *
+ * Conventions: plain pointers and sizes only; every function returns 0 on success or a negative
+ * RS_E* code; rs_last_error() gives the message.  No exceptions cross the ABI, no global state.
+ * A context is bound to one HIP device and one host thread.  Rendering is asynchronous on the
+ * context's stream and synchronises only when a host output pointer is given.
+ */
+#ifndef RESTIR_C_H
+#define RESTIR_C_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RS_OK 0
+#define RS_E_INVALID (-1)     /* bad argument / shape */
+#define RS_E_HIP (-2)         /* HIP runtime error */
+#define RS_E_UNSUPPORTED (-3) /* feature the reference has but this build does not (e.g. sky map) */
+#define RS_E_IO (-4)          /* file not found / parse error (scene loader) */
+
+typedef struct rs_context rs_context;
+typedef struct rs_scene rs_scene;
+
+/* One mesh = one reference Surface / RTCGeometry (pg/ModelLoader.cpp:232-317): de-indexed triangles
+ * (3 unique vertices each, :297-299) with per-vertex normals (vertex attribute slot 0, :280-282). */
+typedef struct {
+    uint32_t n_tris;
+    const float* positions;   /* n_tris * 9 floats: v0.xyz v1.xyz v2.xyz */
+    const float* normals;     /* n_tris * 9 floats: n0.xyz n1.xyz n2.xyz */
+    uint32_t material;        /* index into the material array (Surface::get_material, :213,243) */
+} rs_mesh_desc;
+
+/* Material record as the ReSTIR statics read it (pg/material.cpp:105-134, pg/material.h:105-115).
+ * Colours are linear (the loader's sRGB expansion, pg/ModelLoader.cpp:80-97, already applied). */
+typedef struct {
+    float diffuse[3];         /* Kd */
+    float specular[3];        /* Ks */
+    float emission[3];        /* Ke -- emissive iff Ke.x+Ke.y+Ke.z > 0 (pg/material.h:135-137) */
+    float shininess;          /* Ns */
+    int32_t type;             /* MaterialType (pg/enums.h:3-11): 1 LAMBERT, 2 PHONG, 4 DIELECTRIC, ... */
+} rs_material_desc;
+
+/* Camera(width, height, fov_y, view_from, view_at), Z-up (pg/camera.cpp:12-18, pg/camera.h:68). */
+typedef struct {
+    float eye[3];
+    float at[3];
+    float fov_y_deg;
+} rs_camera;
+
+/* POD snapshot of ReSTIRIntegrator's static knobs (pg/ReSTIRIntegrator.cpp:13-35) and of its private
+ * RenderParams (pg/RenderParams.h:5-17), passed by value per frame. */
+typedef struct {
+    int32_t m_area;                /* M_Area */
+    int32_t m_brdf;                /* M_Brdf */
+    int32_t spatial_neighbors;     /* spatialReuseNeighborCount (k) */
+    int32_t spatial_passes;        /* spatialPassCount (P) */
+    int32_t confidence_cap;        /* confidenceCap */
+    float spatial_radius;          /* spatialReuseRadius (R) */
+    float min_normal_similarity;
+    float max_depth_difference;
+    int32_t do_spatial;
+    int32_t do_temporal;
+    int32_t do_visibility_pass;
+    int32_t reject_dissimilar;
+    int32_t spatial_mis;           /* SpatialWeightCalculation: 0 CONSTANT, 1 DEBIAS_CONTRIB,
+                                      2 DEBIAS_Z_TERM, 3 BALANCE_HEURISTIC, 4 PAIRWISE_MIS */
+    int32_t use_skybox;            /* must be 0: the reference's sky HDR is a missing blob */
+    float bg_color[3];
+    float tnear_offset;
+    float tfar_offset;
+    float normal_offset;
+    uint32_t seed;                 /* counter-RNG seed (replaces Utils' mt19937{123}, pg/utils.cpp:175) */
+    int32_t reserved;
+} rs_frame_params;
+
+/* Per-pass device time in ms (the reference's std::chrono pass timers, pg/simpleguidx11.h:120-127). */
+typedef struct {
+    float gbuffer_initial_ms;      /* gBUfferFillDuration + initialCandidatesGenDuration (fused) */
+    float visibility_ms;           /* visibilityPassDuration */
+    float temporal_ms;             /* temporalReusePassDuration */
+    float spatial_ms;              /* spatialReusePassDuration (all P passes) */
+    float shade_ms;                /* shadingPassDuration (0 when fused into the last reuse pass) */
+    float total_ms;                /* totalFrameDuration (history copy is a pointer swap: 0) */
+    uint64_t rays;                 /* closest-hit + occlusion rays traced this frame (device count) */
+    uint64_t primary_rays;
+} rs_pass_times;
+
+/* ---- device lifecycle (rtcNewDevice / rtcReleaseDevice) ------------------------------------- */
+/* Creates a context bound to HIP device `hip_device` rendering width x height frames.  `hip_stream`
+ * is a hipStream_t to render on (NULL: the context creates its own).  Owns every per-pixel buffer:
+ * 2 G-buffers (current/previous), 3 reservoir buffers, the framebuffer. */
+int rs_context_create(int hip_device, int width, int height, void* hip_stream, rs_context** out);
+void rs_context_destroy(rs_context* ctx);
+const char* rs_last_error(const rs_context* ctx);   /* ctx may be NULL: last global create error */
+
+/* ---- scene load (Scene::Scene + ModelLoader::loadScene + rtcCommitScene) ---------------------- */
+/* Uploads the triangles, builds the emissive-triangle CDF (TriangleCDF ctor, pg/TriangleCDF.cpp:8-34)
+ * and builds the BVH on the GPU (LBVH: Morton codes -> radix sort -> Karras hierarchy -> level refit
+ * -> depth-first skip-pointer layout).  Replaces rtcNewScene/rtcCommitScene (pg/Scene.cpp:10,15). */
+int rs_scene_create(rs_context* ctx, const rs_mesh_desc* meshes, uint32_t n_meshes,
+                    const rs_material_desc* materials, uint32_t n_materials, rs_scene** out);
+/* OBJ/MTL loader honouring Pc (material class), Kd/Ks (sRGB-expanded), Ke, Ns
+ * (pg/ModelLoader.cpp:41-153 conventions), then rs_scene_create.  Textures are not supported. */
+int rs_scene_load_obj(rs_context* ctx, const char* obj_path, rs_scene** out);
+void rs_scene_destroy(rs_scene* scene);
+/* Scene statistics: n_tris, n_emissive, n_bvh_nodes, bvh build time (ms). */
+int rs_scene_info(const rs_scene* scene, uint32_t* n_tris, uint32_t* n_emissive, uint32_t* n_nodes,
+                  float* build_ms);
+
+/* ---- render(frame) (SimpleGuiDX11::produceRestir) ----------------------------------------- */
+/* Renders one frame: G-buffer -> initial RIS -> [visibility] -> [temporal, if a previous frame
+ * exists] -> [spatial x P] -> shade; then swaps history (pointer swap instead of the reference's
+ * memcpy, pg/simpleguidx11.cpp:477-481).  `frame_index` keys the counter RNG.  If frame_rgb_host is
+ * non-NULL the W*H*3 framebuffer is copied to it (synchronous); `times` (optional) receives
+ * per-pass device times (synchronous). */
+int rs_render_frame(rs_context* ctx, const rs_scene* scene, const rs_camera* camera,
+                    const rs_frame_params* params, uint32_t frame_index, float* frame_rgb_host,
+                    rs_pass_times* times);
+/* Device pointer to the framebuffer (frame_data): W*H*3 floats, valid until the next render. */
+int rs_get_frame_device_ptr(rs_context* ctx, const float** dptr);
+/* Forget the previous frame (frameCtr = 0): the next frame skips temporal reuse. */
+int rs_reset_history(rs_context* ctx);
+/* Wait for all work queued on the context's stream. */
+int rs_synchronize(rs_context* ctx);
+
+/* ---- state dumps for golden parity ------------------------------------------------------- */
+/* G-buffer of the last rendered frame (prev=0) or the one before (prev=1): W*H*19 floats per pixel
+ * pos3 normal3 kd3 ks3 Le3 shininess depth type 1/I_M.  Reservoirs shaded last frame: W*H*12
+ * floats per pixel point3 normal3 Li3 w_sum W confidence. */
+int rs_dump_gbuffer(rs_context* ctx, int prev, float* host_out);
+int rs_dump_reservoirs(rs_context* ctx, float* host_out);
+
+/* ---- tile-sharded frames (multi-GPU) ---------------------------------------- */
+/* A rank renders rows [y0, y1) of the full width x height frame.  The G-buffer is computed for the
+ * rows [y0-margin, y1+margin) (recomputed margin, no exchange); the reservoir rows within `halo` of
+ * the band edge are exchanged between neighbouring ranks by the caller (RCCL) between the stages:
+ *   rs_tile_begin      : G-buffer (band+margin) + initial RIS (+ visibility) for the band
+ *   rs_tile_halo_ptr   : device pointers of the current reservoir buffer's halo rows
+ *   rs_tile_temporal   : temporal reuse on the band
+ *   rs_tile_spatial    : one spatial pass on the band (reads the halo rows)
+ *   rs_tile_finish     : shade, history swap; returns the band's framebuffer device pointer
+ * Per-pixel counter RNG keyed by the full-frame pixel index makes the result bit-identical to a
+ * single-GPU frame when margin >= the temporal reprojection displacement. */
+typedef struct {
+    int32_t y0, y1;         /* band rows, 0 <= y0 < y1 <= height */
+    int32_t margin;         /* G-buffer rows recomputed beyond the band (>= halo) */
+    int32_t halo;           /* reservoir rows exchanged each side (floor(sqrt(R)) for spatial reuse) */
+} rs_tile_desc;
+int rs_tile_begin(rs_context* ctx, const rs_scene* scene, const rs_camera* camera,
+                  const rs_frame_params* params, uint32_t frame_index, const rs_tile_desc* tile);
+/* which: 0 = rows [y0-halo, y0) (receive from the rank above), 1 = rows [y1, y1+halo) (from below),
+ *        2 = rows [y0, y0+halo) (send up), 3 = rows [y1-halo, y1) (send down).
+ * *bytes = rows * width * 48; NULL pointer when the rows fall outside the frame. */
+int rs_tile_halo_ptr(rs_context* ctx, int which, void** dptr, size_t* bytes);
+int rs_tile_temporal(rs_context* ctx);
+int rs_tile_spatial(rs_context* ctx, int pass_index);
+int rs_tile_finish(rs_context* ctx, const float** band_rgb_dptr, rs_pass_times* times);
+
+/* ---- test hook: raw BVH queries (rtcIntersect1 / rtcOccluded1 semantics) ----------------------
+ * n rays, host arrays o[3n], d[3n], tnear[n], tfar[n].  any_hit=0: closest hit -> t_out[n] (-1 on miss),
+ * prim_out[n] (original triangle index, -1 on miss); any_hit=1: prim_out[n] = 1 if occluded else 0. */
+int rs_debug_trace(rs_context* ctx, const rs_scene* scene, uint32_t n, const float* o, const float* d,
+                   const float* tnear, const float* tfar, int any_hit, float* t_out, int32_t* prim_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RESTIR_C_H */

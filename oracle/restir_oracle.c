@@ -1,0 +1,1240 @@
+/*
+ * restir_oracle.c -- CPU restatement of the reference ReSTIR DI hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / CPU baseline.
+ * The product (restir-embree_amd/, librestir_amd.so) never links or calls it.
+ *
+ * Reference: Tonz24/restir-embree @ /root/reference (read-only).  Citation legend:
+ *   pg/ = template/src/pg/pg1_embree/
+ * Every function below names the reference file:line it restates.
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - The reference's hot path cannot be compiled here (Embree/D3D11/OIDN/assimp are
+ *     Windows-only binaries; its translation units need stand-ins for stdafx.h and the
+ *     Embree library).  This restatement is therefore pinned by
+ *       (a) tests/golden/ibeta_kat.json  - generated from the reference's vendored
+ *           Boost 1.86 boost::math::beta (oracle/kat/gen_ibeta.cpp), pins calc_I_M;
+ *       (b) tests/golden/glm_kat.json    - generated from the reference's vendored glm
+ *           0.9.9 (oracle/kat/gen_glm.cpp), pins camera matrices, primary rays,
+ *           reflect/normalize/round/trunc semantics;
+ *     and everything else (reservoir logic, pass order, MIS modes) is "parity unpinned":
+ *     restated line by line from the cited source, no reference fixture exists.
+ *   - Embree 3.13.5's triangle/traversal arithmetic is replaced by Moller-Trumbore with
+ *     a fixed tie-break (smaller t, then smaller triangle index) -- parity unpinned at the
+ *     Embree boundary (no Embree here), identical rule in the HIP product.
+ *   - The reference's global mt19937 (pg/utils.cpp:175-202) is replaced by a counter RNG
+ *     keyed by (seed, frame, pass, pixel, draw#), consumed in the reference's per-pixel
+ *     draw order.  The HIP product uses the identical RNG.
+ *
+ * Build: oracle/Makefile -> oracle/_build/librestir_oracle.so  (gcc -O2 -fopenmp)
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------ constants */
+#define OR_PI          3.14159265358979323846264338327950288f   /* glm::pi<float>() */
+#define OR_ONE_OVER_PI 0.318309886183790671537767526745028724f  /* glm::one_over_pi */
+#define OR_ONE_OVER_2PI 0.159154943091895335768883763372514362f /* glm::one_over_two_pi */
+#define OR_TWO_PI      6.28318530717958647692528676655900576f   /* glm::two_pi */
+#define OR_ROOT_PI     1.772453850905516027f                     /* glm::root_pi */
+
+enum { MT_NORMAL = 0, MT_LAMBERT = 1, MT_PHONG = 2, MT_MIRROR = 3, MT_DIELECTRIC = 4,
+       MT_DIELECTRIC_TRANSPARENT = 5, MT_UNSUPPORTED = 6 };           /* pg/enums.h:3-11 */
+enum { MIS_CONSTANT = 0, MIS_DEBIAS_CONTRIB = 1, MIS_DEBIAS_Z = 2, MIS_BALANCE = 3,
+       MIS_PAIRWISE = 4 };                                             /* pg/ReSTIRIntegrator.h:19-25 */
+enum { PASS_INITIAL = 1, PASS_TEMPORAL = 2, PASS_SPATIAL0 = 3 };
+
+/* ------------------------------------------------------------------ glm-semantics math */
+typedef struct { float x, y, z; } v3;
+static inline v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 add(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 mul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 scl(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+static inline v3 neg(v3 a) { return V(-a.x, -a.y, -a.z); }
+/* glm compute_dot<vec3>: tmp = a*b; tmp.x + tmp.y + tmp.z  (glm/detail/func_geometric.inl:48-55) */
+static inline float dot(v3 a, v3 b) { v3 t = mul(a, b); return t.x + t.y + t.z; }
+/* glm compute_cross (func_geometric.inl:68-79) */
+static inline v3 cross(v3 x, v3 y) {
+    return V(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y);
+}
+static inline float len(v3 a) { return sqrtf(dot(a, a)); }
+/* glm normalize = v * inversesqrt(dot(v,v)), inversesqrt = 1/sqrt (func_exponential.inl:136-139) */
+static inline v3 nrmz(v3 a) { return scl(a, 1.0f / sqrtf(dot(a, a))); }
+/* glm reflect: I - N * dot(N, I) * 2 (func_geometric.inl:104-110) */
+static inline v3 reflect(v3 I, v3 N) { return sub(I, scl(scl(N, dot(N, I)), 2.0f)); }
+/* glm scalar max/min (func_common.inl:17-30): NaN propagation of the select form */
+static inline float gmax(float x, float y) { return (x < y) ? y : x; }
+static inline float gmin(float x, float y) { return (y < x) ? y : x; }
+static inline float maxc(v3 a) { return gmax(gmax(a.x, a.y), a.z); }   /* pg/utils.h:61-63 */
+static inline int nonzero_pos(v3 e) { return e.x > 0 || e.y > 0 || e.z > 0; }
+
+/* column-major 4x4, m[c][r] like glm */
+typedef struct { float m[4][4]; } m4;
+
+/* glm::lookAtRH (glm/ext/matrix_transform.inl:99-119) */
+static m4 look_at_rh(v3 eye, v3 center, v3 up) {
+    v3 f = nrmz(sub(center, eye));
+    v3 s = nrmz(cross(f, up));
+    v3 u = cross(s, f);
+    m4 R; memset(&R, 0, sizeof R);
+    R.m[0][0] = 1; R.m[1][1] = 1; R.m[2][2] = 1; R.m[3][3] = 1;
+    R.m[0][0] = s.x; R.m[1][0] = s.y; R.m[2][0] = s.z;
+    R.m[0][1] = u.x; R.m[1][1] = u.y; R.m[2][1] = u.z;
+    R.m[0][2] = -f.x; R.m[1][2] = -f.y; R.m[2][2] = -f.z;
+    R.m[3][0] = -dot(s, eye); R.m[3][1] = -dot(u, eye); R.m[3][2] = dot(f, eye);
+    return R;
+}
+
+/* glm compute_inverse<4,4> (glm/detail/func_matrix.inl:294-351) */
+static m4 inverse4(const m4* M) {
+    const float (*m)[4] = M->m;
+    float c00 = m[2][2] * m[3][3] - m[3][2] * m[2][3];
+    float c02 = m[1][2] * m[3][3] - m[3][2] * m[1][3];
+    float c03 = m[1][2] * m[2][3] - m[2][2] * m[1][3];
+    float c04 = m[2][1] * m[3][3] - m[3][1] * m[2][3];
+    float c06 = m[1][1] * m[3][3] - m[3][1] * m[1][3];
+    float c07 = m[1][1] * m[2][3] - m[2][1] * m[1][3];
+    float c08 = m[2][1] * m[3][2] - m[3][1] * m[2][2];
+    float c10 = m[1][1] * m[3][2] - m[3][1] * m[1][2];
+    float c11 = m[1][1] * m[2][2] - m[2][1] * m[1][2];
+    float c12 = m[2][0] * m[3][3] - m[3][0] * m[2][3];
+    float c14 = m[1][0] * m[3][3] - m[3][0] * m[1][3];
+    float c15 = m[1][0] * m[2][3] - m[2][0] * m[1][3];
+    float c16 = m[2][0] * m[3][2] - m[3][0] * m[2][2];
+    float c18 = m[1][0] * m[3][2] - m[3][0] * m[1][2];
+    float c19 = m[1][0] * m[2][2] - m[2][0] * m[1][2];
+    float c20 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
+    float c22 = m[1][0] * m[3][1] - m[3][0] * m[1][1];
+    float c23 = m[1][0] * m[2][1] - m[2][0] * m[1][1];
+    float F0[4] = {c00, c00, c02, c03}, F1[4] = {c04, c04, c06, c07}, F2[4] = {c08, c08, c10, c11};
+    float F3[4] = {c12, c12, c14, c15}, F4[4] = {c16, c16, c18, c19}, F5[4] = {c20, c20, c22, c23};
+    float V0[4] = {m[1][0], m[0][0], m[0][0], m[0][0]};
+    float V1[4] = {m[1][1], m[0][1], m[0][1], m[0][1]};
+    float V2[4] = {m[1][2], m[0][2], m[0][2], m[0][2]};
+    float V3[4] = {m[1][3], m[0][3], m[0][3], m[0][3]};
+    float SA[4] = {+1, -1, +1, -1}, SB[4] = {-1, +1, -1, +1};
+    m4 I;
+    for (int i = 0; i < 4; ++i) {
+        float i0 = V1[i] * F0[i] - V2[i] * F1[i] + V3[i] * F2[i];
+        float i1 = V0[i] * F0[i] - V2[i] * F3[i] + V3[i] * F4[i];
+        float i2 = V0[i] * F1[i] - V1[i] * F3[i] + V3[i] * F5[i];
+        float i3 = V0[i] * F2[i] - V1[i] * F4[i] + V2[i] * F5[i];
+        I.m[0][i] = i0 * SA[i]; I.m[1][i] = i1 * SB[i]; I.m[2][i] = i2 * SA[i]; I.m[3][i] = i3 * SB[i];
+    }
+    float d0 = m[0][0] * I.m[0][0], d1 = m[0][1] * I.m[1][0], d2 = m[0][2] * I.m[2][0], d3 = m[0][3] * I.m[3][0];
+    float det = (d0 + d1) + (d2 + d3);
+    float ood = 1.0f / det;
+    for (int c = 0; c < 4; ++c) for (int r = 0; r < 4; ++r) I.m[c][r] = I.m[c][r] * ood;
+    return I;
+}
+
+/* glm mat4 * vec4 (glm/detail/type_mat4x4.inl:561-572): (m0*x + m1*y) + (m2*z + m3*w) */
+static v3 m4_mul_point(const m4* M, v3 p) {
+    const float (*m)[4] = M->m;
+    float r[3];
+    for (int i = 0; i < 3; ++i) {
+        float a0 = m[0][i] * p.x + m[1][i] * p.y;
+        float a1 = m[2][i] * p.z + m[3][i] * 1.0f;
+        r[i] = a0 + a1;
+    }
+    return V(r[0], r[1], r[2]);
+}
+/* glm mat3 * vec3 (type_mat3x3.inl:468-474) with mat3(invViewMat) */
+static v3 m3_mul(const m4* M, v3 v) {
+    const float (*m)[4] = M->m;
+    return V(m[0][0] * v.x + m[1][0] * v.y + m[2][0] * v.z,
+             m[0][1] * v.x + m[1][1] * v.y + m[2][1] * v.z,
+             m[0][2] * v.x + m[1][2] * v.y + m[2][2] * v.z);
+}
+
+/* ------------------------------------------------------------------ counter RNG */
+/* Replaces Utils::getRandomValue's shared mt19937 (pg/utils.cpp:175-176,199-202). */
+static inline uint32_t hash32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16; return x;
+}
+typedef struct { uint32_t key, n; } rng_t;
+static inline rng_t rng_init(uint32_t seed, uint32_t frame, uint32_t pass, uint32_t pixel) {
+    uint32_t k = hash32(seed ^ 0x6a09e667u);
+    k = hash32(k ^ frame);
+    k = hash32(k + 0x9e3779b9u * (pass + 1u));
+    k = hash32(k ^ pixel);
+    rng_t r = {k, 0u};
+    return r;
+}
+static inline float rng_u(rng_t* r) {
+    uint32_t x = hash32(r->key ^ hash32(r->n + 0x632be5abu));
+    r->n++;
+    return (float)(x >> 8) * (1.0f / 16777216.0f);
+}
+/* Utils::getRandomValue(a, b) = a + (b - a) * U  (pg/utils.cpp:199-202) */
+static inline float rnd(rng_t* r, float a, float b) { float u = rng_u(r); return a + (b - a) * u; }
+
+/* ------------------------------------------------------------------ incomplete beta */
+/* Non-normalised incomplete beta B_x(a,b) in double: restates boost::math::beta(a,b,x)
+ * (libs/Boost/boost/math/special_functions/beta.hpp:1607-1622, ibeta_imp normalised=false)
+ * with the Lentz continued fraction; pinned by tests/golden/ibeta_kat.json. */
+static double betacf(double a, double b, double x) {
+    const double FPMIN = 1e-300, EPS = 1e-16;
+    double qab = a + b, qap = a + 1.0, qam = a - 1.0;
+    double c = 1.0, d = 1.0 - qab * x / qap;
+    if (fabs(d) < FPMIN) d = FPMIN;
+    d = 1.0 / d;
+    double h = d;
+    for (int m = 1; m <= 10000; ++m) {
+        int m2 = 2 * m;
+        double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
+        d = 1.0 + aa * d; if (fabs(d) < FPMIN) d = FPMIN;
+        c = 1.0 + aa / c; if (fabs(c) < FPMIN) c = FPMIN;
+        d = 1.0 / d; h *= d * c;
+        aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
+        d = 1.0 + aa * d; if (fabs(d) < FPMIN) d = FPMIN;
+        c = 1.0 + aa / c; if (fabs(c) < FPMIN) c = FPMIN;
+        d = 1.0 / d;
+        double del = d * c;
+        h *= del;
+        if (fabs(del - 1.0) < EPS) break;
+    }
+    return h;
+}
+double or_ibeta(double x, double a, double b) {
+    if (!(x > 0.0)) return 0.0;
+    double lbeta = lgamma(a) + lgamma(b) - lgamma(a + b);
+    if (x >= 1.0) return exp(lbeta);
+    double lbt = a * log(x) + b * log1p(-x);
+    if (x < (a + 1.0) / (a + b + 2.0))
+        return exp(lbt) * betacf(a, b, x) / a;
+    return exp(lbeta) - exp(lbt) * betacf(b, a, 1.0 - x) / b;
+}
+/* MaterialPhong::ibeta (pg/MaterialPhong.cpp:246-248): float in, Boost promotes to double, float out */
+static inline float ibeta_f(float x, float a, float b) { return (float)or_ibeta((double)x, (double)a, (double)b); }
+/* MaterialPhong::gamma_quot (pg/MaterialPhong.cpp:224-226) */
+static inline float gamma_quot(float a, float b) { return expf(lgammaf(a) - lgammaf(b)); }
+/* MaterialPhong::calc_I_M (pg/MaterialPhong.cpp:228-244) */
+float or_calc_I_M(float nDotV, float n) {
+    float costerm = nDotV;
+    float sinterm_sq = 1.0f - costerm * costerm;
+    float halfn = 0.5f * n;
+    float negterm = costerm;
+    sinterm_sq = gmin(gmax(sinterm_sq, 0.0f), 1.0f);
+    if (n >= 1e-18f) negterm *= halfn * ibeta_f(sinterm_sq, halfn, 0.5f);
+    return (OR_TWO_PI * costerm + OR_ROOT_PI * gamma_quot(halfn + 0.5f, halfn + 1.0f) *
+            (powf(sinterm_sq, halfn) - negterm)) / (n + 2.0f);
+}
+
+/* ------------------------------------------------------------------ scene */
+typedef struct {
+    v3 kd, ks, le; float shin; int type;
+} or_mat;
+
+typedef struct { float lo[3], hi[3]; int left, right, first, count; } or_node; /* count>0 => leaf */
+
+typedef struct {
+    uint32_t n_tris;
+    v3 *p0, *p1, *p2, *n0, *n1, *n2;
+    uint32_t* mat;
+    int32_t* emis_id;          /* per triangle, -1 if not emissive (pg/ModelLoader.cpp:291-292) */
+    uint32_t n_mat; or_mat* mats;
+    /* emissive list + TriangleCDF (pg/TriangleCDF.cpp:8-34) */
+    uint32_t n_emis; uint32_t* emis_tri;
+    float* cdf;                /* cumulative normalised area, cdf2 */
+    float* pick_pdf;           /* getTriangle's prob (pg/TriangleCDF.cpp:49-53) */
+    float* area;               /* Triangle::area (pg/triangle.cpp:13-16) */
+    float total_area;
+    /* BVH */
+    or_node* nodes; int n_nodes; uint32_t* tri_index;
+} or_scene;
+
+/* Triangle::Triangle area = 0.5 * |cross(v1-v0, v2-v0)|  (pg/triangle.cpp:13-16) */
+static float tri_area(v3 a, v3 b, v3 c) { return 0.5f * len(cross(sub(b, a), sub(c, a))); }
+
+/* ---- binned SAH BVH (oracle's own; any correct BVH finds the same hits) */
+typedef struct { float lo[3], hi[3]; } aabb;
+static void bb_empty(aabb* b) { for (int i = 0; i < 3; ++i) { b->lo[i] = FLT_MAX; b->hi[i] = -FLT_MAX; } }
+static void bb_grow_p(aabb* b, v3 p) {
+    float q[3] = {p.x, p.y, p.z};
+    for (int i = 0; i < 3; ++i) { if (q[i] < b->lo[i]) b->lo[i] = q[i]; if (q[i] > b->hi[i]) b->hi[i] = q[i]; }
+}
+static void bb_grow(aabb* b, const aabb* o) {
+    for (int i = 0; i < 3; ++i) { if (o->lo[i] < b->lo[i]) b->lo[i] = o->lo[i]; if (o->hi[i] > b->hi[i]) b->hi[i] = o->hi[i]; }
+}
+static float bb_area(const aabb* b) {
+    float d0 = b->hi[0] - b->lo[0], d1 = b->hi[1] - b->lo[1], d2 = b->hi[2] - b->lo[2];
+    if (d0 < 0) return 0;
+    return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
+}
+
+typedef struct { aabb* tb; float* cen; uint32_t* idx; or_node* nodes; int n_nodes; } bvh_build_t;
+
+static int bvh_build_rec(bvh_build_t* B, int first, int count) {
+    int ni = B->n_nodes++;
+    or_node* N = &B->nodes[ni];
+    aabb bb, cb; bb_empty(&bb); bb_empty(&cb);
+    for (int i = first; i < first + count; ++i) {
+        uint32_t t = B->idx[i];
+        bb_grow(&bb, &B->tb[t]);
+        bb_grow_p(&cb, V(B->cen[3 * t], B->cen[3 * t + 1], B->cen[3 * t + 2]));
+    }
+    memcpy(N->lo, bb.lo, sizeof bb.lo); memcpy(N->hi, bb.hi, sizeof bb.hi);
+    if (count <= 4) { N->first = first; N->count = count; N->left = N->right = -1; return ni; }
+    enum { NB = 16 };
+    int best_axis = -1, best_split = -1; float best_cost = FLT_MAX;
+    for (int ax = 0; ax < 3; ++ax) {
+        float lo = cb.lo[ax], hi = cb.hi[ax];
+        if (!(hi > lo)) continue;
+        aabb bins[NB]; int cnt[NB];
+        for (int b = 0; b < NB; ++b) { bb_empty(&bins[b]); cnt[b] = 0; }
+        float k = (float)NB / (hi - lo);
+        for (int i = first; i < first + count; ++i) {
+            uint32_t t = B->idx[i];
+            int b = (int)((B->cen[3 * t + ax] - lo) * k); if (b >= NB) b = NB - 1; if (b < 0) b = 0;
+            cnt[b]++; bb_grow(&bins[b], &B->tb[t]);
+        }
+        float la[NB], ra[NB]; int lc[NB], rc[NB];
+        aabb acc; bb_empty(&acc); int c = 0;
+        for (int b = 0; b < NB; ++b) { bb_grow(&acc, &bins[b]); c += cnt[b]; la[b] = bb_area(&acc); lc[b] = c; }
+        bb_empty(&acc); c = 0;
+        for (int b = NB - 1; b >= 0; --b) { bb_grow(&acc, &bins[b]); c += cnt[b]; ra[b] = bb_area(&acc); rc[b] = c; }
+        for (int b = 0; b < NB - 1; ++b) {
+            if (lc[b] == 0 || rc[b + 1] == 0) continue;
+            float cost = la[b] * lc[b] + ra[b + 1] * rc[b + 1];
+            if (cost < best_cost) { best_cost = cost; best_axis = ax; best_split = b; }
+        }
+    }
+    int mid;
+    if (best_axis < 0) {
+        mid = first + count / 2;  /* all centroids equal: median split by index */
+    } else {
+        float lo = cb.lo[best_axis], hi = cb.hi[best_axis];
+        float k = (float)NB / (hi - lo);
+        int i = first, j = first + count - 1;
+        while (i <= j) {
+            uint32_t t = B->idx[i];
+            int b = (int)((B->cen[3 * t + best_axis] - lo) * k); if (b >= NB) b = NB - 1; if (b < 0) b = 0;
+            if (b <= best_split) ++i; else { uint32_t s = B->idx[i]; B->idx[i] = B->idx[j]; B->idx[j] = s; --j; }
+        }
+        mid = i;
+        if (mid == first || mid == first + count) mid = first + count / 2;
+    }
+    int l = bvh_build_rec(B, first, mid - first);
+    int r = bvh_build_rec(B, mid, first + count - mid);
+    N = &B->nodes[ni];
+    N->left = l; N->right = r; N->count = 0; N->first = 0;
+    return ni;
+}
+
+void or_scene_destroy(or_scene* s);
+
+/* Scene ctor (pg/Scene.cpp:8-16) + ModelLoader geometry setup (pg/ModelLoader.cpp:218-321) +
+ * TriangleCDF ctor (pg/TriangleCDF.cpp:8-34).  mat_f: per material kd3 ks3 le3 shininess. */
+or_scene* or_scene_create(uint32_t n_tris, const float* pos, const float* nrm, const uint32_t* tri_mat,
+                          uint32_t n_mat, const float* mat_f, const int32_t* mat_type) {
+    or_scene* s = (or_scene*)calloc(1, sizeof(or_scene));
+    s->n_tris = n_tris; s->n_mat = n_mat;
+    s->p0 = malloc(n_tris * sizeof(v3)); s->p1 = malloc(n_tris * sizeof(v3)); s->p2 = malloc(n_tris * sizeof(v3));
+    s->n0 = malloc(n_tris * sizeof(v3)); s->n1 = malloc(n_tris * sizeof(v3)); s->n2 = malloc(n_tris * sizeof(v3));
+    s->mat = malloc(n_tris * sizeof(uint32_t)); s->emis_id = malloc(n_tris * sizeof(int32_t));
+    s->mats = malloc((n_mat ? n_mat : 1) * sizeof(or_mat));
+    for (uint32_t m = 0; m < n_mat; ++m) {
+        const float* f = mat_f + 10 * m;
+        s->mats[m].kd = V(f[0], f[1], f[2]); s->mats[m].ks = V(f[3], f[4], f[5]);
+        s->mats[m].le = V(f[6], f[7], f[8]); s->mats[m].shin = f[9]; s->mats[m].type = mat_type[m];
+    }
+    uint32_t ne = 0;
+    for (uint32_t t = 0; t < n_tris; ++t) {
+        const float* p = pos + 9 * t; const float* n = nrm + 9 * t;
+        s->p0[t] = V(p[0], p[1], p[2]); s->p1[t] = V(p[3], p[4], p[5]); s->p2[t] = V(p[6], p[7], p[8]);
+        s->n0[t] = V(n[0], n[1], n[2]); s->n1[t] = V(n[3], n[4], n[5]); s->n2[t] = V(n[6], n[7], n[8]);
+        s->mat[t] = tri_mat[t];
+        v3 le = s->mats[tri_mat[t]].le;
+        /* Material::isEmissive: emission.x + emission.y + emission.z > 0 (pg/material.h:135-137) */
+        if (le.x + le.y + le.z > 0) s->emis_id[t] = (int32_t)ne++; else s->emis_id[t] = -1;
+    }
+    s->n_emis = ne;
+    s->emis_tri = malloc((ne ? ne : 1) * sizeof(uint32_t));
+    s->cdf = malloc((ne ? ne : 1) * sizeof(float));
+    s->pick_pdf = malloc((ne ? ne : 1) * sizeof(float));
+    s->area = malloc((ne ? ne : 1) * sizeof(float));
+    for (uint32_t t = 0; t < n_tris; ++t) if (s->emis_id[t] >= 0) s->emis_tri[s->emis_id[t]] = t;
+    float total = 0.0f;
+    for (uint32_t e = 0; e < ne; ++e) {
+        uint32_t t = s->emis_tri[e];
+        s->area[e] = tri_area(s->p0[t], s->p1[t], s->p2[t]);
+        total += s->area[e];
+    }
+    s->total_area = total;
+    for (uint32_t e = 0; e < ne; ++e) {
+        float norm_area = s->area[e] / total;
+        float pred = e == 0 ? 0.0f : s->cdf[e - 1];
+        s->cdf[e] = pred + norm_area;
+    }
+    /* std::sort by cumulative value (pg/TriangleCDF.cpp:27-29): the sequence is already
+       non-decreasing; ties only for zero-area triangles (not produced by our scenes). */
+    for (uint32_t e = 0; e < ne; ++e) s->pick_pdf[e] = e == 0 ? s->cdf[0] : s->cdf[e] - s->cdf[e - 1];
+
+    /* BVH */
+    bvh_build_t B;
+    B.tb = malloc((n_tris ? n_tris : 1) * sizeof(aabb));
+    B.cen = malloc((n_tris ? n_tris : 1) * 3 * sizeof(float));
+    B.idx = malloc((n_tris ? n_tris : 1) * sizeof(uint32_t));
+    B.nodes = malloc((2 * (n_tris ? n_tris : 1)) * sizeof(or_node));
+    B.n_nodes = 0;
+    for (uint32_t t = 0; t < n_tris; ++t) {
+        bb_empty(&B.tb[t]); bb_grow_p(&B.tb[t], s->p0[t]); bb_grow_p(&B.tb[t], s->p1[t]); bb_grow_p(&B.tb[t], s->p2[t]);
+        for (int a = 0; a < 3; ++a) B.cen[3 * t + a] = 0.5f * (B.tb[t].lo[a] + B.tb[t].hi[a]);
+        B.idx[t] = t;
+    }
+    if (n_tris) bvh_build_rec(&B, 0, (int)n_tris);
+    s->nodes = B.nodes; s->n_nodes = B.n_nodes; s->tri_index = B.idx;
+    free(B.tb); free(B.cen);
+    return s;
+}
+
+void or_scene_destroy(or_scene* s) {
+    if (!s) return;
+    free(s->p0); free(s->p1); free(s->p2); free(s->n0); free(s->n1); free(s->n2);
+    free(s->mat); free(s->emis_id); free(s->mats); free(s->emis_tri); free(s->cdf);
+    free(s->pick_pdf); free(s->area); free(s->nodes); free(s->tri_index); free(s);
+}
+
+/* ------------------------------------------------------------------ ray queries */
+/* Moller-Trumbore with fixed operation order; the HIP product uses the same arithmetic.
+ * Replaces Embree's rtcIntersect1/rtcOccluded1 triangle test (pg/Intersection.h:43-83). */
+static inline int tri_hit(const or_scene* s, uint32_t t, v3 o, v3 d, float tnear, float tfar,
+                          float* tt, float* uu, float* vv) {
+    v3 v0 = s->p0[t];
+    v3 e1 = sub(s->p1[t], v0), e2 = sub(s->p2[t], v0);
+    v3 p = cross(d, e2);
+    float det = dot(e1, p);
+    if (det == 0.0f) return 0;
+    float inv = 1.0f / det;
+    v3 sv = sub(o, v0);
+    float u = dot(sv, p) * inv;
+    if (!(u >= 0.0f && u <= 1.0f)) return 0;
+    v3 q = cross(sv, e1);
+    float v = dot(d, q) * inv;
+    if (!(v >= 0.0f && u + v <= 1.0f)) return 0;
+    float t_ = dot(e2, q) * inv;
+    if (!(t_ >= tnear && t_ <= tfar)) return 0;
+    *tt = t_; *uu = u; *vv = v;
+    return 1;
+}
+
+/* conservative slab test: interval widened by (1 +- 4 eps) so it never culls a box whose
+   contents the triangle test would accept */
+static inline int box_hit(const or_node* n, v3 o, v3 inv, float tnear, float tfar, float* tentry) {
+    float oo[3] = {o.x, o.y, o.z}, ii[3] = {inv.x, inv.y, inv.z};
+    float t0 = tnear, t1 = tfar;
+    for (int a = 0; a < 3; ++a) {
+        float ta = (n->lo[a] - oo[a]) * ii[a];
+        float tb = (n->hi[a] - oo[a]) * ii[a];
+        float mn = fminf(ta, tb), mx = fmaxf(ta, tb);
+        t0 = fmaxf(t0, mn); t1 = fminf(t1, mx);
+    }
+    *tentry = t0;
+    return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
+}
+
+typedef struct { int hit; float t, u, v; uint32_t prim; } or_hit;
+
+static or_hit closest_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
+    or_hit h = {0, tfar, 0, 0, 0xffffffffu};
+    if (!s->n_nodes) return h;
+    v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    int stack[128]; int sp = 0; stack[sp++] = 0;
+    while (sp) {
+        const or_node* n = &s->nodes[stack[--sp]];
+        float te;
+        if (!box_hit(n, o, inv, tnear, h.t, &te)) continue;
+        if (n->count) {
+            for (int i = n->first; i < n->first + n->count; ++i) {
+                uint32_t t = s->tri_index[i]; float tt, uu, vv;
+                if (tri_hit(s, t, o, d, tnear, h.t, &tt, &uu, &vv)) {
+                    if (!h.hit || tt < h.t || (tt == h.t && t < h.prim)) {
+                        h.hit = 1; h.t = tt; h.u = uu; h.v = vv; h.prim = t;
+                    }
+                }
+            }
+        } else {
+            stack[sp++] = n->right; stack[sp++] = n->left;
+        }
+    }
+    return h;
+}
+
+static int any_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
+    if (!s->n_nodes) return 0;
+    v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    int stack[128]; int sp = 0; stack[sp++] = 0;
+    while (sp) {
+        const or_node* n = &s->nodes[stack[--sp]];
+        float te;
+        if (!box_hit(n, o, inv, tnear, tfar, &te)) continue;
+        if (n->count) {
+            for (int i = n->first; i < n->first + n->count; ++i) {
+                float tt, uu, vv;
+                if (tri_hit(s, s->tri_index[i], o, d, tnear, tfar, &tt, &uu, &vv)) return 1;
+            }
+        } else {
+            stack[sp++] = n->right; stack[sp++] = n->left;
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ params / buffers */
+typedef struct {
+    int32_t m_area, m_brdf, spatial_neighbors, spatial_passes, confidence_cap;
+    float spatial_radius, min_normal_similarity, max_depth_difference;
+    int32_t do_spatial, do_temporal, do_visibility_pass, reject_dissimilar, spatial_mis;
+    int32_t use_skybox; float bg_color[3];
+    float tnear_offset, tfar_offset, normal_offset;
+    uint32_t seed; int32_t reserved;
+} or_params;  /* snapshot of pg/ReSTIRIntegrator.cpp:13-35 statics + pg/RenderParams.h:5-17 */
+
+typedef struct { v3 pos, nrm, kd, ks, le; float shin, depth; int type; } or_gbe; /* pg/GBufferElement.h:6-17 */
+typedef struct { v3 pos; m4 view, inv_view; float focal; } or_gcam;            /* pg/GBufferElement.h:136-139 */
+typedef struct { v3 p, n, li; float wsum, W; int conf; } or_res;               /* pg/Reservoir.h:6-59 */
+
+typedef struct {
+    int W, H;
+    or_gbe* g[2]; or_gcam gc[2]; int gcur;
+    or_res* r[3]; int r_last;
+    uint64_t frames;          /* frameCtr (pg/simpleguidx11.h:101) */
+    int cache_im;             /* 1: cache calc_I_M per pixel (speed only; identical values) */
+    float* im_cache[2];       /* 1/calc_I_M per pixel for Phong-dispatched surfaces */
+    int rays_closest_pad;
+    uint64_t rays;
+} or_ctx;
+
+or_ctx* or_ctx_create(int W, int H) {
+    or_ctx* c = (or_ctx*)calloc(1, sizeof(or_ctx));
+    c->W = W; c->H = H;
+    size_t n = (size_t)W * H;
+    for (int i = 0; i < 2; ++i) { c->g[i] = calloc(n, sizeof(or_gbe)); c->im_cache[i] = calloc(n, sizeof(float)); }
+    for (int i = 0; i < 3; ++i) c->r[i] = calloc(n, sizeof(or_res));
+    c->r_last = 2;
+    c->cache_im = 1;
+    return c;
+}
+void or_ctx_destroy(or_ctx* c) {
+    if (!c) return;
+    for (int i = 0; i < 2; ++i) { free(c->g[i]); free(c->im_cache[i]); }
+    for (int i = 0; i < 3; ++i) free(c->r[i]);
+    free(c);
+}
+void or_ctx_set_cache_im(or_ctx* c, int on) { c->cache_im = on; }
+void or_ctx_reset_history(or_ctx* c) { c->frames = 0; }
+
+static inline or_res res_empty(void) {
+    or_res r;
+    r.p = V(-FLT_MAX, -FLT_MAX, -FLT_MAX); r.n = r.p; r.li = r.p;
+    r.wsum = 0; r.W = 0; r.conf = 0;
+    return r;
+}
+/* LightSample::isValid (pg/Reservoir.h:11-17) */
+static inline int sample_valid(const or_res* s) {
+    int pok = s->p.x != -FLT_MAX && s->p.y != -FLT_MAX && s->p.z != -FLT_MAX;
+    int nok = s->n.x != -FLT_MAX && s->n.y != -FLT_MAX && s->n.z != -FLT_MAX;
+    int lok = s->li.x > 0 || s->li.y > 0 || s->li.z > 0;
+    return pok && nok && lok;
+}
+typedef struct { v3 p, n, li; } sample_t;
+static inline sample_t smp_of(const or_res* r) { sample_t s = {r->p, r->n, r->li}; return s; }
+static inline sample_t smp_invalid(void) { sample_t s; s.p = V(-FLT_MAX, -FLT_MAX, -FLT_MAX); s.n = s.p; s.li = s.p; return s; }
+static inline int smp_valid(sample_t s) {
+    or_res r; r.p = s.p; r.n = s.n; r.li = s.li; return sample_valid(&r);
+}
+/* Reservoir::addSample (pg/Reservoir.h:33-47) */
+static inline int res_add(or_res* r, sample_t s, float w, int conf, rng_t* rng) {
+    r->wsum += w;
+    r->conf += conf;
+    if (w == 0 && r->wsum == 0) return 0;
+    if (rng_u(rng) < w / r->wsum) { r->p = s.p; r->n = s.n; r->li = s.li; return 1; }
+    return 0;
+}
+/* Reservoir::capConfidence (pg/Reservoir.h:54-56) */
+static inline void res_cap(or_res* r, int cap) { r->conf = r->conf < cap ? r->conf : cap; }
+
+/* ------------------------------------------------------------------ per-frame context */
+typedef struct {
+    const or_scene* s; or_ctx* c; const or_params* P; uint32_t frame;
+    const or_gbe* G; const or_gbe* Gp; const or_gcam* gc; const or_gcam* gcp;
+    const float* im; const float* imp;
+} fctx;
+
+/* Intersection::testOcclusion (pg/Intersection.h:43-60) */
+static int occluded(const fctx* F, v3 from, v3 to, uint64_t* rays) {
+    float dist = len(sub(to, from));
+    v3 dir = nrmz(sub(to, from));
+    float tnear = FLT_MIN + F->P->tnear_offset;
+    float tfar = dist - F->P->tfar_offset;
+    (*rays)++;
+    return any_hit(F->s, from, dir, tnear, tfar);
+}
+
+/* Intersection::intersectEmbree + getGeometryAttributes (pg/Intersection.h:8-41,85-113) */
+typedef struct { int hit; v3 point, normal; uint32_t prim; float t; } hitinfo;
+static hitinfo intersect(const fctx* F, v3 o, v3 d, float tnear, uint64_t* rays) {
+    hitinfo hi; hi.hit = 0; hi.prim = 0xffffffffu; hi.t = FLT_MAX; hi.point = V(0, 0, 0); hi.normal = V(0, 0, 0);
+    (*rays)++;
+    or_hit h = closest_hit(F->s, o, d, tnear, FLT_MAX);
+    if (!h.hit) return hi;
+    const or_scene* s = F->s; uint32_t t = h.prim;
+    /* rtcInterpolate0 slot 0: (1-u-v)*n0 + u*n1 + v*n2 */
+    float w = 1.0f - h.u - h.v;
+    v3 n = add(add(scl(s->n0[t], w), scl(s->n1[t], h.u)), scl(s->n2[t], h.v));
+    n = nrmz(n);
+    if (dot(neg(d), n) <= 0.0f) n = scl(n, -1.0f);
+    hi.hit = 1; hi.normal = n; hi.prim = t; hi.t = h.t;
+    hi.point = add(o, scl(d, h.t));
+    return hi;
+}
+
+/* pdf eval dispatch: always MaterialPhong::evalPdf (pg/ReSTIRIntegrator.h:54-59, pg/MaterialPhong.cpp:150-172) */
+static float phong_eval_pdf(const or_gbe* g, v3 cam, v3 wi) {
+    float maxD = maxc(g->kd), maxS = maxc(g->ks);
+    float pf = maxD / (maxD + maxS);
+    float pdf = gmax(dot(g->nrm, wi), 0.0f) * OR_ONE_OVER_PI * pf;
+    v3 wo = nrmz(sub(g->pos, cam));
+    v3 wr = nrmz(reflect(wo, g->nrm));
+    pdf += (g->shin + 1.0f) * OR_ONE_OVER_2PI * powf(gmax(0.0f, dot(wi, wr)), g->shin) * (1.0f - pf);
+    return pdf;
+}
+
+/* brdf eval dispatch (pg/ReSTIRIntegrator.h:32-41) */
+static v3 eval_brdf(const or_gbe* g, v3 cam, v3 wi, float im_cached, int use_cache) {
+    int phong = g->type == MT_PHONG || g->type == MT_DIELECTRIC;
+    if (!phong) return scl(g->kd, OR_ONE_OVER_PI);     /* MaterialLambert::evalBRDF (pg/MaterialLambert.cpp:33-41) */
+    /* MaterialPhong::evalBRDF (pg/MaterialPhong.cpp:122-148) */
+    v3 Vv = nrmz(sub(cam, g->pos));
+    v3 f = scl(g->kd, OR_ONE_OVER_PI);
+    float i_m;
+    if (use_cache) i_m = im_cached;
+    else { float nDotV = dot(Vv, g->nrm); i_m = 1.0f / or_calc_I_M(nDotV, g->shin); }
+    v3 wr = nrmz(reflect(neg(Vv), g->nrm));
+    float pw = powf(gmax(dot(wi, wr), 0.0f), g->shin);
+    f = add(f, scl(scl(g->ks, i_m), pw));
+    return f;
+}
+
+/* ReSTIRIntegrator::evaluateF (pg/ReSTIRIntegrator.cpp:185-211).  The shadow ray is skipped
+ * when L_i*f_r*G is exactly zero in every channel: the product is then 0 whatever V is. */
+static v3 evaluate_f(const fctx* F, sample_t smp, v3 cam, const or_gbe* g, float im, int test_vis, uint64_t* rays) {
+    if (!smp_valid(smp) || g->le.x > 0 || g->le.y > 0 || g->le.z > 0) return V(0, 0, 0);
+    v3 ld = sub(smp.p, g->pos);
+    float r2 = dot(ld, ld);
+    ld = nrmz(ld);
+    float cI = gmax(dot(ld, g->nrm), 0.0f);
+    float cY = fabsf(dot(neg(ld), smp.n));
+    float G = cI * cY / r2;
+    v3 fr = eval_brdf(g, cam, ld, im, F->c->cache_im);
+    v3 L = scl(mul(smp.li, fr), G);
+    if (test_vis && !(L.x == 0.0f && L.y == 0.0f && L.z == 0.0f)) {
+        int vis = !occluded(F, g->pos, smp.p, rays);
+        L = scl(L, (float)vis);
+    }
+    return L;
+}
+/* evaluatePHat = length(evaluateF) (pg/ReSTIRIntegrator.cpp:180-183) */
+static float eval_phat(const fctx* F, sample_t smp, v3 cam, const or_gbe* g, float im, int test_vis, uint64_t* rays) {
+    return len(evaluate_f(F, smp, cam, g, im, test_vis, rays));
+}
+
+/* CosineWeightedDistribution::sample (pg/Distribution.h:7-28) */
+static v3 ortho(v3 v) {                       /* Utils::orthogonal (pg/utils.cpp:204-207) */
+    return fabsf(v.x) > fabsf(v.z) ? V(v.y, -v.x, 0.0f) : V(0.0f, v.z, -v.y);
+}
+static v3 to_world(v3 smp, v3 n) {
+    v3 o2 = nrmz(ortho(n));
+    v3 o1 = nrmz(cross(n, o2));
+    o2 = nrmz(cross(o1, n));
+    /* glm::mat3{o1,o2,n} * smp */
+    return V(o1.x * smp.x + o2.x * smp.y + n.x * smp.z,
+             o1.y * smp.x + o2.y * smp.y + n.y * smp.z,
+             o1.z * smp.x + o2.z * smp.y + n.z * smp.z);
+}
+static v3 cosine_sample(v3 n, rng_t* rng) {
+    float r1 = rnd(rng, 0, 1), r2 = rnd(rng, 0, 1);
+    float ang = OR_PI * 2.0f * r1;
+    float x = cosf(ang) * sqrtf(1.0f - r2);
+    float y = sinf(ang) * sqrtf(1.0f - r2);
+    float z = sqrtf(r2);
+    return to_world(nrmz(V(x, y, z)), n);
+}
+/* CosineLobeDistribution::sample (pg/Distribution.h:37-57) */
+static v3 lobe_sample(v3 wr, float gamma, rng_t* rng) {
+    float r1 = rnd(rng, 0, 1), r2 = rnd(rng, 0, 1);
+    float ang = 2.0f * OR_PI * r1;
+    float x = cosf(ang) * sqrtf(1.0f - powf(r2, 2.0f / (gamma + 1.0f)));
+    float y = sinf(ang) * sqrtf(1.0f - powf(r2, 2.0f / (gamma + 1.0f)));
+    float z = powf(r2, 1.0f / (gamma + 1.0f));
+    return to_world(nrmz(V(x, y, z)), wr);
+}
+
+/* BRDF sampling dispatch (pg/ReSTIRIntegrator.h:43-52): returns omega_i and pdf */
+static v3 sample_brdf(const or_gbe* g, v3 cam, rng_t* rng, float* pdf_out) {
+    if (g->type == MT_LAMBERT) {
+        /* MaterialLambert::sampleBRDF (pg/MaterialLambert.cpp:43-53) */
+        v3 wi = cosine_sample(g->nrm, rng);
+        *pdf_out = gmax(dot(g->nrm, wi), 0.0f) * OR_ONE_OVER_PI;
+        return wi;
+    }
+    /* MaterialPhong::sampleBRDF (pg/MaterialPhong.cpp:174-222) */
+    v3 wo = nrmz(sub(g->pos, cam));
+    float maxD = maxc(g->kd), maxS = maxc(g->ks);
+    float r0 = rnd(rng, 0.0f, maxD + maxS);
+    float pf = maxD / (maxD + maxS);
+    v3 wr = nrmz(reflect(wo, g->nrm));
+    v3 wi;
+    if (r0 < maxD) wi = cosine_sample(g->nrm, rng);
+    else wi = lobe_sample(wr, g->shin, rng);
+    float pd = gmax(dot(g->nrm, wi), 0.0f) * OR_ONE_OVER_PI * pf;
+    float ps = (g->shin + 1.0f) * OR_ONE_OVER_2PI * powf(gmax(0.0f, dot(wi, wr)), g->shin) * (1.0f - pf);
+    *pdf_out = pd + ps;
+    return wi;
+}
+
+/* m_area / m_brdf (pg/ReSTIRIntegrator.h:62-74) */
+static inline float m_area(const or_params* P, float pa, float pb) {
+    if (pa == 0.0f && pb == 0.0f) return 0.0f;
+    return pa / ((float)P->m_area * pa + (float)P->m_brdf * pb);
+}
+static inline float m_brdf(const or_params* P, float pb, float pa) {
+    if (pa == 0.0f && pb == 0.0f) return 0.0f;
+    return pb / ((float)P->m_area * pa + (float)P->m_brdf * pb);
+}
+
+/* ------------------------------------------------------------------ passes */
+/* Camera (pg/camera.cpp:12-58,81-84) */
+typedef struct { v3 eye; m4 view, inv_view; float focal; } or_cam;
+static or_cam make_cam(const float* cam7, int W, int H) {
+    or_cam c;
+    v3 from = V(cam7[0], cam7[1], cam7[2]), at = V(cam7[3], cam7[4], cam7[5]);
+    float fov = cam7[6];
+    /* setFOV: fov_y = radians(fov); f_y = H / (2 tanf(fov_y/2)) */
+    float fov_rad = fov * 0.01745329251994329576923690768489f;
+    c.focal = (float)H / (2.0f * tanf(fov_rad / 2.0f));
+    /* recalculate_m_c_w */
+    v3 up = V(0.0f, 0.0f, 1.0f);
+    v3 zc = nrmz(sub(from, at));
+    v3 xc = nrmz(cross(up, zc));
+    v3 yc = nrmz(cross(zc, xc));
+    c.view = look_at_rh(from, at, yc);
+    c.inv_view = inverse4(&c.view);
+    c.eye = from;
+    return c;
+}
+/* Camera::GenerateRay (pg/camera.cpp:20-42), CenterSampler => pixel corner */
+static v3 primary_dir(const or_cam* c, int x, int y, int W, int H) {
+    v3 dc = V((float)x - (float)W / 2.0f, (float)H / 2.0f - (float)y, -c->focal);
+    return nrmz(m3_mul(&c->inv_view, dc));
+}
+
+/* gBufferFillPass (pg/ReSTIRIntegrator.cpp:213-234) */
+static void pass_gbuffer(fctx* F, const or_cam* cam, or_gbe* G, float* im, int y0, int y1, uint64_t* rays) {
+    const or_params* P = F->P; const or_scene* s = F->s; int W = F->c->W, H = F->c->H;
+    uint64_t rc = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+:rc)
+    for (int y = y0; y < y1; ++y) {
+        for (int x = 0; x < W; ++x) {
+            v3 d = primary_dir(cam, x, y, W, H);
+            hitinfo h = intersect(F, cam->eye, d, FLT_MIN + 0.01f, &rc);
+            or_gbe e; memset(&e, 0, sizeof e);
+            float imv = 0.0f;
+            if (h.hit) {
+                const or_mat* m = &s->mats[s->mat[h.prim]];
+                e.pos = h.point; e.nrm = h.normal;
+                e.depth = len(sub(h.point, cam->eye));
+                e.type = m->type; e.kd = m->kd; e.ks = m->ks; e.le = m->le; e.shin = m->shin;
+                if (e.type == MT_PHONG || e.type == MT_DIELECTRIC) {
+                    v3 Vv = nrmz(sub(cam->eye, e.pos));
+                    imv = 1.0f / or_calc_I_M(dot(Vv, e.nrm), e.shin);
+                }
+            } else {
+                e.le = P->use_skybox ? V(0, 0, 0) : V(P->bg_color[0], P->bg_color[1], P->bg_color[2]);
+            }
+            G[(size_t)y * W + x] = e;
+            im[(size_t)y * W + x] = imv;
+        }
+    }
+    (void)H;
+    *rays += rc;
+}
+
+/* areaSampleLight (pg/ReSTIRIntegrator.cpp:89-124) + TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54)
+ * + Sampling::sampleTriangle (pg/Sampling.cpp:63-76) */
+static sample_t area_sample(const fctx* F, const or_gbe* g, v3 cam, rng_t* rng, float* W_out, float* mis_out) {
+    const or_scene* s = F->s;
+    float ksi = rnd(rng, 0.0f, 1.0f);
+    /* std::lower_bound(cdf2, ksi) */
+    uint32_t lo = 0, n = s->n_emis;
+    while (n > 0) { uint32_t h = n / 2; if (s->cdf[lo + h] < ksi) { lo = lo + h + 1; n = n - h - 1; } else n = h; }
+    uint32_t idx = lo;
+    if (idx >= s->n_emis) idx = s->n_emis - 1;
+    float pick = s->pick_pdf[idx];
+    uint32_t t = s->emis_tri[idx];
+    float r1 = rnd(rng, 0, 1), r2 = rnd(rng, 0, 1);
+    float x = 1.0f - sqrtf(r1);
+    float y = sqrtf(r1) * (1.0f - r2);
+    float z = sqrtf(r1) * r2;
+    v3 pt = add(add(scl(s->p0[t], x), scl(s->p1[t], y)), scl(s->p2[t], z));
+    v3 nn = nrmz(add(add(scl(s->n0[t], x), scl(s->n1[t], y)), scl(s->n2[t], z)));
+    float tri_pdf = 1.0f / s->area[idx];
+    float pdf_area = pick * tri_pdf;
+    v3 ld = sub(pt, g->pos);
+    float r2s = dot(ld, ld);
+    ld = nrmz(ld);
+    float cY = gmax(dot(neg(ld), nn), 0.0f);
+    float amf = cY / r2s;
+    float pb = phong_eval_pdf(g, cam, ld);
+    float pba = pb * amf;
+    sample_t smp = {pt, nn, s->mats[s->mat[t]].le};
+    *mis_out = m_area(F->P, pdf_area, pba);
+    *W_out = 1.0f / pdf_area;
+    return smp;
+}
+
+/* brdfSampleLight (pg/ReSTIRIntegrator.cpp:126-177) */
+static sample_t brdf_sample(const fctx* F, const or_gbe* g, v3 cam, rng_t* rng, float* W_out, float* mis_out, uint64_t* rays) {
+    const or_scene* s = F->s; const or_params* P = F->P;
+    float pdf;
+    v3 wi = sample_brdf(g, cam, rng, &pdf);
+    v3 org = add(g->pos, scl(g->nrm, P->normal_offset));
+    hitinfo h = intersect(F, org, wi, FLT_MIN + P->tnear_offset, rays);
+    sample_t smp = smp_invalid();
+    *W_out = 0.0f; *mis_out = 0.0f;
+    if (h.hit) {
+        const or_mat* m = &s->mats[s->mat[h.prim]];
+        if (m->le.x + m->le.y + m->le.z > 0) {
+            v3 ld = sub(h.point, g->pos);
+            float r2s = dot(ld, ld);
+            ld = nrmz(ld);
+            float cY = gmax(dot(neg(ld), h.normal), 0.0f);
+            float amf = cY / r2s;
+            int32_t e = s->emis_id[h.prim];
+            /* TriangleCDF::getPDFForTriangle (pg/TriangleCDF.h:25-31) */
+            float pdf_area = s->area[e] / s->total_area;
+            pdf_area *= 1.0f / s->area[e];
+            float bpa = pdf * amf;
+            smp.p = h.point; smp.n = h.normal; smp.li = m->le;
+            *W_out = 1.0f / bpa;
+            *mis_out = m_brdf(P, bpa, pdf_area);
+        }
+    }
+    return smp;
+}
+
+/* initialRenderPass (pg/ReSTIRIntegrator.cpp:236-298) */
+static void pass_initial(fctx* F, or_res* Rw, int y0, int y1, uint64_t* rays) {
+    const or_params* P = F->P; int W = F->c->W; v3 cam = F->gc->pos;
+    uint64_t rc = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+:rc)
+    for (int y = y0; y < y1; ++y) {
+        for (int x = 0; x < W; ++x) {
+            size_t p = (size_t)y * W + x;
+            const or_gbe* g = &F->G[p];
+            float im = F->im[p];
+            if (nonzero_pos(g->le) || F->s->n_emis == 0) { Rw[p] = res_empty(); continue; }
+            rng_t rng = rng_init(P->seed, F->frame, PASS_INITIAL, (uint32_t)p);
+            or_res r = res_empty();
+            int tv = !P->do_visibility_pass;
+            float best_phat = 0.0f;   /* p-hat of the selected candidate: the final p-hat (:289) */
+            if (P->m_area > 0) {
+                float inv_ma = 1.0f / (float)P->m_area;
+                for (int i = 0; i < P->m_area; ++i) {
+                    float Wc, mis;
+                    sample_t smp = area_sample(F, g, cam, &rng, &Wc, &mis);
+                    float ph = eval_phat(F, smp, cam, g, im, tv, &rc);
+                    float w = P->m_brdf > 0 ? mis * ph * Wc : inv_ma * ph * Wc;
+                    if (res_add(&r, smp, w, 1, &rng)) best_phat = ph;
+                }
+            }
+            if (P->m_brdf > 0) {
+                float inv_mb = 1.0f / (float)P->m_brdf;
+                for (int i = 0; i < P->m_brdf; ++i) {
+                    float Wc, mis;
+                    sample_t smp = brdf_sample(F, g, cam, &rng, &Wc, &mis, &rc);
+                    float ph = eval_phat(F, smp, cam, g, im, tv, &rc);
+                    float w = P->m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
+                    if (res_add(&r, smp, w, 1, &rng)) best_phat = ph;
+                }
+            }
+            float ph = sample_valid(&r) ? best_phat : 0.0f;
+            r.W = ph > 0.0f ? 1.0f / ph * r.wsum : 0.0f;
+            res_cap(&r, P->confidence_cap);
+            Rw[p] = r;
+        }
+    }
+    *rays += rc;
+}
+
+/* visibilityPass (pg/ReSTIRIntegrator.cpp:302-312) */
+static void pass_visibility(fctx* F, or_res* Rw, int y0, int y1, uint64_t* rays) {
+    int W = F->c->W; uint64_t rc = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+:rc)
+    for (int y = y0; y < y1; ++y)
+        for (int x = 0; x < W; ++x) {
+            size_t p = (size_t)y * W + x;
+            /* invalid samples only ever carry W == 0 already: skip their (meaningless) ray */
+            if (!sample_valid(&Rw[p])) continue;
+            if (occluded(F, F->G[p].pos, Rw[p].p, &rc)) Rw[p].W = 0;
+        }
+    *rays += rc;
+}
+
+/* reprojectBackward / reprojectForward (pg/ReSTIRIntegrator.cpp:544-587) */
+static int reproject(const or_gcam* gc, v3 ws, int W, int H, int* sx, int* sy) {
+    v3 vs = m4_mul_point(&gc->view, ws);
+    if (vs.z >= 0) return 0;
+    float fx = (-vs.x / vs.z) * gc->focal + (float)W / 2.0f;
+    float fy = (vs.y / vs.z) * gc->focal + (float)H / 2.0f;
+    float rx = roundf(fx), ry = roundf(fy);   /* glm::round = std::round (half away from zero) */
+    /* int conversion of the rounded value; out-of-range values are rejected below */
+    if (!(rx >= -2147483648.0f && rx < 2147483648.0f) || !(ry >= -2147483648.0f && ry < 2147483648.0f)) return 0;
+    int X = (int)rx, Y = (int)ry;
+    if (X < 0 || X > W - 1 || Y < 0 || Y > H - 1) return 0;
+    *sx = X; *sy = Y;
+    return 1;
+}
+
+/* temporalReusePass (pg/ReSTIRIntegrator.cpp:625-732) */
+static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* Rw, int y0, int y1, uint64_t* rays) {
+    const or_params* P = F->P; int W = F->c->W, H = F->c->H;
+    uint64_t rc = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+:rc)
+    for (int y = y0; y < y1; ++y)
+        for (int x = 0; x < W; ++x) {
+            size_t p = (size_t)y * W + x;
+            const or_gbe* cur = &F->G[p];
+            v3 ccam = F->gc->pos, pcam = F->gcp->pos;
+            const or_res* cr = &Rr[p];
+            const or_res* pr = &Rl[p];       /* previous reservoir read at the CURRENT pixel (:641) */
+            int qx, qy;
+            if (!reproject(F->gcp, cur->pos, W, H, &qx, &qy)) { Rw[p] = *cr; continue; }
+            size_t q = (size_t)qy * W + qx;
+            const or_gbe* prev = &F->Gp[q];
+            float cd = len(sub(cur->pos, ccam));
+            float pd = len(sub(prev->pos, pcam));
+            float dr = cd > pd ? pd / cd : cd / pd;
+            if (dr < 0.9f) { Rw[p] = *cr; continue; }
+            const or_gbe* pac = &F->Gp[p];
+            int fx, fy;
+            if (!reproject(F->gc, pac->pos, W, H, &fx, &fy)) { Rw[p] = *cr; continue; }
+            const or_gbe* fw = &F->G[(size_t)fy * W + fx];
+            float cdp = len(sub(pac->pos, pcam));
+            float pdp = len(sub(fw->pos, ccam));
+            float drp = cdp > pdp ? pdp / cdp : cdp / pdp;
+            if (drp < 0.9f) { Rw[p] = *cr; continue; }
+
+            rng_t rng = rng_init(P->seed, F->frame, PASS_TEMPORAL, (uint32_t)p);
+            or_res res = res_empty();
+            float imc = F->im[p], imq = F->imp[q];
+            sample_t cs = smp_of(cr), ps = smp_of(pr);
+            float p_cur = eval_phat(F, cs, ccam, cur, imc, 1, &rc);
+            float p_prev = eval_phat(F, cs, pcam, prev, imq, 1, &rc);
+            float m_cur = p_cur * (float)cr->conf / (p_cur * (float)cr->conf + p_prev * (float)pr->conf);
+            if (!(m_cur > 0)) m_cur = 0.0f;
+            float ph_cur = p_cur;  /* :706 re-evaluates the identical p-hat */
+            float w_cur = m_cur * ph_cur * cr->W;
+            int took_cur = res_add(&res, cs, w_cur, cr->conf, &rng);
+            p_cur = eval_phat(F, ps, ccam, cur, imc, 1, &rc);
+            p_prev = eval_phat(F, ps, pcam, prev, imq, 1, &rc);
+            float m_prev = p_prev * (float)pr->conf / (p_cur * (float)cr->conf + p_prev * (float)pr->conf);
+            if (!(m_prev > 0)) m_prev = 0.0f;
+            float ph_prev = p_cur;  /* :721 re-evaluates the identical p-hat */
+            float w_prev = m_prev * ph_prev * pr->W;
+            int took_prev = res_add(&res, ps, w_prev, pr->conf, &rng);
+            res_cap(&res, P->confidence_cap);
+            /* final p-hat (:727) of the surviving sample at the current pixel */
+            float fph = took_prev ? ph_prev : (took_cur ? ph_cur : 0.0f);
+            res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
+            Rw[p] = res;
+        }
+    *rays += rc;
+}
+
+/* Sampling::sampleDiskUniform (pg/Sampling.cpp:78-87) + vec2 -> ivec2 truncation */
+static void disk_offset(float radius, rng_t* rng, int* ox, int* oy) {
+    float theta = rnd(rng, 0, 2.0f) * OR_PI;
+    float r = sqrtf(rnd(rng, 0, radius));
+    float x = r * cosf(theta);
+    float y = r * sinf(theta);
+    *ox = (int)x; *oy = (int)y;
+}
+
+/* spatialReusePass (pg/ReSTIRIntegrator.cpp:316-542) */
+static void pass_spatial(fctx* F, const or_res* Rr, or_res* Rw, int pass_idx, int y0, int y1, uint64_t* rays) {
+    const or_params* P = F->P; int W = F->c->W, H = F->c->H;
+    v3 cam = F->gc->pos;
+    uint64_t rc = 0;
+    int kmax = P->spatial_neighbors;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+:rc)
+    for (int y = y0; y < y1; ++y) {
+        int* nb = (int*)malloc(sizeof(int) * (size_t)(kmax + 1));
+        for (int x = 0; x < W; ++x) {
+            size_t p = (size_t)y * W + x;
+            const or_gbe* th = &F->G[p];
+            if (nonzero_pos(th->le)) { Rw[p] = Rr[p]; continue; }
+            rng_t rng = rng_init(P->seed, F->frame, PASS_SPATIAL0 + (uint32_t)pass_idx, (uint32_t)p);
+            int M = 1, cnt = 0;
+            nb[cnt++] = (int)p;
+            for (int i = 0; i < kmax; ++i) {
+                int ox, oy;
+                disk_offset(P->spatial_radius, &rng, &ox, &oy);
+                int nx = x + ox, ny = y + oy;
+                nx = nx < 0 ? 0 : (nx > W - 1 ? W - 1 : nx);    /* glm::clamp = min(max()) */
+                ny = ny < 0 ? 0 : (ny > H - 1 ? H - 1 : ny);
+                size_t q = (size_t)ny * W + nx;
+                const or_gbe* ne = &F->G[q];
+                if (nonzero_pos(ne->le)) continue;
+                if (P->reject_dissimilar) {
+                    float ns = dot(ne->nrm, th->nrm);
+                    if (ns < P->min_normal_similarity) continue;
+                    float dr = 0;
+                    if (ne->depth > 0) dr = th->depth / ne->depth;
+                    float hd = P->max_depth_difference * 0.5f;
+                    if (dr < 1.0f - hd || dr > 1.0f + hd) continue;
+                }
+                nb[cnt++] = (int)q; M += 1;
+            }
+            int csum = 0, csum_nc = 0;
+            for (int i = 0; i < cnt; ++i) { int c = Rr[nb[i]].conf; csum += c; if (i) csum_nc += c; }
+            or_res res = res_empty();
+            int sel = 0;
+            float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
+            float sel_phat = 0.0f;
+            for (int i = 0; i < cnt; ++i) {
+                const or_res* ri = &Rr[nb[i]];
+                sample_t si = smp_of(ri);
+                float mis = rcpM;
+                if (P->spatial_mis == MIS_BALANCE) {
+                    float num = 0, den = 0; mis = 0.0f;
+                    for (int j = 0; j < cnt; ++j) {
+                        const or_res* rj = &Rr[nb[j]];
+                        float ph = eval_phat(F, si, cam, &F->G[nb[j]], F->im[nb[j]], 1, &rc);
+                        den += ph * rj->conf;
+                        if (i == j) num = ph * ri->conf;
+                    }
+                    if (den > 0) mis = num / den;
+                }
+                if (P->spatial_mis == MIS_PAIRWISE) {
+                    mis = 0.0f;
+                    if (i == 0) {
+                        float sum = 0.0f;
+                        float phc = eval_phat(F, si, cam, &F->G[nb[i]], F->im[nb[i]], 1, &rc) * (float)ri->conf;
+                        for (int j = 1; j < cnt; ++j) {
+                            const or_res* rj = &Rr[nb[j]];
+                            float phj = eval_phat(F, si, cam, &F->G[nb[j]], F->im[nb[j]], 1, &rc);
+                            float den = phc + phj * (float)csum_nc;
+                            if (den > 0) {
+                                float cf = (float)rj->conf / (float)csum;
+                                sum += cf * (phc / den);
+                            }
+                        }
+                        mis = ((float)ri->conf / (float)csum) + sum;
+                    } else {
+                        float phi = eval_phat(F, si, cam, &F->G[nb[i]], F->im[nb[i]], 1, &rc);
+                        float phc = eval_phat(F, si, cam, &F->G[nb[0]], F->im[nb[0]], 1, &rc);
+                        phi *= (float)csum_nc;
+                        float den = phi + phc * (float)Rr[nb[0]].conf;
+                        if (den > 0 && csum > 0) mis = ((float)ri->conf / (float)csum) * (phi / den);
+                    }
+                }
+                float rph = eval_phat(F, si, cam, th, F->im[p], 1, &rc);
+                float rw = mis * rph * ri->W;
+                if (res_add(&res, si, rw, ri->conf, &rng)) { sel = i; sel_phat = rph; }
+            }
+            /* final p-hat (:481): p-hat of the surviving sample at this pixel = sel_phat */
+            float fph = sample_valid(&res) ? sel_phat : 0.0f;
+            if (P->spatial_mis == MIS_CONSTANT || P->spatial_mis == MIS_BALANCE || P->spatial_mis == MIS_PAIRWISE) {
+                res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
+            } else if (P->spatial_mis == MIS_DEBIAS_Z) {
+                int Z = 0; float corr = 1.0f;
+                for (int i = 0; i < cnt; ++i)
+                    if (!occluded(F, F->G[nb[i]].pos, res.p, &rc)) Z += 1;
+                if (Z > 0 && M > 0) corr = (1.0f / (float)Z) / rcpM;
+                res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
+            } else if (P->spatial_mis == MIS_DEBIAS_CONTRIB) {
+                sample_t ss = smp_of(&Rr[nb[sel]]);
+                float num = 0, den = 0, cw = 0, corr = 0;
+                for (int i = 0; i < cnt; ++i) {
+                    const or_res* ri = &Rr[nb[i]];
+                    float ph = eval_phat(F, ss, cam, &F->G[nb[i]], F->im[nb[i]], 1, &rc);
+                    den += ph * (float)ri->conf;
+                    if (i == sel) num = ph * (float)ri->conf;
+                }
+                if (den > 0) cw = num / den;
+                if (M > 0) corr = cw / rcpM;
+                res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
+            }
+            res_cap(&res, P->confidence_cap);
+            Rw[p] = res;
+        }
+        free(nb);
+    }
+    *rays += rc;
+}
+
+/* Integrator::sanitize (pg/Integrator.cpp:6-22) */
+static v3 sanitize(v3 l) {
+    if (isnan(l.x) || isnan(l.y) || isnan(l.z)) l = V(0, 0, 0);
+    if (l.x < 0 || l.y < 0 || l.z < 0) l = V(0, 0, 0);
+    return l;
+}
+
+/* shade loop (pg/simpleguidx11.cpp:447-472) */
+static void pass_shade(fctx* F, const or_res* Rr, float* out, int y0, int y1, uint64_t* rays) {
+    int W = F->c->W; v3 cam = F->gc->pos; uint64_t rc = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+:rc)
+    for (int y = y0; y < y1; ++y)
+        for (int x = 0; x < W; ++x) {
+            size_t p = (size_t)y * W + x;
+            const or_res* r = &Rr[p];
+            v3 px;
+            if (r->wsum > 0.0f) {     /* Reservoir::hasSample (pg/Reservoir.h:49-52) */
+                v3 f = evaluate_f(F, smp_of(r), cam, &F->G[p], F->im[p], 1, &rc);
+                px = scl(f, r->W);
+            } else px = F->G[p].le;
+            px = sanitize(px);
+            float* o = out + 3 * (size_t)(y - y0) * W + 3 * (size_t)x;
+            o[0] = px.x; o[1] = px.y; o[2] = px.z;
+        }
+    *rays += rc;
+}
+
+/* SimpleGuiDX11::produceRestir (pg/simpleguidx11.cpp:359-487) for one frame.
+ * cam7 = {eye.xyz, at.xyz, fov_y_deg}; out_rgb = W*H*3 floats (frame_data). */
+int or_render_frame(or_ctx* c, const or_scene* s, const float* cam7, const or_params* P,
+                    uint32_t frame_index, float* out_rgb, uint64_t* rays_out) {
+    int W = c->W, H = c->H;
+    /* useSkybox needs the equirect sky (pg/SphericalMap.cpp:10-14), whose HDR is a missing
+       blob in the reference checkout: only the background-colour miss path is restated. */
+    if (P->use_skybox) return -2;
+    or_cam cam = make_cam(cam7, W, H);
+    /* G-buffer ping-pong instead of gBufferLastFrame.setDataFrom (:480) */
+    int gcur = c->gcur ^ 1, gprev = c->gcur;
+    c->gc[gcur].pos = cam.eye; c->gc[gcur].view = cam.view; c->gc[gcur].inv_view = cam.inv_view;
+    c->gc[gcur].focal = cam.focal;
+    fctx F;
+    F.s = s; F.c = c; F.P = P; F.frame = frame_index;
+    F.G = c->g[gcur]; F.Gp = c->g[gprev]; F.gc = &c->gc[gcur]; F.gcp = &c->gc[gprev];
+    F.im = c->im_cache[gcur]; F.imp = c->im_cache[gprev];
+    uint64_t rays = 0;
+    pass_gbuffer(&F, &cam, c->g[gcur], c->im_cache[gcur], 0, H, &rays);
+
+    /* reservoir buffer choice: never overwrite R_last before the temporal pass */
+    int last = c->r_last;
+    int a = (last + 1) % 3, b = (last + 2) % 3;
+    pass_initial(&F, c->r[a], 0, H, &rays);
+    if (P->do_visibility_pass) pass_visibility(&F, c->r[a], 0, H, &rays);
+    int cur = a;
+    if (P->do_temporal && c->frames > 0) {
+        pass_temporal(&F, c->r[cur], c->r[last], c->r[b], 0, H, &rays);
+        cur = b;
+    }
+    if (P->do_spatial) {
+        for (int i = 0; i < P->spatial_passes; ++i) {
+            int dst = (cur == a) ? b : a;   /* after temporal R_last is free to reuse, but a/b suffice */
+            pass_spatial(&F, c->r[cur], c->r[dst], i, 0, H, &rays);
+            cur = dst;
+        }
+    }
+    pass_shade(&F, c->r[cur], out_rgb, 0, H, &rays);
+    c->r_last = cur;
+    c->gcur = gcur;
+    c->frames++;
+    if (rays_out) *rays_out = rays;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ dumps / KAT hooks */
+/* G-buffer dump: 19 floats per pixel: pos3 nrm3 kd3 ks3 le3 shin depth type inv_IM */
+int or_get_gbuffer(const or_ctx* c, int prev, float* out) {
+    int gi = prev ? (c->gcur ^ 1) : c->gcur;
+    size_t n = (size_t)c->W * c->H;
+    for (size_t p = 0; p < n; ++p) {
+        const or_gbe* e = &c->g[gi][p]; float* o = out + 19 * p;
+        o[0] = e->pos.x; o[1] = e->pos.y; o[2] = e->pos.z; o[3] = e->nrm.x; o[4] = e->nrm.y; o[5] = e->nrm.z;
+        o[6] = e->kd.x; o[7] = e->kd.y; o[8] = e->kd.z; o[9] = e->ks.x; o[10] = e->ks.y; o[11] = e->ks.z;
+        o[12] = e->le.x; o[13] = e->le.y; o[14] = e->le.z; o[15] = e->shin; o[16] = e->depth;
+        o[17] = (float)e->type; o[18] = c->im_cache[gi][p];
+    }
+    return 0;
+}
+/* Final reservoir dump (the buffer shaded last frame = R_last): 12 floats per pixel:
+   point3 normal3 Li3 w_sum W confidence */
+int or_get_reservoirs(const or_ctx* c, float* out) {
+    size_t n = (size_t)c->W * c->H;
+    const or_res* R = c->r[c->r_last];
+    for (size_t p = 0; p < n; ++p) {
+        const or_res* r = &R[p]; float* o = out + 12 * p;
+        o[0] = r->p.x; o[1] = r->p.y; o[2] = r->p.z; o[3] = r->n.x; o[4] = r->n.y; o[5] = r->n.z;
+        o[6] = r->li.x; o[7] = r->li.y; o[8] = r->li.z; o[9] = r->wsum; o[10] = r->W; o[11] = (float)r->conf;
+    }
+    return 0;
+}
+/* camera KAT: view16 (column-major), inv16, focal, dir3 for pixel (px,py) */
+int or_camera_kat(const float* cam7, int W, int H, int px, int py, float* out) {
+    or_cam c = make_cam(cam7, W, H);
+    memcpy(out, c.view.m, 64); memcpy(out + 16, c.inv_view.m, 64);
+    out[32] = c.focal;
+    v3 d = primary_dir(&c, px, py, W, H);
+    out[33] = d.x; out[34] = d.y; out[35] = d.z;
+    return 0;
+}
+int or_reproject_kat(const float* cam7, int W, int H, const float* ws, int* out_xy) {
+    or_cam c = make_cam(cam7, W, H);
+    or_gcam g; g.pos = c.eye; g.view = c.view; g.inv_view = c.inv_view; g.focal = c.focal;
+    int x = -1, y = -1;
+    if (!reproject(&g, V(ws[0], ws[1], ws[2]), W, H, &x, &y)) { x = -1; y = -1; }
+    out_xy[0] = x; out_xy[1] = y;
+    return 0;
+}
+float or_rng_u(uint32_t seed, uint32_t frame, uint32_t pass, uint32_t pixel, uint32_t n) {
+    rng_t r = rng_init(seed, frame, pass, pixel); r.n = n; return rng_u(&r);
+}
+/* scene introspection for tests */
+uint32_t or_scene_n_emissive(const or_scene* s) { return s->n_emis; }
+float or_scene_total_area(const or_scene* s) { return s->total_area; }
+int or_scene_cdf(const or_scene* s, float* cdf, float* pick, float* area) {
+    for (uint32_t e = 0; e < s->n_emis; ++e) { cdf[e] = s->cdf[e]; pick[e] = s->pick_pdf[e]; area[e] = s->area[e]; }
+    return 0;
+}
+/* closest-hit / any-hit probes (ray batches) for traversal parity tests */
+int or_trace_closest(const or_scene* s, int n, const float* o, const float* d, float tnear, float tfar,
+                     float* t_out, int32_t* prim_out) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+        or_hit h = closest_hit(s, V(o[3 * i], o[3 * i + 1], o[3 * i + 2]), V(d[3 * i], d[3 * i + 1], d[3 * i + 2]), tnear, tfar);
+        t_out[i] = h.hit ? h.t : -1.0f; prim_out[i] = h.hit ? (int32_t)h.prim : -1;
+    }
+    return 0;
+}
+int or_trace_any(const or_scene* s, int n, const float* o, const float* d, const float* tnear, const float* tfar, int32_t* hit_out) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i)
+        hit_out[i] = any_hit(s, V(o[3 * i], o[3 * i + 1], o[3 * i + 2]), V(d[3 * i], d[3 * i + 1], d[3 * i + 2]), tnear[i], tfar[i]);
+    return 0;
+}
+int or_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+void or_set_num_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}

@@ -1,0 +1,622 @@
+// restir_capi.hip -- C ABI (include/restir_c.h) over the gfx950 kernels.
+//
+// Host side of the drop-in boundary: owns the per-pixel buffers the reference keeps in
+// SimpleGuiDX11 (pg/simpleguidx11.cpp:113-119, pg/simpleguidx11.h:27-66), uploads scenes
+// (pg/Scene.cpp:8-16, pg/ModelLoader.cpp:218-321, pg/TriangleCDF.cpp:8-34), computes the camera
+// (pg/camera.cpp:12-84) and sequences the passes of produceRestir (pg/simpleguidx11.cpp:359-487).
+#include "rs_passes.h"
+#include "../../include/restir_c.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace rs {
+int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes, float4** d_tris,
+              std::string& err);
+int load_obj_file(const char* path, std::vector<float>& pos, std::vector<float>& nrm, std::vector<uint32_t>& tri_mat,
+                  std::vector<rs_material_desc>& mats, std::string& err);
+}
+
+using namespace rs;
+
+static thread_local std::string g_last_error;
+
+struct rs_scene {
+    rs_context* ctx = nullptr;
+    uint32_t n_tris = 0, n_emis = 0, n_mats = 0, n_nodes = 0;
+    float* d_pos = nullptr;
+    float4 *d_nodes = nullptr, *d_tris = nullptr, *d_tri_nrm = nullptr, *d_mats = nullptr, *d_emis = nullptr;
+    float* d_cdf = nullptr;
+    float build_ms = 0.0f;
+    DevScene dev() const {
+        DevScene S;
+        S.nodes = d_nodes; S.tris = d_tris; S.tri_nrm = d_tri_nrm; S.mats = d_mats; S.emis = d_emis; S.cdf = d_cdf;
+        S.n_nodes = n_nodes; S.n_tris = n_tris; S.n_emis = n_emis; S.n_mats = n_mats;
+        return S;
+    }
+};
+
+enum { EV_BEGIN, EV_INIT, EV_VIS, EV_TEMPORAL, EV_SPATIAL, EV_SHADE, EV_COUNT };
+
+struct rs_context {
+    int device = 0, W = 0, H = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    GBuf G[2] = {};
+    GCam gcam[2] = {};
+    int gcur = 0;
+    float4* R[3] = {nullptr, nullptr, nullptr};
+    int r_last = 2;
+    float* fb = nullptr;
+    Counters* d_cnt = nullptr;
+    Counters* h_cnt = nullptr;
+    hipEvent_t ev[EV_COUNT] = {};
+    uint64_t frames = 0;
+    std::string err;
+    // frame / tile in flight
+    bool active = false;
+    const rs_scene* scene = nullptr;
+    FrameConst F = {};
+    rs_frame_params P = {};
+    rs_tile_desc tile = {};
+    int ra = 0, rb = 1, rcur = 0, last = 2;
+    bool temporal_ran = false, spatial_ran = false, shade_fused = false;
+};
+
+// --------------------------------------------------------------------------- helpers
+static int fail(rs_context* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    g_last_error = msg;
+    return code;
+}
+#define HIPCHK(c, x)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess) return fail((c), RS_E_HIP, std::string(#x " -> ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// glm-semantics host maths for the camera (pg/camera.cpp:44-58, glm/ext/matrix_transform.inl:99-119,
+// glm/detail/func_matrix.inl:294-351)
+struct hv3 { float x, y, z; };
+static inline hv3 hsub(hv3 a, hv3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static inline float hdot(hv3 a, hv3 b) { float x = a.x * b.x, y = a.y * b.y, z = a.z * b.z; return x + y + z; }
+static inline hv3 hcross(hv3 x, hv3 y) { return {x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y}; }
+static inline hv3 hnorm(hv3 a) { float s = 1.0f / std::sqrt(hdot(a, a)); return {a.x * s, a.y * s, a.z * s}; }
+static inline float hlen(hv3 a) { return std::sqrt(hdot(a, a)); }
+
+static void look_at_rh(hv3 eye, hv3 center, hv3 up, float m[4][4]) {
+    hv3 f = hnorm(hsub(center, eye));
+    hv3 s = hnorm(hcross(f, up));
+    hv3 u = hcross(s, f);
+    std::memset(m, 0, 64);
+    m[0][0] = s.x; m[1][0] = s.y; m[2][0] = s.z;
+    m[0][1] = u.x; m[1][1] = u.y; m[2][1] = u.z;
+    m[0][2] = -f.x; m[1][2] = -f.y; m[2][2] = -f.z;
+    m[3][0] = -hdot(s, eye); m[3][1] = -hdot(u, eye); m[3][2] = hdot(f, eye);
+    m[3][3] = 1.0f;
+}
+static void inverse4(const float m[4][4], float I[4][4]) {
+    float c00 = m[2][2] * m[3][3] - m[3][2] * m[2][3], c02 = m[1][2] * m[3][3] - m[3][2] * m[1][3];
+    float c03 = m[1][2] * m[2][3] - m[2][2] * m[1][3], c04 = m[2][1] * m[3][3] - m[3][1] * m[2][3];
+    float c06 = m[1][1] * m[3][3] - m[3][1] * m[1][3], c07 = m[1][1] * m[2][3] - m[2][1] * m[1][3];
+    float c08 = m[2][1] * m[3][2] - m[3][1] * m[2][2], c10 = m[1][1] * m[3][2] - m[3][1] * m[1][2];
+    float c11 = m[1][1] * m[2][2] - m[2][1] * m[1][2], c12 = m[2][0] * m[3][3] - m[3][0] * m[2][3];
+    float c14 = m[1][0] * m[3][3] - m[3][0] * m[1][3], c15 = m[1][0] * m[2][3] - m[2][0] * m[1][3];
+    float c16 = m[2][0] * m[3][2] - m[3][0] * m[2][2], c18 = m[1][0] * m[3][2] - m[3][0] * m[1][2];
+    float c19 = m[1][0] * m[2][2] - m[2][0] * m[1][2], c20 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
+    float c22 = m[1][0] * m[3][1] - m[3][0] * m[1][1], c23 = m[1][0] * m[2][1] - m[2][0] * m[1][1];
+    const float F0[4] = {c00, c00, c02, c03}, F1[4] = {c04, c04, c06, c07}, F2[4] = {c08, c08, c10, c11};
+    const float F3[4] = {c12, c12, c14, c15}, F4[4] = {c16, c16, c18, c19}, F5[4] = {c20, c20, c22, c23};
+    const float V0[4] = {m[1][0], m[0][0], m[0][0], m[0][0]}, V1[4] = {m[1][1], m[0][1], m[0][1], m[0][1]};
+    const float V2[4] = {m[1][2], m[0][2], m[0][2], m[0][2]}, V3[4] = {m[1][3], m[0][3], m[0][3], m[0][3]};
+    const float SA[4] = {+1, -1, +1, -1}, SB[4] = {-1, +1, -1, +1};
+    for (int i = 0; i < 4; ++i) {
+        float i0 = V1[i] * F0[i] - V2[i] * F1[i] + V3[i] * F2[i];
+        float i1 = V0[i] * F0[i] - V2[i] * F3[i] + V3[i] * F4[i];
+        float i2 = V0[i] * F1[i] - V1[i] * F3[i] + V3[i] * F5[i];
+        float i3 = V0[i] * F2[i] - V1[i] * F4[i] + V2[i] * F5[i];
+        I[0][i] = i0 * SA[i]; I[1][i] = i1 * SB[i]; I[2][i] = i2 * SA[i]; I[3][i] = i3 * SB[i];
+    }
+    float d0 = m[0][0] * I[0][0], d1 = m[0][1] * I[1][0], d2 = m[0][2] * I[2][0], d3 = m[0][3] * I[3][0];
+    float det = (d0 + d1) + (d2 + d3);
+    float ood = 1.0f / det;
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r) I[c][r] = I[c][r] * ood;
+}
+
+// Camera ctor + setFOV + recalculate_m_c_w (pg/camera.cpp:12-18,44-58,81-84)
+static void make_camera(const rs_camera* c, int H, GCam& g, float inv3[9]) {
+    hv3 from{c->eye[0], c->eye[1], c->eye[2]}, at{c->at[0], c->at[1], c->at[2]};
+    float fov_rad = c->fov_y_deg * 0.01745329251994329576923690768489f;
+    g.focal = (float)H / (2.0f * tanf(fov_rad / 2.0f));
+    hv3 up{0.0f, 0.0f, 1.0f};
+    hv3 zc = hnorm(hsub(from, at));
+    hv3 xc = hnorm(hcross(up, zc));
+    hv3 yc = hnorm(hcross(zc, xc));
+    float V[4][4], I[4][4];
+    look_at_rh(from, at, yc, V);
+    inverse4(V, I);
+    std::memcpy(g.view, V, 64);
+    g.pos = vec3{from.x, from.y, from.z};
+    for (int col = 0; col < 3; ++col)
+        for (int r = 0; r < 3; ++r) inv3[3 * col + r] = I[col][r];
+}
+
+// --------------------------------------------------------------------------- context
+extern "C" int rs_context_create(int hip_device, int width, int height, void* hip_stream, rs_context** out) {
+    if (!out || width <= 0 || height <= 0) return fail(nullptr, RS_E_INVALID, "rs_context_create: bad arguments");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(nullptr, RS_E_HIP, "rs_context_create: no HIP device visible");
+    if (hip_device < 0 || hip_device >= ndev) return fail(nullptr, RS_E_INVALID, "rs_context_create: bad device index");
+    rs_context* c = new rs_context();
+    c->device = hip_device; c->W = width; c->H = height;
+    auto bail = [&](const std::string& m) { g_last_error = m; rs_context_destroy(c); return RS_E_HIP; };
+    if (hipSetDevice(hip_device) != hipSuccess) return bail("hipSetDevice failed");
+    if (hip_stream) c->stream = (hipStream_t)hip_stream;
+    else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail("hipStreamCreate failed");
+        c->own_stream = true;
+    }
+    size_t n = (size_t)width * height;
+    for (int i = 0; i < 2; ++i) {
+        float4** f[5] = {&c->G[i].g0, &c->G[i].g1, &c->G[i].g2, &c->G[i].g3, &c->G[i].g4};
+        for (auto* p : f) {
+            if (hipMalloc(p, n * sizeof(float4)) != hipSuccess) return bail("hipMalloc(G-buffer) failed");
+            hipMemsetAsync(*p, 0, n * sizeof(float4), c->stream);
+        }
+    }
+    for (int i = 0; i < 3; ++i) {
+        if (hipMalloc(&c->R[i], n * 3 * sizeof(float4)) != hipSuccess) return bail("hipMalloc(reservoirs) failed");
+        hipMemsetAsync(c->R[i], 0, n * 3 * sizeof(float4), c->stream);
+    }
+    if (hipMalloc(&c->fb, n * 3 * sizeof(float)) != hipSuccess) return bail("hipMalloc(frame) failed");
+    hipMemsetAsync(c->fb, 0, n * 3 * sizeof(float), c->stream);
+    if (hipMalloc(&c->d_cnt, sizeof(Counters)) != hipSuccess) return bail("hipMalloc(counters) failed");
+    if (hipHostMalloc(&c->h_cnt, sizeof(Counters), hipHostMallocDefault) != hipSuccess) return bail("hipHostMalloc failed");
+    for (auto& e : c->ev)
+        if (hipEventCreate(&e) != hipSuccess) return bail("hipEventCreate failed");
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return bail("context init failed");
+    *out = c;
+    return RS_OK;
+}
+
+extern "C" void rs_context_destroy(rs_context* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (auto& g : c->G) {
+        float4* f[5] = {g.g0, g.g1, g.g2, g.g3, g.g4};
+        for (auto* p : f) if (p) hipFree(p);
+    }
+    for (auto* r : c->R) if (r) hipFree(r);
+    if (c->fb) hipFree(c->fb);
+    if (c->d_cnt) hipFree(c->d_cnt);
+    if (c->h_cnt) hipHostFree(c->h_cnt);
+    for (auto& e : c->ev) if (e) hipEventDestroy(e);
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" const char* rs_last_error(const rs_context* c) {
+    return c ? c->err.c_str() : g_last_error.c_str();
+}
+
+// --------------------------------------------------------------------------- scene
+static int scene_from_arrays(rs_context* c, const std::vector<float>& pos, const std::vector<float>& nrm,
+                             const std::vector<uint32_t>& tri_mat, const rs_material_desc* mats, uint32_t n_mats,
+                             rs_scene** out) {
+    const uint32_t n = (uint32_t)tri_mat.size();
+    for (uint32_t t = 0; t < n; ++t)
+        if (tri_mat[t] >= n_mats) return fail(c, RS_E_INVALID, "rs_scene_create: material index out of range");
+    for (uint32_t m = 0; m < n_mats; ++m)
+        if (mats[m].type < 0 || mats[m].type > 6) return fail(c, RS_E_INVALID, "rs_scene_create: bad material type");
+    // materials (pg/material.h:105-115) + emissive list in triangle order (triIdCtr, pg/ModelLoader.cpp:291-305)
+    std::vector<float4> hm(3 * (size_t)std::max(n_mats, 1u));
+    for (uint32_t m = 0; m < n_mats; ++m) {
+        const rs_material_desc& d = mats[m];
+        int type = d.type;
+        float tb; std::memcpy(&tb, &type, 4);
+        hm[3 * m] = make_float4(d.diffuse[0], d.diffuse[1], d.diffuse[2], d.shininess);
+        hm[3 * m + 1] = make_float4(d.specular[0], d.specular[1], d.specular[2], tb);
+        hm[3 * m + 2] = make_float4(d.emission[0], d.emission[1], d.emission[2], 0.0f);
+    }
+    std::vector<float4> tn(3 * (size_t)std::max(n, 1u));
+    std::vector<uint32_t> emis_tri;
+    for (uint32_t t = 0; t < n; ++t) {
+        const rs_material_desc& d = mats[tri_mat[t]];
+        int eid = -1;
+        if (d.emission[0] + d.emission[1] + d.emission[2] > 0) {   // Material::isEmissive (pg/material.h:135-137)
+            eid = (int)emis_tri.size();
+            emis_tri.push_back(t);
+        }
+        int mi = (int)tri_mat[t];
+        float mb, eb; std::memcpy(&mb, &mi, 4); std::memcpy(&eb, &eid, 4);
+        const float* q = &nrm[9 * (size_t)t];
+        tn[3 * t] = make_float4(q[0], q[1], q[2], mb);
+        tn[3 * t + 1] = make_float4(q[3], q[4], q[5], eb);
+        tn[3 * t + 2] = make_float4(q[6], q[7], q[8], 0.0f);
+    }
+    // TriangleCDF (pg/TriangleCDF.cpp:8-34, pg/TriangleCDF.h:25-31), Triangle::area (pg/triangle.cpp:13-16)
+    const uint32_t ne = (uint32_t)emis_tri.size();
+    std::vector<float> area(ne), cdf(std::max(ne, 1u));
+    float total = 0.0f;
+    for (uint32_t e = 0; e < ne; ++e) {
+        const float* p = &pos[9 * (size_t)emis_tri[e]];
+        hv3 a{p[0], p[1], p[2]}, b{p[3], p[4], p[5]}, cc{p[6], p[7], p[8]};
+        area[e] = 0.5f * hlen(hcross(hsub(b, a), hsub(cc, a)));
+        total += area[e];
+    }
+    for (uint32_t e = 0; e < ne; ++e) {
+        float na = area[e] / total;
+        float pred = e == 0 ? 0.0f : cdf[e - 1];
+        cdf[e] = pred + na;
+    }
+    std::vector<float4> em(8 * (size_t)std::max(ne, 1u));
+    for (uint32_t e = 0; e < ne; ++e) {
+        uint32_t t = emis_tri[e];
+        const float* p = &pos[9 * (size_t)t];
+        const float* q = &nrm[9 * (size_t)t];
+        const rs_material_desc& d = mats[tri_mat[t]];
+        float pick = e == 0 ? cdf[0] : cdf[e] - cdf[e - 1];
+        float inv_area = 1.0f / area[e];
+        float pdf_brdf = area[e] / total;
+        pdf_brdf *= 1.0f / area[e];
+        em[8 * e + 0] = make_float4(p[0], p[1], p[2], pick);
+        em[8 * e + 1] = make_float4(p[3], p[4], p[5], inv_area);
+        em[8 * e + 2] = make_float4(p[6], p[7], p[8], pdf_brdf);
+        em[8 * e + 3] = make_float4(q[0], q[1], q[2], 0.0f);
+        em[8 * e + 4] = make_float4(q[3], q[4], q[5], 0.0f);
+        em[8 * e + 5] = make_float4(q[6], q[7], q[8], 0.0f);
+        em[8 * e + 6] = make_float4(d.emission[0], d.emission[1], d.emission[2], 0.0f);
+        em[8 * e + 7] = make_float4(area[e], 0.0f, 0.0f, 0.0f);
+    }
+    rs_scene* s = new rs_scene();
+    s->ctx = c; s->n_tris = n; s->n_emis = ne; s->n_mats = n_mats;
+    auto bail = [&](const std::string& m) { rs_scene_destroy(s); return fail(c, RS_E_HIP, m); };
+    hipStream_t st = c->stream;
+    if (n) {
+        if (hipMalloc(&s->d_pos, pos.size() * sizeof(float)) != hipSuccess) return bail("hipMalloc(pos) failed");
+        hipMemcpyAsync(s->d_pos, pos.data(), pos.size() * sizeof(float), hipMemcpyHostToDevice, st);
+    }
+    if (hipMalloc(&s->d_tri_nrm, tn.size() * sizeof(float4)) != hipSuccess) return bail("hipMalloc(nrm) failed");
+    hipMemcpyAsync(s->d_tri_nrm, tn.data(), tn.size() * sizeof(float4), hipMemcpyHostToDevice, st);
+    if (hipMalloc(&s->d_mats, hm.size() * sizeof(float4)) != hipSuccess) return bail("hipMalloc(mats) failed");
+    hipMemcpyAsync(s->d_mats, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice, st);
+    if (hipMalloc(&s->d_emis, em.size() * sizeof(float4)) != hipSuccess) return bail("hipMalloc(emis) failed");
+    hipMemcpyAsync(s->d_emis, em.data(), em.size() * sizeof(float4), hipMemcpyHostToDevice, st);
+    if (hipMalloc(&s->d_cdf, cdf.size() * sizeof(float)) != hipSuccess) return bail("hipMalloc(cdf) failed");
+    hipMemcpyAsync(s->d_cdf, cdf.data(), cdf.size() * sizeof(float), hipMemcpyHostToDevice, st);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0); hipEventCreate(&e1);
+    hipEventRecord(e0, st);
+    std::string berr;
+    if (build_bvh(s->d_pos, n, st, &s->d_nodes, &s->n_nodes, &s->d_tris, berr) != 0) {
+        hipEventDestroy(e0); hipEventDestroy(e1);
+        return bail("BVH build failed: " + berr);
+    }
+    hipEventRecord(e1, st);
+    if (hipStreamSynchronize(st) != hipSuccess) { hipEventDestroy(e0); hipEventDestroy(e1); return bail("scene upload failed"); }
+    hipEventElapsedTime(&s->build_ms, e0, e1);
+    hipEventDestroy(e0); hipEventDestroy(e1);
+    *out = s;
+    return RS_OK;
+}
+
+extern "C" int rs_scene_create(rs_context* c, const rs_mesh_desc* meshes, uint32_t n_meshes,
+                               const rs_material_desc* materials, uint32_t n_materials, rs_scene** out) {
+    if (!c || !out || (n_meshes && !meshes) || (n_materials && !materials))
+        return fail(c, RS_E_INVALID, "rs_scene_create: null argument");
+    *out = nullptr;
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<float> pos, nrm;
+    std::vector<uint32_t> tri_mat;
+    for (uint32_t m = 0; m < n_meshes; ++m) {
+        const rs_mesh_desc& d = meshes[m];
+        if (d.n_tris && (!d.positions || !d.normals)) return fail(c, RS_E_INVALID, "rs_scene_create: null mesh buffer");
+        pos.insert(pos.end(), d.positions, d.positions + 9 * (size_t)d.n_tris);
+        nrm.insert(nrm.end(), d.normals, d.normals + 9 * (size_t)d.n_tris);
+        tri_mat.insert(tri_mat.end(), d.n_tris, d.material);
+    }
+    return scene_from_arrays(c, pos, nrm, tri_mat, materials, n_materials, out);
+}
+
+extern "C" int rs_scene_load_obj(rs_context* c, const char* path, rs_scene** out) {
+    if (!c || !path || !out) return fail(c, RS_E_INVALID, "rs_scene_load_obj: null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<float> pos, nrm;
+    std::vector<uint32_t> tri_mat;
+    std::vector<rs_material_desc> mats;
+    std::string err;
+    if (load_obj_file(path, pos, nrm, tri_mat, mats, err) != 0) return fail(c, RS_E_IO, err);
+    return scene_from_arrays(c, pos, nrm, tri_mat, mats.data(), (uint32_t)mats.size(), out);
+}
+
+extern "C" void rs_scene_destroy(rs_scene* s) {
+    if (!s) return;
+    if (s->ctx) hipSetDevice(s->ctx->device);
+    void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf};
+    for (void* p : ptrs) if (p) hipFree(p);
+    delete s;
+}
+
+extern "C" int rs_scene_info(const rs_scene* s, uint32_t* n_tris, uint32_t* n_emissive, uint32_t* n_nodes,
+                             float* build_ms) {
+    if (!s) return fail(nullptr, RS_E_INVALID, "rs_scene_info: null scene");
+    if (n_tris) *n_tris = s->n_tris;
+    if (n_emissive) *n_emissive = s->n_emis;
+    if (n_nodes) *n_nodes = s->n_nodes;
+    if (build_ms) *build_ms = s->build_ms;
+    return RS_OK;
+}
+
+// --------------------------------------------------------------------------- frame / tile driver
+static dim3 grid_rows(int W, int ya, int yb) { return dim3((W + 15) / 16, (yb - ya + 15) / 16); }
+
+extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* cam, const rs_frame_params* P,
+                             uint32_t frame_index, const rs_tile_desc* tile) {
+    if (!c || !s || !cam || !P || !tile) return fail(c, RS_E_INVALID, "rs_tile_begin: null argument");
+    if (s->ctx != c) return fail(c, RS_E_INVALID, "rs_tile_begin: scene belongs to another context");
+    if (P->use_skybox) return fail(c, RS_E_UNSUPPORTED, "useSkybox: the reference's sky HDR (data/env/forest.hdr) is a missing blob");
+    if (P->m_area < 0 || P->m_brdf < 0 || P->spatial_passes < 0 || P->confidence_cap < 0)
+        return fail(c, RS_E_INVALID, "rs_frame_params: negative count");
+    if (P->do_spatial && (P->spatial_neighbors < 0 || P->spatial_neighbors > 64))
+        return fail(c, RS_E_INVALID, "rs_frame_params: spatial_neighbors must be in [0, 64]");
+    if (P->spatial_mis < 0 || P->spatial_mis > 4) return fail(c, RS_E_INVALID, "rs_frame_params: bad spatial_mis");
+    if (tile->y0 < 0 || tile->y1 > c->H || tile->y0 >= tile->y1 || tile->margin < 0 || tile->halo < 0 ||
+        tile->halo > tile->margin)
+        return fail(c, RS_E_INVALID, "rs_tile_begin: bad tile (need 0<=y0<y1<=H, 0<=halo<=margin)");
+    HIPCHK(c, hipSetDevice(c->device));
+    c->scene = s; c->P = *P; c->tile = *tile;
+    FrameConst& F = c->F;
+    F.m_area = P->m_area; F.m_brdf = P->m_brdf; F.k = P->spatial_neighbors; F.spatial_passes = P->spatial_passes;
+    F.cap = P->confidence_cap; F.radius = P->spatial_radius; F.min_normal_sim = P->min_normal_similarity;
+    F.max_depth_diff = P->max_depth_difference; F.do_spatial = P->do_spatial; F.do_temporal = P->do_temporal;
+    F.do_vis_pass = P->do_visibility_pass; F.reject = P->reject_dissimilar; F.mis = P->spatial_mis;
+    F.bg = vec3{P->bg_color[0], P->bg_color[1], P->bg_color[2]};
+    F.tnear_off = P->tnear_offset; F.tfar_off = P->tfar_offset; F.normal_off = P->normal_offset;
+    F.seed = P->seed; F.frame = frame_index;
+    F.W = c->W; F.H = c->H;
+    F.y0 = tile->y0; F.y1 = tile->y1;
+    F.gy0 = std::max(0, tile->y0 - tile->margin); F.gy1 = std::min(c->H, tile->y1 + tile->margin);
+    // G-buffer ping-pong (replaces gBufferLastFrame.setDataFrom, pg/simpleguidx11.cpp:480)
+    int gnew = c->gcur ^ 1;
+    make_camera(cam, c->H, c->gcam[gnew], F.inv_view);
+    F.cam = c->gcam[gnew];
+    F.camp = c->gcam[c->gcur];
+    c->last = c->r_last;
+    c->ra = (c->last + 1) % 3; c->rb = (c->last + 2) % 3; c->rcur = c->ra;
+    const bool temporal = P->do_temporal && c->frames > 0;
+    const bool spatial = P->do_spatial && P->spatial_passes > 0;
+    c->shade_fused = !P->do_visibility_pass && !temporal && !spatial;
+    c->temporal_ran = c->spatial_ran = false;
+    const DevScene S = s->dev();
+    HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[EV_BEGIN], c->stream));
+    k_gbuffer_initial<<<grid_rows(c->W, F.gy0, F.gy1), 256, 0, c->stream>>>(S, F, c->G[gnew], ResBuf{c->R[c->ra]},
+                                                                           c->fb, c->shade_fused ? 1 : 0, c->d_cnt);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev[EV_INIT], c->stream));
+    if (P->do_visibility_pass) {
+        k_visibility<<<grid_rows(c->W, F.y0, F.y1), 256, 0, c->stream>>>(S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->d_cnt);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipEventRecord(c->ev[EV_VIS], c->stream));
+    c->gcur = gnew;       // G[gcur] = this frame, G[gcur^1] = previous frame
+    c->active = true;
+    return RS_OK;
+}
+
+extern "C" int rs_tile_halo_ptr(rs_context* c, int which, void** dptr, size_t* bytes) {
+    if (!c || !dptr || !bytes || !c->active) return fail(c, RS_E_INVALID, "rs_tile_halo_ptr: no frame in flight");
+    const int h = c->tile.halo, W = c->W;
+    int r0;
+    switch (which) {
+        case 0: r0 = c->tile.y0 - h; break;
+        case 1: r0 = c->tile.y1; break;
+        case 2: r0 = c->tile.y0; break;
+        case 3: r0 = c->tile.y1 - h; break;
+        default: return fail(c, RS_E_INVALID, "rs_tile_halo_ptr: which must be 0..3");
+    }
+    if (h == 0 || r0 < 0 || r0 + h > c->H) { *dptr = nullptr; *bytes = 0; return RS_OK; }
+    *dptr = (void*)(c->R[c->rcur] + 3 * (size_t)r0 * W);
+    *bytes = (size_t)h * W * 3 * sizeof(float4);
+    return RS_OK;
+}
+
+extern "C" int rs_tile_temporal(rs_context* c) {
+    if (!c || !c->active) return fail(c, RS_E_INVALID, "rs_tile_temporal: no frame in flight");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->P.do_temporal && c->frames > 0 && !c->temporal_ran) {
+        const DevScene S = c->scene->dev();
+        k_temporal<<<grid_rows(c->W, c->F.y0, c->F.y1), 256, 0, c->stream>>>(
+            S, c->F, c->G[c->gcur], c->G[c->gcur ^ 1], ResBuf{c->R[c->rcur]}, ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]},
+            c->d_cnt);
+        HIPCHK(c, hipGetLastError());
+        c->rcur = c->rb;
+        c->temporal_ran = true;
+    }
+    HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->stream));
+    return RS_OK;
+}
+
+extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
+    if (!c || !c->active) return fail(c, RS_E_INVALID, "rs_tile_spatial: no frame in flight");
+    if (!(c->P.do_spatial && pass_index >= 0 && pass_index < c->P.spatial_passes)) return RS_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->P.do_temporal && c->frames > 0 && !c->temporal_ran) {
+        int rc = rs_tile_temporal(c);
+        if (rc) return rc;
+    }
+    const DevScene S = c->scene->dev();
+    int dst = (c->rcur == c->ra) ? c->rb : c->ra;
+    int fuse = (pass_index == c->P.spatial_passes - 1) ? 1 : 0;
+    k_spatial<<<grid_rows(c->W, c->F.y0, c->F.y1), 256, 0, c->stream>>>(S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]},
+                                                                         ResBuf{c->R[dst]}, pass_index, fuse, c->fb,
+                                                                         c->d_cnt);
+    HIPCHK(c, hipGetLastError());
+    c->rcur = dst;
+    if (fuse) c->shade_fused = true;
+    c->spatial_ran = true;
+    HIPCHK(c, hipEventRecord(c->ev[EV_SPATIAL], c->stream));
+    return RS_OK;
+}
+
+extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_times* t) {
+    if (!c || !c->active) return fail(c, RS_E_INVALID, "rs_tile_finish: no frame in flight");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->P.do_temporal && c->frames > 0 && !c->temporal_ran) {
+        int rc = rs_tile_temporal(c);
+        if (rc) return rc;
+    }
+    if (!c->temporal_ran) HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->stream));
+    if (!c->spatial_ran) HIPCHK(c, hipEventRecord(c->ev[EV_SPATIAL], c->stream));
+    if (!c->shade_fused) {
+        const DevScene S = c->scene->dev();
+        k_shade<<<grid_rows(c->W, c->F.y0, c->F.y1), 256, 0, c->stream>>>(S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]},
+                                                                           c->fb, c->d_cnt);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipEventRecord(c->ev[EV_SHADE], c->stream));
+    c->r_last = c->rcur;   // reservoirsLastFrame = final buffer (pointer swap, :477)
+    c->frames++;
+    c->active = false;
+    if (band_rgb) *band_rgb = c->fb + 3 * (size_t)c->F.y0 * c->W;
+    if (t) {
+        HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->d_cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        float a = 0, b = 0, d = 0, e = 0, f = 0, tot = 0;
+        hipEventElapsedTime(&a, c->ev[EV_BEGIN], c->ev[EV_INIT]);
+        hipEventElapsedTime(&b, c->ev[EV_INIT], c->ev[EV_VIS]);
+        hipEventElapsedTime(&d, c->ev[EV_VIS], c->ev[EV_TEMPORAL]);
+        hipEventElapsedTime(&e, c->ev[EV_TEMPORAL], c->ev[EV_SPATIAL]);
+        hipEventElapsedTime(&f, c->ev[EV_SPATIAL], c->ev[EV_SHADE]);
+        hipEventElapsedTime(&tot, c->ev[EV_BEGIN], c->ev[EV_SHADE]);
+        t->gbuffer_initial_ms = a; t->visibility_ms = b; t->temporal_ms = d; t->spatial_ms = e; t->shade_ms = f;
+        t->total_ms = tot; t->rays = c->h_cnt->rays; t->primary_rays = c->h_cnt->primary;
+    }
+    return RS_OK;
+}
+
+extern "C" int rs_render_frame(rs_context* c, const rs_scene* s, const rs_camera* cam, const rs_frame_params* P,
+                               uint32_t frame_index, float* frame_rgb_host, rs_pass_times* times) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_render_frame: null context");
+    rs_tile_desc full{0, c->H, 0, 0};
+    int rc = rs_tile_begin(c, s, cam, P, frame_index, &full);
+    if (rc) return rc;
+    if ((rc = rs_tile_temporal(c))) return rc;
+    if (P->do_spatial)
+        for (int i = 0; i < P->spatial_passes; ++i)
+            if ((rc = rs_tile_spatial(c, i))) return rc;
+    if ((rc = rs_tile_finish(c, nullptr, times))) return rc;
+    if (frame_rgb_host) {
+        HIPCHK(c, hipMemcpyAsync(frame_rgb_host, c->fb, (size_t)c->W * c->H * 3 * sizeof(float), hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return RS_OK;
+}
+
+extern "C" int rs_get_frame_device_ptr(rs_context* c, const float** dptr) {
+    if (!c || !dptr) return fail(c, RS_E_INVALID, "rs_get_frame_device_ptr: null argument");
+    *dptr = c->fb;
+    return RS_OK;
+}
+
+extern "C" int rs_reset_history(rs_context* c) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_reset_history: null context");
+    c->frames = 0;
+    return RS_OK;
+}
+
+extern "C" int rs_synchronize(rs_context* c) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_synchronize: null context");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RS_OK;
+}
+
+extern "C" int rs_dump_gbuffer(rs_context* c, int prev, float* out) {
+    if (!c || !out) return fail(c, RS_E_INVALID, "rs_dump_gbuffer: null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    size_t n = (size_t)c->W * c->H;
+    const GBuf& g = c->G[prev ? (c->gcur ^ 1) : c->gcur];
+    std::vector<float4> a(n), b(n), d(n), e(n), f(n);
+    HIPCHK(c, hipMemcpyAsync(a.data(), g.g0, n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(b.data(), g.g1, n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d.data(), g.g2, n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(e.data(), g.g3, n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(f.data(), g.g4, n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (size_t p = 0; p < n; ++p) {
+        float* o = out + 19 * p;
+        int type; std::memcpy(&type, &e[p].w, 4);
+        o[0] = a[p].x; o[1] = a[p].y; o[2] = a[p].z; o[3] = b[p].x; o[4] = b[p].y; o[5] = b[p].z;
+        o[6] = d[p].x; o[7] = d[p].y; o[8] = d[p].z; o[9] = e[p].x; o[10] = e[p].y; o[11] = e[p].z;
+        o[12] = f[p].x; o[13] = f[p].y; o[14] = f[p].z; o[15] = b[p].w; o[16] = a[p].w; o[17] = (float)type;
+        o[18] = d[p].w;
+    }
+    return RS_OK;
+}
+
+extern "C" int rs_dump_reservoirs(rs_context* c, float* out) {
+    if (!c || !out) return fail(c, RS_E_INVALID, "rs_dump_reservoirs: null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    size_t n = (size_t)c->W * c->H;
+    std::vector<float4> r(3 * n);
+    HIPCHK(c, hipMemcpyAsync(r.data(), c->R[c->r_last], 3 * n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (size_t p = 0; p < n; ++p) {
+        float* o = out + 12 * p;
+        const float4 &a = r[3 * p], &b = r[3 * p + 1], &d = r[3 * p + 2];
+        int conf; std::memcpy(&conf, &d.w, 4);
+        o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = b.x; o[4] = b.y; o[5] = b.z;
+        o[6] = d.x; o[7] = d.y; o[8] = d.z; o[9] = a.w; o[10] = b.w; o[11] = (float)conf;
+    }
+    return RS_OK;
+}
+
+// --------------------------------------------------------------------------- test hook
+__global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const float* d, const float* tn, const float* tf,
+                              int any, float* t_out, int32_t* prim_out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    vec3 O = mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), D = mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+    if (any) {
+        prim_out[i] = occluded_ray(S, O, D, tn[i], tf[i]) ? 1 : 0;
+        t_out[i] = 0.0f;
+    } else {
+        Hit h = closest_ray(S, O, D, tn[i], tf[i]);
+        prim_out[i] = h.prim;
+        t_out[i] = h.prim >= 0 ? h.t : -1.0f;
+    }
+}
+
+extern "C" int rs_debug_trace(rs_context* c, const rs_scene* s, uint32_t n, const float* o, const float* d,
+                              const float* tnear, const float* tfar, int any_hit, float* t_out, int32_t* prim_out) {
+    if (!c || !s || !o || !d || !tnear || !tfar || !t_out || !prim_out) return fail(c, RS_E_INVALID, "rs_debug_trace: null");
+    if (n == 0) return RS_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    float *dd = nullptr;
+    int32_t* dp = nullptr;
+    size_t fl = (size_t)n * 9;   // o(3n) d(3n) tn(n) tf(n) t(n)
+    HIPCHK(c, hipMalloc(&dd, fl * sizeof(float)));
+    HIPCHK(c, hipMalloc(&dp, (size_t)n * sizeof(int32_t)));
+    hipMemcpyAsync(dd, o, 3 * (size_t)n * 4, hipMemcpyHostToDevice, c->stream);
+    hipMemcpyAsync(dd + 3 * (size_t)n, d, 3 * (size_t)n * 4, hipMemcpyHostToDevice, c->stream);
+    hipMemcpyAsync(dd + 6 * (size_t)n, tnear, (size_t)n * 4, hipMemcpyHostToDevice, c->stream);
+    hipMemcpyAsync(dd + 7 * (size_t)n, tfar, (size_t)n * 4, hipMemcpyHostToDevice, c->stream);
+    k_debug_trace<<<(n + 255) / 256, 256, 0, c->stream>>>(s->dev(), n, dd, dd + 3 * (size_t)n, dd + 6 * (size_t)n,
+                                                          dd + 7 * (size_t)n, any_hit, dd + 8 * (size_t)n, dp);
+    hipError_t e = hipGetLastError();
+    hipMemcpyAsync(t_out, dd + 8 * (size_t)n, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
+    hipMemcpyAsync(prim_out, dp, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
+    hipError_t e2 = hipStreamSynchronize(c->stream);
+    hipFree(dd); hipFree(dp);
+    if (e != hipSuccess || e2 != hipSuccess) return fail(c, RS_E_HIP, "rs_debug_trace: kernel failed");
+    return RS_OK;
+}

@@ -1,0 +1,284 @@
+// rs_bvh_build.hip -- wavefront LBVH build on the GPU; replaces Embree's rtcCommitScene
+// (pg/Scene.cpp:15).  Every stage is a data-parallel kernel; no inter-workgroup hand-off inside a
+// launch (kernel boundaries provide visibility across the 8 non-coherent XCD L2s), so the build is
+// placement-independent and deterministic (identical trees on every rank):
+//   1 k_prim_bounds   per-triangle AABB + centroid; centroid bounds by block reduce + ordered-int
+//                     atomics (min/max are order independent)
+//   2 k_morton        64-bit key = morton30(centroid) << 32 | triangle index (unique keys)
+//   3 radix sort      hipcub::DeviceRadixSort::SortKeys on 62 bits
+//   4 k_karras        Karras 2012 hierarchy: internal node i's range, split, children, parents
+//   5 k_depth         depth of every node (walk to the root)
+//   6 k_refit_level   bottom-up AABB union + collapsed subtree sizes, one launch per depth level
+//   7 k_emit          collapse subtrees of <= kLeafMax triangles into leaves, preorder index by
+//                     walking up (idx = idx(parent) + 1 + [right child] * kept(left sibling)),
+//                     write the 32-B skip-pointer nodes
+//   8 k_leaf_tris     triangles in leaf order as (v0, prim), (e1), (e2)
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+#include <float.h>
+#include <string>
+#include <vector>
+
+namespace rs {
+
+constexpr int kLeafMax = 4;
+
+__device__ __forceinline__ int f2o(float f) {   // order-preserving float -> int
+    int i = __float_as_int(f);
+    return i >= 0 ? i : i ^ 0x7fffffff;
+}
+__device__ __forceinline__ float o2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
+
+struct BuildNode {        // internal nodes [0, n-1), leaves [n-1, 2n-1)
+    float lo[3], hi[3];
+    int parent, left, right;
+    int first, last;
+    int kept;             // nodes this subtree contributes to the output (1 when collapsed)
+    int depth;
+};
+
+__global__ void k_prim_bounds(const float* __restrict__ pos, uint32_t n, float4* lo, float4* hi, int* cb) {
+    __shared__ int s[6][256];
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    int c[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
+    if (i < n) {
+        const float* p = pos + 9 * (size_t)i;
+        float l[3], h[3];
+        for (int a = 0; a < 3; ++a) {
+            l[a] = fminf(fminf(p[a], p[3 + a]), p[6 + a]);
+            h[a] = fmaxf(fmaxf(p[a], p[3 + a]), p[6 + a]);
+        }
+        lo[i] = make_float4(l[0], l[1], l[2], 0.0f);
+        hi[i] = make_float4(h[0], h[1], h[2], 0.0f);
+        for (int a = 0; a < 3; ++a) {
+            float cen = 0.5f * (l[a] + h[a]);
+            c[a] = f2o(cen); c[3 + a] = f2o(cen);
+        }
+    }
+    for (int a = 0; a < 6; ++a) s[a][threadIdx.x] = c[a];
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < (unsigned)w) {
+            for (int a = 0; a < 3; ++a) s[a][threadIdx.x] = min(s[a][threadIdx.x], s[a][threadIdx.x + w]);
+            for (int a = 3; a < 6; ++a) s[a][threadIdx.x] = max(s[a][threadIdx.x], s[a][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        for (int a = 0; a < 3; ++a) atomicMin(&cb[a], s[a][0]);
+        for (int a = 3; a < 6; ++a) atomicMax(&cb[a], s[a][0]);
+    }
+}
+
+__device__ __forceinline__ uint32_t expand10(uint32_t v) {
+    v &= 0x3ffu;
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+__global__ void k_morton(const float4* lo, const float4* hi, uint32_t n, const int* cb, uint64_t* keys) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float l[3] = {lo[i].x, lo[i].y, lo[i].z}, h[3] = {hi[i].x, hi[i].y, hi[i].z};
+    uint32_t q[3];
+    for (int a = 0; a < 3; ++a) {
+        float mn = o2f(cb[a]), mx = o2f(cb[3 + a]);
+        float cen = 0.5f * (l[a] + h[a]);
+        float ext = mx - mn;
+        float t = ext > 0.0f ? (cen - mn) / ext : 0.0f;
+        int v = (int)(t * 1024.0f);
+        q[a] = (uint32_t)(v < 0 ? 0 : (v > 1023 ? 1023 : v));
+    }
+    uint32_t m = (expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2]);
+    keys[i] = ((uint64_t)m << 32) | i;
+}
+
+__device__ __forceinline__ int delta(const uint64_t* k, int n, int i, int j) {
+    if (j < 0 || j >= n) return -1;
+    return __clzll(k[i] ^ k[j]);
+}
+
+__global__ void k_init_leaves(BuildNode* N, uint32_t n, const uint64_t* keys, const float4* lo, const float4* hi) {
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    uint32_t prim = (uint32_t)(keys[j] & 0xffffffffu);
+    BuildNode& L = N[(n - 1) + j];
+    float4 a = lo[prim], b = hi[prim];
+    L.lo[0] = a.x; L.lo[1] = a.y; L.lo[2] = a.z; L.hi[0] = b.x; L.hi[1] = b.y; L.hi[2] = b.z;
+    L.left = L.right = -1; L.first = L.last = (int)j; L.kept = 1; L.depth = 0;
+    if (n == 1) L.parent = -1;
+}
+
+__global__ void k_karras(BuildNode* N, int n, const uint64_t* k) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1) return;
+    int d = (delta(k, n, i, i + 1) - delta(k, n, i, i - 1)) >= 0 ? 1 : -1;
+    int dmin = delta(k, n, i, i - d);
+    int lmax = 2;
+    while (delta(k, n, i, i + lmax * d) > dmin) lmax <<= 1;
+    int l = 0;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (delta(k, n, i, i + (l + t) * d) > dmin) l += t;
+    int j = i + l * d;
+    int dnode = delta(k, n, i, j);
+    int s = 0, t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (delta(k, n, i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    int gamma = i + s * d + min(d, 0);
+    int first = min(i, j), last = max(i, j);
+    int left = (first == gamma) ? (n - 1) + gamma : gamma;
+    int right = (last == gamma + 1) ? (n - 1) + gamma + 1 : gamma + 1;
+    BuildNode& I = N[i];
+    I.left = left; I.right = right; I.first = first; I.last = last;
+    N[left].parent = i; N[right].parent = i;
+    if (i == 0) I.parent = -1;
+}
+
+__global__ void k_depth(BuildNode* N, int total, int* max_depth) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    int d = 0, c = i;
+    while (N[c].parent >= 0) { c = N[c].parent; ++d; }
+    N[i].depth = d;
+    atomicMax(max_depth, d);
+}
+
+__global__ void k_refit_level(BuildNode* N, int n_internal, int level) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_internal || N[i].depth != level) return;
+    BuildNode& I = N[i];
+    const BuildNode& A = N[I.left];
+    const BuildNode& B = N[I.right];
+    for (int a = 0; a < 3; ++a) { I.lo[a] = fminf(A.lo[a], B.lo[a]); I.hi[a] = fmaxf(A.hi[a], B.hi[a]); }
+    int size = I.last - I.first + 1;
+    I.kept = size <= kLeafMax ? 1 : 1 + A.kept + B.kept;
+}
+
+__device__ __forceinline__ bool is_collapsed(const BuildNode* N, int n, int c) {
+    // internal node turned into a leaf
+    return c < n - 1 && (N[c].last - N[c].first + 1) <= kLeafMax;
+}
+__device__ __forceinline__ bool is_emitted(const BuildNode* N, int n, int c) {
+    for (int q = N[c].parent; q >= 0; q = N[q].parent)
+        if (is_collapsed(N, n, q)) return false;
+    return true;
+}
+
+__global__ void k_emit(const BuildNode* N, int n, float4* out) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    int total = 2 * n - 1;
+    if (c >= total || !is_emitted(N, n, c)) return;
+    int idx = 0;
+    for (int ch = c, q = N[c].parent; q >= 0; ch = q, q = N[q].parent) {
+        idx += 1;
+        if (N[q].right == ch) idx += N[N[q].left].kept;
+    }
+    const BuildNode& X = N[c];
+    bool leaf = (c >= n - 1) || is_collapsed(N, n, c);
+    int skip = idx + (leaf ? 1 : X.kept);
+    int info = leaf ? ((X.first << 3) | (X.last - X.first)) : -1;
+    out[2 * idx] = make_float4(X.lo[0], X.lo[1], X.lo[2], __int_as_float(skip));
+    out[2 * idx + 1] = make_float4(X.hi[0], X.hi[1], X.hi[2], __int_as_float(info));
+}
+
+__global__ void k_leaf_tris(const float* __restrict__ pos, const uint64_t* keys, uint32_t n, float4* tris) {
+    uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint32_t prim = (uint32_t)(keys[k] & 0xffffffffu);
+    const float* p = pos + 9 * (size_t)prim;
+    float v0x = p[0], v0y = p[1], v0z = p[2];
+    tris[3 * k] = make_float4(v0x, v0y, v0z, __int_as_float((int)prim));
+    tris[3 * k + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
+    tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
+}
+
+#define BVH_CHECK(x)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) { err = std::string(#x ": ") + hipGetErrorString(e_); goto fail; } \
+    } while (0)
+
+// Builds the BVH for n triangles at d_pos (n*9 floats, device).  On success *d_nodes (2*n_nodes
+// float4) and *d_tris (3*n float4) are new device allocations owned by the caller.
+int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes,
+              float4** d_tris, std::string& err) {
+    *d_nodes = nullptr; *d_tris = nullptr; *n_nodes = 0;
+    if (n == 0) return 0;
+    if (n >= (1u << 28)) { err = "too many triangles for the 28-bit leaf index"; return -1; }
+    float4 *lo = nullptr, *hi = nullptr, *nodes = nullptr, *tris = nullptr;
+    int* cb = nullptr;
+    uint64_t *keys = nullptr, *keys_sorted = nullptr;
+    BuildNode* N = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    int* dmax = nullptr;
+    int max_depth = 0, total = 2 * (int)n - 1, kept_root = 1;
+    const int B = 256;
+    const int gn = (int)((n + B - 1) / B), gt = (total + B - 1) / B;
+    int init_cb[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
+
+    BVH_CHECK(hipMalloc(&lo, n * sizeof(float4)));
+    BVH_CHECK(hipMalloc(&hi, n * sizeof(float4)));
+    BVH_CHECK(hipMalloc(&cb, 6 * sizeof(int)));
+    BVH_CHECK(hipMalloc(&dmax, sizeof(int)));
+    BVH_CHECK(hipMalloc(&keys, n * sizeof(uint64_t)));
+    BVH_CHECK(hipMalloc(&keys_sorted, n * sizeof(uint64_t)));
+    BVH_CHECK(hipMalloc(&N, (size_t)total * sizeof(BuildNode)));
+    BVH_CHECK(hipMemcpyAsync(cb, init_cb, sizeof init_cb, hipMemcpyHostToDevice, st));
+    BVH_CHECK(hipMemsetAsync(dmax, 0, sizeof(int), st));
+
+    k_prim_bounds<<<gn, B, 0, st>>>(d_pos, n, lo, hi, cb);
+    k_morton<<<gn, B, 0, st>>>(lo, hi, n, cb, keys);
+    BVH_CHECK(hipGetLastError());
+    BVH_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, keys_sorted, (int)n, 0, 62, st));
+    BVH_CHECK(hipMalloc(&tmp, tmp_bytes));
+    BVH_CHECK(hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, keys_sorted, (int)n, 0, 62, st));
+
+    k_init_leaves<<<gn, B, 0, st>>>(N, n, keys_sorted, lo, hi);
+    if (n > 1) k_karras<<<gn, B, 0, st>>>(N, (int)n, keys_sorted);
+    k_depth<<<gt, B, 0, st>>>(N, total, dmax);
+    BVH_CHECK(hipGetLastError());
+    BVH_CHECK(hipMemcpyAsync(&max_depth, dmax, sizeof(int), hipMemcpyDeviceToHost, st));
+    BVH_CHECK(hipStreamSynchronize(st));
+    if (n > 1) {
+        int gi = (int)((n - 1 + B - 1) / B);
+        for (int lv = max_depth; lv >= 0; --lv) k_refit_level<<<gi, B, 0, st>>>(N, (int)n - 1, lv);
+        BVH_CHECK(hipGetLastError());
+        BVH_CHECK(hipMemcpyAsync(&kept_root, &N[0].kept, sizeof(int), hipMemcpyDeviceToHost, st));
+        BVH_CHECK(hipStreamSynchronize(st));
+    }
+    BVH_CHECK(hipMalloc(&nodes, (size_t)kept_root * 2 * sizeof(float4)));
+    BVH_CHECK(hipMalloc(&tris, (size_t)n * 3 * sizeof(float4)));
+    if (n > 1) {
+        k_emit<<<gt, B, 0, st>>>(N, (int)n, nodes);
+    } else {
+        k_emit<<<1, B, 0, st>>>(N, 1, nodes);
+    }
+    k_leaf_tris<<<gn, B, 0, st>>>(d_pos, keys_sorted, n, tris);
+    BVH_CHECK(hipGetLastError());
+    BVH_CHECK(hipStreamSynchronize(st));
+    *d_nodes = nodes; *d_tris = tris; *n_nodes = (uint32_t)kept_root;
+    nodes = nullptr; tris = nullptr;
+    hipFree(lo); hipFree(hi); hipFree(cb); hipFree(dmax); hipFree(keys); hipFree(keys_sorted); hipFree(N); hipFree(tmp);
+    return 0;
+fail:
+    if (lo) hipFree(lo);
+    if (hi) hipFree(hi);
+    if (cb) hipFree(cb);
+    if (dmax) hipFree(dmax);
+    if (keys) hipFree(keys);
+    if (keys_sorted) hipFree(keys_sorted);
+    if (N) hipFree(N);
+    if (tmp) hipFree(tmp);
+    if (nodes) hipFree(nodes);
+    if (tris) hipFree(tris);
+    return -1;
+}
+
+}  // namespace rs

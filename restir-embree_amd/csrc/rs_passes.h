@@ -1,0 +1,504 @@
+// rs_passes.h -- the per-pixel ReSTIR passes as device functions + kernels (gfx950).
+//
+// One thread per pixel; a 64-lane wave covers an 8x8 pixel tile (primary/shadow-ray coherence and
+// L1/L2 locality of the neighbour gathers), a 256-thread workgroup a 16x16 tile.
+// Passes (SimpleGuiDX11::produceRestir, pg/simpleguidx11.cpp:359-487):
+//   k_gbuffer_initial : gBufferFillPass (:368-375) fused with initialRenderPass (:381-388) -- the
+//                       initial pass reads only its own pixel's G record, so it stays in registers
+//   k_visibility      : visibilityPass (:393-402)
+//   k_temporal        : temporalReusePass (:408-420)
+//   k_spatial         : spatialReusePass (:428-443), the last pass fused with the shade loop
+//                       (:449-472): the shaded f is the selected candidate's (already visibility-
+//                       tested) f, cached, so shading costs no extra shadow ray
+//   k_shade           : stand-alone shade loop when no reuse pass can carry it
+#pragma once
+#include "rs_scene.h"
+
+namespace rs {
+
+struct FrameConst {
+    // rs_frame_params snapshot
+    int m_area, m_brdf, k, spatial_passes, cap;
+    float radius, min_normal_sim, max_depth_diff;
+    int do_spatial, do_temporal, do_vis_pass, reject, mis;
+    vec3 bg; float tnear_off, tfar_off, normal_off;
+    uint32_t seed, frame;
+    int W, H;             // full frame
+    int y0, y1;           // band this context renders
+    int gy0, gy1;         // G-buffer rows computed (band + margin, clamped)
+    float inv_view[9];    // mat3(invViewMat), column-major (pg/camera.cpp:57)
+    GCam cam, camp;       // current / previous frame camera (pg/GBufferElement.h:136-139)
+};
+
+struct Counters { unsigned long long rays, primary, reproj_outside; };
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ void count_rays(Counters* C, uint32_t rays, uint32_t primary) {
+    uint32_t r = wave_sum(rays), p = wave_sum(primary);
+    if ((threadIdx.x & 63) == 0) {
+        if (r) atomicAdd(&C->rays, (unsigned long long)r);
+        if (p) atomicAdd(&C->primary, (unsigned long long)p);
+    }
+}
+
+// 8x8 tile per wave, 16x16 per workgroup, rows [ya, yb)
+__device__ __forceinline__ bool pixel_of(int ya, int yb, int W, int& x, int& y) {
+    int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    y = ya + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    return x < W && y < yb;
+}
+
+// Intersection::testOcclusion (pg/Intersection.h:43-60): from the surface point, no normal offset
+__device__ __forceinline__ bool occluded(const DevScene& S, const FrameConst& F, vec3 from, vec3 to, uint32_t& rays) {
+    float dist = length(to - from);
+    vec3 dir = normalize(to - from);
+    rays++;
+    return occluded_ray(S, from, dir, FLT_MIN + F.tnear_off, dist - F.tfar_off);
+}
+
+// ReSTIRIntegrator::evaluateF (pg/ReSTIRIntegrator.cpp:185-211).  The shadow ray is skipped when
+// L_i*f_r*G is exactly zero in every channel (the result is 0 whatever V is).
+__device__ __forceinline__ vec3 evaluate_f(const DevScene& S, const FrameConst& F, const Sample& s, vec3 cam,
+                                           const GElem& g, bool test_vis, uint32_t& rays) {
+    if (!smp_valid(s) || g.le.x > 0 || g.le.y > 0 || g.le.z > 0) return mk(0, 0, 0);
+    vec3 ld = s.p - g.pos;
+    float r2 = dot(ld, ld);
+    ld = normalize(ld);
+    float cI = gmax(dot(ld, g.nrm), 0.0f);
+    float cY = fabsf(dot(-ld, s.n));
+    float G = cI * cY / r2;
+    vec3 L = (s.li * eval_brdf(g, cam, ld)) * G;
+    if (test_vis && !(L.x == 0.0f && L.y == 0.0f && L.z == 0.0f)) {
+        bool vis = !occluded(S, F, g.pos, s.p, rays);
+        L = L * (float)vis;
+    }
+    return L;
+}
+
+// m_area / m_brdf (pg/ReSTIRIntegrator.h:62-74)
+__device__ __forceinline__ float m_area(const FrameConst& F, float pa, float pb) {
+    if (pa == 0.0f && pb == 0.0f) return 0.0f;
+    return pa / ((float)F.m_area * pa + (float)F.m_brdf * pb);
+}
+__device__ __forceinline__ float m_brdf(const FrameConst& F, float pb, float pa) {
+    if (pa == 0.0f && pb == 0.0f) return 0.0f;
+    return pb / ((float)F.m_area * pa + (float)F.m_brdf * pb);
+}
+
+// gBufferFillPass (pg/ReSTIRIntegrator.cpp:213-234) + Camera::GenerateRay (pg/camera.cpp:20-42)
+__device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameConst& F, int x, int y) {
+    vec3 dc = mk((float)x - (float)F.W / 2.0f, (float)F.H / 2.0f - (float)y, -F.cam.focal);
+    const float* m = F.inv_view;
+    vec3 dw = mk(m[0] * dc.x + m[3] * dc.y + m[6] * dc.z, m[1] * dc.x + m[4] * dc.y + m[7] * dc.z,
+                 m[2] * dc.x + m[5] * dc.y + m[8] * dc.z);
+    dw = normalize(dw);
+    SurfHit h = intersect(S, F.cam.pos, dw, FLT_MIN + 0.01f);
+    GElem g;
+    g.pos = mk(0, 0, 0); g.nrm = g.pos; g.kd = g.pos; g.ks = g.pos; g.le = g.pos;
+    g.shin = 0; g.depth = 0; g.type = 0; g.inv_im = 0;
+    if (h.hit) {
+        MatRec mr = load_mat(S, h.mat);
+        g.pos = h.point; g.nrm = h.normal; g.depth = length(h.point - F.cam.pos);
+        g.type = mr.type; g.kd = mr.kd; g.ks = mr.ks; g.le = mr.le; g.shin = mr.shin;
+        if (g.type == MT_PHONG || g.type == MT_DIELECTRIC) {
+            vec3 V = normalize(F.cam.pos - g.pos);
+            g.inv_im = 1.0f / calc_I_M(dot(V, g.nrm), g.shin);
+        }
+    } else {
+        g.le = F.bg;      // useSkybox=false path: renderParams.bgColor (:231)
+    }
+    return g;
+}
+
+// areaSampleLight (pg/ReSTIRIntegrator.cpp:89-124), TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54),
+// Sampling::sampleTriangle (pg/Sampling.cpp:63-76)
+__device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameConst& F, const GElem& g, vec3 cam,
+                                              Rng& rng, float& W_out, float& mis_out) {
+    float ksi = rng.range(0.0f, 1.0f);
+    uint32_t lo = 0, n = S.n_emis;          // std::lower_bound(cdf2, ksi)
+    while (n > 0) {
+        uint32_t h = n >> 1;
+        if (S.cdf[lo + h] < ksi) { lo = lo + h + 1; n = n - h - 1; } else n = h;
+    }
+    uint32_t idx = lo < S.n_emis ? lo : S.n_emis - 1;
+    const float4* E = S.emis + 8 * idx;
+    float4 P0 = E[0], P1 = E[1], P2 = E[2];
+    float r1 = rng.range(0, 1), r2 = rng.range(0, 1);
+    float sr = sqrtf(r1);
+    float bx = 1.0f - sr, by = sr * (1.0f - r2), bz = sr * r2;
+    vec3 pt = (xyz(P0) * bx + xyz(P1) * by) + xyz(P2) * bz;
+    vec3 nn = normalize((xyz(E[3]) * bx + xyz(E[4]) * by) + xyz(E[5]) * bz);
+    float pdf_area = P0.w * P1.w;           // pick prob * (1 / area)
+    vec3 ld = pt - g.pos;
+    float r2s = dot(ld, ld);
+    ld = normalize(ld);
+    float cY = gmax(dot(-ld, nn), 0.0f);
+    float amf = cY / r2s;
+    float pba = phong_pdf(g, cam, ld) * amf;
+    mis_out = m_area(F, pdf_area, pba);
+    W_out = 1.0f / pdf_area;
+    return Sample{pt, nn, xyz(E[6])};
+}
+
+// brdfSampleLight (pg/ReSTIRIntegrator.cpp:126-177)
+__device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameConst& F, const GElem& g, vec3 cam,
+                                              Rng& rng, float& W_out, float& mis_out, uint32_t& rays) {
+    float pdf;
+    vec3 wi = sample_brdf(g, cam, rng, pdf);
+    vec3 org = g.pos + g.nrm * F.normal_off;
+    rays++;
+    SurfHit h = intersect(S, org, wi, FLT_MIN + F.tnear_off);
+    W_out = 0.0f; mis_out = 0.0f;
+    if (h.hit) {
+        MatRec mr = load_mat(S, h.mat);
+        if (mr.le.x + mr.le.y + mr.le.z > 0) {      // Material::isEmissive (pg/material.h:135-137)
+            vec3 ld = h.point - g.pos;
+            float r2s = dot(ld, ld);
+            ld = normalize(ld);
+            float cY = gmax(dot(-ld, h.normal), 0.0f);
+            float amf = cY / r2s;
+            float pdf_area = S.emis[8 * h.emis_id + 2].w;   // getPDFForTriangle (pg/TriangleCDF.h:25-31)
+            float bpa = pdf * amf;
+            W_out = 1.0f / bpa;
+            mis_out = m_brdf(F, bpa, pdf_area);
+            return Sample{h.point, h.normal, mr.le};
+        }
+    }
+    return smp_invalid();
+}
+
+// initialRenderPass (pg/ReSTIRIntegrator.cpp:236-298).  f_sel returns the selected candidate's f
+// (for the fused shade); the final p-hat (:289) equals the selected candidate's p-hat (same
+// arguments), so it is not re-evaluated.
+__device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& F, const GElem& g, uint32_t pix,
+                                           vec3& f_sel, uint32_t& rays) {
+    f_sel = mk(0, 0, 0);
+    if (any_pos(g.le) || S.n_emis == 0) return res_empty();
+    Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, pix);
+    Res r = res_empty();
+    const vec3 cam = F.cam.pos;
+    const bool tv = !F.do_vis_pass;
+    float best_phat = 0.0f;
+    if (F.m_area > 0) {
+        float inv_ma = 1.0f / (float)F.m_area;
+        for (int i = 0; i < F.m_area; ++i) {
+            float Wc, mis;
+            Sample s = area_sample(S, F, g, cam, rng, Wc, mis);
+            vec3 f = evaluate_f(S, F, s, cam, g, tv, rays);
+            float ph = length(f);
+            float w = F.m_brdf > 0 ? mis * ph * Wc : inv_ma * ph * Wc;
+            if (res_add(r, s, w, 1, rng)) { best_phat = ph; f_sel = f; }
+        }
+    }
+    if (F.m_brdf > 0) {
+        float inv_mb = 1.0f / (float)F.m_brdf;
+        for (int i = 0; i < F.m_brdf; ++i) {
+            float Wc, mis;
+            Sample s = brdf_sample(S, F, g, cam, rng, Wc, mis, rays);
+            vec3 f = evaluate_f(S, F, s, cam, g, tv, rays);
+            float ph = length(f);
+            float w = F.m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
+            if (res_add(r, s, w, 1, rng)) { best_phat = ph; f_sel = f; }
+        }
+    }
+    float ph = smp_valid(smp_of(r)) ? best_phat : 0.0f;
+    r.W = ph > 0.0f ? 1.0f / ph * r.wsum : 0.0f;
+    res_cap(r, F.cap);
+    return r;
+}
+
+// shade of one pixel (pg/simpleguidx11.cpp:456-468) given the reservoir's f (already visibility-tested)
+__device__ __forceinline__ vec3 shade_px(const Res& r, vec3 f, vec3 le) {
+    vec3 px = r.wsum > 0.0f ? f * r.W : le;   // Reservoir::hasSample (pg/Reservoir.h:49-52)
+    return sanitize(px);
+}
+__device__ __forceinline__ void store_rgb(float* fb, size_t p, vec3 c) {
+    fb[3 * p] = c.x; fb[3 * p + 1] = c.y; fb[3 * p + 2] = c.z;
+}
+
+__global__ void __launch_bounds__(256) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G, ResBuf Rw,
+                                                         float* fb, int fuse_shade, Counters* C) {
+    int x, y;
+    uint32_t rays = 0, prim = 0;
+    if (pixel_of(F.gy0, F.gy1, F.W, x, y)) {
+        size_t p = (size_t)y * F.W + x;
+        GElem g = gbuffer_fill(S, F, x, y);
+        prim = 1;
+        G.store(p, g);
+        if (y >= F.y0 && y < F.y1) {
+            vec3 f;
+            Res r = initial_ris(S, F, g, (uint32_t)p, f, rays);
+            Rw.store(p, r);
+            if (fuse_shade) store_rgb(fb, p, shade_px(r, f, g.le));
+        }
+    }
+    count_rays(C, rays + prim, prim);
+}
+
+// visibilityPass (pg/ReSTIRIntegrator.cpp:302-312).  Invalid samples always carry W == 0 already,
+// so their (meaningless) ray is not traced.
+__global__ void __launch_bounds__(256) k_visibility(DevScene S, FrameConst F, GBuf G, ResBuf R, Counters* C) {
+    int x, y;
+    uint32_t rays = 0;
+    if (pixel_of(F.y0, F.y1, F.W, x, y)) {
+        size_t p = (size_t)y * F.W + x;
+        Res r = R.load(p);
+        if (smp_valid(smp_of(r)) && occluded(S, F, G.pos(p), r.p, rays)) {
+            r.W = 0;
+            R.r[3 * p + 1].w = 0.0f;
+        }
+    }
+    count_rays(C, rays, 0);
+}
+
+// reprojectBackward / reprojectForward (pg/ReSTIRIntegrator.cpp:544-587)
+__device__ __forceinline__ bool reproject(const GCam& c, vec3 ws, int W, int H, int& sx, int& sy) {
+    const float* m = c.view;   // glm mat4 * vec4: (m0*x + m1*y) + (m2*z + m3*1)
+    float vx = (m[0] * ws.x + m[4] * ws.y) + (m[8] * ws.z + m[12] * 1.0f);
+    float vy = (m[1] * ws.x + m[5] * ws.y) + (m[9] * ws.z + m[13] * 1.0f);
+    float vz = (m[2] * ws.x + m[6] * ws.y) + (m[10] * ws.z + m[14] * 1.0f);
+    if (vz >= 0) return false;
+    float fx = (-vx / vz) * c.focal + (float)W / 2.0f;
+    float fy = (vy / vz) * c.focal + (float)H / 2.0f;
+    float rx = roundf(fx), ry = roundf(fy);
+    if (!(rx >= -2147483648.0f && rx < 2147483648.0f) || !(ry >= -2147483648.0f && ry < 2147483648.0f)) return false;
+    int X = (int)rx, Y = (int)ry;
+    if (X < 0 || X > W - 1 || Y < 0 || Y > H - 1) return false;
+    sx = X; sy = Y;
+    return true;
+}
+
+// temporalReusePass (pg/ReSTIRIntegrator.cpp:625-732).  The previous reservoir is read at the
+// CURRENT pixel (:641), the previous G-buffer at the reprojected pixel (:652).
+__global__ void __launch_bounds__(256) k_temporal(DevScene S, FrameConst F, GBuf G, GBuf Gp, ResBuf Rr, ResBuf Rl,
+                                                  ResBuf Rw, Counters* C) {
+    int x, y;
+    uint32_t rays = 0;
+    if (pixel_of(F.y0, F.y1, F.W, x, y)) {
+        size_t p = (size_t)y * F.W + x;
+        Res cr = Rr.load(p);
+        Res out = cr;
+        GElem cur = G.load(p);
+        int qx, qy, fx, fy;
+        bool ok = reproject(F.camp, cur.pos, F.W, F.H, qx, qy);
+        // rows outside the G-buffer margin of a tile are treated as a failed reprojection (counted)
+        if (ok && (qy < F.gy0 || qy >= F.gy1)) { ok = false; atomicAdd(&C->reproj_outside, 1ull); }
+        GElem prev;
+        if (ok) {
+            size_t q = (size_t)qy * F.W + qx;
+            prev = Gp.load(q);
+            float cd = length(cur.pos - F.cam.pos), pd = length(prev.pos - F.camp.pos);
+            float dr = cd > pd ? pd / cd : cd / pd;
+            ok = !(dr < 0.9f);
+            if (ok) {
+                vec3 pac = Gp.pos(p);
+                ok = reproject(F.cam, pac, F.W, F.H, fx, fy);
+                if (ok && (fy < F.gy0 || fy >= F.gy1)) { ok = false; atomicAdd(&C->reproj_outside, 1ull); }
+                if (ok) {
+                    vec3 fw = G.pos((size_t)fy * F.W + fx);
+                    float cdp = length(pac - F.camp.pos), pdp = length(fw - F.cam.pos);
+                    float drp = cdp > pdp ? pdp / cdp : cdp / pdp;
+                    ok = !(drp < 0.9f);
+                }
+            }
+        }
+        if (ok) {
+            Res pr = Rl.load(p);
+            Rng rng; rng.init(F.seed, F.frame, PASS_TEMPORAL, (uint32_t)p);
+            Res res = res_empty();
+            Sample cs = smp_of(cr), ps = smp_of(pr);
+            float p_cur = length(evaluate_f(S, F, cs, F.cam.pos, cur, true, rays));
+            float p_prev = length(evaluate_f(S, F, cs, F.camp.pos, prev, true, rays));
+            float m_cur = p_cur * (float)cr.conf / (p_cur * (float)cr.conf + p_prev * (float)pr.conf);
+            if (!(m_cur > 0)) m_cur = 0.0f;
+            float ph_cur = p_cur;
+            bool took_cur = res_add(res, cs, m_cur * ph_cur * cr.W, cr.conf, rng);
+            p_cur = length(evaluate_f(S, F, ps, F.cam.pos, cur, true, rays));
+            p_prev = length(evaluate_f(S, F, ps, F.camp.pos, prev, true, rays));
+            float m_prev = p_prev * (float)pr.conf / (p_cur * (float)cr.conf + p_prev * (float)pr.conf);
+            if (!(m_prev > 0)) m_prev = 0.0f;
+            float ph_prev = p_cur;
+            bool took_prev = res_add(res, ps, m_prev * ph_prev * pr.W, pr.conf, rng);
+            res_cap(res, F.cap);
+            float fph = took_prev ? ph_prev : (took_cur ? ph_cur : 0.0f);
+            res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
+            out = res;
+        }
+        Rw.store(p, out);
+    }
+    count_rays(C, rays, 0);
+}
+
+// Sampling::sampleDiskUniform (pg/Sampling.cpp:78-87) -> glm::vec<2,int> (truncation), clamped to
+// the screen (pg/ReSTIRIntegrator.cpp:338-340).  Draws 2i and 2i+1 of the pixel's spatial stream.
+__device__ __forceinline__ size_t neighbor_px(const FrameConst& F, const Rng& rng, int i, int x, int y) {
+    float u0 = rng.at(2u * i), u1 = rng.at(2u * i + 1u);
+    float theta = (0.0f + (2.0f - 0.0f) * u0) * kPi;
+    float r = sqrtf(0.0f + (F.radius - 0.0f) * u1);
+    float ox = r * cosf(theta), oy = r * sinf(theta);
+    int nx = x + (int)ox, ny = y + (int)oy;
+    nx = nx < 0 ? 0 : (nx > F.W - 1 ? F.W - 1 : nx);
+    ny = ny < 0 ? 0 : (ny > F.H - 1 ? F.H - 1 : ny);
+    return (size_t)ny * F.W + nx;
+}
+
+// list position i (0 = canonical) -> pixel index; `acc` bit j set <=> neighbour draw j accepted
+__device__ __forceinline__ size_t list_px(const FrameConst& F, const Rng& rng, uint64_t acc, int i, int x, int y,
+                                          size_t p) {
+    if (i == 0) return p;
+    int c = 0;
+    for (int j = 0; j < F.k; ++j) {
+        if ((acc >> j) & 1ull) {
+            if (++c == i) return neighbor_px(F, rng, j, x, y);
+        }
+    }
+    return p;
+}
+
+// spatialReusePass (pg/ReSTIRIntegrator.cpp:316-542); shade fused when this is the last pass.
+__global__ void __launch_bounds__(256) k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw,
+                                                 int pass_idx, int fuse_shade, float* fb, Counters* C) {
+    int x, y;
+    uint32_t rays = 0;
+    if (pixel_of(F.y0, F.y1, F.W, x, y)) {
+        size_t p = (size_t)y * F.W + x;
+        const vec3 cam = F.cam.pos;
+        GElem th = G.load(p);
+        if (any_pos(th.le)) {                              // :319-324
+            Res r = Rr.load(p);
+            Rw.store(p, r);
+            if (fuse_shade) store_rgb(fb, p, shade_px(r, mk(0, 0, 0), th.le));
+        } else {
+            Rng rng; rng.init(F.seed, F.frame, PASS_SPATIAL0 + (uint32_t)pass_idx, (uint32_t)p);
+            // neighbour selection (:334-374)
+            uint64_t acc = 0;
+            int M = 1;
+            for (int i = 0; i < F.k; ++i) {
+                size_t q = neighbor_px(F, rng, i, x, y);
+                if (any_pos(G.le(q))) continue;
+                if (F.reject) {
+                    float4 nq = G.g1[q];
+                    float ns = dot(xyz(nq), th.nrm);
+                    if (ns < F.min_normal_sim) continue;
+                    float nd = G.g0[q].w;
+                    float dr = 0;
+                    if (nd > 0) dr = th.depth / nd;
+                    float hd = F.max_depth_diff * 0.5f;
+                    if (dr < 1.0f - hd || dr > 1.0f + hd) continue;
+                }
+                acc |= 1ull << i;
+                M += 1;
+            }
+            rng.n = 2u * (uint32_t)F.k;
+            const int cnt = M;
+            int csum = 0, csum_nc = 0;                     // :379-385
+            for (int i = 0; i < cnt; ++i) {
+                int c = __float_as_int(Rr.r[3 * list_px(F, rng, acc, i, x, y, p) + 2].w);
+                csum += c;
+                if (i) csum_nc += c;
+            }
+            Res res = res_empty();
+            int sel = 0;
+            float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
+            vec3 f_sel = mk(0, 0, 0);
+            for (int i = 0; i < cnt; ++i) {
+                size_t qi = list_px(F, rng, acc, i, x, y, p);
+                Res ri = Rr.load(qi);
+                Sample si = smp_of(ri);
+                float mis = rcpM;
+                if (F.mis == MIS_BALANCE) {                // :407-424
+                    float num = 0, den = 0;
+                    mis = 0.0f;
+                    for (int j = 0; j < cnt; ++j) {
+                        size_t qj = list_px(F, rng, acc, j, x, y, p);
+                        int cj = __float_as_int(Rr.r[3 * qj + 2].w);
+                        float ph = length(evaluate_f(S, F, si, cam, G.load(qj), true, rays));
+                        den += ph * cj;
+                        if (i == j) num = ph * ri.conf;
+                    }
+                    if (den > 0) mis = num / den;
+                }
+                if (F.mis == MIS_PAIRWISE) {               // :427-467
+                    mis = 0.0f;
+                    if (i == 0) {
+                        float sum = 0.0f;
+                        float phc = length(evaluate_f(S, F, si, cam, G.load(qi), true, rays)) * (float)ri.conf;
+                        for (int j = 1; j < cnt; ++j) {
+                            size_t qj = list_px(F, rng, acc, j, x, y, p);
+                            int cj = __float_as_int(Rr.r[3 * qj + 2].w);
+                            float phj = length(evaluate_f(S, F, si, cam, G.load(qj), true, rays));
+                            float den = phc + phj * (float)csum_nc;
+                            if (den > 0) {
+                                float cf = (float)cj / (float)csum;
+                                sum += cf * (phc / den);
+                            }
+                        }
+                        mis = ((float)ri.conf / (float)csum) + sum;
+                    } else {
+                        float phi = length(evaluate_f(S, F, si, cam, G.load(qi), true, rays));
+                        float phc = length(evaluate_f(S, F, si, cam, G.load(p), true, rays));
+                        phi *= (float)csum_nc;
+                        int c0 = __float_as_int(Rr.r[3 * p + 2].w);
+                        float den = phi + phc * (float)c0;
+                        if (den > 0 && csum > 0) mis = ((float)ri.conf / (float)csum) * (phi / den);
+                    }
+                }
+                vec3 f = evaluate_f(S, F, si, cam, th, true, rays);     // :472
+                float rph = length(f);
+                float rw = mis * rph * ri.W;
+                if (res_add(res, si, rw, ri.conf, rng)) { sel = i; f_sel = f; }
+            }
+            float fph = smp_valid(smp_of(res)) ? length(f_sel) : 0.0f;  // :481
+            if (F.mis == MIS_CONSTANT || F.mis == MIS_BALANCE || F.mis == MIS_PAIRWISE) {
+                res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
+            } else if (F.mis == MIS_DEBIAS_Z) {            // :494-506
+                int Z = 0;
+                float corr = 1.0f;
+                for (int i = 0; i < cnt; ++i) {
+                    size_t qi = list_px(F, rng, acc, i, x, y, p);
+                    if (!occluded(S, F, G.pos(qi), res.p, rays)) Z += 1;
+                }
+                if (Z > 0 && M > 0) corr = (1.0f / (float)Z) / rcpM;
+                res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
+            } else if (F.mis == MIS_DEBIAS_CONTRIB) {      // :515-538
+                Sample ss = smp_of(Rr.load(list_px(F, rng, acc, sel, x, y, p)));
+                float num = 0, den = 0, cw = 0, corr = 0;
+                for (int i = 0; i < cnt; ++i) {
+                    size_t qi = list_px(F, rng, acc, i, x, y, p);
+                    int ci = __float_as_int(Rr.r[3 * qi + 2].w);
+                    float ph = length(evaluate_f(S, F, ss, cam, G.load(qi), true, rays));
+                    den += ph * (float)ci;
+                    if (i == sel) num = ph * (float)ci;
+                }
+                if (den > 0) cw = num / den;
+                if (M > 0) corr = cw / rcpM;
+                res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
+            }
+            res_cap(res, F.cap);
+            Rw.store(p, res);
+            if (fuse_shade) store_rgb(fb, p, shade_px(res, f_sel, th.le));
+        }
+    }
+    count_rays(C, rays, 0);
+}
+
+// shade loop (pg/simpleguidx11.cpp:447-472)
+__global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G, ResBuf Rr, float* fb, Counters* C) {
+    int x, y;
+    uint32_t rays = 0;
+    if (pixel_of(F.y0, F.y1, F.W, x, y)) {
+        size_t p = (size_t)y * F.W + x;
+        Res r = Rr.load(p);
+        GElem g = G.load(p);
+        vec3 f = mk(0, 0, 0);
+        if (r.wsum > 0.0f) f = evaluate_f(S, F, smp_of(r), F.cam.pos, g, true, rays);
+        store_rgb(fb, p, shade_px(r, f, g.le));
+    }
+    count_rays(C, rays, 0);
+}
+
+}  // namespace rs

@@ -1,0 +1,148 @@
+// rs_scene.h -- device scene layout and BVH traversal (replaces Embree's rtcIntersect1/rtcOccluded1,
+// pg/Intersection.h:8-113).
+//
+// BVH: depth-first ("preorder") node array with skip pointers -- stackless traversal.  Node i is
+// 32 B = 2 x float4:  a = (lo.xyz, skip), b = (hi.xyz, leaf)   [skip/leaf as int bits]
+//   skip = index of the node following i's subtree (== n_nodes ends traversal)
+//   leaf = -1 for an interior node (its first child is i + 1), else (first << 3) | (count - 1)
+// Leaf triangles are stored contiguously in leaf order, 48 B each = 3 x float4:
+//   (v0.xyz, prim), (e1.xyz, 0), (e2.xyz, 0)   with e1 = v1 - v0, e2 = v2 - v0 (same float ops the
+//   CPU restatement does on the fly), prim = original triangle index (int bits).
+// Shading attributes are indexed by prim: 3 float4 vertex normals + material/emissive id.
+#pragma once
+#include "rs_device.h"
+
+namespace rs {
+
+struct DevScene {
+    const float4* nodes;      // 2 per node
+    const float4* tris;       // 3 per leaf-ordered triangle
+    const float4* tri_nrm;    // 3 per prim: n0 (w = material id bits), n1 (w = emissive id bits), n2
+    const float4* mats;       // 3 per material: (kd, shin), (ks, type bits), (le, 0)
+    const float4* emis;       // 8 per emissive triangle: p0,p1,p2 (w: pick_pdf, inv_area, pdf_brdf_area),
+                              //   n0, n1, n2, le, (area, 0, 0, 0)
+    const float* cdf;         // cumulative normalised area (TriangleCDF::cdf2)
+    uint32_t n_nodes, n_tris, n_emis, n_mats;
+};
+
+// Moller-Trumbore, fixed op order (identical to oracle/restir_oracle.c tri_hit)
+__device__ __forceinline__ bool tri_test(float4 A, float4 B, float4 C, vec3 o, vec3 d, float tnear,
+                                         float tfar, float& t_out, float& u_out, float& v_out) {
+    vec3 v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
+    vec3 p = cross(d, e2);
+    float det = dot(e1, p);
+    if (det == 0.0f) return false;
+    float inv = 1.0f / det;
+    vec3 sv = o - v0;
+    float u = dot(sv, p) * inv;
+    if (!(u >= 0.0f && u <= 1.0f)) return false;
+    vec3 q = cross(sv, e1);
+    float v = dot(d, q) * inv;
+    if (!(v >= 0.0f && u + v <= 1.0f)) return false;
+    float t = dot(e2, q) * inv;
+    if (!(t >= tnear && t <= tfar)) return false;
+    t_out = t; u_out = u; v_out = v;
+    return true;
+}
+
+// conservative slab test (interval widened by 4 ulp-ish so no box the triangle test accepts is culled)
+__device__ __forceinline__ bool box_test(float4 a, float4 b, vec3 o, vec3 inv, float tnear, float tfar) {
+    float tx0 = (a.x - o.x) * inv.x, tx1 = (b.x - o.x) * inv.x;
+    float ty0 = (a.y - o.y) * inv.y, ty1 = (b.y - o.y) * inv.y;
+    float tz0 = (a.z - o.z) * inv.z, tz1 = (b.z - o.z) * inv.z;
+    float t0 = fmaxf(fmaxf(fmaxf(tnear, fminf(tx0, tx1)), fminf(ty0, ty1)), fminf(tz0, tz1));
+    float t1 = fminf(fminf(fminf(tfar, fmaxf(tx0, tx1)), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
+}
+
+// rtcOccluded1 semantics (pg/Intersection.h:43-60): any hit with t in [tnear, tfar]
+__device__ __noinline__ bool occluded_ray(const DevScene& S, vec3 o, vec3 d, float tnear, float tfar) {
+    vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    uint32_t i = 0;
+    const uint32_t n = S.n_nodes;
+    while (i < n) {
+        float4 a = S.nodes[2 * i], b = S.nodes[2 * i + 1];
+        int skip = __float_as_int(a.w);
+        if (box_test(a, b, o, inv, tnear, tfar)) {
+            int leaf = __float_as_int(b.w);
+            if (leaf >= 0) {
+                int first = leaf >> 3, cnt = (leaf & 7) + 1;
+                for (int k = 0; k < cnt; ++k) {
+                    const float4* T = S.tris + 3 * (first + k);
+                    float t, u, v;
+                    if (tri_test(T[0], T[1], T[2], o, d, tnear, tfar, t, u, v)) return true;
+                }
+                i = (uint32_t)skip;
+            } else {
+                i = i + 1;
+            }
+        } else {
+            i = (uint32_t)skip;
+        }
+    }
+    return false;
+}
+
+struct Hit { float t, u, v; int prim; };
+
+// rtcIntersect1 semantics: closest hit in [tnear, tfar]; ties broken by the smaller triangle index
+__device__ __noinline__ Hit closest_ray(const DevScene& S, vec3 o, vec3 d, float tnear, float tfar) {
+    vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
+    uint32_t i = 0;
+    const uint32_t n = S.n_nodes;
+    while (i < n) {
+        float4 a = S.nodes[2 * i], b = S.nodes[2 * i + 1];
+        int skip = __float_as_int(a.w);
+        if (box_test(a, b, o, inv, tnear, h.t)) {
+            int leaf = __float_as_int(b.w);
+            if (leaf >= 0) {
+                int first = leaf >> 3, cnt = (leaf & 7) + 1;
+                for (int k = 0; k < cnt; ++k) {
+                    const float4* T = S.tris + 3 * (first + k);
+                    float t, u, v;
+                    if (tri_test(T[0], T[1], T[2], o, d, tnear, h.t, t, u, v)) {
+                        int prim = __float_as_int(T[0].w);
+                        if (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim)) {
+                            h.t = t; h.u = u; h.v = v; h.prim = prim;
+                        }
+                    }
+                }
+                i = (uint32_t)skip;
+            } else {
+                i = i + 1;
+            }
+        } else {
+            i = (uint32_t)skip;
+        }
+    }
+    return h;
+}
+
+// Material record (pg/material.h:105-115)
+struct MatRec { vec3 kd; float shin; vec3 ks; int type; vec3 le; };
+__device__ __forceinline__ MatRec load_mat(const DevScene& S, uint32_t m) {
+    float4 a = S.mats[3 * m], b = S.mats[3 * m + 1], c = S.mats[3 * m + 2];
+    return MatRec{xyz(a), a.w, xyz(b), __float_as_int(b.w), xyz(c)};
+}
+
+// Intersection::intersectEmbree + getGeometryAttributes (pg/Intersection.h:8-41,85-113):
+// hit point = org + dir*t, interpolated normal (1-u-v)n0 + u n1 + v n2, normalised, flipped to face
+// the ray; material; emissive id (vertex-0 attribute, :103-110).
+struct SurfHit { bool hit; vec3 point, normal; uint32_t mat; int emis_id; };
+__device__ __forceinline__ SurfHit intersect(const DevScene& S, vec3 o, vec3 d, float tnear) {
+    SurfHit r; r.hit = false; r.mat = 0; r.emis_id = -1; r.point = mk(0, 0, 0); r.normal = mk(0, 0, 0);
+    Hit h = closest_ray(S, o, d, tnear, FLT_MAX);
+    if (h.prim < 0) return r;
+    const float4* N = S.tri_nrm + 3 * h.prim;
+    float4 n0 = N[0], n1 = N[1], n2 = N[2];
+    float w = 1.0f - h.u - h.v;
+    vec3 n = (xyz(n0) * w + xyz(n1) * h.u) + xyz(n2) * h.v;
+    n = normalize(n);
+    if (dot(-d, n) <= 0.0f) n = n * -1.0f;
+    r.hit = true; r.normal = n; r.point = o + d * h.t;
+    r.mat = (uint32_t)__float_as_int(n0.w); r.emis_id = __float_as_int(n1.w);
+    return r;
+}
+
+}  // namespace rs

@@ -1,0 +1,275 @@
+"""ctypes binding of librestir_amd.so (include/restir_c.h) with the reference's frame API.
+
+Mirrors the reference's surface:
+  * ``Renderer(width, height)``             ~ SimpleGuiDX11(width, height) + rtcNewDevice
+  * ``Renderer.load_scene(scene | path)``    ~ Raytracer::LoadScene (pg/raytracer.cpp:34-38)
+  * ``Renderer.produce_restir(camera, params, frame)`` ~ SimpleGuiDX11::produceRestir (pg/simpleguidx11.cpp:359)
+  * ``Renderer.frame_data``                  ~ glm::vec3* frame_data (pg/simpleguidx11.h:152), (H, W, 3) f32
+There is no CPU fallback: constructing a Renderer without the built library or without a HIP
+device raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .params import FrameParams
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "librestir_amd.so")
+
+RS_OK, RS_E_INVALID, RS_E_HIP, RS_E_UNSUPPORTED, RS_E_IO = 0, -1, -2, -3, -4
+
+# Every symbol include/restir_c.h declares (checked by tests/test_capi_symbols.py).
+EXPORTED_SYMBOLS = [
+    "rs_context_create", "rs_context_destroy", "rs_last_error", "rs_scene_create", "rs_scene_load_obj",
+    "rs_scene_destroy", "rs_scene_info", "rs_render_frame", "rs_get_frame_device_ptr", "rs_reset_history",
+    "rs_synchronize", "rs_dump_gbuffer", "rs_dump_reservoirs", "rs_tile_begin", "rs_tile_halo_ptr",
+    "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace",
+]
+
+
+class MeshDesc(ctypes.Structure):
+    _fields_ = [("n_tris", ctypes.c_uint32), ("positions", ctypes.POINTER(ctypes.c_float)),
+                ("normals", ctypes.POINTER(ctypes.c_float)), ("material", ctypes.c_uint32)]
+
+
+class MaterialDesc(ctypes.Structure):
+    _fields_ = [("diffuse", ctypes.c_float * 3), ("specular", ctypes.c_float * 3), ("emission", ctypes.c_float * 3),
+                ("shininess", ctypes.c_float), ("type", ctypes.c_int32)]
+
+
+class CameraDesc(ctypes.Structure):
+    _fields_ = [("eye", ctypes.c_float * 3), ("at", ctypes.c_float * 3), ("fov_y_deg", ctypes.c_float)]
+
+
+class PassTimes(ctypes.Structure):
+    _fields_ = [("gbuffer_initial_ms", ctypes.c_float), ("visibility_ms", ctypes.c_float),
+                ("temporal_ms", ctypes.c_float), ("spatial_ms", ctypes.c_float), ("shade_ms", ctypes.c_float),
+                ("total_ms", ctypes.c_float), ("rays", ctypes.c_uint64), ("primary_rays", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class TileDesc(ctypes.Structure):
+    _fields_ = [("y0", ctypes.c_int32), ("y1", ctypes.c_int32), ("margin", ctypes.c_int32), ("halo", ctypes.c_int32)]
+
+
+class RestirError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load librestir_amd.so.  Raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RestirError(f"{path} not found: build it with `make -C restir-embree_amd` (hipcc, gfx950)")
+    L = ctypes.CDLL(path)
+    vp, i32, u32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32
+    fp = ctypes.POINTER(ctypes.c_float)
+    L.rs_context_create.argtypes = [i32, i32, i32, vp, ctypes.POINTER(vp)]
+    L.rs_context_destroy.argtypes = [vp]
+    L.rs_context_destroy.restype = None
+    L.rs_last_error.argtypes = [vp]
+    L.rs_last_error.restype = ctypes.c_char_p
+    L.rs_scene_create.argtypes = [vp, ctypes.POINTER(MeshDesc), u32, ctypes.POINTER(MaterialDesc), u32,
+                                  ctypes.POINTER(vp)]
+    L.rs_scene_load_obj.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
+    L.rs_scene_destroy.argtypes = [vp]
+    L.rs_scene_destroy.restype = None
+    L.rs_scene_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32),
+                                ctypes.POINTER(ctypes.c_float)]
+    L.rs_render_frame.argtypes = [vp, vp, ctypes.POINTER(CameraDesc), ctypes.POINTER(FrameParams), u32, fp,
+                                  ctypes.POINTER(PassTimes)]
+    L.rs_get_frame_device_ptr.argtypes = [vp, ctypes.POINTER(vp)]
+    L.rs_reset_history.argtypes = [vp]
+    L.rs_synchronize.argtypes = [vp]
+    L.rs_dump_gbuffer.argtypes = [vp, i32, fp]
+    L.rs_dump_reservoirs.argtypes = [vp, fp]
+    L.rs_tile_begin.argtypes = [vp, vp, ctypes.POINTER(CameraDesc), ctypes.POINTER(FrameParams), u32,
+                                ctypes.POINTER(TileDesc)]
+    L.rs_tile_halo_ptr.argtypes = [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+    L.rs_tile_temporal.argtypes = [vp]
+    L.rs_tile_spatial.argtypes = [vp, i32]
+    L.rs_tile_finish.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(PassTimes)]
+    L.rs_debug_trace.argtypes = [vp, vp, u32, fp, fp, fp, fp, i32, fp, ctypes.POINTER(ctypes.c_int32)]
+    _lib = L
+    return L
+
+
+def camera_desc(camera) -> CameraDesc:
+    c = CameraDesc()
+    arr = camera.as_array() if hasattr(camera, "as_array") else np.asarray(camera, np.float32)
+    for i in range(3):
+        c.eye[i] = float(arr[i])
+        c.at[i] = float(arr[3 + i])
+    c.fov_y_deg = float(arr[6])
+    return c
+
+
+class Scene:
+    """A scene uploaded to one context (Scene::Scene, pg/Scene.cpp:8-16; BVH built on the GPU)."""
+
+    def __init__(self, renderer: "Renderer", handle):
+        self.renderer = renderer
+        self.h = handle
+        n_tris, n_emis, n_nodes, ms = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_float()
+        renderer._check(renderer.lib.rs_scene_info(handle, ctypes.byref(n_tris), ctypes.byref(n_emis),
+                                                   ctypes.byref(n_nodes), ctypes.byref(ms)))
+        self.n_tris, self.n_emissive, self.n_nodes, self.build_ms = n_tris.value, n_emis.value, n_nodes.value, ms.value
+
+    def close(self):
+        if self.h:
+            self.renderer.lib.rs_scene_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Renderer:
+    """One HIP device + its per-pixel buffers (G x2, reservoirs x3, framebuffer)."""
+
+    def __init__(self, width: int, height: int, device: int = 0, stream: int | None = None):
+        self.lib = load_library()
+        self.W, self.H = int(width), int(height)
+        h = ctypes.c_void_p()
+        rc = self.lib.rs_context_create(device, self.W, self.H, ctypes.c_void_p(stream) if stream else None,
+                                        ctypes.byref(h))
+        if rc != RS_OK:
+            raise RestirError(f"rs_context_create failed ({rc}): {self.lib.rs_last_error(None).decode()}")
+        self.h = h
+        self.frame_data = np.zeros((self.H, self.W, 3), np.float32)
+        self.last_times = PassTimes()
+
+    def _check(self, rc):
+        if rc != RS_OK:
+            msg = self.lib.rs_last_error(self.h).decode()
+            raise RestirError(f"librestir_amd error {rc}: {msg}")
+        return rc
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.rs_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- scene-load ---------------------------------------------------------------------
+    def load_scene(self, scene) -> Scene:
+        if isinstance(scene, (str, os.PathLike)):
+            out = ctypes.c_void_p()
+            self._check(self.lib.rs_scene_load_obj(self.h, os.fsencode(scene), ctypes.byref(out)))
+            return Scene(self, out)
+        pos = np.ascontiguousarray(scene.positions, np.float32)
+        nrm = np.ascontiguousarray(scene.normals, np.float32)
+        tm = np.ascontiguousarray(scene.tri_material, np.uint32)
+        # group consecutive triangles with equal material into meshes (keeps triangle order)
+        cuts = np.flatnonzero(np.diff(tm)) + 1
+        starts = np.concatenate([[0], cuts]).astype(np.int64)
+        ends = np.concatenate([cuts, [tm.shape[0]]]).astype(np.int64)
+        meshes = (MeshDesc * max(1, len(starts)))()
+        fp = ctypes.POINTER(ctypes.c_float)
+        for i, (a, b) in enumerate(zip(starts, ends)):
+            meshes[i].n_tris = int(b - a)
+            meshes[i].positions = pos[a:b].ctypes.data_as(fp)
+            meshes[i].normals = nrm[a:b].ctypes.data_as(fp)
+            meshes[i].material = int(tm[a]) if b > a else 0
+        mats = (MaterialDesc * max(1, len(scene.materials)))()
+        for i, m in enumerate(scene.materials):
+            for j in range(3):
+                mats[i].diffuse[j] = m.kd[j]
+                mats[i].specular[j] = m.ks[j]
+                mats[i].emission[j] = m.le[j]
+            mats[i].shininess = m.shininess
+            mats[i].type = m.type
+        out = ctypes.c_void_p()
+        n_mesh = len(starts) if tm.shape[0] else 0
+        self._check(self.lib.rs_scene_create(self.h, meshes, n_mesh, mats, len(scene.materials), ctypes.byref(out)))
+        return Scene(self, out)
+
+    # ---- render(frame) ------------------------------------------------------------------
+    def produce_restir(self, scene: Scene, camera, params: FrameParams, frame_index: int = 0,
+                       copy_out: bool = True, timed: bool = True) -> np.ndarray | None:
+        cam = camera_desc(camera)
+        out = self.frame_data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) if copy_out else None
+        self._check(self.lib.rs_render_frame(self.h, scene.h, ctypes.byref(cam), ctypes.byref(params),
+                                             int(frame_index), out, ctypes.byref(self.last_times) if timed else None))
+        return self.frame_data if copy_out else None
+
+    render = produce_restir
+
+    def reset_history(self):
+        self._check(self.lib.rs_reset_history(self.h))
+
+    def synchronize(self):
+        self._check(self.lib.rs_synchronize(self.h))
+
+    def frame_device_ptr(self) -> int:
+        p = ctypes.c_void_p()
+        self._check(self.lib.rs_get_frame_device_ptr(self.h, ctypes.byref(p)))
+        return int(p.value or 0)
+
+    # ---- dumps ----------------------------------------------------------------------------
+    def gbuffer(self, prev: bool = False) -> np.ndarray:
+        out = np.zeros((self.H, self.W, 19), np.float32)
+        self._check(self.lib.rs_dump_gbuffer(self.h, 1 if prev else 0, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+        return out
+
+    def reservoirs(self) -> np.ndarray:
+        out = np.zeros((self.H, self.W, 12), np.float32)
+        self._check(self.lib.rs_dump_reservoirs(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+        return out
+
+    def debug_trace(self, scene: Scene, o, d, tnear, tfar, any_hit: bool):
+        o = np.ascontiguousarray(o, np.float32)
+        d = np.ascontiguousarray(d, np.float32)
+        n = o.shape[0]
+        tn = np.ascontiguousarray(np.broadcast_to(np.asarray(tnear, np.float32), (n,)))
+        tf = np.ascontiguousarray(np.broadcast_to(np.asarray(tfar, np.float32), (n,)))
+        t = np.zeros(n, np.float32)
+        prim = np.zeros(n, np.int32)
+        fp = ctypes.POINTER(ctypes.c_float)
+        self._check(self.lib.rs_debug_trace(self.h, scene.h, n, o.ctypes.data_as(fp), d.ctypes.data_as(fp),
+                                            tn.ctypes.data_as(fp), tf.ctypes.data_as(fp), 1 if any_hit else 0,
+                                            t.ctypes.data_as(fp), prim.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return t, prim
+
+    # ---- tile stages (multi-GPU) ------------------------------------------------------------
+    def tile_begin(self, scene: Scene, camera, params: FrameParams, frame_index: int, y0: int, y1: int,
+                   margin: int, halo: int):
+        cam = camera_desc(camera)
+        t = TileDesc(y0, y1, margin, halo)
+        self._check(self.lib.rs_tile_begin(self.h, scene.h, ctypes.byref(cam), ctypes.byref(params),
+                                           int(frame_index), ctypes.byref(t)))
+
+    def tile_halo_ptr(self, which: int):
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(self.lib.rs_tile_halo_ptr(self.h, which, ctypes.byref(p), ctypes.byref(n)))
+        return int(p.value or 0), int(n.value)
+
+    def tile_temporal(self):
+        self._check(self.lib.rs_tile_temporal(self.h))
+
+    def tile_spatial(self, pass_index: int):
+        self._check(self.lib.rs_tile_spatial(self.h, pass_index))
+
+    def tile_finish(self, timed: bool = False):
+        p = ctypes.c_void_p()
+        self._check(self.lib.rs_tile_finish(self.h, ctypes.byref(p), ctypes.byref(self.last_times) if timed else None))
+        return int(p.value or 0)

@@ -1,0 +1,161 @@
+"""ctypes wrapper for the CPU oracle (oracle/restir_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg as the checker / CPU baseline.  The product never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "restir-embree_amd"))
+
+from restir_amd.params import FrameParams  # noqa: E402
+
+LIB_PATH = os.path.join(ROOT, "oracle", "_build", "librestir_oracle.so")
+_lib = None
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+def _ptr(a, t=_f32p):
+    return a.ctypes.data_as(t)
+
+
+def build():
+    src = os.path.join(ROOT, "oracle", "restir_oracle.c")
+    if (not os.path.exists(LIB_PATH)) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.or_scene_create.restype = ctypes.c_void_p
+        L.or_scene_create.argtypes = [ctypes.c_uint32, _f32p, _f32p, _u32p, ctypes.c_uint32, _f32p, _i32p]
+        L.or_scene_destroy.argtypes = [ctypes.c_void_p]
+        L.or_ctx_create.restype = ctypes.c_void_p
+        L.or_ctx_create.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.or_ctx_destroy.argtypes = [ctypes.c_void_p]
+        L.or_ctx_set_cache_im.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.or_ctx_reset_history.argtypes = [ctypes.c_void_p]
+        L.or_render_frame.restype = ctypes.c_int
+        L.or_render_frame.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _f32p, ctypes.POINTER(FrameParams),
+                                      ctypes.c_uint32, _f32p, ctypes.POINTER(ctypes.c_uint64)]
+        L.or_get_gbuffer.argtypes = [ctypes.c_void_p, ctypes.c_int, _f32p]
+        L.or_get_reservoirs.argtypes = [ctypes.c_void_p, _f32p]
+        L.or_calc_I_M.restype = ctypes.c_float
+        L.or_calc_I_M.argtypes = [ctypes.c_float, ctypes.c_float]
+        L.or_ibeta.restype = ctypes.c_double
+        L.or_ibeta.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double]
+        L.or_camera_kat.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p]
+        L.or_reproject_kat.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _f32p, _i32p]
+        L.or_rng_u.restype = ctypes.c_float
+        L.or_rng_u.argtypes = [ctypes.c_uint32] * 5
+        L.or_scene_n_emissive.restype = ctypes.c_uint32
+        L.or_scene_n_emissive.argtypes = [ctypes.c_void_p]
+        L.or_scene_total_area.restype = ctypes.c_float
+        L.or_scene_total_area.argtypes = [ctypes.c_void_p]
+        L.or_scene_cdf.argtypes = [ctypes.c_void_p, _f32p, _f32p, _f32p]
+        L.or_trace_closest.argtypes = [ctypes.c_void_p, ctypes.c_int, _f32p, _f32p, ctypes.c_float, ctypes.c_float,
+                                       _f32p, _i32p]
+        L.or_trace_any.argtypes = [ctypes.c_void_p, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _i32p]
+        L.or_num_threads.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+class OracleScene:
+    def __init__(self, scene):
+        L = lib()
+        self.scene = scene
+        self._pos = np.ascontiguousarray(scene.positions, dtype=np.float32)
+        self._nrm = np.ascontiguousarray(scene.normals, dtype=np.float32)
+        self._mat = np.ascontiguousarray(scene.tri_material, dtype=np.uint32)
+        mf, mt = scene.material_arrays()
+        self._mf, self._mt = np.ascontiguousarray(mf), np.ascontiguousarray(mt)
+        self.h = L.or_scene_create(scene.n_tris, _ptr(self._pos), _ptr(self._nrm), _ptr(self._mat, _u32p),
+                                   len(scene.materials), _ptr(self._mf), _ptr(self._mt, _i32p))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.or_scene_destroy(self.h)
+            self.h = None
+
+    @property
+    def n_emissive(self):
+        return int(lib().or_scene_n_emissive(self.h))
+
+    def cdf(self):
+        n = self.n_emissive
+        c, p, a = (np.zeros(n, np.float32) for _ in range(3))
+        lib().or_scene_cdf(self.h, _ptr(c), _ptr(p), _ptr(a))
+        return c, p, a
+
+    def trace_closest(self, o, d, tnear=0.0, tfar=3.0e38):
+        o = np.ascontiguousarray(o, np.float32)
+        d = np.ascontiguousarray(d, np.float32)
+        n = o.shape[0]
+        t = np.zeros(n, np.float32)
+        prim = np.zeros(n, np.int32)
+        lib().or_trace_closest(self.h, n, _ptr(o), _ptr(d), tnear, tfar, _ptr(t), _ptr(prim, _i32p))
+        return t, prim
+
+    def trace_any(self, o, d, tnear, tfar):
+        o = np.ascontiguousarray(o, np.float32)
+        d = np.ascontiguousarray(d, np.float32)
+        tn = np.ascontiguousarray(tnear, np.float32)
+        tf = np.ascontiguousarray(tfar, np.float32)
+        n = o.shape[0]
+        hit = np.zeros(n, np.int32)
+        lib().or_trace_any(self.h, n, _ptr(o), _ptr(d), _ptr(tn), _ptr(tf), _ptr(hit, _i32p))
+        return hit
+
+
+class OracleRenderer:
+    """Mirror of the product's frame API over the oracle: render(frame) -> framebuffer."""
+
+    def __init__(self, width, height, cache_im=True):
+        self.W, self.H = width, height
+        self.h = lib().or_ctx_create(width, height)
+        lib().or_ctx_set_cache_im(self.h, 1 if cache_im else 0)
+        self.rays = 0
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.or_ctx_destroy(self.h)
+            self.h = None
+
+    def reset_history(self):
+        lib().or_ctx_reset_history(self.h)
+
+    def render(self, oscene: OracleScene, camera, params, frame_index=0):
+        out = np.zeros((self.H, self.W, 3), np.float32)
+        cam = np.ascontiguousarray(camera.as_array() if hasattr(camera, "as_array") else camera, np.float32)
+        rays = ctypes.c_uint64(0)
+        rc = lib().or_render_frame(self.h, oscene.h, _ptr(cam), ctypes.byref(params), frame_index, _ptr(out),
+                                   ctypes.byref(rays))
+        if rc != 0:
+            raise RuntimeError(f"or_render_frame failed: {rc}")
+        self.rays = int(rays.value)
+        return out
+
+    def gbuffer(self, prev=False):
+        out = np.zeros((self.H, self.W, 19), np.float32)
+        lib().or_get_gbuffer(self.h, 1 if prev else 0, _ptr(out))
+        return out
+
+    def reservoirs(self):
+        out = np.zeros((self.H, self.W, 12), np.float32)
+        lib().or_get_reservoirs(self.h, _ptr(out))
+        return out
