@@ -63,7 +63,7 @@ struct rs_context {
     rs_frame_params P = {};
     rs_tile_desc tile = {};
     int ra = 0, rb = 1, rcur = 0, last = 2;
-    bool temporal_ran = false, spatial_ran = false, shade_fused = false;
+    bool temporal_ran = false, spatial_ran = false, shade_fused = false, ev_temporal = false;
 };
 
 // --------------------------------------------------------------------------- helpers
@@ -393,7 +393,7 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     const bool temporal = P->do_temporal && c->frames > 0;
     const bool spatial = P->do_spatial && P->spatial_passes > 0;
     c->shade_fused = !P->do_visibility_pass && !temporal && !spatial;
-    c->temporal_ran = c->spatial_ran = false;
+    c->temporal_ran = c->spatial_ran = c->ev_temporal = false;
     const DevScene S = s->dev();
     HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->stream));
     HIPCHK(c, hipEventRecord(c->ev[EV_BEGIN], c->stream));
@@ -440,7 +440,10 @@ extern "C" int rs_tile_temporal(rs_context* c) {
         c->rcur = c->rb;
         c->temporal_ran = true;
     }
-    HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->stream));
+    if (!c->ev_temporal) {
+        HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->stream));
+        c->ev_temporal = true;
+    }
     return RS_OK;
 }
 
@@ -451,6 +454,10 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
     if (c->P.do_temporal && c->frames > 0 && !c->temporal_ran) {
         int rc = rs_tile_temporal(c);
         if (rc) return rc;
+    }
+    if (!c->ev_temporal) {
+        HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->stream));
+        c->ev_temporal = true;
     }
     const DevScene S = c->scene->dev();
     int dst = (c->rcur == c->ra) ? c->rb : c->ra;
@@ -473,7 +480,10 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
         int rc = rs_tile_temporal(c);
         if (rc) return rc;
     }
-    if (!c->temporal_ran) HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->stream));
+    if (!c->ev_temporal) {
+        HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->stream));
+        c->ev_temporal = true;
+    }
     if (!c->spatial_ran) HIPCHK(c, hipEventRecord(c->ev[EV_SPATIAL], c->stream));
     if (!c->shade_fused) {
         const DevScene S = c->scene->dev();
