@@ -510,8 +510,7 @@ typedef struct {
     uint64_t frames;          /* frameCtr (pg/simpleguidx11.h:101) */
     int cache_im;             /* 1: cache calc_I_M per pixel (speed only; identical values) */
     float* im_cache[2];       /* 1/calc_I_M per pixel for Phong-dispatched surfaces */
-    int rays_closest_pad;
-    uint64_t rays;
+    void* tile;               /* or_tile_state, allocated on first use */
 } or_ctx;
 
 or_ctx* or_ctx_create(int W, int H) {
@@ -524,8 +523,10 @@ or_ctx* or_ctx_create(int W, int H) {
     c->cache_im = 1;
     return c;
 }
+static void tile_release(or_ctx* c);
 void or_ctx_destroy(or_ctx* c) {
     if (!c) return;
+    tile_release(c);
     for (int i = 0; i < 2; ++i) { free(c->g[i]); free(c->im_cache[i]); }
     for (int i = 0; i < 3; ++i) free(c->r[i]);
     free(c);
@@ -568,6 +569,7 @@ typedef struct {
     const or_scene* s; or_ctx* c; const or_params* P; uint32_t frame;
     const or_gbe* G; const or_gbe* Gp; const or_gcam* gc; const or_gcam* gcp;
     const float* im; const float* imp;
+    int gy0, gy1;             /* G-buffer rows available (tile band + margin) */
 } fctx;
 
 /* Intersection::testOcclusion (pg/Intersection.h:43-60) */
@@ -919,6 +921,8 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             const or_res* pr = &Rl[p];       /* previous reservoir read at the CURRENT pixel (:641) */
             int qx, qy;
             if (!reproject(F->gcp, cur->pos, W, H, &qx, &qy)) { Rw[p] = *cr; continue; }
+            /* tile mode: a reprojection outside the G-buffer margin counts as failed (full frame: never) */
+            if (qy < F->gy0 || qy >= F->gy1) { Rw[p] = *cr; continue; }
             size_t q = (size_t)qy * W + qx;
             const or_gbe* prev = &F->Gp[q];
             float cd = len(sub(cur->pos, ccam));
@@ -928,6 +932,7 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             const or_gbe* pac = &F->Gp[p];
             int fx, fy;
             if (!reproject(F->gc, pac->pos, W, H, &fx, &fy)) { Rw[p] = *cr; continue; }
+            if (fy < F->gy0 || fy >= F->gy1) { Rw[p] = *cr; continue; }
             const or_gbe* fw = &F->G[(size_t)fy * W + fx];
             float cdp = len(sub(pac->pos, pcam));
             float pdp = len(sub(fw->pos, ccam));
@@ -1110,49 +1115,119 @@ static void pass_shade(fctx* F, const or_res* Rr, float* out, int y0, int y1, ui
     *rays += rc;
 }
 
-/* SimpleGuiDX11::produceRestir (pg/simpleguidx11.cpp:359-487) for one frame.
- * cam7 = {eye.xyz, at.xyz, fov_y_deg}; out_rgb = W*H*3 floats (frame_data). */
-int or_render_frame(or_ctx* c, const or_scene* s, const float* cam7, const or_params* P,
-                    uint32_t frame_index, float* out_rgb, uint64_t* rays_out) {
+/* ------------------------------------------------------------------ frame / tile driver
+ * SimpleGuiDX11::produceRestir (pg/simpleguidx11.cpp:359-487) split into the stages a row band of a
+ * tile-sharded frame runs (same stages as the HIP product's rs_tile_* C ABI):
+ *   begin    : G-buffer rows [y0-margin, y1+margin), initial RIS (+ visibility) rows [y0, y1)
+ *   halo     : the caller exchanges reservoir rows [y0-halo, y0) / [y1, y1+halo) between stages
+ *   temporal : rows [y0, y1);  spatial(p): rows [y0, y1);  finish: shade rows [y0, y1), swap history */
+typedef struct {
+    int active, y0, y1, halo, ra, rb, rcur, last, temporal_ran;
+    or_params P; fctx F; or_cam cam; uint64_t rays;
+} or_tile_state;
+static or_tile_state* tile_of(or_ctx* c) {
+    if (!c->tile) c->tile = calloc(1, sizeof(or_tile_state));
+    return (or_tile_state*)c->tile;
+}
+static void tile_release(or_ctx* c) { free(c->tile); c->tile = NULL; }
+
+int or_tile_begin(or_ctx* c, const or_scene* s, const float* cam7, const or_params* P, uint32_t frame_index,
+                  int y0, int y1, int margin, int halo) {
     int W = c->W, H = c->H;
     /* useSkybox needs the equirect sky (pg/SphericalMap.cpp:10-14), whose HDR is a missing
        blob in the reference checkout: only the background-colour miss path is restated. */
     if (P->use_skybox) return -2;
-    or_cam cam = make_cam(cam7, W, H);
+    if (y0 < 0 || y1 > H || y0 >= y1 || margin < 0 || halo < 0 || halo > margin) return -1;
+    or_tile_state* T = tile_of(c);
+    if (!T) return -1;
+    T->P = *P; T->y0 = y0; T->y1 = y1; T->halo = halo; T->rays = 0;
+    T->cam = make_cam(cam7, W, H);
     /* G-buffer ping-pong instead of gBufferLastFrame.setDataFrom (:480) */
     int gcur = c->gcur ^ 1, gprev = c->gcur;
-    c->gc[gcur].pos = cam.eye; c->gc[gcur].view = cam.view; c->gc[gcur].inv_view = cam.inv_view;
-    c->gc[gcur].focal = cam.focal;
-    fctx F;
-    F.s = s; F.c = c; F.P = P; F.frame = frame_index;
-    F.G = c->g[gcur]; F.Gp = c->g[gprev]; F.gc = &c->gc[gcur]; F.gcp = &c->gc[gprev];
-    F.im = c->im_cache[gcur]; F.imp = c->im_cache[gprev];
-    uint64_t rays = 0;
-    pass_gbuffer(&F, &cam, c->g[gcur], c->im_cache[gcur], 0, H, &rays);
-
+    c->gc[gcur].pos = T->cam.eye; c->gc[gcur].view = T->cam.view; c->gc[gcur].inv_view = T->cam.inv_view;
+    c->gc[gcur].focal = T->cam.focal;
+    fctx* F = &T->F;
+    F->s = s; F->c = c; F->P = &T->P; F->frame = frame_index;
+    F->G = c->g[gcur]; F->Gp = c->g[gprev]; F->gc = &c->gc[gcur]; F->gcp = &c->gc[gprev];
+    F->im = c->im_cache[gcur]; F->imp = c->im_cache[gprev];
+    F->gy0 = y0 - margin < 0 ? 0 : y0 - margin;
+    F->gy1 = y1 + margin > H ? H : y1 + margin;
+    pass_gbuffer(F, &T->cam, c->g[gcur], c->im_cache[gcur], F->gy0, F->gy1, &T->rays);
     /* reservoir buffer choice: never overwrite R_last before the temporal pass */
-    int last = c->r_last;
-    int a = (last + 1) % 3, b = (last + 2) % 3;
-    pass_initial(&F, c->r[a], 0, H, &rays);
-    if (P->do_visibility_pass) pass_visibility(&F, c->r[a], 0, H, &rays);
-    int cur = a;
-    if (P->do_temporal && c->frames > 0) {
-        pass_temporal(&F, c->r[cur], c->r[last], c->r[b], 0, H, &rays);
-        cur = b;
-    }
-    if (P->do_spatial) {
-        for (int i = 0; i < P->spatial_passes; ++i) {
-            int dst = (cur == a) ? b : a;   /* after temporal R_last is free to reuse, but a/b suffice */
-            pass_spatial(&F, c->r[cur], c->r[dst], i, 0, H, &rays);
-            cur = dst;
-        }
-    }
-    pass_shade(&F, c->r[cur], out_rgb, 0, H, &rays);
-    c->r_last = cur;
+    T->last = c->r_last;
+    T->ra = (T->last + 1) % 3; T->rb = (T->last + 2) % 3;
+    pass_initial(F, c->r[T->ra], y0, y1, &T->rays);
+    if (P->do_visibility_pass) pass_visibility(F, c->r[T->ra], y0, y1, &T->rays);
+    T->rcur = T->ra;
+    T->temporal_ran = 0;
+    T->active = 1;
     c->gcur = gcur;
-    c->frames++;
-    if (rays_out) *rays_out = rays;
     return 0;
+}
+
+/* which: 0 rows [y0-halo, y0), 1 rows [y1, y1+halo), 2 rows [y0, y0+halo), 3 rows [y1-halo, y1)
+   of the current reservoir buffer (48 B per pixel); NULL when outside the frame */
+int or_tile_halo_ptr(or_ctx* c, int which, void** ptr, size_t* bytes) {
+    or_tile_state* T = tile_of(c);
+    if (!T || !T->active) return -1;
+    int h = T->halo, r0;
+    switch (which) {
+        case 0: r0 = T->y0 - h; break;
+        case 1: r0 = T->y1; break;
+        case 2: r0 = T->y0; break;
+        case 3: r0 = T->y1 - h; break;
+        default: return -1;
+    }
+    if (h == 0 || r0 < 0 || r0 + h > c->H) { *ptr = NULL; *bytes = 0; return 0; }
+    *ptr = (void*)(c->r[T->rcur] + (size_t)r0 * c->W);
+    *bytes = (size_t)h * c->W * sizeof(or_res);
+    return 0;
+}
+
+int or_tile_temporal(or_ctx* c) {
+    or_tile_state* T = tile_of(c);
+    if (!T || !T->active) return -1;
+    if (T->P.do_temporal && c->frames > 0 && !T->temporal_ran) {
+        pass_temporal(&T->F, c->r[T->rcur], c->r[T->last], c->r[T->rb], T->y0, T->y1, &T->rays);
+        T->rcur = T->rb;
+        T->temporal_ran = 1;
+    }
+    return 0;
+}
+
+int or_tile_spatial(or_ctx* c, int pass_index) {
+    or_tile_state* T = tile_of(c);
+    if (!T || !T->active) return -1;
+    if (!(T->P.do_spatial && pass_index >= 0 && pass_index < T->P.spatial_passes)) return 0;
+    or_tile_temporal(c);
+    int dst = (T->rcur == T->ra) ? T->rb : T->ra;
+    pass_spatial(&T->F, c->r[T->rcur], c->r[dst], pass_index, T->y0, T->y1, &T->rays);
+    T->rcur = dst;
+    return 0;
+}
+
+/* out_rgb: (y1-y0)*W*3 floats of the band */
+int or_tile_finish(or_ctx* c, float* out_rgb, uint64_t* rays_out) {
+    or_tile_state* T = tile_of(c);
+    if (!T || !T->active) return -1;
+    or_tile_temporal(c);
+    pass_shade(&T->F, c->r[T->rcur], out_rgb, T->y0, T->y1, &T->rays);
+    c->r_last = T->rcur;
+    c->frames++;
+    T->active = 0;
+    if (rays_out) *rays_out = T->rays;
+    return 0;
+}
+
+/* one full frame (no tiling); out_rgb = W*H*3 floats (frame_data) */
+int or_render_frame(or_ctx* c, const or_scene* s, const float* cam7, const or_params* P,
+                    uint32_t frame_index, float* out_rgb, uint64_t* rays_out) {
+    int rc = or_tile_begin(c, s, cam7, P, frame_index, 0, c->H, 0, 0);
+    if (rc) return rc;
+    or_tile_temporal(c);
+    if (P->do_spatial)
+        for (int i = 0; i < P->spatial_passes; ++i) or_tile_spatial(c, i);
+    return or_tile_finish(c, out_rgb, rays_out);
 }
 
 /* ------------------------------------------------------------------ dumps / KAT hooks */

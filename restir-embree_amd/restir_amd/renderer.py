@@ -150,6 +150,7 @@ class Renderer:
         if rc != RS_OK:
             raise RestirError(f"rs_context_create failed ({rc}): {self.lib.rs_last_error(None).decode()}")
         self.h = h
+        self.stream = stream            # hipStream_t the context renders on (None: its own stream)
         self.frame_data = np.zeros((self.H, self.W, 3), np.float32)
         self.last_times = PassTimes()
 

@@ -159,3 +159,54 @@ class OracleRenderer:
         out = np.zeros((self.H, self.W, 12), np.float32)
         lib().or_get_reservoirs(self.h, _ptr(out))
         return out
+
+
+class OracleTileBackend:
+    """Tile stages of the oracle (or_tile_*), same interface as restir_amd.distributed.GpuTileBackend,
+    so the distributed orchestration can be checked on CPU with gloo."""
+
+    def __init__(self, width, height):
+        L = lib()
+        vp = ctypes.c_void_p
+        L.or_tile_begin.argtypes = [vp, vp, _f32p, ctypes.POINTER(FrameParams), ctypes.c_uint32, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.or_tile_halo_ptr.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+        L.or_tile_temporal.argtypes = [vp]
+        L.or_tile_spatial.argtypes = [vp, ctypes.c_int]
+        L.or_tile_finish.argtypes = [vp, _f32p, ctypes.POINTER(ctypes.c_uint64)]
+        self.r = OracleRenderer(width, height)
+        self.W, self.H = width, height
+        self.last_times = None
+
+    def load_scene(self, scene):
+        return OracleScene(scene)
+
+    def begin(self, scene, camera, params, frame, y0, y1, margin, halo):
+        self.y0, self.y1 = y0, y1
+        self._params = params
+        cam = np.ascontiguousarray(camera.as_array() if hasattr(camera, "as_array") else camera, np.float32)
+        rc = lib().or_tile_begin(self.r.h, scene.h, _ptr(cam), ctypes.byref(params), frame, y0, y1, margin, halo)
+        if rc:
+            raise RuntimeError(f"or_tile_begin failed {rc}")
+
+    def halo_tensor(self, which):
+        import torch
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        lib().or_tile_halo_ptr(self.r.h, which, ctypes.byref(p), ctypes.byref(n))
+        if not p.value:
+            return None
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * n.value).from_address(p.value))
+        return torch.from_numpy(arr)
+
+    def temporal(self):
+        lib().or_tile_temporal(self.r.h)
+
+    def spatial(self, p):
+        lib().or_tile_spatial(self.r.h, p)
+
+    def finish(self, timed=False):
+        import torch
+        out = np.zeros((self.y1 - self.y0) * self.W * 3, np.float32)
+        rays = ctypes.c_uint64(0)
+        lib().or_tile_finish(self.r.h, _ptr(out), ctypes.byref(rays))
+        return torch.from_numpy(out)
