@@ -92,6 +92,9 @@ def main():
         sc, prm = scenes.cornell_many_lights(1024), metric_params()
     else:
         sc, prm = scenes.sponza_like(), c3_params()
+    # render on a dedicated torch stream shared with the library, so RCCL ops and the kernels of
+    # librestir_amd.so are ordered on one stream (torch's default stream has handle 0 = "none")
+    torch.cuda.set_stream(torch.cuda.Stream(device=local))
     stream = torch.cuda.current_stream().cuda_stream
 
     if world == 1:

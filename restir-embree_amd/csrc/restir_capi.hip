@@ -78,6 +78,14 @@ static int fail(rs_context* c, int code, const std::string& msg) {
         if (e_ != hipSuccess) return fail((c), RS_E_HIP, std::string(#x " -> ") + hipGetErrorString(e_)); \
     } while (0)
 
+// Every entry point: bind the context's device and drop any stale error another library (e.g. torch's
+// pointer-attribute queries) left in HIP's per-thread last-error slot, so the post-launch
+// hipGetLastError() checks only see errors of our own launches.
+static hipError_t enter(rs_context* c) {
+    (void)hipGetLastError();
+    return hipSetDevice(c->device);
+}
+
 // glm-semantics host maths for the camera (pg/camera.cpp:44-58, glm/ext/matrix_transform.inl:99-119,
 // glm/detail/func_matrix.inl:294-351)
 struct hv3 { float x, y, z; };
@@ -312,7 +320,7 @@ extern "C" int rs_scene_create(rs_context* c, const rs_mesh_desc* meshes, uint32
     if (!c || !out || (n_meshes && !meshes) || (n_materials && !materials))
         return fail(c, RS_E_INVALID, "rs_scene_create: null argument");
     *out = nullptr;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, enter(c));
     std::vector<float> pos, nrm;
     std::vector<uint32_t> tri_mat;
     for (uint32_t m = 0; m < n_meshes; ++m) {
@@ -327,7 +335,7 @@ extern "C" int rs_scene_create(rs_context* c, const rs_mesh_desc* meshes, uint32
 
 extern "C" int rs_scene_load_obj(rs_context* c, const char* path, rs_scene** out) {
     if (!c || !path || !out) return fail(c, RS_E_INVALID, "rs_scene_load_obj: null argument");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, enter(c));
     std::vector<float> pos, nrm;
     std::vector<uint32_t> tri_mat;
     std::vector<rs_material_desc> mats;
@@ -370,7 +378,7 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     if (tile->y0 < 0 || tile->y1 > c->H || tile->y0 >= tile->y1 || tile->margin < 0 || tile->halo < 0 ||
         tile->halo > tile->margin)
         return fail(c, RS_E_INVALID, "rs_tile_begin: bad tile (need 0<=y0<y1<=H, 0<=halo<=margin)");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, enter(c));
     c->scene = s; c->P = *P; c->tile = *tile;
     FrameConst& F = c->F;
     F.m_area = P->m_area; F.m_brdf = P->m_brdf; F.k = P->spatial_neighbors; F.spatial_passes = P->spatial_passes;
@@ -430,7 +438,7 @@ extern "C" int rs_tile_halo_ptr(rs_context* c, int which, void** dptr, size_t* b
 
 extern "C" int rs_tile_temporal(rs_context* c) {
     if (!c || !c->active) return fail(c, RS_E_INVALID, "rs_tile_temporal: no frame in flight");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, enter(c));
     if (c->P.do_temporal && c->frames > 0 && !c->temporal_ran) {
         const DevScene S = c->scene->dev();
         k_temporal<<<grid_rows(c->W, c->F.y0, c->F.y1), 256, 0, c->stream>>>(
@@ -450,7 +458,7 @@ extern "C" int rs_tile_temporal(rs_context* c) {
 extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
     if (!c || !c->active) return fail(c, RS_E_INVALID, "rs_tile_spatial: no frame in flight");
     if (!(c->P.do_spatial && pass_index >= 0 && pass_index < c->P.spatial_passes)) return RS_OK;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, enter(c));
     if (c->P.do_temporal && c->frames > 0 && !c->temporal_ran) {
         int rc = rs_tile_temporal(c);
         if (rc) return rc;
@@ -475,7 +483,7 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
 
 extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_times* t) {
     if (!c || !c->active) return fail(c, RS_E_INVALID, "rs_tile_finish: no frame in flight");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, enter(c));
     if (c->P.do_temporal && c->frames > 0 && !c->temporal_ran) {
         int rc = rs_tile_temporal(c);
         if (rc) return rc;
@@ -545,14 +553,14 @@ extern "C" int rs_reset_history(rs_context* c) {
 
 extern "C" int rs_synchronize(rs_context* c) {
     if (!c) return fail(nullptr, RS_E_INVALID, "rs_synchronize: null context");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, enter(c));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return RS_OK;
 }
 
 extern "C" int rs_dump_gbuffer(rs_context* c, int prev, float* out) {
     if (!c || !out) return fail(c, RS_E_INVALID, "rs_dump_gbuffer: null argument");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, enter(c));
     size_t n = (size_t)c->W * c->H;
     const GBuf& g = c->G[prev ? (c->gcur ^ 1) : c->gcur];
     std::vector<float4> a(n), b(n), d(n), e(n), f(n);
@@ -575,7 +583,7 @@ extern "C" int rs_dump_gbuffer(rs_context* c, int prev, float* out) {
 
 extern "C" int rs_dump_reservoirs(rs_context* c, float* out) {
     if (!c || !out) return fail(c, RS_E_INVALID, "rs_dump_reservoirs: null argument");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, enter(c));
     size_t n = (size_t)c->W * c->H;
     std::vector<float4> r(3 * n);
     HIPCHK(c, hipMemcpyAsync(r.data(), c->R[c->r_last], 3 * n * 16, hipMemcpyDeviceToHost, c->stream));
@@ -610,7 +618,7 @@ extern "C" int rs_debug_trace(rs_context* c, const rs_scene* s, uint32_t n, cons
                               const float* tnear, const float* tfar, int any_hit, float* t_out, int32_t* prim_out) {
     if (!c || !s || !o || !d || !tnear || !tfar || !t_out || !prim_out) return fail(c, RS_E_INVALID, "rs_debug_trace: null");
     if (n == 0) return RS_OK;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, enter(c));
     float *dd = nullptr;
     int32_t* dp = nullptr;
     size_t fl = (size_t)n * 9;   // o(3n) d(3n) tn(n) tf(n) t(n)

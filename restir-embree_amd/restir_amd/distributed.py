@@ -57,7 +57,7 @@ class GpuTileBackend:
         """Tensor views are consumed on torch's current stream; if the context renders on a stream of
         its own, wait for it (the bench creates contexts on torch's stream, so this is a no-op there)."""
         import torch
-        if self.r.stream != torch.cuda.current_stream().cuda_stream:
+        if self.r.stream is None or self.r.stream != torch.cuda.current_stream().cuda_stream:
             self.r.synchronize()
 
     def load_scene(self, scene):

@@ -150,7 +150,8 @@ class Renderer:
         if rc != RS_OK:
             raise RestirError(f"rs_context_create failed ({rc}): {self.lib.rs_last_error(None).decode()}")
         self.h = h
-        self.stream = stream            # hipStream_t the context renders on (None: its own stream)
+        # hipStream_t the context renders on; None (or 0, the legacy null stream) -> a stream of its own
+        self.stream = stream if stream else None
         self.frame_data = np.zeros((self.H, self.W, 3), np.float32)
         self.last_times = PassTimes()
 

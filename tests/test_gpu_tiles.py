@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 
 def _emulate(sc, W, H, prm, n_ranks, cams, margin):
     import torch
+    torch.cuda.set_stream(torch.cuda.Stream())      # a real (non-null) stream shared with the contexts
     st = torch.cuda.current_stream().cuda_stream
     bes = [GpuTileBackend(Renderer(W, H, stream=st)) for _ in range(n_ranks)]
     hs = [be.load_scene(sc) for be in bes]
