@@ -1,0 +1,125 @@
+// restir.hpp -- C++ host-side mirror of the reference's ReSTIR frame API over the C ABI (restir_c.h).
+//
+// The reference drives the hot path from C++ members of one object:
+//   Raytracer::LoadScene(std::string)        pg/raytracer.cpp:34-38
+//   SimpleGuiDX11::produceRestir(float t)    pg/simpleguidx11.cpp:359-487
+//   glm::vec3* frame_data                    pg/simpleguidx11.h:152
+//   ReSTIRIntegrator static knobs            pg/ReSTIRIntegrator.cpp:13-35 (M_Area, M_Brdf, ...)
+//   per-pass timers                          pg/simpleguidx11.h:120-127 (gBUfferFillDuration, ...)
+// restir::Renderer keeps those names so a reference caller switches by replacing the object type.
+// Errors become restir::Error exceptions on the C++ side (the reference throws std::runtime_error
+// for Embree errors, pg/tutorials.cpp:6-24); nothing throws across the C ABI itself.
+#pragma once
+#include "restir_c.h"
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace restir {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+inline void check(int rc, const rs_context* ctx) {
+    if (rc != RS_OK) throw Error(rc, std::string("librestir_amd: ") + rs_last_error(ctx));
+}
+
+// ReSTIRIntegrator's statics + ReSTIR's private RenderParams, with the reference defaults
+// (pg/ReSTIRIntegrator.cpp:13-33, pg/RenderParams.h:5-17); useSkybox off (missing sky HDR).
+struct Params : rs_frame_params {
+    enum SpatialWeightCalculation { CONSTANT = 0, CONSTANT_DEBIAS_CONTRIB = 1, CONSTANT_DEBIAS_Z_TERM = 2,
+                                    BALANCE_HEURISTIC = 3, PAIRWISE_MIS = 4 };
+    Params() {
+        std::memset(static_cast<rs_frame_params*>(this), 0, sizeof(rs_frame_params));
+        m_area = 1; m_brdf = 1; spatial_neighbors = 5; spatial_passes = 1; confidence_cap = 20;
+        spatial_radius = 30.0f; min_normal_similarity = 0.85f; max_depth_difference = 0.2f;
+        spatial_mis = CONSTANT; use_skybox = 0; bg_color[0] = bg_color[1] = bg_color[2] = 0.5f;
+        tnear_offset = 0.01f; tfar_offset = 0.001f; normal_offset = 0.001f; seed = 123;
+    }
+};
+
+struct Camera : rs_camera {   // Camera(width, height, fov_y, view_from, view_at), Z-up
+    Camera(float ex = 0, float ey = 0, float ez = 0, float ax = 0, float ay = 0, float az = 0, float fov = 40.0f) {
+        eye[0] = ex; eye[1] = ey; eye[2] = ez; at[0] = ax; at[1] = ay; at[2] = az; fov_y_deg = fov;
+    }
+    void setPosition(float x, float y, float z) { eye[0] = x; eye[1] = y; eye[2] = z; }   // pg/camera.cpp:60-64
+    void setViewAt(float x, float y, float z) { at[0] = x; at[1] = y; at[2] = z; }        // pg/camera.h:31-35
+    void setFOV(float deg) { fov_y_deg = deg; }                                            // pg/camera.cpp:81-84
+};
+
+class Renderer {
+public:
+    Renderer(int width, int height, int hip_device = 0, void* hip_stream = nullptr) : width_(width), height_(height) {
+        check(rs_context_create(hip_device, width, height, hip_stream, &ctx_), nullptr);
+        frame_.assign((size_t)width * height * 3, 0.0f);
+    }
+    ~Renderer() {
+        if (scene_) rs_scene_destroy(scene_);
+        if (ctx_) rs_context_destroy(ctx_);
+    }
+    Renderer(const Renderer&) = delete;
+    Renderer& operator=(const Renderer&) = delete;
+
+    // Raytracer::LoadScene(file): OBJ/MTL (Pc/Kd/Ks/Ke/Ns) -> GPU LBVH + emissive CDF
+    void LoadScene(const std::string& obj_path) {
+        rs_scene* s = nullptr;
+        check(rs_scene_load_obj(ctx_, obj_path.c_str(), &s), ctx_);
+        replace_scene(s);
+    }
+    // Scene from in-memory meshes (what ModelLoader hands Embree, pg/ModelLoader.cpp:232-317)
+    void LoadScene(const std::vector<rs_mesh_desc>& meshes, const std::vector<rs_material_desc>& materials) {
+        rs_scene* s = nullptr;
+        check(rs_scene_create(ctx_, meshes.data(), (uint32_t)meshes.size(), materials.data(),
+                              (uint32_t)materials.size(), &s), ctx_);
+        replace_scene(s);
+    }
+
+    // SimpleGuiDX11::produceRestir(t): one frame with the current camera_ and params; frame_data()
+    // then holds the linear-HDR framebuffer, the duration members the per-pass device times.
+    void produceRestir(float t = 0.0f) {
+        (void)t;
+        if (!scene_) throw Error(RS_E_INVALID, "produceRestir: no scene loaded");
+        rs_pass_times pt{};
+        check(rs_render_frame(ctx_, scene_, &camera_, &params, frameCtr, frame_.data(), &pt), ctx_);
+        gBUfferFillDuration = pt.gbuffer_initial_ms;   // G-buffer fill and initial RIS run fused
+        initialCandidatesGenDuration = 0.0f;
+        visibilityPassDuration = pt.visibility_ms;
+        temporalReusePassDuration = pt.temporal_ms;
+        spatialReusePassDuration = pt.spatial_ms;
+        shadingPassDuration = pt.shade_ms;
+        bufferCopyDuration = 0.0f;                      // history is a pointer swap
+        totalFrameDuration = pt.total_ms;
+        raysTraced = pt.rays;
+        ++frameCtr;
+    }
+    void resetHistory() { check(rs_reset_history(ctx_), ctx_); }
+
+    const float* frame_data() const { return frame_.data(); }    // W*H*3, row-major, y=0 top
+    int width() const { return width_; }
+    int height() const { return height_; }
+    rs_context* handle() { return ctx_; }
+
+    Camera camera_;
+    Params params;
+    uint32_t frameCtr = 0;
+    float gBUfferFillDuration = 0, initialCandidatesGenDuration = 0, visibilityPassDuration = 0,
+          temporalReusePassDuration = 0, spatialReusePassDuration = 0, shadingPassDuration = 0,
+          bufferCopyDuration = 0, totalFrameDuration = 0;
+    uint64_t raysTraced = 0;
+
+private:
+    void replace_scene(rs_scene* s) {
+        if (scene_) rs_scene_destroy(scene_);
+        scene_ = s;
+    }
+    int width_, height_;
+    rs_context* ctx_ = nullptr;
+    rs_scene* scene_ = nullptr;
+    std::vector<float> frame_;
+};
+
+}  // namespace restir
