@@ -12,6 +12,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <algorithm>
 
 namespace rs {
 int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes, float4** d_tris,
@@ -30,10 +31,11 @@ struct rs_scene {
     float* d_pos = nullptr;
     float4 *d_nodes = nullptr, *d_tris = nullptr, *d_tri_nrm = nullptr, *d_mats = nullptr, *d_emis = nullptr;
     float* d_cdf = nullptr;
+    int* d_cdf_guide = nullptr;
     float build_ms = 0.0f;
     DevScene dev() const {
         DevScene S;
-        S.nodes = d_nodes; S.tris = d_tris; S.tri_nrm = d_tri_nrm; S.mats = d_mats; S.emis = d_emis; S.cdf = d_cdf;
+        S.nodes = d_nodes; S.tris = d_tris; S.tri_nrm = d_tri_nrm; S.mats = d_mats; S.emis = d_emis; S.cdf = d_cdf; S.cdf_guide = d_cdf_guide;
         S.n_nodes = n_nodes; S.n_tris = n_tris; S.n_emis = n_emis; S.n_mats = n_mats;
         return S;
     }
@@ -299,6 +301,16 @@ static int scene_from_arrays(rs_context* c, const std::vector<float>& pos, const
     hipMemcpyAsync(s->d_emis, em.data(), em.size() * sizeof(float4), hipMemcpyHostToDevice, st);
     if (hipMalloc(&s->d_cdf, cdf.size() * sizeof(float)) != hipSuccess) return bail("hipMalloc(cdf) failed");
     hipMemcpyAsync(s->d_cdf, cdf.data(), cdf.size() * sizeof(float), hipMemcpyHostToDevice, st);
+    {   // guide table for the exact lower_bound: guide[j] = lower_bound(cdf, j / kCdfGuide)
+        std::vector<int> guide(kCdfGuide + 1);
+        for (int j = 0; j <= kCdfGuide; ++j) {
+            float key = (float)j / (float)kCdfGuide;
+            guide[j] = (int)(std::lower_bound(cdf.begin(), cdf.begin() + ne, key) - cdf.begin());
+        }
+        if (hipMalloc(&s->d_cdf_guide, guide.size() * sizeof(int)) != hipSuccess) return bail("hipMalloc(guide) failed");
+        hipMemcpyAsync(s->d_cdf_guide, guide.data(), guide.size() * sizeof(int), hipMemcpyHostToDevice, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return bail("guide upload failed");
+    }
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
     hipEventRecord(e0, st);
@@ -347,7 +359,7 @@ extern "C" int rs_scene_load_obj(rs_context* c, const char* path, rs_scene** out
 extern "C" void rs_scene_destroy(rs_scene* s) {
     if (!s) return;
     if (s->ctx) hipSetDevice(s->ctx->device);
-    void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf};
+    void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide};
     for (void* p : ptrs) if (p) hipFree(p);
     delete s;
 }

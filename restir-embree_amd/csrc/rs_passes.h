@@ -14,6 +14,14 @@
 #pragma once
 #include "rs_scene.h"
 
+// waves per SIMD the ray-tracing kernels are register-budgeted for (launch_bounds 2nd argument)
+#ifndef RS_INITIAL_WAVES
+#define RS_INITIAL_WAVES 4
+#endif
+#ifndef RS_SPATIAL_WAVES
+#define RS_SPATIAL_WAVES 4
+#endif
+
 namespace rs {
 
 struct FrameConst {
@@ -119,7 +127,11 @@ __device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameCons
 __device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameConst& F, const GElem& g, vec3 cam,
                                               Rng& rng, float& W_out, float& mis_out) {
     float ksi = rng.range(0.0f, 1.0f);
-    uint32_t lo = 0, n = S.n_emis;          // std::lower_bound(cdf2, ksi)
+    // std::lower_bound(cdf2, ksi), narrowed by the guide table: ksi*kCdfGuide is exact (ksi = k*2^-24),
+    // and lower_bound(j/G) <= lower_bound(ksi) <= lower_bound((j+1)/G) for j = floor(ksi*G)
+    uint32_t j = (uint32_t)(ksi * (float)kCdfGuide);
+    uint32_t lo = (uint32_t)S.cdf_guide[j], n = (uint32_t)S.cdf_guide[j + 1] + 1u - lo;
+    if (lo + n > S.n_emis) n = S.n_emis - lo;
     while (n > 0) {
         uint32_t h = n >> 1;
         if (S.cdf[lo + h] < ksi) { lo = lo + h + 1; n = n - h - 1; } else n = h;
@@ -220,7 +232,7 @@ __device__ __forceinline__ void store_rgb(float* fb, size_t p, vec3 c) {
     fb[3 * p] = c.x; fb[3 * p + 1] = c.y; fb[3 * p + 2] = c.z;
 }
 
-__global__ void __launch_bounds__(256) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G, ResBuf Rw,
+__global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G, ResBuf Rw,
                                                          float* fb, int fuse_shade, Counters* C) {
     int x, y;
     uint32_t rays = 0, prim = 0;
@@ -237,6 +249,34 @@ __global__ void __launch_bounds__(256) k_gbuffer_initial(DevScene S, FrameConst 
         }
     }
     count_rays(C, rays + prim, prim);
+}
+
+// G-buffer fill alone (rows [gy0, gy1)); the initial RIS then runs as k_initial
+__global__ void __launch_bounds__(256) k_gbuffer(DevScene S, FrameConst F, GBuf G, Counters* C) {
+    int x, y;
+    uint32_t prim = 0;
+    if (pixel_of(F.gy0, F.gy1, F.W, x, y)) {
+        size_t p = (size_t)y * F.W + x;
+        G.store(p, gbuffer_fill(S, F, x, y));
+        prim = 1;
+    }
+    count_rays(C, prim, prim);
+}
+
+// initialRenderPass alone: reads the pixel's G record written by k_gbuffer
+__global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_initial(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb,
+                                                 int fuse_shade, Counters* C) {
+    int x, y;
+    uint32_t rays = 0;
+    if (pixel_of(F.y0, F.y1, F.W, x, y)) {
+        size_t p = (size_t)y * F.W + x;
+        GElem g = G.load(p);
+        vec3 f;
+        Res r = initial_ris(S, F, g, (uint32_t)p, f, rays);
+        Rw.store(p, r);
+        if (fuse_shade) store_rgb(fb, p, shade_px(r, f, g.le));
+    }
+    count_rays(C, rays, 0);
 }
 
 // visibilityPass (pg/ReSTIRIntegrator.cpp:302-312).  Invalid samples always carry W == 0 already,
@@ -360,7 +400,7 @@ __device__ __forceinline__ size_t list_px(const FrameConst& F, const Rng& rng, u
 }
 
 // spatialReusePass (pg/ReSTIRIntegrator.cpp:316-542); shade fused when this is the last pass.
-__global__ void __launch_bounds__(256) k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw,
+__global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw,
                                                  int pass_idx, int fuse_shade, float* fb, Counters* C) {
     int x, y;
     uint32_t rays = 0;

@@ -12,6 +12,14 @@
 #pragma once
 #include "rs_device.h"
 
+#ifndef RS_TRAV_ATTR
+#if defined(RS_TRAV_INLINE) && RS_TRAV_INLINE
+#define RS_TRAV_ATTR __device__ __forceinline__
+#else
+#define RS_TRAV_ATTR __device__ __noinline__
+#endif
+#endif
+
 namespace rs {
 
 struct DevScene {
@@ -22,8 +30,10 @@ struct DevScene {
     const float4* emis;       // 8 per emissive triangle: p0,p1,p2 (w: pick_pdf, inv_area, pdf_brdf_area),
                               //   n0, n1, n2, le, (area, 0, 0, 0)
     const float* cdf;         // cumulative normalised area (TriangleCDF::cdf2)
+    const int* cdf_guide;     // kCdfGuide+1 entries: lower_bound(cdf, j / kCdfGuide)
     uint32_t n_nodes, n_tris, n_emis, n_mats;
 };
+constexpr int kCdfGuide = 1024;
 
 // Moller-Trumbore, fixed op order (identical to oracle/restir_oracle.c tri_hit)
 __device__ __forceinline__ bool tri_test(float4 A, float4 B, float4 C, vec3 o, vec3 d, float tnear,
@@ -56,7 +66,7 @@ __device__ __forceinline__ bool box_test(float4 a, float4 b, vec3 o, vec3 inv, f
 }
 
 // rtcOccluded1 semantics (pg/Intersection.h:43-60): any hit with t in [tnear, tfar]
-__device__ __noinline__ bool occluded_ray(const DevScene& S, vec3 o, vec3 d, float tnear, float tfar) {
+RS_TRAV_ATTR bool occluded_ray(const DevScene& S, vec3 o, vec3 d, float tnear, float tfar) {
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     uint32_t i = 0;
     const uint32_t n = S.n_nodes;
@@ -86,7 +96,7 @@ __device__ __noinline__ bool occluded_ray(const DevScene& S, vec3 o, vec3 d, flo
 struct Hit { float t, u, v; int prim; };
 
 // rtcIntersect1 semantics: closest hit in [tnear, tfar]; ties broken by the smaller triangle index
-__device__ __noinline__ Hit closest_ray(const DevScene& S, vec3 o, vec3 d, float tnear, float tfar) {
+RS_TRAV_ATTR Hit closest_ray(const DevScene& S, vec3 o, vec3 d, float tnear, float tfar) {
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
     uint32_t i = 0;

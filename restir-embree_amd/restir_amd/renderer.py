@@ -70,6 +70,7 @@ def load_library(path: str = LIB_PATH):
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("RESTIR_LIB", path)     # A/B builds of the same ABI (scripts/ab_variants.sh)
     if not os.path.exists(path):
         raise RestirError(f"{path} not found: build it with `make -C restir-embree_amd` (hipcc, gfx950)")
     L = ctypes.CDLL(path)
