@@ -613,16 +613,21 @@ extern "C" int rs_dump_reservoirs(rs_context* c, float* out) {
 // --------------------------------------------------------------------------- test hook
 __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const float* d, const float* tn, const float* tf,
                               int any, float* t_out, int32_t* prim_out) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    // mode (`any`): 0 closest / 1 any-hit with the lockstep wave traversal the passes use,
+    //               2 closest / 3 any-hit with the per-lane traversal
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = i0 < n;
+    const uint32_t i = act ? i0 : n - 1;
     vec3 O = mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), D = mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    if (any) {
-        prim_out[i] = occluded_ray(S, O, D, tn[i], tf[i]) ? 1 : 0;
-        t_out[i] = 0.0f;
+    if (any == 1 || any == 3) {
+        bool occ = any == 1 ? occluded_wave(S, act, O, D, tn[i], tf[i])
+                            : (act ? occluded_ray(S, O, D, tn[i], tf[i]) : false);
+        if (act) { prim_out[i] = occ ? 1 : 0; t_out[i] = 0.0f; }
     } else {
-        Hit h = closest_ray(S, O, D, tn[i], tf[i]);
-        prim_out[i] = h.prim;
-        t_out[i] = h.prim >= 0 ? h.t : -1.0f;
+        Hit h;
+        if (any == 0) h = closest_wave(S, act, O, D, tn[i], tf[i]);
+        else { h.prim = -1; h.t = 0; if (act) h = closest_ray(S, O, D, tn[i], tf[i]); }
+        if (act) { prim_out[i] = h.prim; t_out[i] = h.prim >= 0 ? h.t : -1.0f; }
     }
 }
 

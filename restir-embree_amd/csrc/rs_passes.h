@@ -11,6 +11,11 @@
 //                       (:449-472): the shaded f is the selected candidate's (already visibility-
 //                       tested) f, cached, so shading costs no extra shadow ray
 //   k_shade           : stand-alone shade loop when no reuse pass can carry it
+//
+// Convergence: every ray query is made by the whole wave (lanes without a ray pass active=false), so
+// the lockstep traversal (rs_scene.h) sees a full EXEC mask.  Per-pixel early-outs of the reference
+// (emissive pixel, invalid sample, zero contribution) are therefore predicates, not branches; lanes
+// outside the image work on a clamped pixel and store nothing.
 #pragma once
 #include "rs_scene.h"
 
@@ -52,27 +57,32 @@ __device__ __forceinline__ void count_rays(Counters* C, uint32_t rays, uint32_t 
     }
 }
 
-// 8x8 tile per wave, 16x16 per workgroup, rows [ya, yb)
+// 8x8 tile per wave, 16x16 per workgroup, rows [ya, yb).  Returns whether the pixel exists; x/y are
+// clamped into the image so out-of-range lanes can run the (convergent) code on a valid pixel.
 __device__ __forceinline__ bool pixel_of(int ya, int yb, int W, int& x, int& y) {
     int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     y = ya + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    return x < W && y < yb;
+    bool in = x < W && y < yb;
+    x = x < W ? x : W - 1;
+    y = y < yb ? y : yb - 1;
+    return in;
 }
 
 // Intersection::testOcclusion (pg/Intersection.h:43-60): from the surface point, no normal offset
-__device__ __forceinline__ bool occluded(const DevScene& S, const FrameConst& F, vec3 from, vec3 to, uint32_t& rays) {
+__device__ __forceinline__ bool occluded(const DevScene& S, const FrameConst& F, bool active, vec3 from, vec3 to,
+                                         uint32_t& rays) {
     float dist = length(to - from);
     vec3 dir = normalize(to - from);
-    rays++;
-    return occluded_ray(S, from, dir, FLT_MIN + F.tnear_off, dist - F.tfar_off);
+    rays += active ? 1u : 0u;
+    return trace_any(S, active, from, dir, FLT_MIN + F.tnear_off, dist - F.tfar_off);
 }
 
-// ReSTIRIntegrator::evaluateF (pg/ReSTIRIntegrator.cpp:185-211).  The shadow ray is skipped when
-// L_i*f_r*G is exactly zero in every channel (the result is 0 whatever V is).
+// ReSTIRIntegrator::evaluateF (pg/ReSTIRIntegrator.cpp:185-211) for the lanes with `alive`.  The
+// shadow ray is skipped when L_i*f_r*G is exactly zero in every channel (0 whatever V is).
 __device__ __forceinline__ vec3 evaluate_f(const DevScene& S, const FrameConst& F, const Sample& s, vec3 cam,
-                                           const GElem& g, bool test_vis, uint32_t& rays) {
-    if (!smp_valid(s) || g.le.x > 0 || g.le.y > 0 || g.le.z > 0) return mk(0, 0, 0);
+                                           const GElem& g, bool test_vis, bool alive, uint32_t& rays) {
+    const bool ok = alive && smp_valid(s) && !(g.le.x > 0 || g.le.y > 0 || g.le.z > 0);
     vec3 ld = s.p - g.pos;
     float r2 = dot(ld, ld);
     ld = normalize(ld);
@@ -80,11 +90,11 @@ __device__ __forceinline__ vec3 evaluate_f(const DevScene& S, const FrameConst& 
     float cY = fabsf(dot(-ld, s.n));
     float G = cI * cY / r2;
     vec3 L = (s.li * eval_brdf(g, cam, ld)) * G;
-    if (test_vis && !(L.x == 0.0f && L.y == 0.0f && L.z == 0.0f)) {
-        bool vis = !occluded(S, F, g.pos, s.p, rays);
-        L = L * (float)vis;
-    }
-    return L;
+    const bool need = ok && test_vis && !(L.x == 0.0f && L.y == 0.0f && L.z == 0.0f);
+    bool occ = false;
+    if (test_vis) occ = occluded(S, F, need, g.pos, s.p, rays);     // test_vis is wave-uniform
+    if (need) L = L * (float)(!occ);
+    return ok ? L : mk(0, 0, 0);
 }
 
 // m_area / m_brdf (pg/ReSTIRIntegrator.h:62-74)
@@ -98,13 +108,13 @@ __device__ __forceinline__ float m_brdf(const FrameConst& F, float pb, float pa)
 }
 
 // gBufferFillPass (pg/ReSTIRIntegrator.cpp:213-234) + Camera::GenerateRay (pg/camera.cpp:20-42)
-__device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameConst& F, int x, int y) {
+__device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameConst& F, int x, int y, bool active) {
     vec3 dc = mk((float)x - (float)F.W / 2.0f, (float)F.H / 2.0f - (float)y, -F.cam.focal);
     const float* m = F.inv_view;
     vec3 dw = mk(m[0] * dc.x + m[3] * dc.y + m[6] * dc.z, m[1] * dc.x + m[4] * dc.y + m[7] * dc.z,
                  m[2] * dc.x + m[5] * dc.y + m[8] * dc.z);
     dw = normalize(dw);
-    SurfHit h = intersect(S, F.cam.pos, dw, FLT_MIN + 0.01f);
+    SurfHit h = intersect(S, active, F.cam.pos, dw, FLT_MIN + 0.01f);
     GElem g;
     g.pos = mk(0, 0, 0); g.nrm = g.pos; g.kd = g.pos; g.ks = g.pos; g.le = g.pos;
     g.shin = 0; g.depth = 0; g.type = 0; g.inv_im = 0;
@@ -158,12 +168,12 @@ __device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameCons
 
 // brdfSampleLight (pg/ReSTIRIntegrator.cpp:126-177)
 __device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameConst& F, const GElem& g, vec3 cam,
-                                              Rng& rng, float& W_out, float& mis_out, uint32_t& rays) {
+                                              bool alive, Rng& rng, float& W_out, float& mis_out, uint32_t& rays) {
     float pdf;
     vec3 wi = sample_brdf(g, cam, rng, pdf);
     vec3 org = g.pos + g.nrm * F.normal_off;
-    rays++;
-    SurfHit h = intersect(S, org, wi, FLT_MIN + F.tnear_off);
+    rays += alive ? 1u : 0u;
+    SurfHit h = intersect(S, alive, org, wi, FLT_MIN + F.tnear_off);
     W_out = 0.0f; mis_out = 0.0f;
     if (h.hit) {
         MatRec mr = load_mat(S, h.mat);
@@ -183,15 +193,16 @@ __device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameCons
     return smp_invalid();
 }
 
-// initialRenderPass (pg/ReSTIRIntegrator.cpp:236-298).  f_sel returns the selected candidate's f
-// (for the fused shade); the final p-hat (:289) equals the selected candidate's p-hat (same
-// arguments), so it is not re-evaluated.
+// initialRenderPass (pg/ReSTIRIntegrator.cpp:236-298) for the lanes with `in_pass`.  f_sel returns the
+// selected candidate's f (for the fused shade); the final p-hat (:289) equals the selected candidate's
+// p-hat (same arguments), so it is not re-evaluated.
 __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& F, const GElem& g, uint32_t pix,
-                                           vec3& f_sel, uint32_t& rays) {
+                                           bool in_pass, vec3& f_sel, uint32_t& rays) {
     f_sel = mk(0, 0, 0);
-    if (any_pos(g.le) || S.n_emis == 0) return res_empty();
-    Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, pix);
     Res r = res_empty();
+    const bool alive = in_pass && !any_pos(g.le) && S.n_emis > 0;     // :238-244
+    if (__ballot(alive) == 0) return r;                                 // wave-uniform exit
+    Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, pix);
     const vec3 cam = F.cam.pos;
     const bool tv = !F.do_vis_pass;
     float best_phat = 0.0f;
@@ -200,23 +211,24 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
         for (int i = 0; i < F.m_area; ++i) {
             float Wc, mis;
             Sample s = area_sample(S, F, g, cam, rng, Wc, mis);
-            vec3 f = evaluate_f(S, F, s, cam, g, tv, rays);
+            vec3 f = evaluate_f(S, F, s, cam, g, tv, alive, rays);
             float ph = length(f);
             float w = F.m_brdf > 0 ? mis * ph * Wc : inv_ma * ph * Wc;
-            if (res_add(r, s, w, 1, rng)) { best_phat = ph; f_sel = f; }
+            if (alive && res_add(r, s, w, 1, rng)) { best_phat = ph; f_sel = f; }
         }
     }
     if (F.m_brdf > 0) {
         float inv_mb = 1.0f / (float)F.m_brdf;
         for (int i = 0; i < F.m_brdf; ++i) {
             float Wc, mis;
-            Sample s = brdf_sample(S, F, g, cam, rng, Wc, mis, rays);
-            vec3 f = evaluate_f(S, F, s, cam, g, tv, rays);
+            Sample s = brdf_sample(S, F, g, cam, alive, rng, Wc, mis, rays);
+            vec3 f = evaluate_f(S, F, s, cam, g, tv, alive, rays);
             float ph = length(f);
             float w = F.m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
-            if (res_add(r, s, w, 1, rng)) { best_phat = ph; f_sel = f; }
+            if (alive && res_add(r, s, w, 1, rng)) { best_phat = ph; f_sel = f; }
         }
     }
+    if (!alive) { f_sel = mk(0, 0, 0); return res_empty(); }
     float ph = smp_valid(smp_of(r)) ? best_phat : 0.0f;
     r.W = ph > 0.0f ? 1.0f / ph * r.wsum : 0.0f;
     res_cap(r, F.cap);
@@ -232,51 +244,23 @@ __device__ __forceinline__ void store_rgb(float* fb, size_t p, vec3 c) {
     fb[3 * p] = c.x; fb[3 * p + 1] = c.y; fb[3 * p + 2] = c.z;
 }
 
-__global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G, ResBuf Rw,
-                                                         float* fb, int fuse_shade, Counters* C) {
-    int x, y;
-    uint32_t rays = 0, prim = 0;
-    if (pixel_of(F.gy0, F.gy1, F.W, x, y)) {
-        size_t p = (size_t)y * F.W + x;
-        GElem g = gbuffer_fill(S, F, x, y);
-        prim = 1;
-        G.store(p, g);
-        if (y >= F.y0 && y < F.y1) {
-            vec3 f;
-            Res r = initial_ris(S, F, g, (uint32_t)p, f, rays);
-            Rw.store(p, r);
-            if (fuse_shade) store_rgb(fb, p, shade_px(r, f, g.le));
-        }
-    }
-    count_rays(C, rays + prim, prim);
-}
-
-// G-buffer fill alone (rows [gy0, gy1)); the initial RIS then runs as k_initial
-__global__ void __launch_bounds__(256) k_gbuffer(DevScene S, FrameConst F, GBuf G, Counters* C) {
-    int x, y;
-    uint32_t prim = 0;
-    if (pixel_of(F.gy0, F.gy1, F.W, x, y)) {
-        size_t p = (size_t)y * F.W + x;
-        G.store(p, gbuffer_fill(S, F, x, y));
-        prim = 1;
-    }
-    count_rays(C, prim, prim);
-}
-
-// initialRenderPass alone: reads the pixel's G record written by k_gbuffer
-__global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_initial(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb,
-                                                 int fuse_shade, Counters* C) {
+__global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G,
+                                                                            ResBuf Rw, float* fb, int fuse_shade,
+                                                                            Counters* C) {
     int x, y;
     uint32_t rays = 0;
-    if (pixel_of(F.y0, F.y1, F.W, x, y)) {
-        size_t p = (size_t)y * F.W + x;
-        GElem g = G.load(p);
-        vec3 f;
-        Res r = initial_ris(S, F, g, (uint32_t)p, f, rays);
+    const bool in = pixel_of(F.gy0, F.gy1, F.W, x, y);
+    const size_t p = (size_t)y * F.W + x;
+    GElem g = gbuffer_fill(S, F, x, y, in);
+    if (in) G.store(p, g);
+    const bool ris = in && y >= F.y0 && y < F.y1;
+    vec3 f;
+    Res r = initial_ris(S, F, g, (uint32_t)p, ris, f, rays);
+    if (ris) {
         Rw.store(p, r);
         if (fuse_shade) store_rgb(fb, p, shade_px(r, f, g.le));
     }
-    count_rays(C, rays, 0);
+    count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u);
 }
 
 // visibilityPass (pg/ReSTIRIntegrator.cpp:302-312).  Invalid samples always carry W == 0 already,
@@ -284,14 +268,11 @@ __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_initial(DevScene S, F
 __global__ void __launch_bounds__(256) k_visibility(DevScene S, FrameConst F, GBuf G, ResBuf R, Counters* C) {
     int x, y;
     uint32_t rays = 0;
-    if (pixel_of(F.y0, F.y1, F.W, x, y)) {
-        size_t p = (size_t)y * F.W + x;
-        Res r = R.load(p);
-        if (smp_valid(smp_of(r)) && occluded(S, F, G.pos(p), r.p, rays)) {
-            r.W = 0;
-            R.r[3 * p + 1].w = 0.0f;
-        }
-    }
+    const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const size_t p = (size_t)y * F.W + x;
+    Res r = R.load(p);
+    const bool need = in && smp_valid(smp_of(r));
+    if (occluded(S, F, need, G.pos(p), r.p, rays) && need) R.r[3 * p + 1].w = 0.0f;
     count_rays(C, rays, 0);
 }
 
@@ -318,58 +299,58 @@ __global__ void __launch_bounds__(256) k_temporal(DevScene S, FrameConst F, GBuf
                                                   ResBuf Rw, Counters* C) {
     int x, y;
     uint32_t rays = 0;
-    if (pixel_of(F.y0, F.y1, F.W, x, y)) {
-        size_t p = (size_t)y * F.W + x;
-        Res cr = Rr.load(p);
-        Res out = cr;
-        GElem cur = G.load(p);
-        int qx, qy, fx, fy;
-        bool ok = reproject(F.camp, cur.pos, F.W, F.H, qx, qy);
-        // rows outside the G-buffer margin of a tile are treated as a failed reprojection (counted)
-        if (ok && (qy < F.gy0 || qy >= F.gy1)) { ok = false; atomicAdd(&C->reproj_outside, 1ull); }
-        GElem prev;
+    const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const size_t p = (size_t)y * F.W + x;
+    Res cr = Rr.load(p);
+    GElem cur = G.load(p);
+    int qx = x, qy = y, fx = x, fy = y;
+    bool ok = in && reproject(F.camp, cur.pos, F.W, F.H, qx, qy);
+    // rows outside the G-buffer margin of a tile are treated as a failed reprojection (counted)
+    if (ok && (qy < F.gy0 || qy >= F.gy1)) { ok = false; atomicAdd(&C->reproj_outside, 1ull); }
+    const size_t q = ok ? (size_t)qy * F.W + qx : p;
+    GElem prev = Gp.load(q);
+    if (ok) {
+        float cd = length(cur.pos - F.cam.pos), pd = length(prev.pos - F.camp.pos);
+        float dr = cd > pd ? pd / cd : cd / pd;
+        ok = !(dr < 0.9f);
+    }
+    if (ok) {
+        vec3 pac = Gp.pos(p);
+        ok = reproject(F.cam, pac, F.W, F.H, fx, fy);
+        if (ok && (fy < F.gy0 || fy >= F.gy1)) { ok = false; atomicAdd(&C->reproj_outside, 1ull); }
         if (ok) {
-            size_t q = (size_t)qy * F.W + qx;
-            prev = Gp.load(q);
-            float cd = length(cur.pos - F.cam.pos), pd = length(prev.pos - F.camp.pos);
-            float dr = cd > pd ? pd / cd : cd / pd;
-            ok = !(dr < 0.9f);
-            if (ok) {
-                vec3 pac = Gp.pos(p);
-                ok = reproject(F.cam, pac, F.W, F.H, fx, fy);
-                if (ok && (fy < F.gy0 || fy >= F.gy1)) { ok = false; atomicAdd(&C->reproj_outside, 1ull); }
-                if (ok) {
-                    vec3 fw = G.pos((size_t)fy * F.W + fx);
-                    float cdp = length(pac - F.camp.pos), pdp = length(fw - F.cam.pos);
-                    float drp = cdp > pdp ? pdp / cdp : cdp / pdp;
-                    ok = !(drp < 0.9f);
-                }
-            }
+            vec3 fw = G.pos((size_t)fy * F.W + fx);
+            float cdp = length(pac - F.camp.pos), pdp = length(fw - F.cam.pos);
+            float drp = cdp > pdp ? pdp / cdp : cdp / pdp;
+            ok = !(drp < 0.9f);
         }
+    }
+    Res out = cr;
+    if (__ballot(ok) != 0) {
+        Res pr = Rl.load(p);
+        Rng rng; rng.init(F.seed, F.frame, PASS_TEMPORAL, (uint32_t)p);
+        Res res = res_empty();
+        Sample cs = smp_of(cr), ps = smp_of(pr);
+        float p_cur = length(evaluate_f(S, F, cs, F.cam.pos, cur, true, ok, rays));
+        float p_prev = length(evaluate_f(S, F, cs, F.camp.pos, prev, true, ok, rays));
+        float m_cur = p_cur * (float)cr.conf / (p_cur * (float)cr.conf + p_prev * (float)pr.conf);
+        if (!(m_cur > 0)) m_cur = 0.0f;
+        float ph_cur = p_cur;
+        float p_cur2 = length(evaluate_f(S, F, ps, F.cam.pos, cur, true, ok, rays));
+        float p_prev2 = length(evaluate_f(S, F, ps, F.camp.pos, prev, true, ok, rays));
         if (ok) {
-            Res pr = Rl.load(p);
-            Rng rng; rng.init(F.seed, F.frame, PASS_TEMPORAL, (uint32_t)p);
-            Res res = res_empty();
-            Sample cs = smp_of(cr), ps = smp_of(pr);
-            float p_cur = length(evaluate_f(S, F, cs, F.cam.pos, cur, true, rays));
-            float p_prev = length(evaluate_f(S, F, cs, F.camp.pos, prev, true, rays));
-            float m_cur = p_cur * (float)cr.conf / (p_cur * (float)cr.conf + p_prev * (float)pr.conf);
-            if (!(m_cur > 0)) m_cur = 0.0f;
-            float ph_cur = p_cur;
             bool took_cur = res_add(res, cs, m_cur * ph_cur * cr.W, cr.conf, rng);
-            p_cur = length(evaluate_f(S, F, ps, F.cam.pos, cur, true, rays));
-            p_prev = length(evaluate_f(S, F, ps, F.camp.pos, prev, true, rays));
-            float m_prev = p_prev * (float)pr.conf / (p_cur * (float)cr.conf + p_prev * (float)pr.conf);
+            float m_prev = p_prev2 * (float)pr.conf / (p_cur2 * (float)cr.conf + p_prev2 * (float)pr.conf);
             if (!(m_prev > 0)) m_prev = 0.0f;
-            float ph_prev = p_cur;
+            float ph_prev = p_cur2;
             bool took_prev = res_add(res, ps, m_prev * ph_prev * pr.W, pr.conf, rng);
             res_cap(res, F.cap);
             float fph = took_prev ? ph_prev : (took_cur ? ph_cur : 0.0f);
             res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
             out = res;
         }
-        Rw.store(p, out);
     }
+    if (in) Rw.store(p, out);
     count_rays(C, rays, 0);
 }
 
@@ -400,125 +381,142 @@ __device__ __forceinline__ size_t list_px(const FrameConst& F, const Rng& rng, u
 }
 
 // spatialReusePass (pg/ReSTIRIntegrator.cpp:316-542); shade fused when this is the last pass.
-__global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw,
-                                                 int pass_idx, int fuse_shade, float* fb, Counters* C) {
+// List loops run to the uniform bound k+1 with `i < cnt` as a predicate (convergent ray queries).
+__global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr,
+                                                                   ResBuf Rw, int pass_idx, int fuse_shade, float* fb,
+                                                                   Counters* C) {
     int x, y;
     uint32_t rays = 0;
-    if (pixel_of(F.y0, F.y1, F.W, x, y)) {
-        size_t p = (size_t)y * F.W + x;
-        const vec3 cam = F.cam.pos;
-        GElem th = G.load(p);
-        if (any_pos(th.le)) {                              // :319-324
-            Res r = Rr.load(p);
-            Rw.store(p, r);
-            if (fuse_shade) store_rgb(fb, p, shade_px(r, mk(0, 0, 0), th.le));
-        } else {
-            Rng rng; rng.init(F.seed, F.frame, PASS_SPATIAL0 + (uint32_t)pass_idx, (uint32_t)p);
-            // neighbour selection (:334-374)
-            uint64_t acc = 0;
-            int M = 1;
-            for (int i = 0; i < F.k; ++i) {
-                size_t q = neighbor_px(F, rng, i, x, y);
-                if (any_pos(G.le(q))) continue;
-                if (F.reject) {
-                    float4 nq = G.g1[q];
-                    float ns = dot(xyz(nq), th.nrm);
-                    if (ns < F.min_normal_sim) continue;
-                    float nd = G.g0[q].w;
-                    float dr = 0;
-                    if (nd > 0) dr = th.depth / nd;
-                    float hd = F.max_depth_diff * 0.5f;
-                    if (dr < 1.0f - hd || dr > 1.0f + hd) continue;
-                }
-                acc |= 1ull << i;
-                M += 1;
+    const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const size_t p = (size_t)y * F.W + x;
+    const vec3 cam = F.cam.pos;
+    GElem th = G.load(p);
+    const bool emissive = any_pos(th.le);
+    const bool alive = in && !emissive;
+    if (in && emissive) {                                  // :319-324
+        Res r = Rr.load(p);
+        Rw.store(p, r);
+        if (fuse_shade) store_rgb(fb, p, shade_px(r, mk(0, 0, 0), th.le));
+    }
+    if (__ballot(alive) != 0) {
+        Rng rng; rng.init(F.seed, F.frame, PASS_SPATIAL0 + (uint32_t)pass_idx, (uint32_t)p);
+        // neighbour selection (:334-374)
+        uint64_t acc = 0;
+        int M = 1;
+        for (int i = 0; i < F.k; ++i) {
+            size_t q = neighbor_px(F, rng, i, x, y);
+            if (any_pos(G.le(q))) continue;
+            if (F.reject) {
+                float4 nq = G.g1[q];
+                float ns = dot(xyz(nq), th.nrm);
+                if (ns < F.min_normal_sim) continue;
+                float nd = G.g0[q].w;
+                float dr = 0;
+                if (nd > 0) dr = th.depth / nd;
+                float hd = F.max_depth_diff * 0.5f;
+                if (dr < 1.0f - hd || dr > 1.0f + hd) continue;
             }
-            rng.n = 2u * (uint32_t)F.k;
-            const int cnt = M;
-            int csum = 0, csum_nc = 0;                     // :379-385
-            for (int i = 0; i < cnt; ++i) {
-                int c = __float_as_int(Rr.r[3 * list_px(F, rng, acc, i, x, y, p) + 2].w);
-                csum += c;
-                if (i) csum_nc += c;
-            }
-            Res res = res_empty();
-            int sel = 0;
-            float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
-            vec3 f_sel = mk(0, 0, 0);
-            for (int i = 0; i < cnt; ++i) {
-                size_t qi = list_px(F, rng, acc, i, x, y, p);
-                Res ri = Rr.load(qi);
-                Sample si = smp_of(ri);
-                float mis = rcpM;
-                if (F.mis == MIS_BALANCE) {                // :407-424
-                    float num = 0, den = 0;
-                    mis = 0.0f;
-                    for (int j = 0; j < cnt; ++j) {
-                        size_t qj = list_px(F, rng, acc, j, x, y, p);
-                        int cj = __float_as_int(Rr.r[3 * qj + 2].w);
-                        float ph = length(evaluate_f(S, F, si, cam, G.load(qj), true, rays));
+            acc |= 1ull << i;
+            M += 1;
+        }
+        rng.n = 2u * (uint32_t)F.k;
+        const int cnt = M;
+        const int kk = F.k + 1;                            // uniform list bound
+        int csum = 0, csum_nc = 0;                         // :379-385
+        for (int i = 0; i < cnt; ++i) {
+            int c = __float_as_int(Rr.r[3 * list_px(F, rng, acc, i, x, y, p) + 2].w);
+            csum += c;
+            if (i) csum_nc += c;
+        }
+        Res res = res_empty();
+        int sel = 0;
+        float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
+        vec3 f_sel = mk(0, 0, 0);
+        for (int i = 0; i < kk; ++i) {
+            const bool li = alive && i < cnt;
+            size_t qi = list_px(F, rng, acc, i, x, y, p);
+            Res ri = Rr.load(qi);
+            Sample si = smp_of(ri);
+            float mis = rcpM;
+            if (F.mis == MIS_BALANCE) {                    // :407-424
+                float num = 0, den = 0;
+                mis = 0.0f;
+                for (int j = 0; j < kk; ++j) {
+                    const bool lj = li && j < cnt;
+                    size_t qj = list_px(F, rng, acc, j, x, y, p);
+                    int cj = __float_as_int(Rr.r[3 * qj + 2].w);
+                    float ph = length(evaluate_f(S, F, si, cam, G.load(qj), true, lj, rays));
+                    if (lj) {
                         den += ph * cj;
                         if (i == j) num = ph * ri.conf;
                     }
-                    if (den > 0) mis = num / den;
                 }
-                if (F.mis == MIS_PAIRWISE) {               // :427-467
-                    mis = 0.0f;
-                    if (i == 0) {
-                        float sum = 0.0f;
-                        float phc = length(evaluate_f(S, F, si, cam, G.load(qi), true, rays)) * (float)ri.conf;
-                        for (int j = 1; j < cnt; ++j) {
-                            size_t qj = list_px(F, rng, acc, j, x, y, p);
-                            int cj = __float_as_int(Rr.r[3 * qj + 2].w);
-                            float phj = length(evaluate_f(S, F, si, cam, G.load(qj), true, rays));
-                            float den = phc + phj * (float)csum_nc;
-                            if (den > 0) {
-                                float cf = (float)cj / (float)csum;
-                                sum += cf * (phc / den);
-                            }
-                        }
-                        mis = ((float)ri.conf / (float)csum) + sum;
-                    } else {
-                        float phi = length(evaluate_f(S, F, si, cam, G.load(qi), true, rays));
-                        float phc = length(evaluate_f(S, F, si, cam, G.load(p), true, rays));
-                        phi *= (float)csum_nc;
-                        int c0 = __float_as_int(Rr.r[3 * p + 2].w);
-                        float den = phi + phc * (float)c0;
-                        if (den > 0 && csum > 0) mis = ((float)ri.conf / (float)csum) * (phi / den);
-                    }
-                }
-                vec3 f = evaluate_f(S, F, si, cam, th, true, rays);     // :472
-                float rph = length(f);
-                float rw = mis * rph * ri.W;
-                if (res_add(res, si, rw, ri.conf, rng)) { sel = i; f_sel = f; }
+                if (den > 0) mis = num / den;
             }
-            float fph = smp_valid(smp_of(res)) ? length(f_sel) : 0.0f;  // :481
-            if (F.mis == MIS_CONSTANT || F.mis == MIS_BALANCE || F.mis == MIS_PAIRWISE) {
-                res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
-            } else if (F.mis == MIS_DEBIAS_Z) {            // :494-506
-                int Z = 0;
-                float corr = 1.0f;
-                for (int i = 0; i < cnt; ++i) {
-                    size_t qi = list_px(F, rng, acc, i, x, y, p);
-                    if (!occluded(S, F, G.pos(qi), res.p, rays)) Z += 1;
+            if (F.mis == MIS_PAIRWISE) {                   // :427-467
+                mis = 0.0f;
+                if (i == 0) {
+                    float sum = 0.0f;
+                    float phc = length(evaluate_f(S, F, si, cam, G.load(qi), true, li, rays)) * (float)ri.conf;
+                    for (int j = 1; j < kk; ++j) {
+                        const bool lj = li && j < cnt;
+                        size_t qj = list_px(F, rng, acc, j, x, y, p);
+                        int cj = __float_as_int(Rr.r[3 * qj + 2].w);
+                        float phj = length(evaluate_f(S, F, si, cam, G.load(qj), true, lj, rays));
+                        float den = phc + phj * (float)csum_nc;
+                        if (lj && den > 0) {
+                            float cf = (float)cj / (float)csum;
+                            sum += cf * (phc / den);
+                        }
+                    }
+                    mis = ((float)ri.conf / (float)csum) + sum;
+                } else {
+                    float phi = length(evaluate_f(S, F, si, cam, G.load(qi), true, li, rays));
+                    float phc = length(evaluate_f(S, F, si, cam, G.load(p), true, li, rays));
+                    phi *= (float)csum_nc;
+                    int c0 = __float_as_int(Rr.r[3 * p + 2].w);
+                    float den = phi + phc * (float)c0;
+                    if (den > 0 && csum > 0) mis = ((float)ri.conf / (float)csum) * (phi / den);
                 }
-                if (Z > 0 && M > 0) corr = (1.0f / (float)Z) / rcpM;
-                res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
-            } else if (F.mis == MIS_DEBIAS_CONTRIB) {      // :515-538
-                Sample ss = smp_of(Rr.load(list_px(F, rng, acc, sel, x, y, p)));
-                float num = 0, den = 0, cw = 0, corr = 0;
-                for (int i = 0; i < cnt; ++i) {
-                    size_t qi = list_px(F, rng, acc, i, x, y, p);
-                    int ci = __float_as_int(Rr.r[3 * qi + 2].w);
-                    float ph = length(evaluate_f(S, F, ss, cam, G.load(qi), true, rays));
+            }
+            vec3 f = evaluate_f(S, F, si, cam, th, true, li, rays);     // :472
+            float rph = length(f);
+            float rw = mis * rph * ri.W;
+            if (li && res_add(res, si, rw, ri.conf, rng)) { sel = i; f_sel = f; }
+        }
+        float fph = smp_valid(smp_of(res)) ? length(f_sel) : 0.0f;  // :481
+        if (F.mis == MIS_CONSTANT || F.mis == MIS_BALANCE || F.mis == MIS_PAIRWISE) {
+            res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
+        } else if (F.mis == MIS_DEBIAS_Z) {                // :494-506
+            int Z = 0;
+            float corr = 1.0f;
+            for (int i = 0; i < kk; ++i) {
+                const bool li = alive && i < cnt;
+                size_t qi = list_px(F, rng, acc, i, x, y, p);
+                bool occ = occluded(S, F, li, G.pos(qi), res.p, rays);
+                if (li && !occ) Z += 1;
+            }
+            if (Z > 0 && M > 0) corr = (1.0f / (float)Z) / rcpM;
+            res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
+        } else if (F.mis == MIS_DEBIAS_CONTRIB) {          // :515-538
+            Sample ss = smp_of(Rr.load(list_px(F, rng, acc, sel, x, y, p)));
+            float num = 0, den = 0, cw = 0, corr = 0;
+            for (int i = 0; i < kk; ++i) {
+                const bool li = alive && i < cnt;
+                size_t qi = list_px(F, rng, acc, i, x, y, p);
+                int ci = __float_as_int(Rr.r[3 * qi + 2].w);
+                float ph = length(evaluate_f(S, F, ss, cam, G.load(qi), true, li, rays));
+                if (li) {
                     den += ph * (float)ci;
                     if (i == sel) num = ph * (float)ci;
                 }
-                if (den > 0) cw = num / den;
-                if (M > 0) corr = cw / rcpM;
-                res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
             }
-            res_cap(res, F.cap);
+            if (den > 0) cw = num / den;
+            if (M > 0) corr = cw / rcpM;
+            res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
+        }
+        res_cap(res, F.cap);
+        if (alive) {
             Rw.store(p, res);
             if (fuse_shade) store_rgb(fb, p, shade_px(res, f_sel, th.le));
         }
@@ -530,14 +528,12 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
 __global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G, ResBuf Rr, float* fb, Counters* C) {
     int x, y;
     uint32_t rays = 0;
-    if (pixel_of(F.y0, F.y1, F.W, x, y)) {
-        size_t p = (size_t)y * F.W + x;
-        Res r = Rr.load(p);
-        GElem g = G.load(p);
-        vec3 f = mk(0, 0, 0);
-        if (r.wsum > 0.0f) f = evaluate_f(S, F, smp_of(r), F.cam.pos, g, true, rays);
-        store_rgb(fb, p, shade_px(r, f, g.le));
-    }
+    const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const size_t p = (size_t)y * F.W + x;
+    Res r = Rr.load(p);
+    GElem g = G.load(p);
+    vec3 f = evaluate_f(S, F, smp_of(r), F.cam.pos, g, true, in && r.wsum > 0.0f, rays);
+    if (in) store_rgb(fb, p, shade_px(r, f, g.le));
     count_rays(C, rays, 0);
 }
 

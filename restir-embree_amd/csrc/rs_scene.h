@@ -95,6 +95,124 @@ RS_TRAV_ATTR bool occluded_ray(const DevScene& S, vec3 o, vec3 d, float tnear, f
 
 struct Hit { float t, u, v; int prim; };
 
+// ---------------------------------------------------------------- wave-coherent (lockstep) traversal
+// The skip-pointer order is a global order and every ray only moves forward through it, so a wave
+// can walk the node array together: each step it takes m = min over lanes of their next node, loads
+// node m ONCE with scalar loads (uniform address, no 64-address gather), and only the lanes whose
+// next node is m test it.  The number of steps is the size of the union of the lanes' paths -- for
+// a wave's shadow rays from one 8x8 tile this is ~ the longest single path (scripts/bvh_analysis.py:
+// union 30.4 vs longest 28.9 nodes on C2) -- while per-step memory traffic drops from up to 64 cache
+// lines to one.  Results are identical to the per-lane traversal (same tests, same tie rule).
+// uniform-index load through the constant address space -> s_load (scalar cache), no VGPR address
+__device__ __forceinline__ float4 sload(const float4* p, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const float __attribute__((address_space(4)))* cfloat_ptr;
+    cfloat_ptr q = (cfloat_ptr)(const float*)(p + i);
+    return make_float4(q[0], q[1], q[2], q[3]);
+#else
+    return p[i];   // host pass only type-checks device code
+#endif
+}
+
+// min over all 64 lanes (EXEC must be all ones): DPP butterfly in-row, then row broadcasts
+__device__ __forceinline__ uint32_t wave_min_full(uint32_t v) {
+    const int I = (int)0xffffffff;   // identity for unsigned min (lanes masked off by row/bank masks)
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// exact min over the ACTIVE lanes for a partially masked wave (slow path; kernels keep waves full)
+__device__ __forceinline__ uint32_t wave_min_partial(uint32_t v) {
+    uint32_t m = 0xffffffffu;
+    uint64_t act = __ballot(1);
+    while (act) {
+        int lane = __builtin_ctzll(act);
+        act &= act - 1;
+        uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+        m = x < m ? x : m;
+    }
+    return m;
+}
+
+// rtcOccluded1 semantics, lockstep.  Every lane of the wave must call it (inactive: active=false).
+__device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    const bool full = __ballot(1) == ~0ull;
+    vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const uint32_t n = S.n_nodes;
+    uint32_t i = active ? 0u : 0xffffffffu;
+    bool occ = false;
+    while (true) {
+        uint32_t m = full ? wave_min_full(i) : wave_min_partial(i);
+        if (m >= n) break;
+        float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+        if (i == m) {
+            const uint32_t skip = (uint32_t)__float_as_int(a.w);
+            if (box_test(a, b, o, inv, tnear, tfar)) {
+                const int leaf = __float_as_int(b.w);
+                if (leaf >= 0) {
+                    const int first = leaf >> 3, cnt = (leaf & 7) + 1;
+                    for (int k = 0; k < cnt && !occ; ++k) {
+                        const uint32_t tri = 3u * (uint32_t)(first + k);
+                        float t, u, v;
+                        occ = tri_test(sload(S.tris, tri), sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d,
+                                       tnear, tfar, t, u, v);
+                    }
+                    i = occ ? 0xffffffffu : skip;
+                } else {
+                    i = m + 1;
+                }
+            } else {
+                i = skip;
+            }
+        }
+    }
+    return occ;
+}
+
+// rtcIntersect1 semantics, lockstep: closest hit in [tnear, tfar], ties to the smaller triangle index.
+__device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    const bool full = __ballot(1) == ~0ull;
+    vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
+    const uint32_t n = S.n_nodes;
+    uint32_t i = active ? 0u : 0xffffffffu;
+    while (true) {
+        uint32_t m = full ? wave_min_full(i) : wave_min_partial(i);
+        if (m >= n) break;
+        float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+        if (i == m) {
+            const uint32_t skip = (uint32_t)__float_as_int(a.w);
+            if (box_test(a, b, o, inv, tnear, h.t)) {
+                const int leaf = __float_as_int(b.w);
+                if (leaf >= 0) {
+                    const int first = leaf >> 3, cnt = (leaf & 7) + 1;
+                    for (int k = 0; k < cnt; ++k) {
+                        const uint32_t tri = 3u * (uint32_t)(first + k);
+                        float4 T0 = sload(S.tris, tri);
+                        float t, u, v;
+                        if (tri_test(T0, sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d, tnear, h.t, t, u, v)) {
+                            int prim = __float_as_int(T0.w);
+                            if (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim)) {
+                                h.t = t; h.u = u; h.v = v; h.prim = prim;
+                            }
+                        }
+                    }
+                    i = skip;
+                } else {
+                    i = m + 1;
+                }
+            } else {
+                i = skip;
+            }
+        }
+    }
+    return h;
+}
+
 // rtcIntersect1 semantics: closest hit in [tnear, tfar]; ties broken by the smaller triangle index
 RS_TRAV_ATTR Hit closest_ray(const DevScene& S, vec3 o, vec3 d, float tnear, float tfar) {
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -139,10 +257,32 @@ __device__ __forceinline__ MatRec load_mat(const DevScene& S, uint32_t m) {
 // Intersection::intersectEmbree + getGeometryAttributes (pg/Intersection.h:8-41,85-113):
 // hit point = org + dir*t, interpolated normal (1-u-v)n0 + u n1 + v n2, normalised, flipped to face
 // the ray; material; emissive id (vertex-0 attribute, :103-110).
+// Traversal used by the passes: lockstep (default) or per-lane (RS_LOCKSTEP=0, for A/B).  Both must
+// be called by every lane of the wave (convergent call sites); `active` selects the lanes with a ray.
+#ifndef RS_LOCKSTEP
+#define RS_LOCKSTEP 1
+#endif
+__device__ __forceinline__ bool trace_any(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+#if RS_LOCKSTEP
+    return occluded_wave(S, active, o, d, tnear, tfar);
+#else
+    return active ? occluded_ray(S, o, d, tnear, tfar) : false;
+#endif
+}
+__device__ __forceinline__ Hit trace_closest(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+#if RS_LOCKSTEP
+    return closest_wave(S, active, o, d, tnear, tfar);
+#else
+    if (active) return closest_ray(S, o, d, tnear, tfar);
+    Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
+    return h;
+#endif
+}
+
 struct SurfHit { bool hit; vec3 point, normal; uint32_t mat; int emis_id; };
-__device__ __forceinline__ SurfHit intersect(const DevScene& S, vec3 o, vec3 d, float tnear) {
+__device__ __forceinline__ SurfHit intersect(const DevScene& S, bool active, vec3 o, vec3 d, float tnear) {
     SurfHit r; r.hit = false; r.mat = 0; r.emis_id = -1; r.point = mk(0, 0, 0); r.normal = mk(0, 0, 0);
-    Hit h = closest_ray(S, o, d, tnear, FLT_MAX);
+    Hit h = trace_closest(S, active, o, d, tnear, FLT_MAX);
     if (h.prim < 0) return r;
     const float4* N = S.tri_nrm + 3 * h.prim;
     float4 n0 = N[0], n1 = N[1], n2 = N[2];

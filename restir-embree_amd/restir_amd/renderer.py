@@ -239,7 +239,7 @@ class Renderer:
         self._check(self.lib.rs_dump_reservoirs(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
         return out
 
-    def debug_trace(self, scene: Scene, o, d, tnear, tfar, any_hit: bool):
+    def debug_trace(self, scene: Scene, o, d, tnear, tfar, any_hit: bool, lockstep: bool = True):
         o = np.ascontiguousarray(o, np.float32)
         d = np.ascontiguousarray(d, np.float32)
         n = o.shape[0]
@@ -249,7 +249,8 @@ class Renderer:
         prim = np.zeros(n, np.int32)
         fp = ctypes.POINTER(ctypes.c_float)
         self._check(self.lib.rs_debug_trace(self.h, scene.h, n, o.ctypes.data_as(fp), d.ctypes.data_as(fp),
-                                            tn.ctypes.data_as(fp), tf.ctypes.data_as(fp), 1 if any_hit else 0,
+                                            tn.ctypes.data_as(fp), tf.ctypes.data_as(fp),
+                                            (1 if any_hit else 0) + (0 if lockstep else 2),
                                             t.ctypes.data_as(fp), prim.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
         return t, prim
 

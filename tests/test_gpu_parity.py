@@ -69,15 +69,16 @@ def test_bvh_queries_bit_exact(scene_fn):
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     d[:100, 0] = 0.0                      # axis-parallel rays (inf reciprocals)
     d[100:200, 1] = 0.0
-    t, prim = g.debug_trace(gs, o, d, 0.01, 3.0e38, any_hit=False)
     tr, pr = os_.trace_closest(o, d, 0.01, 3.0e38)
-    assert np.array_equal(prim, pr)
-    assert np.array_equal(t, tr)
     tf = np.where(tr > 0, tr * np.float32(0.999), np.float32(2.0)).astype(np.float32)
     tf[::3] = np.where(tr[::3] > 0, tr[::3] * np.float32(1.001), np.float32(5.0))
-    _, anyg = g.debug_trace(gs, o, d, np.full(n, 0.01, np.float32), tf, any_hit=True)
     anyr = os_.trace_any(o, d, np.full(n, 0.01, np.float32), tf)
-    assert np.array_equal(anyg, anyr)
+    for lockstep in (True, False):          # wave-coherent traversal used by the passes, and per-lane
+        t, prim = g.debug_trace(gs, o, d, 0.01, 3.0e38, any_hit=False, lockstep=lockstep)
+        assert np.array_equal(prim, pr)
+        assert np.array_equal(t, tr)
+        _, anyg = g.debug_trace(gs, o, d, np.full(n, 0.01, np.float32), tf, any_hit=True, lockstep=lockstep)
+        assert np.array_equal(anyg, anyr)
 
 
 def test_bvh_degenerate_scenes():
@@ -91,8 +92,9 @@ def test_bvh_degenerate_scenes():
         gs = g.load_scene(sc)
         o = np.array([[0, -0.2, 1], [0.9, 0.9, 1], [0, 0, -1]], np.float32)
         d = np.array([[0, 0, -1], [0, 0, -1], [0, 0, 1]], np.float32)
-        t, prim = g.debug_trace(gs, o, d, 0.0, 3e38, any_hit=False)
-        assert list(prim) == [0, -1, 0] and t[0] == 1.0 and t[2] == 1.0
+        for lockstep in (True, False):
+            t, prim = g.debug_trace(gs, o, d, 0.0, 3e38, any_hit=False, lockstep=lockstep)
+            assert list(prim) == [0, -1, 0] and t[0] == 1.0 and t[2] == 1.0
 
 
 # ---------------------------------------------------------------- per-pass state
