@@ -176,6 +176,10 @@ static inline float rng_u(rng_t* r) {
 }
 /* Utils::getRandomValue(a, b) = a + (b - a) * U  (pg/utils.cpp:199-202) */
 static inline float rnd(rng_t* r, float a, float b) { float u = rng_u(r); return a + (b - a) * u; }
+/* Initial-pass draw slots: candidate c (area candidates 0..A-1, then BRDF candidates) owns draws
+ * 4c..4c+3 -- up to 3 for its sample, 4c+3 for its reservoir update -- so candidates are independent
+ * of one another's outcome (the reference's shared mt19937 stream has no observable order). */
+static inline uint32_t cand_slot(int c) { return 4u * (uint32_t)c; }
 
 /* ------------------------------------------------------------------ incomplete beta */
 /* Non-normalised incomplete beta B_x(a,b) in double: restates boost::math::beta(a,b,x)
@@ -853,9 +857,11 @@ static void pass_initial(fctx* F, or_res* Rw, int y0, int y1, uint64_t* rays) {
                 float inv_ma = 1.0f / (float)P->m_area;
                 for (int i = 0; i < P->m_area; ++i) {
                     float Wc, mis;
+                    rng.n = cand_slot(i);
                     sample_t smp = area_sample(F, g, cam, &rng, &Wc, &mis);
                     float ph = eval_phat(F, smp, cam, g, im, tv, &rc);
                     float w = P->m_brdf > 0 ? mis * ph * Wc : inv_ma * ph * Wc;
+                    rng.n = cand_slot(i) + 3u;
                     if (res_add(&r, smp, w, 1, &rng)) best_phat = ph;
                 }
             }
@@ -863,9 +869,11 @@ static void pass_initial(fctx* F, or_res* Rw, int y0, int y1, uint64_t* rays) {
                 float inv_mb = 1.0f / (float)P->m_brdf;
                 for (int i = 0; i < P->m_brdf; ++i) {
                     float Wc, mis;
+                    rng.n = cand_slot(P->m_area + i);
                     sample_t smp = brdf_sample(F, g, cam, &rng, &Wc, &mis, &rc);
                     float ph = eval_phat(F, smp, cam, g, im, tv, &rc);
                     float w = P->m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
+                    rng.n = cand_slot(P->m_area + i) + 3u;
                     if (res_add(&r, smp, w, 1, &rng)) best_phat = ph;
                 }
             }

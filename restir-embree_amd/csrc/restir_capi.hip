@@ -55,6 +55,8 @@ struct rs_context {
     float* fb = nullptr;
     Counters* d_cnt = nullptr;
     Counters* h_cnt = nullptr;
+    uint2* d_part = nullptr;               // per-wave ray-count slots of this frame's launches
+    size_t part_cap = 0, part_used = 0;
     hipEvent_t ev[EV_COUNT] = {};
     uint64_t frames = 0;
     std::string err;
@@ -206,6 +208,7 @@ extern "C" void rs_context_destroy(rs_context* c) {
     for (auto* r : c->R) if (r) hipFree(r);
     if (c->fb) hipFree(c->fb);
     if (c->d_cnt) hipFree(c->d_cnt);
+    if (c->d_part) hipFree(c->d_part);
     if (c->h_cnt) hipHostFree(c->h_cnt);
     for (auto& e : c->ev) if (e) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -376,6 +379,39 @@ extern "C" int rs_scene_info(const rs_scene* s, uint32_t* n_tris, uint32_t* n_em
 
 // --------------------------------------------------------------------------- frame / tile driver
 static dim3 grid_rows(int W, int ya, int yb) { return dim3((W + 15) / 16, (yb - ya + 15) / 16); }
+static size_t grid_waves(dim3 g) { return (size_t)g.x * g.y * 4; }
+
+// ray-count slots for one launch (rs_passes.h CountSlot); capacity is reserved in rs_tile_begin
+static CountSlot count_slot(rs_context* c, dim3 grid) {
+    const size_t n = grid_waves(grid);
+    if (c->part_used + n > c->part_cap) {       // more launches than reserved (a pass re-run): grow, keep slots
+        const size_t cap = 2 * (c->part_used + n);
+        uint2* np = nullptr;
+        hipStreamSynchronize(c->stream);
+        if (hipMalloc(&np, cap * sizeof(uint2)) == hipSuccess) {
+            if (c->part_used) hipMemcpy(np, c->d_part, c->part_used * sizeof(uint2), hipMemcpyDeviceToDevice);
+            hipFree(c->d_part);
+            c->d_part = np; c->part_cap = cap;
+        } else {
+            c->part_used = 0;                   // out of memory: recount from slot 0 (totals undercount)
+        }
+    }
+    CountSlot s{c->d_part + c->part_used, &c->d_cnt->reproj_outside};
+    c->part_used += n;
+    return s;
+}
+// reserve slots for every launch of a frame: initial + visibility + temporal + P spatial + shade
+static bool reserve_count_slots(rs_context* c, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
+    size_t need = grid_waves(grid_rows(c->W, gy0, gy1)) +
+                  grid_waves(grid_rows(c->W, y0, y1)) * (3 + (size_t)std::max(0, P->spatial_passes));
+    c->part_used = 0;
+    if (need <= c->part_cap) return true;
+    if (c->d_part) hipFree(c->d_part);
+    c->d_part = nullptr; c->part_cap = 0;
+    if (hipMalloc(&c->d_part, need * sizeof(uint2)) != hipSuccess) return false;
+    c->part_cap = need;
+    return true;
+}
 
 extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* cam, const rs_frame_params* P,
                              uint32_t frame_index, const rs_tile_desc* tile) {
@@ -415,14 +451,16 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     c->shade_fused = !P->do_visibility_pass && !temporal && !spatial;
     c->temporal_ran = c->spatial_ran = c->ev_temporal = false;
     const DevScene S = s->dev();
+    if (!reserve_count_slots(c, P, F.gy0, F.gy1, F.y0, F.y1)) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
     HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->stream));
     HIPCHK(c, hipEventRecord(c->ev[EV_BEGIN], c->stream));
-    k_gbuffer_initial<<<grid_rows(c->W, F.gy0, F.gy1), 256, 0, c->stream>>>(S, F, c->G[gnew], ResBuf{c->R[c->ra]},
-                                                                           c->fb, c->shade_fused ? 1 : 0, c->d_cnt);
+    const dim3 gg = grid_rows(c->W, F.gy0, F.gy1), gb = grid_rows(c->W, F.y0, F.y1);
+    k_gbuffer_initial<<<gg, 256, 0, c->stream>>>(S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
+                                                 count_slot(c, gg));
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[EV_INIT], c->stream));
     if (P->do_visibility_pass) {
-        k_visibility<<<grid_rows(c->W, F.y0, F.y1), 256, 0, c->stream>>>(S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->d_cnt);
+        k_visibility<<<gb, 256, 0, c->stream>>>(S, F, c->G[gnew], ResBuf{c->R[c->ra]}, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(c->ev[EV_VIS], c->stream));
@@ -453,9 +491,9 @@ extern "C" int rs_tile_temporal(rs_context* c) {
     HIPCHK(c, enter(c));
     if (c->P.do_temporal && c->frames > 0 && !c->temporal_ran) {
         const DevScene S = c->scene->dev();
-        k_temporal<<<grid_rows(c->W, c->F.y0, c->F.y1), 256, 0, c->stream>>>(
-            S, c->F, c->G[c->gcur], c->G[c->gcur ^ 1], ResBuf{c->R[c->rcur]}, ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]},
-            c->d_cnt);
+        const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
+        k_temporal<<<gb, 256, 0, c->stream>>>(S, c->F, c->G[c->gcur], c->G[c->gcur ^ 1], ResBuf{c->R[c->rcur]},
+                                              ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
         c->rcur = c->rb;
         c->temporal_ran = true;
@@ -482,9 +520,9 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
     const DevScene S = c->scene->dev();
     int dst = (c->rcur == c->ra) ? c->rb : c->ra;
     int fuse = (pass_index == c->P.spatial_passes - 1) ? 1 : 0;
-    k_spatial<<<grid_rows(c->W, c->F.y0, c->F.y1), 256, 0, c->stream>>>(S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]},
-                                                                         ResBuf{c->R[dst]}, pass_index, fuse, c->fb,
-                                                                         c->d_cnt);
+    const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
+    k_spatial<<<gb, 256, 0, c->stream>>>(S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]}, ResBuf{c->R[dst]}, pass_index,
+                                         fuse, c->fb, count_slot(c, gb));
     HIPCHK(c, hipGetLastError());
     c->rcur = dst;
     if (fuse) c->shade_fused = true;
@@ -507,8 +545,8 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
     if (!c->spatial_ran) HIPCHK(c, hipEventRecord(c->ev[EV_SPATIAL], c->stream));
     if (!c->shade_fused) {
         const DevScene S = c->scene->dev();
-        k_shade<<<grid_rows(c->W, c->F.y0, c->F.y1), 256, 0, c->stream>>>(S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]},
-                                                                           c->fb, c->d_cnt);
+        const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
+        k_shade<<<gb, 256, 0, c->stream>>>(S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]}, c->fb, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(c->ev[EV_SHADE], c->stream));
@@ -517,6 +555,8 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
     c->active = false;
     if (band_rgb) *band_rgb = c->fb + 3 * (size_t)c->F.y0 * c->W;
     if (t) {
+        k_reduce_counts<<<1, 1024, 0, c->stream>>>(c->d_part, c->part_used, c->d_cnt);
+        HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->d_cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         float a = 0, b = 0, d = 0, e = 0, f = 0, tot = 0;

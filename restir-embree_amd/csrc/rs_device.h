@@ -178,13 +178,21 @@ __device__ __forceinline__ bool smp_valid(const Sample& s) {
     return pok && nok && lok;
 }
 // Reservoir::addSample (pg/Reservoir.h:33-47)
-__device__ __forceinline__ bool res_add(Res& r, const Sample& s, float w, int conf, Rng& rng) {
+// the update without the sample copy: returns whether the new sample is selected
+__device__ __forceinline__ bool res_add_w(Res& r, float w, int conf, Rng& rng) {
     r.wsum += w;
     r.conf += conf;
     if (w == 0 && r.wsum == 0) return false;
-    if (rng.u() < w / r.wsum) { r.p = s.p; r.n = s.n; r.li = s.li; return true; }
-    return false;
+    return rng.u() < w / r.wsum;
 }
+__device__ __forceinline__ bool res_add(Res& r, const Sample& s, float w, int conf, Rng& rng) {
+    if (!res_add_w(r, w, conf, rng)) return false;
+    r.p = s.p; r.n = s.n; r.li = s.li;
+    return true;
+}
+// Initial-pass draw slots (oracle/restir_oracle.c cand_slot): candidate c owns draws 4c..4c+3 --
+// up to 3 for its sample, 4c+3 for its reservoir update -- independent of other candidates' outcome.
+__device__ __forceinline__ uint32_t cand_slot(int c) { return 4u * (uint32_t)c; }
 __device__ __forceinline__ void res_cap(Res& r, int cap) { r.conf = r.conf < cap ? r.conf : cap; }
 
 // ---------------------------------------------------------------- BRDF statics

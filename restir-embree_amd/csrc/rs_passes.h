@@ -26,6 +26,10 @@
 #ifndef RS_SPATIAL_WAVES
 #define RS_SPATIAL_WAVES 4
 #endif
+// area candidates whose shadow rays share one lockstep traversal (occluded_wave_multi)
+#ifndef RS_RIS_BATCH
+#define RS_RIS_BATCH 2
+#endif
 
 namespace rs {
 
@@ -43,18 +47,39 @@ struct FrameConst {
     GCam cam, camp;       // current / previous frame camera (pg/GBufferElement.h:136-139)
 };
 
-struct Counters { unsigned long long rays, primary, reproj_outside; };
+struct Counters { unsigned long long rays, primary, reproj_outside; };   // per-frame totals
+
+// Per-launch ray counting without atomics: every wave stores its (rays, primary) pair into its own
+// slot of a per-launch array, k_reduce_counts sums all slots once per frame.  (Same-address device
+// atomics from all 8 XCDs serialise at the memory side: one 64-bit atomicAdd per wave cost ~0.7 ms
+// per 1080p kernel, more than the G-buffer pass itself -- scripts/initial_breakdown.py.)
+struct CountSlot {
+    uint2* part;                         // gridDim.x * gridDim.y * 4 entries (4 waves per workgroup)
+    unsigned long long* outside;         // Counters::reproj_outside (rare: tile-edge reprojections)
+};
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-__device__ __forceinline__ void count_rays(Counters* C, uint32_t rays, uint32_t primary) {
+__device__ __forceinline__ void count_rays(CountSlot C, uint32_t rays, uint32_t primary) {
     uint32_t r = wave_sum(rays), p = wave_sum(primary);
-    if ((threadIdx.x & 63) == 0) {
-        if (r) atomicAdd(&C->rays, (unsigned long long)r);
-        if (p) atomicAdd(&C->primary, (unsigned long long)p);
+    if ((threadIdx.x & 63) == 0)
+        C.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)] = make_uint2(r, p);
+}
+
+// one workgroup: sum n slot pairs into the frame totals
+__global__ void __launch_bounds__(1024) k_reduce_counts(const uint2* part, size_t n, Counters* out) {
+    __shared__ unsigned long long sr[1024], sp[1024];
+    unsigned long long r = 0, p = 0;
+    for (size_t i = threadIdx.x; i < n; i += 1024) { uint2 v = part[i]; r += v.x; p += v.y; }
+    sr[threadIdx.x] = r; sp[threadIdx.x] = p;
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) { sr[threadIdx.x] += sr[threadIdx.x + s]; sp[threadIdx.x] += sp[threadIdx.x + s]; }
+        __syncthreads();
     }
+    if (threadIdx.x == 0) { out->rays = sr[0]; out->primary = sp[0]; }
 }
 
 // 8x8 tile per wave, 16x16 per workgroup, rows [ya, yb).  Returns whether the pixel exists; x/y are
@@ -80,21 +105,40 @@ __device__ __forceinline__ bool occluded(const DevScene& S, const FrameConst& F,
 
 // ReSTIRIntegrator::evaluateF (pg/ReSTIRIntegrator.cpp:185-211) for the lanes with `alive`.  The
 // shadow ray is skipped when L_i*f_r*G is exactly zero in every channel (0 whatever V is).
-__device__ __forceinline__ vec3 evaluate_f(const DevScene& S, const FrameConst& F, const Sample& s, vec3 cam,
-                                           const GElem& g, bool test_vis, bool alive, uint32_t& rays) {
-    const bool ok = alive && smp_valid(s) && !(g.le.x > 0 || g.le.y > 0 || g.le.z > 0);
+// Split in two around the shadow ray so callers can batch several rays into one traversal:
+// evaluate_f_pre computes the unoccluded L and the testOcclusion ray (dir = normalize(p - pos),
+// tfar = |p - pos| - tfarOffset, exactly as occluded() forms them); evaluate_f_post applies V.
+struct FPre { vec3 L, dir; float tfar; bool ok, need; };
+__device__ __forceinline__ FPre evaluate_f_pre(const FrameConst& F, const Sample& s, vec3 cam, const GElem& g,
+                                               bool test_vis, bool alive) {
+    FPre r;
+    r.ok = alive && smp_valid(s) && !(g.le.x > 0 || g.le.y > 0 || g.le.z > 0);
     vec3 ld = s.p - g.pos;
     float r2 = dot(ld, ld);
     ld = normalize(ld);
     float cI = gmax(dot(ld, g.nrm), 0.0f);
     float cY = fabsf(dot(-ld, s.n));
     float G = cI * cY / r2;
-    vec3 L = (s.li * eval_brdf(g, cam, ld)) * G;
-    const bool need = ok && test_vis && !(L.x == 0.0f && L.y == 0.0f && L.z == 0.0f);
+    r.L = (s.li * eval_brdf(g, cam, ld)) * G;
+    r.need = r.ok && test_vis && !(r.L.x == 0.0f && r.L.y == 0.0f && r.L.z == 0.0f);
+    r.dir = ld;
+    r.tfar = sqrtf(r2) - F.tfar_off;
+    return r;
+}
+__device__ __forceinline__ vec3 evaluate_f_post(const FPre& p, bool occ) {
+    vec3 L = p.L;
+    if (p.need) L = L * (float)(!occ);
+    return p.ok ? L : mk(0, 0, 0);
+}
+__device__ __forceinline__ vec3 evaluate_f(const DevScene& S, const FrameConst& F, const Sample& s, vec3 cam,
+                                           const GElem& g, bool test_vis, bool alive, uint32_t& rays) {
+    FPre p = evaluate_f_pre(F, s, cam, g, test_vis, alive);
     bool occ = false;
-    if (test_vis) occ = occluded(S, F, need, g.pos, s.p, rays);     // test_vis is wave-uniform
-    if (need) L = L * (float)(!occ);
-    return ok ? L : mk(0, 0, 0);
+    if (test_vis) {                                                   // test_vis is wave-uniform
+        rays += p.need ? 1u : 0u;
+        occ = trace_any(S, p.need, g.pos, p.dir, FLT_MIN + F.tnear_off, p.tfar);
+    }
+    return evaluate_f_post(p, occ);
 }
 
 // m_area / m_brdf (pg/ReSTIRIntegrator.h:62-74)
@@ -124,7 +168,11 @@ __device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameCons
         g.type = mr.type; g.kd = mr.kd; g.ks = mr.ks; g.le = mr.le; g.shin = mr.shin;
         if (g.type == MT_PHONG || g.type == MT_DIELECTRIC) {
             vec3 V = normalize(F.cam.pos - g.pos);
+#ifdef RS_DIAG_NO_IM   // timing diagnostic only (scripts/initial_breakdown.py); breaks parity
+            g.inv_im = 1.0f + 0.0f * dot(V, g.nrm);
+#else
             g.inv_im = 1.0f / calc_I_M(dot(V, g.nrm), g.shin);
+#endif
         }
     } else {
         g.le = F.bg;      // useSkybox=false path: renderParams.bgColor (:231)
@@ -207,24 +255,55 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
     const bool tv = !F.do_vis_pass;
     float best_phat = 0.0f;
     if (F.m_area > 0) {
+        // area candidates in batches of RS_RIS_BATCH: sample + unoccluded f for the batch, ONE lockstep
+        // walk for the batch's shadow rays, then the reservoir updates in candidate order.  The selected
+        // sample is re-drawn from its slots once at the end instead of being carried per candidate.
         float inv_ma = 1.0f / (float)F.m_area;
-        for (int i = 0; i < F.m_area; ++i) {
+        int sel = -1;
+        for (int c0 = 0; c0 < F.m_area; c0 += RS_RIS_BATCH) {
+            FPre pre[RS_RIS_BATCH];
+            float Wc[RS_RIS_BATCH], mis[RS_RIS_BATCH];
+            bool act[RS_RIS_BATCH], occ[RS_RIS_BATCH];
+            vec3 dir[RS_RIS_BATCH];
+            float tf[RS_RIS_BATCH];
+#pragma unroll
+            for (int k = 0; k < RS_RIS_BATCH; ++k) {
+                const bool inb = c0 + k < F.m_area;
+                rng.n = cand_slot(c0 + k);
+                Sample s = area_sample(S, F, g, cam, rng, Wc[k], mis[k]);
+                pre[k] = evaluate_f_pre(F, s, cam, g, tv, alive && inb);
+                act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
+                rays += act[k] ? 1u : 0u;
+            }
+            if (tv) trace_any_multi<RS_RIS_BATCH>(S, act, g.pos, dir, FLT_MIN + F.tnear_off, tf, occ);
+#pragma unroll
+            for (int k = 0; k < RS_RIS_BATCH; ++k) {
+                if (c0 + k < F.m_area) {
+                    vec3 f = evaluate_f_post(pre[k], occ[k]);
+                    float ph = length(f);
+                    float w = F.m_brdf > 0 ? mis[k] * ph * Wc[k] : inv_ma * ph * Wc[k];
+                    rng.n = cand_slot(c0 + k) + 3u;
+                    if (alive && res_add_w(r, w, 1, rng)) { sel = c0 + k; best_phat = ph; f_sel = f; }
+                }
+            }
+        }
+        if (sel >= 0) {
             float Wc, mis;
+            rng.n = cand_slot(sel);
             Sample s = area_sample(S, F, g, cam, rng, Wc, mis);
-            vec3 f = evaluate_f(S, F, s, cam, g, tv, alive, rays);
-            float ph = length(f);
-            float w = F.m_brdf > 0 ? mis * ph * Wc : inv_ma * ph * Wc;
-            if (alive && res_add(r, s, w, 1, rng)) { best_phat = ph; f_sel = f; }
+            r.p = s.p; r.n = s.n; r.li = s.li;
         }
     }
     if (F.m_brdf > 0) {
         float inv_mb = 1.0f / (float)F.m_brdf;
         for (int i = 0; i < F.m_brdf; ++i) {
             float Wc, mis;
+            rng.n = cand_slot(F.m_area + i);
             Sample s = brdf_sample(S, F, g, cam, alive, rng, Wc, mis, rays);
             vec3 f = evaluate_f(S, F, s, cam, g, tv, alive, rays);
             float ph = length(f);
             float w = F.m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
+            rng.n = cand_slot(F.m_area + i) + 3u;
             if (alive && res_add(r, s, w, 1, rng)) { best_phat = ph; f_sel = f; }
         }
     }
@@ -246,7 +325,7 @@ __device__ __forceinline__ void store_rgb(float* fb, size_t p, vec3 c) {
 
 __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G,
                                                                             ResBuf Rw, float* fb, int fuse_shade,
-                                                                            Counters* C) {
+                                                                            CountSlot C) {
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.gy0, F.gy1, F.W, x, y);
@@ -265,7 +344,7 @@ __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevSc
 
 // visibilityPass (pg/ReSTIRIntegrator.cpp:302-312).  Invalid samples always carry W == 0 already,
 // so their (meaningless) ray is not traced.
-__global__ void __launch_bounds__(256) k_visibility(DevScene S, FrameConst F, GBuf G, ResBuf R, Counters* C) {
+__global__ void __launch_bounds__(256) k_visibility(DevScene S, FrameConst F, GBuf G, ResBuf R, CountSlot C) {
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
@@ -296,7 +375,7 @@ __device__ __forceinline__ bool reproject(const GCam& c, vec3 ws, int W, int H, 
 // temporalReusePass (pg/ReSTIRIntegrator.cpp:625-732).  The previous reservoir is read at the
 // CURRENT pixel (:641), the previous G-buffer at the reprojected pixel (:652).
 __global__ void __launch_bounds__(256) k_temporal(DevScene S, FrameConst F, GBuf G, GBuf Gp, ResBuf Rr, ResBuf Rl,
-                                                  ResBuf Rw, Counters* C) {
+                                                  ResBuf Rw, CountSlot C) {
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
@@ -306,7 +385,7 @@ __global__ void __launch_bounds__(256) k_temporal(DevScene S, FrameConst F, GBuf
     int qx = x, qy = y, fx = x, fy = y;
     bool ok = in && reproject(F.camp, cur.pos, F.W, F.H, qx, qy);
     // rows outside the G-buffer margin of a tile are treated as a failed reprojection (counted)
-    if (ok && (qy < F.gy0 || qy >= F.gy1)) { ok = false; atomicAdd(&C->reproj_outside, 1ull); }
+    if (ok && (qy < F.gy0 || qy >= F.gy1)) { ok = false; atomicAdd(C.outside, 1ull); }
     const size_t q = ok ? (size_t)qy * F.W + qx : p;
     GElem prev = Gp.load(q);
     if (ok) {
@@ -317,7 +396,7 @@ __global__ void __launch_bounds__(256) k_temporal(DevScene S, FrameConst F, GBuf
     if (ok) {
         vec3 pac = Gp.pos(p);
         ok = reproject(F.cam, pac, F.W, F.H, fx, fy);
-        if (ok && (fy < F.gy0 || fy >= F.gy1)) { ok = false; atomicAdd(&C->reproj_outside, 1ull); }
+        if (ok && (fy < F.gy0 || fy >= F.gy1)) { ok = false; atomicAdd(C.outside, 1ull); }
         if (ok) {
             vec3 fw = G.pos((size_t)fy * F.W + fx);
             float cdp = length(pac - F.camp.pos), pdp = length(fw - F.cam.pos);
@@ -384,7 +463,7 @@ __device__ __forceinline__ size_t list_px(const FrameConst& F, const Rng& rng, u
 // List loops run to the uniform bound k+1 with `i < cnt` as a predicate (convergent ray queries).
 __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr,
                                                                    ResBuf Rw, int pass_idx, int fuse_shade, float* fb,
-                                                                   Counters* C) {
+                                                                   CountSlot C) {
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
@@ -525,7 +604,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
 }
 
 // shade loop (pg/simpleguidx11.cpp:447-472)
-__global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G, ResBuf Rr, float* fb, Counters* C) {
+__global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G, ResBuf Rr, float* fb, CountSlot C) {
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.y0, F.y1, F.W, x, y);

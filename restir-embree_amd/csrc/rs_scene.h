@@ -173,6 +173,64 @@ __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, ve
     return occ;
 }
 
+// K any-hit rays per lane sharing one origin (a pixel's shadow rays to K light samples), one lockstep
+// walk: each lane keeps K cursors, the wave steps through the union of all 64*K paths.  Shadow rays
+// of one tile overlap so heavily that the union barely grows with K (scripts/bvh_analysis.py: ~31
+// steps for K = 1..8 on C2), so steps per ray fall ~K-fold; each step's node (and leaf triangles) is
+// loaded once and tested against every ray whose cursor is on it.  Per ray, identical to occluded_ray.
+template <int K>
+__device__ __forceinline__ void occluded_wave_multi(const DevScene& S, const bool* active, vec3 o, const vec3* d,
+                                                    float tnear, const float* tfar, bool* occ) {
+    const bool full = __ballot(1) == ~0ull;
+    vec3 inv[K];
+    uint32_t cur[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        inv[k] = mk(1.0f / d[k].x, 1.0f / d[k].y, 1.0f / d[k].z);
+        cur[k] = active[k] ? 0u : 0xffffffffu;
+        occ[k] = false;
+    }
+    const uint32_t n = S.n_nodes;
+    while (true) {
+        uint32_t lm = cur[0];
+#pragma unroll
+        for (int k = 1; k < K; ++k) lm = cur[k] < lm ? cur[k] : lm;
+        const uint32_t m = full ? wave_min_full(lm) : wave_min_partial(lm);
+        if (m >= n) break;
+        const float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+        const uint32_t skip = (uint32_t)__float_as_int(a.w);
+        const int leaf = __float_as_int(b.w);
+        bool hb[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) hb[k] = cur[k] == m && box_test(a, b, o, inv[k], tnear, tfar[k]);
+        if (leaf >= 0) {                                      // wave-uniform
+            const int first = leaf >> 3, cnt = (leaf & 7) + 1;
+            for (int j = 0; j < cnt; ++j) {
+                bool want = false;
+#pragma unroll
+                for (int k = 0; k < K; ++k) want = want || (hb[k] && !occ[k]);
+                if (__ballot(want) == 0) break;
+                const uint32_t tri = 3u * (uint32_t)(first + j);
+                const float4 T0 = sload(S.tris, tri), T1 = sload(S.tris, tri + 1), T2 = sload(S.tris, tri + 2);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    if (hb[k] && !occ[k]) {
+                        float t, u, v;
+                        occ[k] = tri_test(T0, T1, T2, o, d[k], tnear, tfar[k], t, u, v);
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (cur[k] == m) cur[k] = (hb[k] && occ[k]) ? 0xffffffffu : skip;
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (cur[k] == m) cur[k] = hb[k] ? m + 1 : skip;
+        }
+    }
+}
+
 // rtcIntersect1 semantics, lockstep: closest hit in [tnear, tfar], ties to the smaller triangle index.
 __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     const bool full = __ballot(1) == ~0ull;
@@ -267,6 +325,16 @@ __device__ __forceinline__ bool trace_any(const DevScene& S, bool active, vec3 o
     return occluded_wave(S, active, o, d, tnear, tfar);
 #else
     return active ? occluded_ray(S, o, d, tnear, tfar) : false;
+#endif
+}
+template <int K>
+__device__ __forceinline__ void trace_any_multi(const DevScene& S, const bool* active, vec3 o, const vec3* d,
+                                                float tnear, const float* tfar, bool* occ) {
+#if RS_LOCKSTEP
+    occluded_wave_multi<K>(S, active, o, d, tnear, tfar, occ);
+#else
+#pragma unroll
+    for (int k = 0; k < K; ++k) occ[k] = active[k] ? occluded_ray(S, o, d[k], tnear, tfar[k]) : false;
 #endif
 }
 __device__ __forceinline__ Hit trace_closest(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
