@@ -27,6 +27,11 @@ sys.path.insert(0, os.path.join(ROOT, "restir-embree_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+WORKLOADS = {
+    "C1": "Cornell box, 8 emissive quads, reference defaults (A=1 B=1, no reuse)",
+    "C2": "Cornell box + 1024 emissive quads, A=32 B=1, spatial k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20",
+    "C3": "Sponza-like ~250k tris, 4096 emissive triangles (2048 lamp quads), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
+}
 # algorithmic bytes per pixel of the dominant kernel k_gbuffer_initial: G-buffer record write
 # (5 x float4 = 80 B) + reservoir write (3 x float4 = 48 B); scene/BVH reads are cache-resident
 # shared data, not per-pixel traffic.  DESIGN.md "Roofline".
@@ -154,6 +159,10 @@ def main():
                 traffic = pmc.get("k_gbuffer_initial_bytes_per_launch")
         except Exception:
             traffic = None
+    trav_name = None
+    if world == 1:
+        _, last_kind, _ = r.traversal(gs)
+        trav_name = {0: "lockstep", 1: "lane"}.get(last_kind)
     if rank == 0:
         out = {
             "metric": "Mrays/s + frames/s at 1080p, 32 candidates, 4 spatial neighbours",
@@ -167,10 +176,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (procedural scene, BASELINE.json configs[1])",
-            "config": {"workload": f"{args.scene}: Cornell box + 1024 emissive quads, {W}x{H}, A=32 B=1, "
-                                   f"spatial k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20",
-                       "width": W, "height": H, "parallelism": f"row-bands x{world}" if world > 1 else "1 GPU"},
+            "data": f"synthetic (procedural scene, BASELINE.json configs[{ {'C1': 0, 'C2': 1, 'C3': 2}[args.scene]}])",
+            "config": {"workload": f"{args.scene}: {WORKLOADS[args.scene]}, {W}x{H}",
+                       "width": W, "height": H, "parallelism": f"row-bands x{world}" if world > 1 else "1 GPU",
+                       "traversal": trav_name},
             "mrays_per_s": round(mrays, 2),
             "rays_per_frame": rays // max(1, args.steps),
             "pass_ms": {k: round(v / args.steps, 4) for k, v in acc.items()},

@@ -110,8 +110,9 @@ const char* rs_last_error(const rs_context* ctx);   /* ctx may be NULL: last glo
 
 /* ---- scene load (Scene::Scene + ModelLoader::loadScene + rtcCommitScene) ---------------------- */
 /* Uploads the triangles, builds the emissive-triangle CDF (TriangleCDF ctor, pg/TriangleCDF.cpp:8-34)
- * and builds the BVH on the GPU (LBVH: Morton codes -> radix sort -> Karras hierarchy -> level refit
- * -> depth-first skip-pointer layout).  Replaces rtcNewScene/rtcCommitScene (pg/Scene.cpp:10,15). */
+ * and builds the BVH on the GPU (PLOC agglomerative clustering over Morton-sorted triangles -> SAH
+ * leaf collapse -> depth-first skip-pointer layout; env RESTIR_BVH=lbvh selects the Karras LBVH).
+ * Replaces rtcNewScene/rtcCommitScene (pg/Scene.cpp:10,15). */
 int rs_scene_create(rs_context* ctx, const rs_mesh_desc* meshes, uint32_t n_meshes,
                     const rs_material_desc* materials, uint32_t n_materials, rs_scene** out);
 /* OBJ/MTL loader honouring Pc (material class), Kd/Ks (sRGB-expanded), Ke, Ns
@@ -137,6 +138,21 @@ int rs_get_frame_device_ptr(rs_context* ctx, const float** dptr);
 int rs_reset_history(rs_context* ctx);
 /* Wait for all work queued on the context's stream. */
 int rs_synchronize(rs_context* ctx);
+
+/* ---- BVH traversal kind (no reference counterpart: Embree picks its own kernels) ---------------
+ * LOCKSTEP: a wave walks the node array together (scalar node loads) -- best for coherent rays.
+ * LANE: every lane walks its own path (vector loads) -- best for incoherent rays in large scenes.
+ * AUTO (default; env RESTIR_TRAVERSAL=lockstep|lane overrides at context creation): the first four
+ * frames of a scene alternate the kinds and time them (the first frame of each kind is a warm-up),
+ * later frames use the faster one.  Both kinds return bit-identical frames. */
+#define RS_TRAVERSAL_AUTO (-1)
+#define RS_TRAVERSAL_LOCKSTEP 0
+#define RS_TRAVERSAL_LANE 1
+int rs_context_set_traversal(rs_context* ctx, int mode);
+/* mode: the requested mode; last_kind: kind the last frame ran with; scene_choice: the kind AUTO
+ * settled on for `scene` (-1 while still timing; scene may be NULL). */
+int rs_context_get_traversal(const rs_context* ctx, const rs_scene* scene, int* mode, int* last_kind,
+                             int* scene_choice);
 
 /* ---- state dumps for golden parity ------------------------------------------------------- */
 /* G-buffer of the last rendered frame (prev=0) or the one before (prev=1): W*H*19 floats per pixel

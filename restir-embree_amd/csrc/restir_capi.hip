@@ -33,6 +33,10 @@ struct rs_scene {
     float* d_cdf = nullptr;
     int* d_cdf_guide = nullptr;
     float build_ms = 0.0f;
+    // per-scene traversal choice (RS_TRAVERSAL_AUTO): frame times of each kind, tuning frames counted
+    mutable int trav_choice = -1;
+    mutable int trav_runs[2] = {0, 0};
+    mutable float trav_ms[2] = {0.0f, 0.0f};
     DevScene dev() const {
         DevScene S;
         S.nodes = d_nodes; S.tris = d_tris; S.tri_nrm = d_tri_nrm; S.mats = d_mats; S.emis = d_emis; S.cdf = d_cdf; S.cdf_guide = d_cdf_guide;
@@ -68,6 +72,10 @@ struct rs_context {
     rs_tile_desc tile = {};
     int ra = 0, rb = 1, rcur = 0, last = 2;
     bool temporal_ran = false, spatial_ran = false, shade_fused = false, ev_temporal = false;
+    // traversal kind (rs_scene.h Trav): requested mode, kind of the frame in flight, tuning frame flag
+    int trav_mode = RS_TRAVERSAL_AUTO;
+    int trav = TRAV_LOCKSTEP;
+    bool tuning = false;
 };
 
 // --------------------------------------------------------------------------- helpers
@@ -193,7 +201,27 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
     for (auto& e : c->ev)
         if (hipEventCreate(&e) != hipSuccess) return bail("hipEventCreate failed");
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail("context init failed");
+    if (const char* t = std::getenv("RESTIR_TRAVERSAL")) {     // auto (default) | lockstep | lane
+        if (!std::strcmp(t, "lockstep")) c->trav_mode = RS_TRAVERSAL_LOCKSTEP;
+        else if (!std::strcmp(t, "lane")) c->trav_mode = RS_TRAVERSAL_LANE;
+    }
     *out = c;
+    return RS_OK;
+}
+
+extern "C" int rs_context_set_traversal(rs_context* c, int mode) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_context_set_traversal: null context");
+    if (mode != RS_TRAVERSAL_AUTO && mode != RS_TRAVERSAL_LOCKSTEP && mode != RS_TRAVERSAL_LANE)
+        return fail(c, RS_E_INVALID, "rs_context_set_traversal: mode must be RS_TRAVERSAL_AUTO/LOCKSTEP/LANE");
+    c->trav_mode = mode;
+    return RS_OK;
+}
+extern "C" int rs_context_get_traversal(const rs_context* c, const rs_scene* s, int* mode, int* last_kind,
+                                        int* scene_choice) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_context_get_traversal: null context");
+    if (mode) *mode = c->trav_mode;
+    if (last_kind) *last_kind = c->trav;
+    if (scene_choice) *scene_choice = s ? s->trav_choice : -1;
     return RS_OK;
 }
 
@@ -379,6 +407,37 @@ extern "C" int rs_scene_info(const rs_scene* s, uint32_t* n_tris, uint32_t* n_em
 
 // --------------------------------------------------------------------------- frame / tile driver
 static dim3 grid_rows(int W, int ya, int yb) { return dim3((W + 15) / 16, (yb - ya + 15) / 16); }
+
+// launch kernel<Trav> for the frame's traversal kind
+#define LAUNCH_TRAV(c, kernel, grid, ...)                                                      \
+    do {                                                                                       \
+        if ((c)->trav == TRAV_LANE) kernel<TRAV_LANE><<<(grid), 256, 0, (c)->stream>>>(__VA_ARGS__); \
+        else kernel<TRAV_LOCKSTEP><<<(grid), 256, 0, (c)->stream>>>(__VA_ARGS__);           \
+    } while (0)
+
+// RS_TRAVERSAL_AUTO: the first frames of a scene alternate the two kinds; per kind the first run is a
+// warm-up (lazy code-object load, cold caches), the next kTuneRuns-1 are timed (EV_BEGIN..EV_SHADE).
+constexpr int kTuneRuns = 2;
+static void pick_traversal(rs_context* c, const rs_scene* s) {
+    c->tuning = false;
+    if (c->trav_mode == RS_TRAVERSAL_LOCKSTEP) { c->trav = TRAV_LOCKSTEP; return; }
+    if (c->trav_mode == RS_TRAVERSAL_LANE) { c->trav = TRAV_LANE; return; }
+    if (s->trav_choice >= 0) { c->trav = s->trav_choice; return; }
+    c->trav = s->trav_runs[TRAV_LOCKSTEP] <= s->trav_runs[TRAV_LANE] ? TRAV_LOCKSTEP : TRAV_LANE;
+    c->tuning = true;
+}
+static void record_traversal_time(rs_context* c) {
+    if (!c->tuning) return;
+    c->tuning = false;
+    float ms = 0.0f;
+    if (hipEventSynchronize(c->ev[EV_SHADE]) != hipSuccess ||
+        hipEventElapsedTime(&ms, c->ev[EV_BEGIN], c->ev[EV_SHADE]) != hipSuccess)
+        return;
+    const rs_scene* s = c->scene;
+    if (++s->trav_runs[c->trav] > 1) s->trav_ms[c->trav] += ms;
+    if (s->trav_runs[TRAV_LOCKSTEP] >= kTuneRuns && s->trav_runs[TRAV_LANE] >= kTuneRuns)
+        s->trav_choice = s->trav_ms[TRAV_LANE] < s->trav_ms[TRAV_LOCKSTEP] ? TRAV_LANE : TRAV_LOCKSTEP;
+}
 static size_t grid_waves(dim3 g) { return (size_t)g.x * g.y * 4; }
 
 // ray-count slots for one launch (rs_passes.h CountSlot); capacity is reserved in rs_tile_begin
@@ -454,13 +513,14 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     if (!reserve_count_slots(c, P, F.gy0, F.gy1, F.y0, F.y1)) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
     HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->stream));
     HIPCHK(c, hipEventRecord(c->ev[EV_BEGIN], c->stream));
+    pick_traversal(c, s);
     const dim3 gg = grid_rows(c->W, F.gy0, F.gy1), gb = grid_rows(c->W, F.y0, F.y1);
-    k_gbuffer_initial<<<gg, 256, 0, c->stream>>>(S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
-                                                 count_slot(c, gg));
+    LAUNCH_TRAV(c, k_gbuffer_initial, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
+                count_slot(c, gg));
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[EV_INIT], c->stream));
     if (P->do_visibility_pass) {
-        k_visibility<<<gb, 256, 0, c->stream>>>(S, F, c->G[gnew], ResBuf{c->R[c->ra]}, count_slot(c, gb));
+        LAUNCH_TRAV(c, k_visibility, gb, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(c->ev[EV_VIS], c->stream));
@@ -492,8 +552,8 @@ extern "C" int rs_tile_temporal(rs_context* c) {
     if (c->P.do_temporal && c->frames > 0 && !c->temporal_ran) {
         const DevScene S = c->scene->dev();
         const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
-        k_temporal<<<gb, 256, 0, c->stream>>>(S, c->F, c->G[c->gcur], c->G[c->gcur ^ 1], ResBuf{c->R[c->rcur]},
-                                              ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
+        LAUNCH_TRAV(c, k_temporal, gb, S, c->F, c->G[c->gcur], c->G[c->gcur ^ 1], ResBuf{c->R[c->rcur]},
+                    ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
         c->rcur = c->rb;
         c->temporal_ran = true;
@@ -521,8 +581,8 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
     int dst = (c->rcur == c->ra) ? c->rb : c->ra;
     int fuse = (pass_index == c->P.spatial_passes - 1) ? 1 : 0;
     const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
-    k_spatial<<<gb, 256, 0, c->stream>>>(S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]}, ResBuf{c->R[dst]}, pass_index,
-                                         fuse, c->fb, count_slot(c, gb));
+    LAUNCH_TRAV(c, k_spatial, gb, S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]}, ResBuf{c->R[dst]}, pass_index, fuse,
+                c->fb, count_slot(c, gb));
     HIPCHK(c, hipGetLastError());
     c->rcur = dst;
     if (fuse) c->shade_fused = true;
@@ -546,10 +606,11 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
     if (!c->shade_fused) {
         const DevScene S = c->scene->dev();
         const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
-        k_shade<<<gb, 256, 0, c->stream>>>(S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]}, c->fb, count_slot(c, gb));
+        LAUNCH_TRAV(c, k_shade, gb, S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]}, c->fb, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(c->ev[EV_SHADE], c->stream));
+    record_traversal_time(c);
     c->r_last = c->rcur;   // reservoirsLastFrame = final buffer (pointer swap, :477)
     c->frames++;
     c->active = false;
@@ -660,13 +721,12 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
     const uint32_t i = act ? i0 : n - 1;
     vec3 O = mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), D = mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
     if (any == 1 || any == 3) {
-        bool occ = any == 1 ? occluded_wave(S, act, O, D, tn[i], tf[i])
-                            : (act ? occluded_ray(S, O, D, tn[i], tf[i]) : false);
+        bool occ = any == 1 ? trace_any<TRAV_LOCKSTEP>(S, act, O, D, tn[i], tf[i])
+                            : trace_any<TRAV_LANE>(S, act, O, D, tn[i], tf[i]);
         if (act) { prim_out[i] = occ ? 1 : 0; t_out[i] = 0.0f; }
     } else {
-        Hit h;
-        if (any == 0) h = closest_wave(S, act, O, D, tn[i], tf[i]);
-        else { h.prim = -1; h.t = 0; if (act) h = closest_ray(S, O, D, tn[i], tf[i]); }
+        Hit h = any == 0 ? trace_closest<TRAV_LOCKSTEP>(S, act, O, D, tn[i], tf[i])
+                         : trace_closest<TRAV_LANE>(S, act, O, D, tn[i], tf[i]);
         if (act) { prim_out[i] = h.prim; t_out[i] = h.prim >= 0 ? h.t : -1.0f; }
     }
 }

@@ -297,8 +297,14 @@ fail:
 // ============================================================================================
 constexpr int kRadius = 16;
 constexpr int kPlocBlock = 256;
-constexpr int kLeafMaxSah = 8;
-constexpr float kCtrav = 1.0f, kCtri = 1.0f;
+#ifndef RS_LEAF_MAX
+#define RS_LEAF_MAX 8
+#endif
+#ifndef RS_SAH_CTRI
+#define RS_SAH_CTRI 1.0f
+#endif
+constexpr int kLeafMaxSah = RS_LEAF_MAX;          // <= 8 (leaf word: (first << 3) | (count - 1))
+constexpr float kCtrav = 1.0f, kCtri = RS_SAH_CTRI;
 
 __device__ __forceinline__ float half_area(float4 lo, float4 hi) {
     float ex = hi.x - lo.x, ey = hi.y - lo.y, ez = hi.z - lo.z;

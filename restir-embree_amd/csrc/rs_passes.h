@@ -95,19 +95,20 @@ __device__ __forceinline__ bool pixel_of(int ya, int yb, int W, int& x, int& y) 
 }
 
 // Intersection::testOcclusion (pg/Intersection.h:43-60): from the surface point, no normal offset
+template <int T>
 __device__ __forceinline__ bool occluded(const DevScene& S, const FrameConst& F, bool active, vec3 from, vec3 to,
                                          uint32_t& rays) {
     float dist = length(to - from);
     vec3 dir = normalize(to - from);
     rays += active ? 1u : 0u;
-    return trace_any(S, active, from, dir, FLT_MIN + F.tnear_off, dist - F.tfar_off);
+    return trace_any<T>(S, active, from, dir, FLT_MIN + F.tnear_off, dist - F.tfar_off);
 }
 
 // ReSTIRIntegrator::evaluateF (pg/ReSTIRIntegrator.cpp:185-211) for the lanes with `alive`.  The
 // shadow ray is skipped when L_i*f_r*G is exactly zero in every channel (0 whatever V is).
 // Split in two around the shadow ray so callers can batch several rays into one traversal:
 // evaluate_f_pre computes the unoccluded L and the testOcclusion ray (dir = normalize(p - pos),
-// tfar = |p - pos| - tfarOffset, exactly as occluded() forms them); evaluate_f_post applies V.
+// tfar = |p - pos| - tfarOffset, exactly as occluded<T>() forms them); evaluate_f_post applies V.
 struct FPre { vec3 L, dir; float tfar; bool ok, need; };
 __device__ __forceinline__ FPre evaluate_f_pre(const FrameConst& F, const Sample& s, vec3 cam, const GElem& g,
                                                bool test_vis, bool alive) {
@@ -130,13 +131,14 @@ __device__ __forceinline__ vec3 evaluate_f_post(const FPre& p, bool occ) {
     if (p.need) L = L * (float)(!occ);
     return p.ok ? L : mk(0, 0, 0);
 }
+template <int T>
 __device__ __forceinline__ vec3 evaluate_f(const DevScene& S, const FrameConst& F, const Sample& s, vec3 cam,
                                            const GElem& g, bool test_vis, bool alive, uint32_t& rays) {
     FPre p = evaluate_f_pre(F, s, cam, g, test_vis, alive);
     bool occ = false;
     if (test_vis) {                                                   // test_vis is wave-uniform
         rays += p.need ? 1u : 0u;
-        occ = trace_any(S, p.need, g.pos, p.dir, FLT_MIN + F.tnear_off, p.tfar);
+        occ = trace_any<T>(S, p.need, g.pos, p.dir, FLT_MIN + F.tnear_off, p.tfar);
     }
     return evaluate_f_post(p, occ);
 }
@@ -152,13 +154,14 @@ __device__ __forceinline__ float m_brdf(const FrameConst& F, float pb, float pa)
 }
 
 // gBufferFillPass (pg/ReSTIRIntegrator.cpp:213-234) + Camera::GenerateRay (pg/camera.cpp:20-42)
+template <int T>
 __device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameConst& F, int x, int y, bool active) {
     vec3 dc = mk((float)x - (float)F.W / 2.0f, (float)F.H / 2.0f - (float)y, -F.cam.focal);
     const float* m = F.inv_view;
     vec3 dw = mk(m[0] * dc.x + m[3] * dc.y + m[6] * dc.z, m[1] * dc.x + m[4] * dc.y + m[7] * dc.z,
                  m[2] * dc.x + m[5] * dc.y + m[8] * dc.z);
     dw = normalize(dw);
-    SurfHit h = intersect(S, active, F.cam.pos, dw, FLT_MIN + 0.01f);
+    SurfHit h = intersect<T>(S, active, F.cam.pos, dw, FLT_MIN + 0.01f);
     GElem g;
     g.pos = mk(0, 0, 0); g.nrm = g.pos; g.kd = g.pos; g.ks = g.pos; g.le = g.pos;
     g.shin = 0; g.depth = 0; g.type = 0; g.inv_im = 0;
@@ -215,13 +218,14 @@ __device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameCons
 }
 
 // brdfSampleLight (pg/ReSTIRIntegrator.cpp:126-177)
+template <int T>
 __device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameConst& F, const GElem& g, vec3 cam,
                                               bool alive, Rng& rng, float& W_out, float& mis_out, uint32_t& rays) {
     float pdf;
     vec3 wi = sample_brdf(g, cam, rng, pdf);
     vec3 org = g.pos + g.nrm * F.normal_off;
     rays += alive ? 1u : 0u;
-    SurfHit h = intersect(S, alive, org, wi, FLT_MIN + F.tnear_off);
+    SurfHit h = intersect<T>(S, alive, org, wi, FLT_MIN + F.tnear_off);
     W_out = 0.0f; mis_out = 0.0f;
     if (h.hit) {
         MatRec mr = load_mat(S, h.mat);
@@ -244,6 +248,7 @@ __device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameCons
 // initialRenderPass (pg/ReSTIRIntegrator.cpp:236-298) for the lanes with `in_pass`.  f_sel returns the
 // selected candidate's f (for the fused shade); the final p-hat (:289) equals the selected candidate's
 // p-hat (same arguments), so it is not re-evaluated.
+template <int T>
 __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& F, const GElem& g, uint32_t pix,
                                            bool in_pass, vec3& f_sel, uint32_t& rays) {
     f_sel = mk(0, 0, 0);
@@ -275,7 +280,7 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
                 act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
                 rays += act[k] ? 1u : 0u;
             }
-            if (tv) trace_any_multi<RS_RIS_BATCH>(S, act, g.pos, dir, FLT_MIN + F.tnear_off, tf, occ);
+            if (tv) trace_any_multi<T, RS_RIS_BATCH>(S, act, g.pos, dir, FLT_MIN + F.tnear_off, tf, occ);
 #pragma unroll
             for (int k = 0; k < RS_RIS_BATCH; ++k) {
                 if (c0 + k < F.m_area) {
@@ -299,8 +304,8 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
         for (int i = 0; i < F.m_brdf; ++i) {
             float Wc, mis;
             rng.n = cand_slot(F.m_area + i);
-            Sample s = brdf_sample(S, F, g, cam, alive, rng, Wc, mis, rays);
-            vec3 f = evaluate_f(S, F, s, cam, g, tv, alive, rays);
+            Sample s = brdf_sample<T>(S, F, g, cam, alive, rng, Wc, mis, rays);
+            vec3 f = evaluate_f<T>(S, F, s, cam, g, tv, alive, rays);
             float ph = length(f);
             float w = F.m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
             rng.n = cand_slot(F.m_area + i) + 3u;
@@ -323,6 +328,7 @@ __device__ __forceinline__ void store_rgb(float* fb, size_t p, vec3 c) {
     fb[3 * p] = c.x; fb[3 * p + 1] = c.y; fb[3 * p + 2] = c.z;
 }
 
+template <int T>
 __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G,
                                                                             ResBuf Rw, float* fb, int fuse_shade,
                                                                             CountSlot C) {
@@ -330,11 +336,11 @@ __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevSc
     uint32_t rays = 0;
     const bool in = pixel_of(F.gy0, F.gy1, F.W, x, y);
     const size_t p = (size_t)y * F.W + x;
-    GElem g = gbuffer_fill(S, F, x, y, in);
+    GElem g = gbuffer_fill<T>(S, F, x, y, in);
     if (in) G.store(p, g);
     const bool ris = in && y >= F.y0 && y < F.y1;
     vec3 f;
-    Res r = initial_ris(S, F, g, (uint32_t)p, ris, f, rays);
+    Res r = initial_ris<T>(S, F, g, (uint32_t)p, ris, f, rays);
     if (ris) {
         Rw.store(p, r);
         if (fuse_shade) store_rgb(fb, p, shade_px(r, f, g.le));
@@ -344,6 +350,7 @@ __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevSc
 
 // visibilityPass (pg/ReSTIRIntegrator.cpp:302-312).  Invalid samples always carry W == 0 already,
 // so their (meaningless) ray is not traced.
+template <int T>
 __global__ void __launch_bounds__(256) k_visibility(DevScene S, FrameConst F, GBuf G, ResBuf R, CountSlot C) {
     int x, y;
     uint32_t rays = 0;
@@ -351,7 +358,7 @@ __global__ void __launch_bounds__(256) k_visibility(DevScene S, FrameConst F, GB
     const size_t p = (size_t)y * F.W + x;
     Res r = R.load(p);
     const bool need = in && smp_valid(smp_of(r));
-    if (occluded(S, F, need, G.pos(p), r.p, rays) && need) R.r[3 * p + 1].w = 0.0f;
+    if (occluded<T>(S, F, need, G.pos(p), r.p, rays) && need) R.r[3 * p + 1].w = 0.0f;
     count_rays(C, rays, 0);
 }
 
@@ -374,6 +381,7 @@ __device__ __forceinline__ bool reproject(const GCam& c, vec3 ws, int W, int H, 
 
 // temporalReusePass (pg/ReSTIRIntegrator.cpp:625-732).  The previous reservoir is read at the
 // CURRENT pixel (:641), the previous G-buffer at the reprojected pixel (:652).
+template <int T>
 __global__ void __launch_bounds__(256) k_temporal(DevScene S, FrameConst F, GBuf G, GBuf Gp, ResBuf Rr, ResBuf Rl,
                                                   ResBuf Rw, CountSlot C) {
     int x, y;
@@ -410,13 +418,13 @@ __global__ void __launch_bounds__(256) k_temporal(DevScene S, FrameConst F, GBuf
         Rng rng; rng.init(F.seed, F.frame, PASS_TEMPORAL, (uint32_t)p);
         Res res = res_empty();
         Sample cs = smp_of(cr), ps = smp_of(pr);
-        float p_cur = length(evaluate_f(S, F, cs, F.cam.pos, cur, true, ok, rays));
-        float p_prev = length(evaluate_f(S, F, cs, F.camp.pos, prev, true, ok, rays));
+        float p_cur = length(evaluate_f<T>(S, F, cs, F.cam.pos, cur, true, ok, rays));
+        float p_prev = length(evaluate_f<T>(S, F, cs, F.camp.pos, prev, true, ok, rays));
         float m_cur = p_cur * (float)cr.conf / (p_cur * (float)cr.conf + p_prev * (float)pr.conf);
         if (!(m_cur > 0)) m_cur = 0.0f;
         float ph_cur = p_cur;
-        float p_cur2 = length(evaluate_f(S, F, ps, F.cam.pos, cur, true, ok, rays));
-        float p_prev2 = length(evaluate_f(S, F, ps, F.camp.pos, prev, true, ok, rays));
+        float p_cur2 = length(evaluate_f<T>(S, F, ps, F.cam.pos, cur, true, ok, rays));
+        float p_prev2 = length(evaluate_f<T>(S, F, ps, F.camp.pos, prev, true, ok, rays));
         if (ok) {
             bool took_cur = res_add(res, cs, m_cur * ph_cur * cr.W, cr.conf, rng);
             float m_prev = p_prev2 * (float)pr.conf / (p_cur2 * (float)cr.conf + p_prev2 * (float)pr.conf);
@@ -461,6 +469,7 @@ __device__ __forceinline__ size_t list_px(const FrameConst& F, const Rng& rng, u
 
 // spatialReusePass (pg/ReSTIRIntegrator.cpp:316-542); shade fused when this is the last pass.
 // List loops run to the uniform bound k+1 with `i < cnt` as a predicate (convergent ray queries).
+template <int T>
 __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr,
                                                                    ResBuf Rw, int pass_idx, int fuse_shade, float* fb,
                                                                    CountSlot C) {
@@ -524,7 +533,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
                     const bool lj = li && j < cnt;
                     size_t qj = list_px(F, rng, acc, j, x, y, p);
                     int cj = __float_as_int(Rr.r[3 * qj + 2].w);
-                    float ph = length(evaluate_f(S, F, si, cam, G.load(qj), true, lj, rays));
+                    float ph = length(evaluate_f<T>(S, F, si, cam, G.load(qj), true, lj, rays));
                     if (lj) {
                         den += ph * cj;
                         if (i == j) num = ph * ri.conf;
@@ -536,12 +545,12 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
                 mis = 0.0f;
                 if (i == 0) {
                     float sum = 0.0f;
-                    float phc = length(evaluate_f(S, F, si, cam, G.load(qi), true, li, rays)) * (float)ri.conf;
+                    float phc = length(evaluate_f<T>(S, F, si, cam, G.load(qi), true, li, rays)) * (float)ri.conf;
                     for (int j = 1; j < kk; ++j) {
                         const bool lj = li && j < cnt;
                         size_t qj = list_px(F, rng, acc, j, x, y, p);
                         int cj = __float_as_int(Rr.r[3 * qj + 2].w);
-                        float phj = length(evaluate_f(S, F, si, cam, G.load(qj), true, lj, rays));
+                        float phj = length(evaluate_f<T>(S, F, si, cam, G.load(qj), true, lj, rays));
                         float den = phc + phj * (float)csum_nc;
                         if (lj && den > 0) {
                             float cf = (float)cj / (float)csum;
@@ -550,15 +559,15 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
                     }
                     mis = ((float)ri.conf / (float)csum) + sum;
                 } else {
-                    float phi = length(evaluate_f(S, F, si, cam, G.load(qi), true, li, rays));
-                    float phc = length(evaluate_f(S, F, si, cam, G.load(p), true, li, rays));
+                    float phi = length(evaluate_f<T>(S, F, si, cam, G.load(qi), true, li, rays));
+                    float phc = length(evaluate_f<T>(S, F, si, cam, G.load(p), true, li, rays));
                     phi *= (float)csum_nc;
                     int c0 = __float_as_int(Rr.r[3 * p + 2].w);
                     float den = phi + phc * (float)c0;
                     if (den > 0 && csum > 0) mis = ((float)ri.conf / (float)csum) * (phi / den);
                 }
             }
-            vec3 f = evaluate_f(S, F, si, cam, th, true, li, rays);     // :472
+            vec3 f = evaluate_f<T>(S, F, si, cam, th, true, li, rays);     // :472
             float rph = length(f);
             float rw = mis * rph * ri.W;
             if (li && res_add(res, si, rw, ri.conf, rng)) { sel = i; f_sel = f; }
@@ -572,7 +581,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
             for (int i = 0; i < kk; ++i) {
                 const bool li = alive && i < cnt;
                 size_t qi = list_px(F, rng, acc, i, x, y, p);
-                bool occ = occluded(S, F, li, G.pos(qi), res.p, rays);
+                bool occ = occluded<T>(S, F, li, G.pos(qi), res.p, rays);
                 if (li && !occ) Z += 1;
             }
             if (Z > 0 && M > 0) corr = (1.0f / (float)Z) / rcpM;
@@ -584,7 +593,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
                 const bool li = alive && i < cnt;
                 size_t qi = list_px(F, rng, acc, i, x, y, p);
                 int ci = __float_as_int(Rr.r[3 * qi + 2].w);
-                float ph = length(evaluate_f(S, F, ss, cam, G.load(qi), true, li, rays));
+                float ph = length(evaluate_f<T>(S, F, ss, cam, G.load(qi), true, li, rays));
                 if (li) {
                     den += ph * (float)ci;
                     if (i == sel) num = ph * (float)ci;
@@ -604,6 +613,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
 }
 
 // shade loop (pg/simpleguidx11.cpp:447-472)
+template <int T>
 __global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G, ResBuf Rr, float* fb, CountSlot C) {
     int x, y;
     uint32_t rays = 0;
@@ -611,7 +621,7 @@ __global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G,
     const size_t p = (size_t)y * F.W + x;
     Res r = Rr.load(p);
     GElem g = G.load(p);
-    vec3 f = evaluate_f(S, F, smp_of(r), F.cam.pos, g, true, in && r.wsum > 0.0f, rays);
+    vec3 f = evaluate_f<T>(S, F, smp_of(r), F.cam.pos, g, true, in && r.wsum > 0.0f, rays);
     if (in) store_rgb(fb, p, shade_px(r, f, g.le));
     count_rays(C, rays, 0);
 }

@@ -9,16 +9,14 @@
 //   (v0.xyz, prim), (e1.xyz, 0), (e2.xyz, 0)   with e1 = v1 - v0, e2 = v2 - v0 (same float ops the
 //   CPU restatement does on the fly), prim = original triangle index (int bits).
 // Shading attributes are indexed by prim: 3 float4 vertex normals + material/emissive id.
+//
+// Two traversal kinds, selected per launch as a template parameter (Trav); both return bit-identical
+// results (same box/triangle tests, same tie rule), they differ only in how a wave walks the array:
+//   TRAV_LOCKSTEP  the wave walks the node array together (coherent rays: C2's shadow/primary rays)
+//   TRAV_LANE      every lane walks its own path with vector loads (incoherent rays: C3)
+// The context picks the faster kind per scene by timing (restir_capi.hip pick_traversal).
 #pragma once
 #include "rs_device.h"
-
-#ifndef RS_TRAV_ATTR
-#if defined(RS_TRAV_INLINE) && RS_TRAV_INLINE
-#define RS_TRAV_ATTR __device__ __forceinline__
-#else
-#define RS_TRAV_ATTR __device__ __noinline__
-#endif
-#endif
 
 namespace rs {
 
@@ -34,6 +32,8 @@ struct DevScene {
     uint32_t n_nodes, n_tris, n_emis, n_mats;
 };
 constexpr int kCdfGuide = 1024;
+
+enum Trav : int { TRAV_LOCKSTEP = 0, TRAV_LANE = 1 };
 
 // Moller-Trumbore, fixed op order (identical to oracle/restir_oracle.c tri_hit)
 __device__ __forceinline__ bool tri_test(float4 A, float4 B, float4 C, vec3 o, vec3 d, float tnear,
@@ -65,8 +65,51 @@ __device__ __forceinline__ bool box_test(float4 a, float4 b, vec3 o, vec3 inv, f
     return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
 }
 
-// rtcOccluded1 semantics (pg/Intersection.h:43-60): any hit with t in [tnear, tfar]
-RS_TRAV_ATTR bool occluded_ray(const DevScene& S, vec3 o, vec3 d, float tnear, float tfar) {
+struct Hit { float t, u, v; int prim; };
+
+// uniform-index load through the constant address space -> s_load (scalar cache), no VGPR address
+__device__ __forceinline__ float4 sload(const float4* p, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const float __attribute__((address_space(4)))* cfloat_ptr;
+    cfloat_ptr q = (cfloat_ptr)(const float*)(p + i);
+    return make_float4(q[0], q[1], q[2], q[3]);
+#else
+    return p[i];   // host pass only type-checks device code
+#endif
+}
+template <bool Uniform>
+__device__ __forceinline__ float4 ld4(const float4* p, uint32_t i) {
+    if (Uniform) return sload(p, i);
+    return p[i];
+}
+
+// ---------------------------------------------------------------- node visit
+// one node of a closest-hit walk (rtcIntersect1; ties: smaller t, then smaller triangle index).  The box
+// test culls against the running closest t; with the tie rule applied at every accepted triangle the
+// result does not depend on the visit order.
+template <bool Uniform>
+__device__ __forceinline__ void closest_visit(const DevScene& S, float4 a, float4 b, uint32_t i, vec3 o, vec3 d,
+                                              vec3 inv, float tnear, uint32_t& cur, Hit& h) {
+    const uint32_t skip = (uint32_t)__float_as_int(a.w);
+    if (!box_test(a, b, o, inv, tnear, h.t)) { cur = skip; return; }
+    const int leaf = __float_as_int(b.w);
+    if (leaf < 0) { cur = i + 1; return; }
+    const int first = leaf >> 3, cnt = (leaf & 7) + 1;
+    for (int j = 0; j < cnt; ++j) {
+        const uint32_t tri = 3u * (uint32_t)(first + j);
+        const float4 T0 = ld4<Uniform>(S.tris, tri);
+        float t, u, v;
+        if (tri_test(T0, ld4<Uniform>(S.tris, tri + 1), ld4<Uniform>(S.tris, tri + 2), o, d, tnear, h.t, t, u, v)) {
+            const int prim = __float_as_int(T0.w);
+            if (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim)) { h.t = t; h.u = u; h.v = v; h.prim = prim; }
+        }
+    }
+    cur = skip;
+}
+
+// ---------------------------------------------------------------- per-lane walks (TRAV_LANE)
+__device__ __forceinline__ bool occluded_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    if (!active) return false;
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     uint32_t i = 0;
     const uint32_t n = S.n_nodes;
@@ -92,27 +135,27 @@ RS_TRAV_ATTR bool occluded_ray(const DevScene& S, vec3 o, vec3 d, float tnear, f
     }
     return false;
 }
+__device__ __forceinline__ Hit closest_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
+    const uint32_t n = S.n_nodes;
+    uint32_t cur = active ? 0u : 0xffffffffu;
+    while (cur < n) {
+        const uint32_t i = cur;
+        closest_visit<false>(S, S.nodes[2 * i], S.nodes[2 * i + 1], i, o, d, inv, tnear, cur, h);
+    }
+    return h;
+}
 
-struct Hit { float t, u, v; int prim; };
-
-// ---------------------------------------------------------------- wave-coherent (lockstep) traversal
+// ---------------------------------------------------------------- wave-coherent walks (TRAV_LOCKSTEP)
 // The skip-pointer order is a global order and every ray only moves forward through it, so a wave
 // can walk the node array together: each step it takes m = min over lanes of their next node, loads
 // node m ONCE with scalar loads (uniform address, no 64-address gather), and only the lanes whose
 // next node is m test it.  The number of steps is the size of the union of the lanes' paths -- for
 // a wave's shadow rays from one 8x8 tile this is ~ the longest single path (scripts/bvh_analysis.py:
 // union 30.4 vs longest 28.9 nodes on C2) -- while per-step memory traffic drops from up to 64 cache
-// lines to one.  Results are identical to the per-lane traversal (same tests, same tie rule).
-// uniform-index load through the constant address space -> s_load (scalar cache), no VGPR address
-__device__ __forceinline__ float4 sload(const float4* p, uint32_t i) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    typedef const float __attribute__((address_space(4)))* cfloat_ptr;
-    cfloat_ptr q = (cfloat_ptr)(const float*)(p + i);
-    return make_float4(q[0], q[1], q[2], q[3]);
-#else
-    return p[i];   // host pass only type-checks device code
-#endif
-}
+// lines to one.  For incoherent rays the union approaches the sum of the paths (C3: 4x slower than
+// TRAV_LANE), hence the per-scene choice.
 
 // min over all 64 lanes (EXEC must be all ones): DPP butterfly in-row, then row broadcasts
 __device__ __forceinline__ uint32_t wave_min_full(uint32_t v) {
@@ -138,46 +181,9 @@ __device__ __forceinline__ uint32_t wave_min_partial(uint32_t v) {
     return m;
 }
 
-// rtcOccluded1 semantics, lockstep.  Every lane of the wave must call it (inactive: active=false).
-__device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-    const bool full = __ballot(1) == ~0ull;
-    vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const uint32_t n = S.n_nodes;
-    uint32_t i = active ? 0u : 0xffffffffu;
-    bool occ = false;
-    while (true) {
-        uint32_t m = full ? wave_min_full(i) : wave_min_partial(i);
-        if (m >= n) break;
-        float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
-        if (i == m) {
-            const uint32_t skip = (uint32_t)__float_as_int(a.w);
-            if (box_test(a, b, o, inv, tnear, tfar)) {
-                const int leaf = __float_as_int(b.w);
-                if (leaf >= 0) {
-                    const int first = leaf >> 3, cnt = (leaf & 7) + 1;
-                    for (int k = 0; k < cnt && !occ; ++k) {
-                        const uint32_t tri = 3u * (uint32_t)(first + k);
-                        float t, u, v;
-                        occ = tri_test(sload(S.tris, tri), sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d,
-                                       tnear, tfar, t, u, v);
-                    }
-                    i = occ ? 0xffffffffu : skip;
-                } else {
-                    i = m + 1;
-                }
-            } else {
-                i = skip;
-            }
-        }
-    }
-    return occ;
-}
-
 // K any-hit rays per lane sharing one origin (a pixel's shadow rays to K light samples), one lockstep
-// walk: each lane keeps K cursors, the wave steps through the union of all 64*K paths.  Shadow rays
-// of one tile overlap so heavily that the union barely grows with K (scripts/bvh_analysis.py: ~31
-// steps for K = 1..8 on C2), so steps per ray fall ~K-fold; each step's node (and leaf triangles) is
-// loaded once and tested against every ray whose cursor is on it.  Per ray, identical to occluded_ray.
+// walk: each lane keeps K cursors, the wave steps through the union of all 64*K paths; each step's node
+// (and leaf triangles) is loaded once and tested against every ray whose cursor is on it.
 template <int K>
 __device__ __forceinline__ void occluded_wave_multi(const DevScene& S, const bool* active, vec3 o, const vec3* d,
                                                     float tnear, const float* tfar, bool* occ) {
@@ -230,8 +236,40 @@ __device__ __forceinline__ void occluded_wave_multi(const DevScene& S, const boo
         }
     }
 }
-
-// rtcIntersect1 semantics, lockstep: closest hit in [tnear, tfar], ties to the smaller triangle index.
+// one any-hit ray per lane (the K = 1 walk, written out: the leaf loop exits per lane)
+__device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    const bool full = __ballot(1) == ~0ull;
+    vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const uint32_t n = S.n_nodes;
+    uint32_t i = active ? 0u : 0xffffffffu;
+    bool occ = false;
+    while (true) {
+        uint32_t m = full ? wave_min_full(i) : wave_min_partial(i);
+        if (m >= n) break;
+        float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+        if (i == m) {
+            const uint32_t skip = (uint32_t)__float_as_int(a.w);
+            if (box_test(a, b, o, inv, tnear, tfar)) {
+                const int leaf = __float_as_int(b.w);
+                if (leaf >= 0) {
+                    const int first = leaf >> 3, cnt = (leaf & 7) + 1;
+                    for (int k = 0; k < cnt && !occ; ++k) {
+                        const uint32_t tri = 3u * (uint32_t)(first + k);
+                        float t, u, v;
+                        occ = tri_test(sload(S.tris, tri), sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d,
+                                       tnear, tfar, t, u, v);
+                    }
+                    i = occ ? 0xffffffffu : skip;
+                } else {
+                    i = m + 1;
+                }
+            } else {
+                i = skip;
+            }
+        }
+    }
+    return occ;
+}
 __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     const bool full = __ballot(1) == ~0ull;
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -271,38 +309,27 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
     return h;
 }
 
-// rtcIntersect1 semantics: closest hit in [tnear, tfar]; ties broken by the smaller triangle index
-RS_TRAV_ATTR Hit closest_ray(const DevScene& S, vec3 o, vec3 d, float tnear, float tfar) {
-    vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
-    uint32_t i = 0;
-    const uint32_t n = S.n_nodes;
-    while (i < n) {
-        float4 a = S.nodes[2 * i], b = S.nodes[2 * i + 1];
-        int skip = __float_as_int(a.w);
-        if (box_test(a, b, o, inv, tnear, h.t)) {
-            int leaf = __float_as_int(b.w);
-            if (leaf >= 0) {
-                int first = leaf >> 3, cnt = (leaf & 7) + 1;
-                for (int k = 0; k < cnt; ++k) {
-                    const float4* T = S.tris + 3 * (first + k);
-                    float t, u, v;
-                    if (tri_test(T[0], T[1], T[2], o, d, tnear, h.t, t, u, v)) {
-                        int prim = __float_as_int(T[0].w);
-                        if (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim)) {
-                            h.t = t; h.u = u; h.v = v; h.prim = prim;
-                        }
-                    }
-                }
-                i = (uint32_t)skip;
-            } else {
-                i = i + 1;
-            }
-        } else {
-            i = (uint32_t)skip;
-        }
+// ---------------------------------------------------------------- dispatch
+// Every lane of the wave must make the call (convergent call sites); `active` selects the lanes with a ray.
+template <int T, int K>
+__device__ __forceinline__ void trace_any_multi(const DevScene& S, const bool* active, vec3 o, const vec3* d,
+                                                float tnear, const float* tfar, bool* occ) {
+    if (T == TRAV_LOCKSTEP) {
+        occluded_wave_multi<K>(S, active, o, d, tnear, tfar, occ);
+    } else {   // one walk after the other (measured faster than interleaving the K walks)
+#pragma unroll
+        for (int k = 0; k < K; ++k) occ[k] = occluded_lane(S, active[k], o, d[k], tnear, tfar[k]);
     }
-    return h;
+}
+template <int T>
+__device__ __forceinline__ bool trace_any(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    if (T == TRAV_LOCKSTEP) return occluded_wave(S, active, o, d, tnear, tfar);
+    return occluded_lane(S, active, o, d, tnear, tfar);
+}
+template <int T>
+__device__ __forceinline__ Hit trace_closest(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    if (T == TRAV_LOCKSTEP) return closest_wave(S, active, o, d, tnear, tfar);
+    return closest_lane(S, active, o, d, tnear, tfar);
 }
 
 // Material record (pg/material.h:105-115)
@@ -315,42 +342,11 @@ __device__ __forceinline__ MatRec load_mat(const DevScene& S, uint32_t m) {
 // Intersection::intersectEmbree + getGeometryAttributes (pg/Intersection.h:8-41,85-113):
 // hit point = org + dir*t, interpolated normal (1-u-v)n0 + u n1 + v n2, normalised, flipped to face
 // the ray; material; emissive id (vertex-0 attribute, :103-110).
-// Traversal used by the passes: lockstep (default) or per-lane (RS_LOCKSTEP=0, for A/B).  Both must
-// be called by every lane of the wave (convergent call sites); `active` selects the lanes with a ray.
-#ifndef RS_LOCKSTEP
-#define RS_LOCKSTEP 1
-#endif
-__device__ __forceinline__ bool trace_any(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-#if RS_LOCKSTEP
-    return occluded_wave(S, active, o, d, tnear, tfar);
-#else
-    return active ? occluded_ray(S, o, d, tnear, tfar) : false;
-#endif
-}
-template <int K>
-__device__ __forceinline__ void trace_any_multi(const DevScene& S, const bool* active, vec3 o, const vec3* d,
-                                                float tnear, const float* tfar, bool* occ) {
-#if RS_LOCKSTEP
-    occluded_wave_multi<K>(S, active, o, d, tnear, tfar, occ);
-#else
-#pragma unroll
-    for (int k = 0; k < K; ++k) occ[k] = active[k] ? occluded_ray(S, o, d[k], tnear, tfar[k]) : false;
-#endif
-}
-__device__ __forceinline__ Hit trace_closest(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-#if RS_LOCKSTEP
-    return closest_wave(S, active, o, d, tnear, tfar);
-#else
-    if (active) return closest_ray(S, o, d, tnear, tfar);
-    Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
-    return h;
-#endif
-}
-
 struct SurfHit { bool hit; vec3 point, normal; uint32_t mat; int emis_id; };
+template <int T>
 __device__ __forceinline__ SurfHit intersect(const DevScene& S, bool active, vec3 o, vec3 d, float tnear) {
     SurfHit r; r.hit = false; r.mat = 0; r.emis_id = -1; r.point = mk(0, 0, 0); r.normal = mk(0, 0, 0);
-    Hit h = trace_closest(S, active, o, d, tnear, FLT_MAX);
+    Hit h = trace_closest<T>(S, active, o, d, tnear, FLT_MAX);
     if (h.prim < 0) return r;
     const float4* N = S.tri_nrm + 3 * h.prim;
     float4 n0 = N[0], n1 = N[1], n2 = N[2];

@@ -27,8 +27,13 @@ EXPORTED_SYMBOLS = [
     "rs_context_create", "rs_context_destroy", "rs_last_error", "rs_scene_create", "rs_scene_load_obj",
     "rs_scene_destroy", "rs_scene_info", "rs_render_frame", "rs_get_frame_device_ptr", "rs_reset_history",
     "rs_synchronize", "rs_dump_gbuffer", "rs_dump_reservoirs", "rs_tile_begin", "rs_tile_halo_ptr",
-    "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace",
+    "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_context_set_traversal",
+    "rs_context_get_traversal",
 ]
+
+# BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
+TRAVERSAL_AUTO, TRAVERSAL_LOCKSTEP, TRAVERSAL_LANE = -1, 0, 1
+TRAVERSAL_NAMES = {"auto": TRAVERSAL_AUTO, "lockstep": TRAVERSAL_LOCKSTEP, "lane": TRAVERSAL_LANE}
 
 
 class MeshDesc(ctypes.Structure):
@@ -102,6 +107,9 @@ def load_library(path: str = LIB_PATH):
     L.rs_tile_spatial.argtypes = [vp, i32]
     L.rs_tile_finish.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(PassTimes)]
     L.rs_debug_trace.argtypes = [vp, vp, u32, fp, fp, fp, fp, i32, fp, ctypes.POINTER(ctypes.c_int32)]
+    L.rs_context_set_traversal.argtypes = [vp, i32]
+    ip = ctypes.POINTER(ctypes.c_int32)
+    L.rs_context_get_traversal.argtypes = [vp, vp, ip, ip, ip]
     _lib = L
     return L
 
@@ -222,6 +230,18 @@ class Renderer:
 
     def synchronize(self):
         self._check(self.lib.rs_synchronize(self.h))
+
+    def set_traversal(self, mode):
+        """BVH traversal kind: "auto" (default), "lockstep" or "lane" (or the TRAVERSAL_* ints)."""
+        m = TRAVERSAL_NAMES[mode] if isinstance(mode, str) else int(mode)
+        self._check(self.lib.rs_context_set_traversal(self.h, m))
+
+    def traversal(self, scene: "Scene | None" = None):
+        """(requested mode, kind the last frame ran with, kind AUTO settled on for `scene` or -1)."""
+        m, k, s = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        self._check(self.lib.rs_context_get_traversal(self.h, scene.h if scene is not None else None,
+                                                      ctypes.byref(m), ctypes.byref(k), ctypes.byref(s)))
+        return m.value, k.value, s.value
 
     def frame_device_ptr(self) -> int:
         p = ctypes.c_void_p()

@@ -163,6 +163,34 @@ def test_phong_scene_c3_small():
         _assert_close(a, b, "sponza-like")
 
 
+@pytest.mark.parametrize("which", ["c2", "c3"])
+def test_traversal_kinds_bit_identical(which):
+    """LOCKSTEP, LANE and AUTO (which alternates the kinds over its first four frames) render
+    bit-identical frames, matching the oracle; AUTO has settled on a kind after four frames."""
+    if which == "c2":
+        sc, prm, W, H = scenes.cornell_many_lights(1024), P.metric_params(), 64, 48
+        cam = lambda f: sc.camera
+    else:
+        sc, prm, W, H = scenes.sponza_like(target_tris=30_000, n_lamps=128), P.c3_params(m_area=8), 64, 40
+        cam = lambda f: scenes.orbit_camera(sc.camera, f, 240, 0.3)
+    n_frames = 5
+    frames = {}
+    for mode in ("lockstep", "lane", "auto"):
+        g = Renderer(W, H)
+        g.set_traversal(mode)
+        gs = g.load_scene(sc)
+        frames[mode] = [g.produce_restir(gs, cam(f), prm, f).copy() for f in range(n_frames)]
+        if mode == "auto":
+            m, last, choice = g.traversal(gs)
+            assert m == -1 and choice in (0, 1) and last == choice
+    for f in range(n_frames):
+        assert np.array_equal(frames["lockstep"][f], frames["lane"][f]), f"frame {f}: lockstep != lane"
+        assert np.array_equal(frames["lockstep"][f], frames["auto"][f]), f"frame {f}: lockstep != auto"
+    o, os_ = O.OracleRenderer(W, H), O.OracleScene(sc)
+    for f in range(2):
+        _assert_close(frames["lane"][f], o.render(os_, cam(f), prm, f), f"{which} frame {f}")
+
+
 # ---------------------------------------------------------------- edge cases + API behaviour
 @pytest.mark.parametrize("wh", [(1, 1), (17, 9), (3, 64)])
 def test_odd_sizes(wh):
