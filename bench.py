@@ -27,6 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "restir-embree_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2   # wave64 VALU instr/ns: 1024 SIMD-32s, 2 cycles each, 2.4 GHz
 WORKLOADS = {
     "C1": "Cornell box, 8 emissive quads, reference defaults (A=1 B=1, no reuse)",
     "C2": "Cornell box + 1024 emissive quads, A=32 B=1, spatial k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20",
@@ -149,7 +150,7 @@ def main():
     k_ms = acc["gbuffer_initial_ms"] / args.steps
     px_band = W * math.ceil(H / world)
     achieved = DOMINANT_BYTES_PER_PX * px_band / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
-    traffic = None
+    traffic = valu = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf) and world == 1:
         try:
@@ -157,8 +158,9 @@ def main():
                 pmc = json.load(f)
             if pmc.get("config") == f"{args.scene}_{W}x{H}":
                 traffic = pmc.get("k_gbuffer_initial_bytes_per_launch")
+                valu = pmc.get("k_gbuffer_initial_valu_per_launch")
         except Exception:
-            traffic = None
+            traffic = valu = None
     trav_name = None
     if world == 1:
         _, last_kind, _ = r.traversal(gs)
@@ -187,6 +189,12 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": "k_gbuffer_initial", "bytes_per_px": DOMINANT_BYTES_PER_PX,
                          "kernel_ms": round(k_ms, 4)},
+            # the kernel's real limiter is instruction issue / latency, not HBM: VALU wave-instructions
+            # per launch (PMC SQ_INSTS_VALU, profiles/pmc_traffic.json) over the live kernel time, against
+            # 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU op (MI355X_MICROARCH.md)
+            "valu_issue": None if not valu or k_ms <= 0 else {
+                "achieved": round(valu / (k_ms * 1e-3) / 1e9, 2), "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
+                "frac": round(valu / (k_ms * 1e-3) / 1e9 / VALU_PEAK_GIPS, 4), "valu_per_launch": valu},
         }
         if world == 1 and not args.no_cpu_baseline:
             try:

@@ -189,7 +189,9 @@ int rs_tile_finish(rs_context* ctx, const float** band_rgb_dptr, rs_pass_times* 
 
 /* ---- test hook: raw BVH queries (rtcIntersect1 / rtcOccluded1 semantics) ----------------------
  * n rays, host arrays o[3n], d[3n], tnear[n], tfar[n].  any_hit=0: closest hit -> t_out[n] (-1 on miss),
- * prim_out[n] (original triangle index, -1 on miss); any_hit=1: prim_out[n] = 1 if occluded else 0. */
+ * prim_out[n] (original triangle index, -1 on miss); any_hit=1: prim_out[n] = 1 if occluded else 0.
+ * Modes 0/1 use the lockstep traversal, 2/3 the same queries per-lane; 4 (closest) / 5 (any) return
+ * per-ray walk statistics instead: prim_out[n] = node visits << 16 | triangle tests. */
 int rs_debug_trace(rs_context* ctx, const rs_scene* scene, uint32_t n, const float* o, const float* d,
                    const float* tnear, const float* tfar, int any_hit, float* t_out, int32_t* prim_out);
 

@@ -720,7 +720,36 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
     const bool act = i0 < n;
     const uint32_t i = act ? i0 : n - 1;
     vec3 O = mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), D = mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    if (any == 1 || any == 3) {
+    if (any == 4 || any == 5) {   // BVH statistics of the per-lane walk: visits << 16 | triangle tests
+        vec3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+        uint32_t cur = act ? 0u : 0xffffffffu, visits = 0, tris = 0;
+        bool occ = false;
+        Hit h; h.t = tf[i]; h.u = h.v = 0; h.prim = -1;
+        while (cur < S.n_nodes && !occ) {
+            const uint32_t k = cur;
+            const float4 a = S.nodes[2 * k], b = S.nodes[2 * k + 1];
+            const float tmax = any == 5 ? tf[i] : h.t;
+            ++visits;
+            const int leaf = __float_as_int(b.w);
+            if (any == 4 && leaf >= 0 && box_test(a, b, O, inv, tn[i], tmax)) tris += (leaf & 7) + 1;
+            if (any == 5) {
+                cur = (uint32_t)__float_as_int(a.w);
+                if (box_test(a, b, O, inv, tn[i], tf[i])) {
+                    if (leaf < 0) cur = k + 1;
+                    else
+                        for (int j = 0; j < (leaf & 7) + 1 && !occ; ++j) {
+                            const float4* T = S.tris + 3 * ((leaf >> 3) + j);
+                            float t, u, v;
+                            ++tris;
+                            occ = tri_test(T[0], T[1], T[2], O, D, tn[i], tf[i], t, u, v);
+                        }
+                }
+            } else {
+                closest_visit<false>(S, a, b, k, O, D, inv, tn[i], cur, h);
+            }
+        }
+        if (act) { prim_out[i] = (int32_t)((visits << 16) | (tris & 0xffff)); t_out[i] = occ ? 1.0f : 0.0f; }
+    } else if (any == 1 || any == 3) {
         bool occ = any == 1 ? trace_any<TRAV_LOCKSTEP>(S, act, O, D, tn[i], tf[i])
                             : trace_any<TRAV_LANE>(S, act, O, D, tn[i], tf[i]);
         if (act) { prim_out[i] = occ ? 1 : 0; t_out[i] = 0.0f; }

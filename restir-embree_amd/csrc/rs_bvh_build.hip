@@ -256,7 +256,9 @@ int build_bvh_lbvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
         BVH_CHECK(hipMemcpyAsync(&kept_root, &N[0].kept, sizeof(int), hipMemcpyDeviceToHost, st));
         BVH_CHECK(hipStreamSynchronize(st));
     }
-    BVH_CHECK(hipMalloc(&nodes, (size_t)kept_root * 2 * sizeof(float4)));
+    // + 1 zeroed pad node (node n is readable: room for speculative next-node loads)
+    BVH_CHECK(hipMalloc(&nodes, ((size_t)kept_root + 1) * 2 * sizeof(float4)));
+    BVH_CHECK(hipMemsetAsync(nodes + 2 * (size_t)kept_root, 0, 2 * sizeof(float4), st));
     BVH_CHECK(hipMalloc(&tris, (size_t)n * 3 * sizeof(float4)));
     if (n > 1) {
         k_emit<<<gt, B, 0, st>>>(N, (int)n, nodes);
@@ -541,7 +543,9 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
         PLOC_CHECK(hipMemcpyAsync(&kept_root, kept + root, sizeof(int), hipMemcpyDeviceToHost, st));
         PLOC_CHECK(hipStreamSynchronize(st));
     }
-    PLOC_CHECK(hipMalloc(&nodes, (size_t)kept_root * 2 * sizeof(float4)));
+    // + 1 zeroed pad node (node n is readable: room for speculative next-node loads)
+    PLOC_CHECK(hipMalloc(&nodes, ((size_t)kept_root + 1) * 2 * sizeof(float4)));
+    PLOC_CHECK(hipMemsetAsync(nodes + 2 * (size_t)kept_root, 0, 2 * sizeof(float4), st));
     PLOC_CHECK(hipMalloc(&tris, (size_t)n * 3 * sizeof(float4)));
     k_ploc_emit<<<(total + B - 1) / B, B, 0, st>>>(nlo, nhi, parent, cnt, kept, collapsed, (int)n, d_pos, nodes, tris);
     PLOC_CHECK(hipGetLastError());

@@ -181,6 +181,24 @@ __device__ __forceinline__ uint32_t wave_min_partial(uint32_t v) {
     return m;
 }
 
+__device__ __forceinline__ uint32_t wave_min(bool full, uint32_t v) {
+    return full ? wave_min_full(v) : wave_min_partial(v);
+}
+template <int K>
+__device__ __forceinline__ uint32_t lane_min(const uint32_t* cur) {
+    uint32_t lm = cur[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) lm = cur[k] < lm ? cur[k] : lm;
+    return lm;
+}
+// Next step's node after a lockstep step at m.  Every cursor is > m afterwards (lanes on m moved to
+// m + 1, skip(m) > m or done; the others were already > m), so if any lane descended to m + 1 that is
+// the minimum -- the cross-lane reduction is only needed when no lane descended.
+__device__ __forceinline__ uint32_t next_min(bool full, bool descended, uint32_t m, uint32_t lane_min_v) {
+    if (__ballot(descended) != 0) return m + 1;
+    return wave_min(full, lane_min_v);
+}
+
 // K any-hit rays per lane sharing one origin (a pixel's shadow rays to K light samples), one lockstep
 // walk: each lane keeps K cursors, the wave steps through the union of all 64*K paths; each step's node
 // (and leaf triangles) is loaded once and tested against every ray whose cursor is on it.
@@ -197,12 +215,8 @@ __device__ __forceinline__ void occluded_wave_multi(const DevScene& S, const boo
         occ[k] = false;
     }
     const uint32_t n = S.n_nodes;
-    while (true) {
-        uint32_t lm = cur[0];
-#pragma unroll
-        for (int k = 1; k < K; ++k) lm = cur[k] < lm ? cur[k] : lm;
-        const uint32_t m = full ? wave_min_full(lm) : wave_min_partial(lm);
-        if (m >= n) break;
+    uint32_t m = wave_min(full, lane_min<K>(cur));
+    while (m < n) {
         const float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
@@ -229,10 +243,15 @@ __device__ __forceinline__ void occluded_wave_multi(const DevScene& S, const boo
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 if (cur[k] == m) cur[k] = (hb[k] && occ[k]) ? 0xffffffffu : skip;
+            m = wave_min(full, lane_min<K>(cur));
         } else {
+            bool desc = false;
 #pragma unroll
-            for (int k = 0; k < K; ++k)
+            for (int k = 0; k < K; ++k) {
+                desc = desc || hb[k];
                 if (cur[k] == m) cur[k] = hb[k] ? m + 1 : skip;
+            }
+            m = next_min(full, desc, m, lane_min<K>(cur));
         }
     }
 }
@@ -243,10 +262,10 @@ __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, ve
     const uint32_t n = S.n_nodes;
     uint32_t i = active ? 0u : 0xffffffffu;
     bool occ = false;
-    while (true) {
-        uint32_t m = full ? wave_min_full(i) : wave_min_partial(i);
-        if (m >= n) break;
-        float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+    uint32_t m = wave_min(full, i);
+    while (m < n) {
+        const float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+        bool desc = false;
         if (i == m) {
             const uint32_t skip = (uint32_t)__float_as_int(a.w);
             if (box_test(a, b, o, inv, tnear, tfar)) {
@@ -262,11 +281,13 @@ __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, ve
                     i = occ ? 0xffffffffu : skip;
                 } else {
                     i = m + 1;
+                    desc = true;
                 }
             } else {
                 i = skip;
             }
         }
+        m = next_min(full, desc, m, i);
     }
     return occ;
 }
@@ -276,10 +297,10 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
     Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
     const uint32_t n = S.n_nodes;
     uint32_t i = active ? 0u : 0xffffffffu;
-    while (true) {
-        uint32_t m = full ? wave_min_full(i) : wave_min_partial(i);
-        if (m >= n) break;
-        float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+    uint32_t m = wave_min(full, i);
+    while (m < n) {
+        const float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+        bool desc = false;
         if (i == m) {
             const uint32_t skip = (uint32_t)__float_as_int(a.w);
             if (box_test(a, b, o, inv, tnear, h.t)) {
@@ -300,11 +321,13 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
                     i = skip;
                 } else {
                     i = m + 1;
+                    desc = true;
                 }
             } else {
                 i = skip;
             }
         }
+        m = next_min(full, desc, m, i);
     }
     return h;
 }

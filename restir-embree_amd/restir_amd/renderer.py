@@ -259,7 +259,17 @@ class Renderer:
         self._check(self.lib.rs_dump_reservoirs(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
         return out
 
-    def debug_trace(self, scene: Scene, o, d, tnear, tfar, any_hit: bool, lockstep: bool = True):
+    def debug_trace(self, scene: Scene, o, d, tnear, tfar, any_hit: bool, lockstep: bool = True,
+                    stats: bool = False):
+        """Raw BVH queries.  stats=True: per-lane walk statistics instead -- returns
+        (visits, triangle_tests) int arrays per ray."""
+        if stats:
+            t, prim = self._debug_trace(scene, o, d, tnear, tfar, 5 if any_hit else 4)
+            p = prim.view(np.uint32)
+            return (p >> 16).astype(np.int64), (p & 0xFFFF).astype(np.int64)
+        return self._debug_trace(scene, o, d, tnear, tfar, (1 if any_hit else 0) + (0 if lockstep else 2))
+
+    def _debug_trace(self, scene: Scene, o, d, tnear, tfar, mode: int):
         o = np.ascontiguousarray(o, np.float32)
         d = np.ascontiguousarray(d, np.float32)
         n = o.shape[0]
@@ -269,8 +279,7 @@ class Renderer:
         prim = np.zeros(n, np.int32)
         fp = ctypes.POINTER(ctypes.c_float)
         self._check(self.lib.rs_debug_trace(self.h, scene.h, n, o.ctypes.data_as(fp), d.ctypes.data_as(fp),
-                                            tn.ctypes.data_as(fp), tf.ctypes.data_as(fp),
-                                            (1 if any_hit else 0) + (0 if lockstep else 2),
+                                            tn.ctypes.data_as(fp), tf.ctypes.data_as(fp), int(mode),
                                             t.ctypes.data_as(fp), prim.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
         return t, prim
 

@@ -18,7 +18,8 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     with open(os.path.join(src, f"pmc_{c}", "run_counter_collection.csv")) as f:
         for row in csv.DictReader(f):
-            k = row["Kernel_Name"].split("(")[0].replace("rs::", "")
+            # "void rs::k_gbuffer_initial<0>(...)" -> "k_gbuffer_initial" (<0> lockstep / <1> lane kind)
+            k = row["Kernel_Name"].split("(")[0].replace("rs::", "").replace("void ", "").split("<")[0]
             if k.startswith("k_gbuffer_initial") or k.startswith("k_spatial") or k.startswith("k_temporal") \
                     or k.startswith("k_shade"):
                 vals[k][c].append(float(row["Counter_Value"]))
@@ -33,6 +34,23 @@ for k, d in vals.items():
                          "bytes_per_px_corrected": round((2 * fe + wr) * 1024 / px, 2)}
 if "k_gbuffer_initial" in res["kernels"]:
     res["k_gbuffer_initial_bytes_per_launch"] = res["kernels"]["k_gbuffer_initial"]["hbm_bytes_corrected"]
+# instruction-issue pass (SQ counters; SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* / SQ_WAIT_* are quad-cycles)
+sq_csv = os.path.join(src, "pmc_SQ_WAVES", "run_counter_collection.csv")
+if os.path.exists(sq_csv):
+    sq = collections.defaultdict(lambda: collections.defaultdict(list))
+    with open(sq_csv) as f:
+        for row in csv.DictReader(f):
+            k = row["Kernel_Name"].split("(")[0].replace("rs::", "").replace("void ", "").split("<")[0]
+            sq[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    for k, d in sq.items():
+        if k in res["kernels"]:
+            res["kernels"][k]["sq"] = {c: round(sum(v) / len(v), 1) for c, v in d.items()}
+    if "k_gbuffer_initial" in sq:
+        g = res["kernels"]["k_gbuffer_initial"]["sq"]
+        res["k_gbuffer_initial_valu_per_launch"] = g.get("SQ_INSTS_VALU")
+        res["k_gbuffer_initial_salu_per_launch"] = g.get("SQ_INSTS_SALU")
+    res["source"] += "; SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY (one run)"
+res["traversal"] = os.environ.get("RESTIR_TRAVERSAL", "lockstep")
 with open(out, "w") as f:
     json.dump(res, f, indent=1)
 print(json.dumps(res, indent=1))
