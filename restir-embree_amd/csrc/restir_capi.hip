@@ -462,7 +462,7 @@ static CountSlot count_slot(rs_context* c, dim3 grid) {
 // reserve slots for every launch of a frame: initial + visibility + temporal + P spatial + shade
 static bool reserve_count_slots(rs_context* c, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
     size_t need = grid_waves(grid_rows(c->W, gy0, gy1)) +
-                  grid_waves(grid_rows(c->W, y0, y1)) * (3 + (size_t)std::max(0, P->spatial_passes));
+                  grid_waves(grid_rows(c->W, y0, y1)) * (4 + (size_t)std::max(0, P->spatial_passes));
     c->part_used = 0;
     if (need <= c->part_cap) return true;
     if (c->d_part) hipFree(c->d_part);

@@ -196,27 +196,50 @@ __device__ __forceinline__ uint32_t cand_slot(int c) { return 4u * (uint32_t)c; 
 __device__ __forceinline__ void res_cap(Res& r, int cap) { r.conf = r.conf < cap ? r.conf : cap; }
 
 // ---------------------------------------------------------------- BRDF statics
+// The per-pixel invariants of every BRDF evaluation / pdf / sample at a G element seen from `cam`,
+// computed once (each in the reference's operation order).  The Phong eval's mirror direction
+// normalize(reflect(-normalize(cam - p), n)) and the pdf's normalize(reflect(normalize(p - cam), n))
+// are the same bits (p - cam = -(cam - p) exactly; normalize commutes with negation), so one wr.
+struct ShadeFrame {
+    vec3 nrm; float pf;        // pf = maxD / (maxD + maxS)             (pg/MaterialPhong.cpp:152-154)
+    vec3 wr; float omp;        // mirror direction; omp = 1 - pf
+    vec3 kd_pi; float shin;    // kd * 1/pi                             (pg/MaterialLambert.cpp:33-41)
+    vec3 ks_im; float a;       // ks * 1/I_M;  a = (shin + 1) * 1/(2 pi)  (pg/MaterialPhong.cpp:122-172)
+    float maxD, maxS; int type;
+};
+__device__ __forceinline__ ShadeFrame make_frame(const GElem& g, vec3 cam) {
+    ShadeFrame s;
+    s.maxD = maxc(g.kd); s.maxS = maxc(g.ks);
+    s.pf = s.maxD / (s.maxD + s.maxS);
+    s.omp = 1.0f - s.pf;
+    s.nrm = g.nrm;
+    vec3 wo = normalize(g.pos - cam);
+    s.wr = normalize(reflect(wo, g.nrm));
+    s.kd_pi = g.kd * kOneOverPi;
+    s.ks_im = g.ks * g.inv_im;
+    s.shin = g.shin;
+    s.a = (g.shin + 1.0f) * kOneOver2Pi;
+    s.type = g.type;
+    return s;
+}
+__device__ __forceinline__ bool is_phong(int type) { return type == MT_PHONG || type == MT_DIELECTRIC; }
 // MaterialPhong::evalPdf -- the MIS pdf is always Phong's (pg/ReSTIRIntegrator.h:54-59,
 // pg/MaterialPhong.cpp:150-172)
-__device__ __forceinline__ float phong_pdf(const GElem& g, vec3 cam, vec3 wi) {
-    float maxD = maxc(g.kd), maxS = maxc(g.ks);
-    float pf = maxD / (maxD + maxS);
-    float pdf = gmax(dot(g.nrm, wi), 0.0f) * kOneOverPi * pf;
-    vec3 wo = normalize(g.pos - cam);
-    vec3 wr = normalize(reflect(wo, g.nrm));
-    pdf += (g.shin + 1.0f) * kOneOver2Pi * powf(gmax(0.0f, dot(wi, wr)), g.shin) * (1.0f - pf);
+__device__ __forceinline__ float phong_pdf(const ShadeFrame& s, vec3 wi) {
+    float pdf = gmax(dot(s.nrm, wi), 0.0f) * kOneOverPi * s.pf;
+    pdf += s.a * powf(gmax(0.0f, dot(wi, s.wr)), s.shin) * s.omp;
     return pdf;
 }
 // BRDF eval dispatch (pg/ReSTIRIntegrator.h:32-41): Phong for PHONG/DIELECTRIC
 // (pg/MaterialPhong.cpp:122-148, with the cached 1/I_M), Lambert otherwise (pg/MaterialLambert.cpp:33-41)
-__device__ __forceinline__ vec3 eval_brdf(const GElem& g, vec3 cam, vec3 wi) {
-    vec3 f = g.kd * kOneOverPi;
-    if (!(g.type == MT_PHONG || g.type == MT_DIELECTRIC)) return f;
-    vec3 V = normalize(cam - g.pos);
-    vec3 wr = normalize(reflect(-V, g.nrm));
-    float pw = powf(gmax(dot(wi, wr), 0.0f), g.shin);
-    return f + (g.ks * g.inv_im) * pw;
+__device__ __forceinline__ vec3 eval_brdf(const ShadeFrame& s, vec3 wi) {
+    vec3 f = s.kd_pi;
+    if (!is_phong(s.type)) return f;
+    float pw = powf(gmax(dot(wi, s.wr), 0.0f), s.shin);
+    return f + s.ks_im * pw;
 }
+__device__ __forceinline__ float phong_pdf(const GElem& g, vec3 cam, vec3 wi) { return phong_pdf(make_frame(g, cam), wi); }
+__device__ __forceinline__ vec3 eval_brdf(const GElem& g, vec3 cam, vec3 wi) { return eval_brdf(make_frame(g, cam), wi); }
 
 // Utils::orthogonal (pg/utils.cpp:204-207) + the ONB of pg/Distribution.h:15-24
 __device__ __forceinline__ vec3 to_world(vec3 s, vec3 n) {
@@ -246,20 +269,16 @@ __device__ __forceinline__ vec3 lobe_sample(vec3 wr, float gamma, Rng& rng) {
 }
 // BRDF sampling dispatch (pg/ReSTIRIntegrator.h:43-52): Lambert (pg/MaterialLambert.cpp:43-53) or
 // Phong (pg/MaterialPhong.cpp:174-222; also DIELECTRIC and every other type).  Returns omega_i, pdf.
-__device__ __forceinline__ vec3 sample_brdf(const GElem& g, vec3 cam, Rng& rng, float& pdf) {
-    if (g.type == MT_LAMBERT) {
-        vec3 wi = cosine_sample(g.nrm, rng);
-        pdf = gmax(dot(g.nrm, wi), 0.0f) * kOneOverPi;
+__device__ __forceinline__ vec3 sample_brdf(const ShadeFrame& s, Rng& rng, float& pdf) {
+    if (s.type == MT_LAMBERT) {
+        vec3 wi = cosine_sample(s.nrm, rng);
+        pdf = gmax(dot(s.nrm, wi), 0.0f) * kOneOverPi;
         return wi;
     }
-    vec3 wo = normalize(g.pos - cam);
-    float maxD = maxc(g.kd), maxS = maxc(g.ks);
-    float r0 = rng.range(0.0f, maxD + maxS);
-    float pf = maxD / (maxD + maxS);
-    vec3 wr = normalize(reflect(wo, g.nrm));
-    vec3 wi = (r0 < maxD) ? cosine_sample(g.nrm, rng) : lobe_sample(wr, g.shin, rng);
-    float pd = gmax(dot(g.nrm, wi), 0.0f) * kOneOverPi * pf;
-    float ps = (g.shin + 1.0f) * kOneOver2Pi * powf(gmax(0.0f, dot(wi, wr)), g.shin) * (1.0f - pf);
+    float r0 = rng.range(0.0f, s.maxD + s.maxS);
+    vec3 wi = (r0 < s.maxD) ? cosine_sample(s.nrm, rng) : lobe_sample(s.wr, s.shin, rng);
+    float pd = gmax(dot(s.nrm, wi), 0.0f) * kOneOverPi * s.pf;
+    float ps = s.a * powf(gmax(0.0f, dot(wi, s.wr)), s.shin) * s.omp;
     pdf = pd + ps;
     return wi;
 }

@@ -110,26 +110,42 @@ __device__ __forceinline__ bool occluded(const DevScene& S, const FrameConst& F,
 // evaluate_f_pre computes the unoccluded L and the testOcclusion ray (dir = normalize(p - pos),
 // tfar = |p - pos| - tfarOffset, exactly as occluded<T>() forms them); evaluate_f_post applies V.
 struct FPre { vec3 L, dir; float tfar; bool ok, need; };
-__device__ __forceinline__ FPre evaluate_f_pre(const FrameConst& F, const Sample& s, vec3 cam, const GElem& g,
-                                               bool test_vis, bool alive) {
+__device__ __forceinline__ FPre evaluate_f_pre(const FrameConst& F, const Sample& s, vec3 pos, bool emissive,
+                                               const ShadeFrame& sf, bool test_vis, bool alive) {
     FPre r;
-    r.ok = alive && smp_valid(s) && !(g.le.x > 0 || g.le.y > 0 || g.le.z > 0);
-    vec3 ld = s.p - g.pos;
+    r.ok = alive && smp_valid(s) && !emissive;
+    vec3 ld = s.p - pos;
     float r2 = dot(ld, ld);
     ld = normalize(ld);
-    float cI = gmax(dot(ld, g.nrm), 0.0f);
+    float cI = gmax(dot(ld, sf.nrm), 0.0f);
     float cY = fabsf(dot(-ld, s.n));
     float G = cI * cY / r2;
-    r.L = (s.li * eval_brdf(g, cam, ld)) * G;
+    r.L = (s.li * eval_brdf(sf, ld)) * G;
     r.need = r.ok && test_vis && !(r.L.x == 0.0f && r.L.y == 0.0f && r.L.z == 0.0f);
     r.dir = ld;
     r.tfar = sqrtf(r2) - F.tfar_off;
     return r;
 }
+__device__ __forceinline__ FPre evaluate_f_pre(const FrameConst& F, const Sample& s, vec3 cam, const GElem& g,
+                                               bool test_vis, bool alive) {
+    return evaluate_f_pre(F, s, g.pos, g.le.x > 0 || g.le.y > 0 || g.le.z > 0, make_frame(g, cam), test_vis, alive);
+}
 __device__ __forceinline__ vec3 evaluate_f_post(const FPre& p, bool occ) {
     vec3 L = p.L;
     if (p.need) L = L * (float)(!occ);
     return p.ok ? L : mk(0, 0, 0);
+}
+template <int T>
+__device__ __forceinline__ vec3 evaluate_f(const DevScene& S, const FrameConst& F, const Sample& s, vec3 pos,
+                                           bool emissive, const ShadeFrame& sf, bool test_vis, bool alive,
+                                           uint32_t& rays) {
+    FPre p = evaluate_f_pre(F, s, pos, emissive, sf, test_vis, alive);
+    bool occ = false;
+    if (test_vis) {                                                   // test_vis is wave-uniform
+        rays += p.need ? 1u : 0u;
+        occ = trace_any<T>(S, p.need, pos, p.dir, FLT_MIN + F.tnear_off, p.tfar);
+    }
+    return evaluate_f_post(p, occ);
 }
 template <int T>
 __device__ __forceinline__ vec3 evaluate_f(const DevScene& S, const FrameConst& F, const Sample& s, vec3 cam,
@@ -185,7 +201,7 @@ __device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameCons
 
 // areaSampleLight (pg/ReSTIRIntegrator.cpp:89-124), TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54),
 // Sampling::sampleTriangle (pg/Sampling.cpp:63-76)
-__device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameConst& F, const GElem& g, vec3 cam,
+__device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
                                               Rng& rng, float& W_out, float& mis_out) {
     float ksi = rng.range(0.0f, 1.0f);
     // std::lower_bound(cdf2, ksi), narrowed by the guide table: ksi*kCdfGuide is exact (ksi = k*2^-24),
@@ -206,12 +222,12 @@ __device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameCons
     vec3 pt = (xyz(P0) * bx + xyz(P1) * by) + xyz(P2) * bz;
     vec3 nn = normalize((xyz(E[3]) * bx + xyz(E[4]) * by) + xyz(E[5]) * bz);
     float pdf_area = P0.w * P1.w;           // pick prob * (1 / area)
-    vec3 ld = pt - g.pos;
+    vec3 ld = pt - pos;
     float r2s = dot(ld, ld);
     ld = normalize(ld);
     float cY = gmax(dot(-ld, nn), 0.0f);
     float amf = cY / r2s;
-    float pba = phong_pdf(g, cam, ld) * amf;
+    float pba = phong_pdf(sf, ld) * amf;
     mis_out = m_area(F, pdf_area, pba);
     W_out = 1.0f / pdf_area;
     return Sample{pt, nn, xyz(E[6])};
@@ -219,18 +235,18 @@ __device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameCons
 
 // brdfSampleLight (pg/ReSTIRIntegrator.cpp:126-177)
 template <int T>
-__device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameConst& F, const GElem& g, vec3 cam,
+__device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
                                               bool alive, Rng& rng, float& W_out, float& mis_out, uint32_t& rays) {
     float pdf;
-    vec3 wi = sample_brdf(g, cam, rng, pdf);
-    vec3 org = g.pos + g.nrm * F.normal_off;
+    vec3 wi = sample_brdf(sf, rng, pdf);
+    vec3 org = pos + sf.nrm * F.normal_off;
     rays += alive ? 1u : 0u;
     SurfHit h = intersect<T>(S, alive, org, wi, FLT_MIN + F.tnear_off);
     W_out = 0.0f; mis_out = 0.0f;
     if (h.hit) {
         MatRec mr = load_mat(S, h.mat);
         if (mr.le.x + mr.le.y + mr.le.z > 0) {      // Material::isEmissive (pg/material.h:135-137)
-            vec3 ld = h.point - g.pos;
+            vec3 ld = h.point - pos;
             float r2s = dot(ld, ld);
             ld = normalize(ld);
             float cY = gmax(dot(-ld, h.normal), 0.0f);
@@ -245,18 +261,43 @@ __device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameCons
     return smp_invalid();
 }
 
+// The initial pass keeps its pixel's ShadeFrame in LDS (5 float4 per thread, component-major so a
+// wave's ds_read_b128 of one component is conflict-free) and re-reads it for every candidate batch:
+// the ~20 per-pixel invariants then occupy no VGPRs across the shadow-ray walks (the compiler barrier
+// in load() keeps LICM from hoisting the reads back out of the candidate loop).  256 threads x 80 B =
+// 20 KB per workgroup.
+struct FrameSlot {
+    float4* base;   // __shared__ float4[5 * 256]
+    __device__ __forceinline__ void store(const ShadeFrame& s) const {
+        const int t = threadIdx.x;
+        base[t] = f4(s.nrm, s.pf);
+        base[256 + t] = f4(s.wr, s.omp);
+        base[512 + t] = f4(s.kd_pi, s.shin);
+        base[768 + t] = f4(s.ks_im, s.a);
+        base[1024 + t] = make_float4(s.maxD, s.maxS, __int_as_float(s.type), 0.0f);
+    }
+    __device__ __forceinline__ ShadeFrame load() const {
+        asm volatile("" ::: "memory");
+        const int t = threadIdx.x;
+        const float4 a = base[t], b = base[256 + t], c = base[512 + t], d = base[768 + t], e = base[1024 + t];
+        ShadeFrame s;
+        s.nrm = xyz(a); s.pf = a.w; s.wr = xyz(b); s.omp = b.w; s.kd_pi = xyz(c); s.shin = c.w;
+        s.ks_im = xyz(d); s.a = d.w; s.maxD = e.x; s.maxS = e.y; s.type = __float_as_int(e.z);
+        return s;
+    }
+};
+
 // initialRenderPass (pg/ReSTIRIntegrator.cpp:236-298) for the lanes with `in_pass`.  f_sel returns the
 // selected candidate's f (for the fused shade); the final p-hat (:289) equals the selected candidate's
 // p-hat (same arguments), so it is not re-evaluated.
 template <int T>
-__device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& F, const GElem& g, uint32_t pix,
-                                           bool in_pass, vec3& f_sel, uint32_t& rays) {
+__device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& F, vec3 pos, bool emissive,
+                                           FrameSlot fs, uint32_t pix, bool in_pass, vec3& f_sel, uint32_t& rays) {
     f_sel = mk(0, 0, 0);
     Res r = res_empty();
-    const bool alive = in_pass && !any_pos(g.le) && S.n_emis > 0;     // :238-244
+    const bool alive = in_pass && !emissive && S.n_emis > 0;           // :238-244
     if (__ballot(alive) == 0) return r;                                 // wave-uniform exit
     Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, pix);
-    const vec3 cam = F.cam.pos;
     const bool tv = !F.do_vis_pass;
     float best_phat = 0.0f;
     if (F.m_area > 0) {
@@ -271,16 +312,17 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
             bool act[RS_RIS_BATCH], occ[RS_RIS_BATCH];
             vec3 dir[RS_RIS_BATCH];
             float tf[RS_RIS_BATCH];
+            const ShadeFrame sf = fs.load();
 #pragma unroll
             for (int k = 0; k < RS_RIS_BATCH; ++k) {
                 const bool inb = c0 + k < F.m_area;
                 rng.n = cand_slot(c0 + k);
-                Sample s = area_sample(S, F, g, cam, rng, Wc[k], mis[k]);
-                pre[k] = evaluate_f_pre(F, s, cam, g, tv, alive && inb);
+                Sample s = area_sample(S, F, pos, sf, rng, Wc[k], mis[k]);
+                pre[k] = evaluate_f_pre(F, s, pos, false, sf, tv, alive && inb);
                 act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
                 rays += act[k] ? 1u : 0u;
             }
-            if (tv) trace_any_multi<T, RS_RIS_BATCH>(S, act, g.pos, dir, FLT_MIN + F.tnear_off, tf, occ);
+            if (tv) trace_any_multi<T, RS_RIS_BATCH>(S, act, pos, dir, FLT_MIN + F.tnear_off, tf, occ);
 #pragma unroll
             for (int k = 0; k < RS_RIS_BATCH; ++k) {
                 if (c0 + k < F.m_area) {
@@ -295,7 +337,7 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
         if (sel >= 0) {
             float Wc, mis;
             rng.n = cand_slot(sel);
-            Sample s = area_sample(S, F, g, cam, rng, Wc, mis);
+            Sample s = area_sample(S, F, pos, fs.load(), rng, Wc, mis);
             r.p = s.p; r.n = s.n; r.li = s.li;
         }
     }
@@ -304,8 +346,9 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
         for (int i = 0; i < F.m_brdf; ++i) {
             float Wc, mis;
             rng.n = cand_slot(F.m_area + i);
-            Sample s = brdf_sample<T>(S, F, g, cam, alive, rng, Wc, mis, rays);
-            vec3 f = evaluate_f<T>(S, F, s, cam, g, tv, alive, rays);
+            const ShadeFrame sf = fs.load();
+            Sample s = brdf_sample<T>(S, F, pos, sf, alive, rng, Wc, mis, rays);
+            vec3 f = evaluate_f<T>(S, F, s, pos, false, sf, tv, alive, rays);
             float ph = length(f);
             float w = F.m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
             rng.n = cand_slot(F.m_area + i) + 3u;
@@ -336,18 +379,20 @@ __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevSc
     uint32_t rays = 0;
     const bool in = pixel_of(F.gy0, F.gy1, F.W, x, y);
     const size_t p = (size_t)y * F.W + x;
+    __shared__ float4 frame_lds[5 * 256];
+    const FrameSlot fs{frame_lds};
     GElem g = gbuffer_fill<T>(S, F, x, y, in);
     if (in) G.store(p, g);
+    fs.store(make_frame(g, F.cam.pos));
     const bool ris = in && y >= F.y0 && y < F.y1;
     vec3 f;
-    Res r = initial_ris<T>(S, F, g, (uint32_t)p, ris, f, rays);
+    Res r = initial_ris<T>(S, F, g.pos, any_pos(g.le), fs, (uint32_t)p, ris, f, rays);
     if (ris) {
         Rw.store(p, r);
         if (fuse_shade) store_rgb(fb, p, shade_px(r, f, g.le));
     }
     count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u);
 }
-
 // visibilityPass (pg/ReSTIRIntegrator.cpp:302-312).  Invalid samples always carry W == 0 already,
 // so their (meaningless) ray is not traced.
 template <int T>
