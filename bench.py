@@ -64,13 +64,22 @@ def cpu_baseline(sc, prm, W, H, threads):
     osc = oracle_lib.OracleScene(sc)
     rr = oracle_lib.OracleRenderer(W, H)
     rr.render(osc, sc.camera, prm, 0)          # warm-up frame (page-in, caches)
-    t0 = time.perf_counter()
-    rr.render(osc, sc.camera, prm, 1)
-    dt = time.perf_counter() - t0
+    # median of up to 10 frames, bounded to ~10 s of CPU time (SURVEY.md §8d procedure, scaled down)
+    times, rays = [], []
+    t_start = time.perf_counter()
+    for f in range(1, 11):
+        t0 = time.perf_counter()
+        rr.render(osc, sc.camera, prm, f)
+        times.append(time.perf_counter() - t0)
+        rays.append(rr.rays)
+        if time.perf_counter() - t_start > 10.0:
+            break
+    dt = float(np.median(times))
+    mr = float(np.median([r / t for r, t in zip(rays, times)])) / 1e6
     return {"value": round(1.0 / dt, 5), "unit": "frames/s", "cores": n_threads, "kind": "port",
-            "sample": f"1 full {W}x{H} frame of the same C2 workload after 1 warm-up frame "
+            "sample": f"median of {len(times)} full {W}x{H} frames of the same workload after 1 warm-up frame "
                       f"(oracle/restir_oracle.c, OpenMP, {n_threads} threads); s/frame={dt:.3f}; "
-                      f"Mrays/s={rr.rays / dt / 1e6:.2f}"}
+                      f"Mrays/s={mr:.2f}"}
 
 
 def main():
@@ -106,35 +115,42 @@ def main():
     if world == 1:
         r = Renderer(W, H, device=local, stream=stream)
         gs = r.load_scene(sc)
-        step = lambda f: r.produce_restir(gs, sc.camera, prm, f, copy_out=False, timed=True)
-        times = lambda: r.last_times
+        step = lambda f: r.produce_restir(gs, sc.camera, prm, f, copy_out=False, timed=False)
+        eng = r
     else:
         from restir_amd.distributed import TiledRenderer
         tr = TiledRenderer(W, H, rank, world, device=local, stream=stream)
         gs = tr.load_scene(sc)
-        step = lambda f: tr.render(gs, sc.camera, prm, f, gather=True, timed=True)
-        times = lambda: tr.last_times
+        step = lambda f: tr.render(gs, sc.camera, prm, f, gather=True, timed=False)
+        eng = tr
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
+    # initialisation (like the scene load, outside warm-up and timing): RS_TRAVERSAL_AUTO times the two
+    # BVH walk kinds over a scene's first 4 frames, then the history is reset
+    for f in range(4):
+        step(f)
+    eng.reset_history()
     for f in range(args.warmup):
         step(f)
     barrier()
     torch.cuda.synchronize()
-    acc = {"gbuffer_initial_ms": 0.0, "spatial_ms": 0.0, "temporal_ms": 0.0, "shade_ms": 0.0, "total_ms": 0.0}
-    rays = 0
+    eng.timing_totals(reset=True)            # folds the warm-up frames away; no per-frame sync below
+    barrier()
     t0 = time.perf_counter()
     for f in range(args.steps):
         step(args.warmup + f)
-        t = times()
-        for k in acc:
-            acc[k] += getattr(t, k)
-        rays += int(t.rays)
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    tot, n_timed = eng.timing_totals()
+    if n_timed != args.steps:
+        print(f"warning: {n_timed} frames timed by events, expected {args.steps}", file=sys.stderr)
+    keys = ("gbuffer_initial_ms", "spatial_ms", "temporal_ms", "shade_ms", "total_ms")
+    acc = {k: float(getattr(tot, k)) for k in keys}
+    rays = int(tot.rays)
     if dist is not None:
         tt = torch.tensor([dt, float(rays)], dtype=torch.float64, device="cuda")
         dmax = tt.clone()
@@ -165,6 +181,9 @@ def main():
     if world == 1:
         _, last_kind, _ = r.traversal(gs)
         trav_name = {0: "lockstep", 1: "lane"}.get(last_kind)
+    else:
+        _, last_kind, _ = tr.be.r.traversal(gs)
+        trav_name = {0: "lockstep", 1: "lane"}.get(last_kind) + " (rank 0)"
     if rank == 0:
         out = {
             "metric": "Mrays/s + frames/s at 1080p, 32 candidates, 4 spatial neighbours",

@@ -132,6 +132,11 @@ int rs_scene_info(const rs_scene* scene, uint32_t* n_tris, uint32_t* n_emissive,
 int rs_render_frame(rs_context* ctx, const rs_scene* scene, const rs_camera* camera,
                     const rs_frame_params* params, uint32_t frame_index, float* frame_rgb_host,
                     rs_pass_times* times);
+/* Pass times and rays summed over every frame finished since context creation (or the last reset),
+ * without a host sync per frame: each frame records into its own slot of an event ring and the rays
+ * are summed on the device.  Synchronises the stream; sum->*_ms are totals (divide by *n_frames).
+ * Replaces reading the per-pass std::chrono members every frame (pg/simpleguidx11.h:120-127). */
+int rs_get_timing_totals(rs_context* ctx, rs_pass_times* sum, uint32_t* n_frames, int reset);
 /* Device pointer to the framebuffer (frame_data): W*H*3 floats, valid until the next render. */
 int rs_get_frame_device_ptr(rs_context* ctx, const float** dptr);
 /* Forget the previous frame (frameCtr = 0): the next frame skips temporal reuse. */

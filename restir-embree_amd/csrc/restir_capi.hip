@@ -61,7 +61,17 @@ struct rs_context {
     Counters* h_cnt = nullptr;
     uint2* d_part = nullptr;               // per-wave ray-count slots of this frame's launches
     size_t part_cap = 0, part_used = 0;
-    hipEvent_t ev[EV_COUNT] = {};
+    Counters* d_tot = nullptr;             // running totals over frames (rs_get_timing_totals)
+    // pass timing without a per-frame host sync: every frame records into its own slot of an event
+    // ring; slots are folded into the running totals lazily (when reused, or on rs_get_timing_totals)
+    static constexpr int kEvRing = 64;
+    hipEvent_t evr[kEvRing][EV_COUNT] = {};
+    bool ev_pending[kEvRing] = {};
+    int slot = 0;
+    uint64_t seq = 0;
+    double tot_ms[6] = {};                 // gbuffer_initial, visibility, temporal, spatial, shade, total
+    uint64_t tot_frames = 0;
+    hipEvent_t ev[EV_COUNT] = {};          // the frame in flight's slot
     uint64_t frames = 0;
     std::string err;
     // frame / tile in flight
@@ -198,8 +208,12 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
     hipMemsetAsync(c->fb, 0, n * 3 * sizeof(float), c->stream);
     if (hipMalloc(&c->d_cnt, sizeof(Counters)) != hipSuccess) return bail("hipMalloc(counters) failed");
     if (hipHostMalloc(&c->h_cnt, sizeof(Counters), hipHostMallocDefault) != hipSuccess) return bail("hipHostMalloc failed");
-    for (auto& e : c->ev)
-        if (hipEventCreate(&e) != hipSuccess) return bail("hipEventCreate failed");
+    if (hipMalloc(&c->d_tot, sizeof(Counters)) != hipSuccess) return bail("hipMalloc(totals) failed");
+    hipMemsetAsync(c->d_tot, 0, sizeof(Counters), c->stream);
+    for (auto& slot : c->evr)
+        for (auto& e : slot)
+            if (hipEventCreate(&e) != hipSuccess) return bail("hipEventCreate failed");
+    for (int i = 0; i < EV_COUNT; ++i) c->ev[i] = c->evr[0][i];
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail("context init failed");
     if (const char* t = std::getenv("RESTIR_TRAVERSAL")) {     // auto (default) | lockstep | lane
         if (!std::strcmp(t, "lockstep")) c->trav_mode = RS_TRAVERSAL_LOCKSTEP;
@@ -236,9 +250,11 @@ extern "C" void rs_context_destroy(rs_context* c) {
     for (auto* r : c->R) if (r) hipFree(r);
     if (c->fb) hipFree(c->fb);
     if (c->d_cnt) hipFree(c->d_cnt);
+    if (c->d_tot) hipFree(c->d_tot);
     if (c->d_part) hipFree(c->d_part);
     if (c->h_cnt) hipHostFree(c->h_cnt);
-    for (auto& e : c->ev) if (e) hipEventDestroy(e);
+    for (auto& slot : c->evr)
+        for (auto& e : slot) if (e) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -415,6 +431,23 @@ static dim3 grid_rows(int W, int ya, int yb) { return dim3((W + 15) / 16, (yb - 
         else kernel<TRAV_LOCKSTEP><<<(grid), 256, 0, (c)->stream>>>(__VA_ARGS__);           \
     } while (0)
 
+// fold a finished frame's pass times (event-ring slot s) into the running totals
+static void fold_slot(rs_context* c, int s) {
+    if (!c->ev_pending[s]) return;
+    c->ev_pending[s] = false;
+    hipEvent_t* e = c->evr[s];
+    if (hipEventSynchronize(e[EV_SHADE]) != hipSuccess) return;
+    float v[6] = {};
+    (void)hipEventElapsedTime(&v[0], e[EV_BEGIN], e[EV_INIT]);
+    (void)hipEventElapsedTime(&v[1], e[EV_INIT], e[EV_VIS]);
+    (void)hipEventElapsedTime(&v[2], e[EV_VIS], e[EV_TEMPORAL]);
+    (void)hipEventElapsedTime(&v[3], e[EV_TEMPORAL], e[EV_SPATIAL]);
+    (void)hipEventElapsedTime(&v[4], e[EV_SPATIAL], e[EV_SHADE]);
+    (void)hipEventElapsedTime(&v[5], e[EV_BEGIN], e[EV_SHADE]);
+    for (int i = 0; i < 6; ++i) c->tot_ms[i] += v[i];
+    c->tot_frames++;
+}
+
 // RS_TRAVERSAL_AUTO: the first frames of a scene alternate the two kinds; per kind the first run is a
 // warm-up (lazy code-object load, cold caches), the next kTuneRuns-1 are timed (EV_BEGIN..EV_SHADE).
 constexpr int kTuneRuns = 2;
@@ -512,6 +545,9 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     const DevScene S = s->dev();
     if (!reserve_count_slots(c, P, F.gy0, F.gy1, F.y0, F.y1)) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
     HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->stream));
+    c->slot = (int)(c->seq++ % rs_context::kEvRing);
+    fold_slot(c, c->slot);                      // the slot's previous frame (kEvRing frames ago)
+    for (int i = 0; i < EV_COUNT; ++i) c->ev[i] = c->evr[c->slot][i];
     HIPCHK(c, hipEventRecord(c->ev[EV_BEGIN], c->stream));
     pick_traversal(c, s);
     const dim3 gg = grid_rows(c->W, F.gy0, F.gy1), gb = grid_rows(c->W, F.y0, F.y1);
@@ -610,14 +646,15 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
         HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(c->ev[EV_SHADE], c->stream));
+    c->ev_pending[c->slot] = true;
+    k_reduce_counts<<<1, 1024, 0, c->stream>>>(c->d_part, c->part_used, c->d_cnt, c->d_tot);
+    HIPCHK(c, hipGetLastError());
     record_traversal_time(c);
     c->r_last = c->rcur;   // reservoirsLastFrame = final buffer (pointer swap, :477)
     c->frames++;
     c->active = false;
     if (band_rgb) *band_rgb = c->fb + 3 * (size_t)c->F.y0 * c->W;
     if (t) {
-        k_reduce_counts<<<1, 1024, 0, c->stream>>>(c->d_part, c->part_used, c->d_cnt);
-        HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->d_cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         float a = 0, b = 0, d = 0, e = 0, f = 0, tot = 0;
@@ -629,6 +666,28 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
         hipEventElapsedTime(&tot, c->ev[EV_BEGIN], c->ev[EV_SHADE]);
         t->gbuffer_initial_ms = a; t->visibility_ms = b; t->temporal_ms = d; t->spatial_ms = e; t->shade_ms = f;
         t->total_ms = tot; t->rays = c->h_cnt->rays; t->primary_rays = c->h_cnt->primary;
+        fold_slot(c, c->slot);
+    }
+    return RS_OK;
+}
+
+extern "C" int rs_get_timing_totals(rs_context* c, rs_pass_times* sum, uint32_t* n_frames, int reset) {
+    if (!c || !sum) return fail(c, RS_E_INVALID, "rs_get_timing_totals: null argument");
+    if (c->active) return fail(c, RS_E_INVALID, "rs_get_timing_totals: a frame is in flight");
+    HIPCHK(c, enter(c));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int s = 0; s < rs_context::kEvRing; ++s) fold_slot(c, s);
+    Counters tot{};
+    HIPCHK(c, hipMemcpy(&tot, c->d_tot, sizeof(Counters), hipMemcpyDeviceToHost));
+    sum->gbuffer_initial_ms = (float)c->tot_ms[0]; sum->visibility_ms = (float)c->tot_ms[1];
+    sum->temporal_ms = (float)c->tot_ms[2]; sum->spatial_ms = (float)c->tot_ms[3];
+    sum->shade_ms = (float)c->tot_ms[4]; sum->total_ms = (float)c->tot_ms[5];
+    sum->rays = tot.rays; sum->primary_rays = tot.primary;
+    if (n_frames) *n_frames = (uint32_t)c->tot_frames;
+    if (reset) {
+        for (double& v : c->tot_ms) v = 0.0;
+        c->tot_frames = 0;
+        HIPCHK(c, hipMemset(c->d_tot, 0, sizeof(Counters)));
     }
     return RS_OK;
 }

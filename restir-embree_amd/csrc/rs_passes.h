@@ -68,8 +68,8 @@ __device__ __forceinline__ void count_rays(CountSlot C, uint32_t rays, uint32_t 
         C.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)] = make_uint2(r, p);
 }
 
-// one workgroup: sum n slot pairs into the frame totals
-__global__ void __launch_bounds__(1024) k_reduce_counts(const uint2* part, size_t n, Counters* out) {
+// one workgroup: sum n slot pairs into the frame totals (and the context's running totals)
+__global__ void __launch_bounds__(1024) k_reduce_counts(const uint2* part, size_t n, Counters* out, Counters* tot) {
     __shared__ unsigned long long sr[1024], sp[1024];
     unsigned long long r = 0, p = 0;
     for (size_t i = threadIdx.x; i < n; i += 1024) { uint2 v = part[i]; r += v.x; p += v.y; }
@@ -79,7 +79,10 @@ __global__ void __launch_bounds__(1024) k_reduce_counts(const uint2* part, size_
         if ((int)threadIdx.x < s) { sr[threadIdx.x] += sr[threadIdx.x + s]; sp[threadIdx.x] += sp[threadIdx.x + s]; }
         __syncthreads();
     }
-    if (threadIdx.x == 0) { out->rays = sr[0]; out->primary = sp[0]; }
+    if (threadIdx.x == 0) {
+        out->rays = sr[0]; out->primary = sp[0];
+        tot->rays += sr[0]; tot->primary += sp[0];
+    }
 }
 
 // 8x8 tile per wave, 16x16 per workgroup, rows [ya, yb).  Returns whether the pixel exists; x/y are

@@ -92,6 +92,12 @@ class GpuTileBackend:
     def last_times(self):
         return self.r.last_times
 
+    def timing_totals(self, reset=False):
+        return self.r.timing_totals(reset)
+
+    def reset_history(self):
+        self.r.reset_history()
+
 
 class TiledRenderer:
     def __init__(self, W: int, H: int, rank: int, world: int, device: int = 0, stream=None, backend=None,
@@ -112,6 +118,13 @@ class TiledRenderer:
     @property
     def last_times(self):
         return self.be.last_times
+
+    def timing_totals(self, reset=False):
+        """This rank's (PassTimes totals, n_frames) -- see Renderer.timing_totals."""
+        return self.be.timing_totals(reset)
+
+    def reset_history(self):
+        self.be.reset_history()
 
     def _exchange_halo(self):
         import torch.distributed as dist

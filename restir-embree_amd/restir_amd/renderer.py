@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = [
     "rs_scene_destroy", "rs_scene_info", "rs_render_frame", "rs_get_frame_device_ptr", "rs_reset_history",
     "rs_synchronize", "rs_dump_gbuffer", "rs_dump_reservoirs", "rs_tile_begin", "rs_tile_halo_ptr",
     "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_context_set_traversal",
-    "rs_context_get_traversal",
+    "rs_context_get_traversal", "rs_get_timing_totals",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -110,6 +110,7 @@ def load_library(path: str = LIB_PATH):
     L.rs_context_set_traversal.argtypes = [vp, i32]
     ip = ctypes.POINTER(ctypes.c_int32)
     L.rs_context_get_traversal.argtypes = [vp, vp, ip, ip, ip]
+    L.rs_get_timing_totals.argtypes = [vp, ctypes.POINTER(PassTimes), ctypes.POINTER(u32), i32]
     _lib = L
     return L
 
@@ -230,6 +231,13 @@ class Renderer:
 
     def synchronize(self):
         self._check(self.lib.rs_synchronize(self.h))
+
+    def timing_totals(self, reset: bool = False):
+        """(PassTimes with ms / ray totals, n_frames) over all frames finished since creation or the last
+        reset -- no per-frame host sync needed (rs_get_timing_totals)."""
+        t, n = PassTimes(), ctypes.c_uint32()
+        self._check(self.lib.rs_get_timing_totals(self.h, ctypes.byref(t), ctypes.byref(n), 1 if reset else 0))
+        return t, n.value
 
     def set_traversal(self, mode):
         """BVH traversal kind: "auto" (default), "lockstep" or "lane" (or the TRAVERSAL_* ints)."""

@@ -191,6 +191,33 @@ def test_traversal_kinds_bit_identical(which):
         _assert_close(frames["lane"][f], o.render(os_, cam(f), prm, f), f"{which} frame {f}")
 
 
+def test_timing_totals_match_per_frame_times():
+    """rs_get_timing_totals (no per-frame sync) sums the same rays as per-frame timed readback and
+    counts every frame, across more frames than the event ring holds."""
+    sc, prm = scenes.cornell_many_lights(1024), P.metric_params()
+    W, H, n = 64, 48, 70
+    a = Renderer(W, H)
+    ga = a.load_scene(sc)
+    a.set_traversal("lockstep")
+    per_frame = 0
+    for f in range(n):
+        a.produce_restir(ga, sc.camera, prm, f, copy_out=False, timed=True)
+        per_frame += int(a.last_times.rays)
+    b = Renderer(W, H)
+    gb = b.load_scene(sc)
+    b.set_traversal("lockstep")
+    b.produce_restir(gb, sc.camera, prm, 0, copy_out=False, timed=False)
+    _, k = b.timing_totals(reset=True)
+    assert k == 1
+    for f in range(n):
+        b.produce_restir(gb, sc.camera, prm, f, copy_out=False, timed=False)
+    tot, k = b.timing_totals()
+    assert k == n and int(tot.rays) == per_frame and tot.primary_rays == n * W * H
+    assert 0.0 < tot.gbuffer_initial_ms <= tot.total_ms
+    tot_a, k_a = a.timing_totals()
+    assert k_a == n and int(tot_a.rays) == per_frame
+
+
 # ---------------------------------------------------------------- edge cases + API behaviour
 @pytest.mark.parametrize("wh", [(1, 1), (17, 9), (3, 64)])
 def test_odd_sizes(wh):
