@@ -27,11 +27,13 @@ sys.path.insert(0, os.path.join(ROOT, "restir-embree_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+C5_FRAMES = 240
 VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2   # wave64 VALU instr/ns: 1024 SIMD-32s, 2 cycles each, 2.4 GHz
 WORKLOADS = {
     "C1": "Cornell box, 8 emissive quads, reference defaults (A=1 B=1, no reuse)",
     "C2": "Cornell box + 1024 emissive quads, A=32 B=1, spatial k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20",
     "C3": "Sponza-like ~250k tris, 4096 emissive triangles (2048 lamp quads), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
+    "C5": "C2 scene, 240-frame camera orbit (r=0.3) + moving lights (light CDF + BVH rebuilt every frame), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
 }
 # algorithmic bytes per pixel of the dominant kernel k_gbuffer_initial: G-buffer record write
 # (5 x float4 = 80 B) + reservoir write (3 x float4 = 48 B); scene/BVH reads are cache-resident
@@ -46,7 +48,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--scene", default="C2", choices=["C1", "C2", "C3"])
+    ap.add_argument("--scene", default="C2", choices=["C1", "C2", "C3", "C5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
@@ -101,12 +103,18 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     W, H = args.width, args.height
+    camera = None                       # per-frame camera (C5 orbit); None = the scene's static camera
+    light_pos = None                    # per-frame emissive positions (C5 moving lights)
     if args.scene == "C1":
         sc, prm = scenes.cornell_box(8), default_params()
     elif args.scene == "C2":
         sc, prm = scenes.cornell_many_lights(1024), metric_params()
-    else:
+    elif args.scene == "C3":
         sc, prm = scenes.sponza_like(), c3_params()
+    else:   # C5: C2's scene, 240-frame camera orbit + moving lights, temporal reuse with M-cap 20
+        sc, prm = scenes.cornell_many_lights(1024), c3_params()
+        camera = lambda f: scenes.orbit_camera(sc.camera, f % C5_FRAMES, C5_FRAMES, 0.3)
+        light_pos = [scenes.moving_light_positions(sc, f, C5_FRAMES) for f in range(C5_FRAMES)]
     # render on a dedicated torch stream shared with the library, so RCCL ops and the kernels of
     # librestir_amd.so are ordered on one stream (torch's default stream has handle 0 = "none")
     torch.cuda.set_stream(torch.cuda.Stream(device=local))
@@ -115,14 +123,20 @@ def main():
     if world == 1:
         r = Renderer(W, H, device=local, stream=stream)
         gs = r.load_scene(sc)
-        step = lambda f: r.produce_restir(gs, sc.camera, prm, f, copy_out=False, timed=False)
+        render = lambda f: r.produce_restir(gs, camera(f) if camera else sc.camera, prm, f, copy_out=False,
+                                            timed=False)
         eng = r
     else:
         from restir_amd.distributed import TiledRenderer
         tr = TiledRenderer(W, H, rank, world, device=local, stream=stream)
         gs = tr.load_scene(sc)
-        step = lambda f: tr.render(gs, sc.camera, prm, f, gather=True, timed=False)
+        render = lambda f: tr.render(gs, camera(f) if camera else sc.camera, prm, f, gather=True, timed=False)
         eng = tr
+
+    def step(f):
+        if light_pos is not None:       # moving lights: new positions -> light CDF + BVH rebuilt (timed)
+            gs.update_positions(light_pos[f % C5_FRAMES])
+        return render(f)
 
     def barrier():
         if dist is not None:
@@ -197,7 +211,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic (procedural scene, BASELINE.json configs[{ {'C1': 0, 'C2': 1, 'C3': 2}[args.scene]}])",
+            "data": f"synthetic (procedural scene, BASELINE.json configs[{ {'C1': 0, 'C2': 1, 'C3': 2, 'C5': 4}[args.scene]}])",
             "config": {"workload": f"{args.scene}: {WORKLOADS[args.scene]}, {W}x{H}",
                        "width": W, "height": H, "parallelism": f"row-bands x{world}" if world > 1 else "1 GPU",
                        "traversal": trav_name},

@@ -119,6 +119,12 @@ int rs_scene_create(rs_context* ctx, const rs_mesh_desc* meshes, uint32_t n_mesh
  * (pg/ModelLoader.cpp:41-153 conventions), then rs_scene_create.  Textures are not supported. */
 int rs_scene_load_obj(rs_context* ctx, const char* obj_path, rs_scene** out);
 void rs_scene_destroy(rs_scene* scene);
+/* Animated geometry (C5 moving lights; the reference cannot move geometry -- the Embree analogue is
+ * rtcUpdateGeometryBuffer + rtcCommitGeometry + rtcCommitScene): replaces all n_tris*9 vertex
+ * positions (and, if normals != NULL, the vertex normals) in the scene's triangle order, then rebuilds
+ * the emissive-triangle CDF and the BVH.  Materials and triangle count are unchanged.  Synchronises
+ * the context's stream; no frame may be in flight. */
+int rs_scene_update_positions(rs_scene* scene, const float* positions, const float* normals);
 /* Scene statistics: n_tris, n_emissive, n_bvh_nodes, bvh build time (ms). */
 int rs_scene_info(const rs_scene* scene, uint32_t* n_tris, uint32_t* n_emissive, uint32_t* n_nodes,
                   float* build_ms);

@@ -33,6 +33,10 @@ struct rs_scene {
     float* d_cdf = nullptr;
     int* d_cdf_guide = nullptr;
     float build_ms = 0.0f;
+    // host copies for rs_scene_update_positions (rebuilds the geometry-dependent tables)
+    std::vector<float> h_nrm;
+    std::vector<uint32_t> h_tri_mat;
+    std::vector<rs_material_desc> h_mats;
     // per-scene traversal choice (RS_TRAVERSAL_AUTO): frame times of each kind, tuning frames counted
     mutable int trav_choice = -1;
     mutable int trav_runs[2] = {0, 0};
@@ -264,6 +268,7 @@ extern "C" const char* rs_last_error(const rs_context* c) {
 }
 
 // --------------------------------------------------------------------------- scene
+static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& pos, std::string& err);
 static int scene_from_arrays(rs_context* c, const std::vector<float>& pos, const std::vector<float>& nrm,
                              const std::vector<uint32_t>& tri_mat, const rs_material_desc* mats, uint32_t n_mats,
                              rs_scene** out) {
@@ -298,7 +303,34 @@ static int scene_from_arrays(rs_context* c, const std::vector<float>& pos, const
         tn[3 * t + 1] = make_float4(q[3], q[4], q[5], eb);
         tn[3 * t + 2] = make_float4(q[6], q[7], q[8], 0.0f);
     }
-    // TriangleCDF (pg/TriangleCDF.cpp:8-34, pg/TriangleCDF.h:25-31), Triangle::area (pg/triangle.cpp:13-16)
+    rs_scene* s = new rs_scene();
+    s->ctx = c; s->n_tris = n; s->n_mats = n_mats;
+    s->h_nrm = nrm; s->h_tri_mat = tri_mat; s->h_mats.assign(mats, mats + n_mats);
+    auto bail = [&](const std::string& m) { rs_scene_destroy(s); return fail(c, RS_E_HIP, m); };
+    hipStream_t st = c->stream;
+    if (hipMalloc(&s->d_tri_nrm, tn.size() * sizeof(float4)) != hipSuccess) return bail("hipMalloc(nrm) failed");
+    hipMemcpyAsync(s->d_tri_nrm, tn.data(), tn.size() * sizeof(float4), hipMemcpyHostToDevice, st);
+    if (hipMalloc(&s->d_mats, hm.size() * sizeof(float4)) != hipSuccess) return bail("hipMalloc(mats) failed");
+    hipMemcpyAsync(s->d_mats, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice, st);
+    std::string err;
+    if (build_geometry(c, s, pos, err) != 0) return bail(err);
+    *out = s;
+    return RS_OK;
+}
+
+// Everything that depends on the vertex positions: the emissive-triangle table + CDF + guide table
+// (TriangleCDF ctor, pg/TriangleCDF.cpp:8-34, pg/TriangleCDF.h:25-31; Triangle::area,
+// pg/triangle.cpp:13-16) and the BVH.  Used at scene creation and by rs_scene_update_positions.
+static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& pos, std::string& err) {
+    const uint32_t n = s->n_tris;
+    const std::vector<float>& nrm = s->h_nrm;
+    const std::vector<uint32_t>& tri_mat = s->h_tri_mat;
+    const rs_material_desc* mats = s->h_mats.data();
+    std::vector<uint32_t> emis_tri;
+    for (uint32_t t = 0; t < n; ++t) {
+        const rs_material_desc& d = mats[tri_mat[t]];
+        if (d.emission[0] + d.emission[1] + d.emission[2] > 0) emis_tri.push_back(t);   // same order as eid
+    }
     const uint32_t ne = (uint32_t)emis_tri.size();
     std::vector<float> area(ne), cdf(std::max(ne, 1u));
     float total = 0.0f;
@@ -332,45 +364,61 @@ static int scene_from_arrays(rs_context* c, const std::vector<float>& pos, const
         em[8 * e + 6] = make_float4(d.emission[0], d.emission[1], d.emission[2], 0.0f);
         em[8 * e + 7] = make_float4(area[e], 0.0f, 0.0f, 0.0f);
     }
-    rs_scene* s = new rs_scene();
-    s->ctx = c; s->n_tris = n; s->n_emis = ne; s->n_mats = n_mats;
-    auto bail = [&](const std::string& m) { rs_scene_destroy(s); return fail(c, RS_E_HIP, m); };
+    std::vector<int> guide(kCdfGuide + 1);     // guide[j] = lower_bound(cdf, j / kCdfGuide)
+    for (int j = 0; j <= kCdfGuide; ++j) {
+        float key = (float)j / (float)kCdfGuide;
+        guide[j] = (int)(std::lower_bound(cdf.begin(), cdf.begin() + ne, key) - cdf.begin());
+    }
     hipStream_t st = c->stream;
+    if (hipStreamSynchronize(st) != hipSuccess) { err = "stream sync failed"; return -1; }   // frames in flight
+    void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide};
+    for (void* p : old) if (p) hipFree(p);
+    s->d_pos = nullptr; s->d_nodes = nullptr; s->d_tris = nullptr; s->d_emis = nullptr; s->d_cdf = nullptr;
+    s->d_cdf_guide = nullptr; s->n_nodes = 0;
+    s->n_emis = ne;
     if (n) {
-        if (hipMalloc(&s->d_pos, pos.size() * sizeof(float)) != hipSuccess) return bail("hipMalloc(pos) failed");
+        if (hipMalloc(&s->d_pos, pos.size() * sizeof(float)) != hipSuccess) { err = "hipMalloc(pos) failed"; return -1; }
         hipMemcpyAsync(s->d_pos, pos.data(), pos.size() * sizeof(float), hipMemcpyHostToDevice, st);
     }
-    if (hipMalloc(&s->d_tri_nrm, tn.size() * sizeof(float4)) != hipSuccess) return bail("hipMalloc(nrm) failed");
-    hipMemcpyAsync(s->d_tri_nrm, tn.data(), tn.size() * sizeof(float4), hipMemcpyHostToDevice, st);
-    if (hipMalloc(&s->d_mats, hm.size() * sizeof(float4)) != hipSuccess) return bail("hipMalloc(mats) failed");
-    hipMemcpyAsync(s->d_mats, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice, st);
-    if (hipMalloc(&s->d_emis, em.size() * sizeof(float4)) != hipSuccess) return bail("hipMalloc(emis) failed");
+    if (hipMalloc(&s->d_emis, em.size() * sizeof(float4)) != hipSuccess) { err = "hipMalloc(emis) failed"; return -1; }
     hipMemcpyAsync(s->d_emis, em.data(), em.size() * sizeof(float4), hipMemcpyHostToDevice, st);
-    if (hipMalloc(&s->d_cdf, cdf.size() * sizeof(float)) != hipSuccess) return bail("hipMalloc(cdf) failed");
+    if (hipMalloc(&s->d_cdf, cdf.size() * sizeof(float)) != hipSuccess) { err = "hipMalloc(cdf) failed"; return -1; }
     hipMemcpyAsync(s->d_cdf, cdf.data(), cdf.size() * sizeof(float), hipMemcpyHostToDevice, st);
-    {   // guide table for the exact lower_bound: guide[j] = lower_bound(cdf, j / kCdfGuide)
-        std::vector<int> guide(kCdfGuide + 1);
-        for (int j = 0; j <= kCdfGuide; ++j) {
-            float key = (float)j / (float)kCdfGuide;
-            guide[j] = (int)(std::lower_bound(cdf.begin(), cdf.begin() + ne, key) - cdf.begin());
-        }
-        if (hipMalloc(&s->d_cdf_guide, guide.size() * sizeof(int)) != hipSuccess) return bail("hipMalloc(guide) failed");
-        hipMemcpyAsync(s->d_cdf_guide, guide.data(), guide.size() * sizeof(int), hipMemcpyHostToDevice, st);
-        if (hipStreamSynchronize(st) != hipSuccess) return bail("guide upload failed");
-    }
+    if (hipMalloc(&s->d_cdf_guide, guide.size() * sizeof(int)) != hipSuccess) { err = "hipMalloc(guide) failed"; return -1; }
+    hipMemcpyAsync(s->d_cdf_guide, guide.data(), guide.size() * sizeof(int), hipMemcpyHostToDevice, st);
+    if (hipStreamSynchronize(st) != hipSuccess) { err = "geometry upload failed"; return -1; }   // host vectors die
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
     hipEventRecord(e0, st);
     std::string berr;
-    if (build_bvh(s->d_pos, n, st, &s->d_nodes, &s->n_nodes, &s->d_tris, berr) != 0) {
-        hipEventDestroy(e0); hipEventDestroy(e1);
-        return bail("BVH build failed: " + berr);
-    }
+    int rc = build_bvh(s->d_pos, n, st, &s->d_nodes, &s->n_nodes, &s->d_tris, berr);
     hipEventRecord(e1, st);
-    if (hipStreamSynchronize(st) != hipSuccess) { hipEventDestroy(e0); hipEventDestroy(e1); return bail("scene upload failed"); }
-    hipEventElapsedTime(&s->build_ms, e0, e1);
+    if (rc == 0 && hipStreamSynchronize(st) == hipSuccess) hipEventElapsedTime(&s->build_ms, e0, e1);
+    else { err = "BVH build failed: " + berr; rc = -1; }
     hipEventDestroy(e0); hipEventDestroy(e1);
-    *out = s;
+    return rc;
+}
+
+extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, const float* normals) {
+    if (!s || !positions) return fail(s ? s->ctx : nullptr, RS_E_INVALID, "rs_scene_update_positions: null argument");
+    rs_context* c = s->ctx;
+    if (c->active) return fail(c, RS_E_INVALID, "rs_scene_update_positions: a frame is in flight");
+    HIPCHK(c, enter(c));
+    std::vector<float> pos(positions, positions + 9 * (size_t)s->n_tris);
+    if (normals) {
+        s->h_nrm.assign(normals, normals + 9 * (size_t)s->n_tris);
+        std::vector<float4> tn(3 * (size_t)std::max(s->n_tris, 1u));
+        HIPCHK(c, hipMemcpy(tn.data(), s->d_tri_nrm, tn.size() * sizeof(float4), hipMemcpyDeviceToHost));
+        for (uint32_t t = 0; t < s->n_tris; ++t) {
+            const float* q = &s->h_nrm[9 * (size_t)t];
+            tn[3 * t] = make_float4(q[0], q[1], q[2], tn[3 * t].w);
+            tn[3 * t + 1] = make_float4(q[3], q[4], q[5], tn[3 * t + 1].w);
+            tn[3 * t + 2] = make_float4(q[6], q[7], q[8], 0.0f);
+        }
+        HIPCHK(c, hipMemcpy(s->d_tri_nrm, tn.data(), tn.size() * sizeof(float4), hipMemcpyHostToDevice));
+    }
+    std::string err;
+    if (build_geometry(c, s, pos, err) != 0) return fail(c, RS_E_HIP, "rs_scene_update_positions: " + err);
     return RS_OK;
 }
 

@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = [
     "rs_scene_destroy", "rs_scene_info", "rs_render_frame", "rs_get_frame_device_ptr", "rs_reset_history",
     "rs_synchronize", "rs_dump_gbuffer", "rs_dump_reservoirs", "rs_tile_begin", "rs_tile_halo_ptr",
     "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_context_set_traversal",
-    "rs_context_get_traversal", "rs_get_timing_totals",
+    "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -111,6 +111,7 @@ def load_library(path: str = LIB_PATH):
     ip = ctypes.POINTER(ctypes.c_int32)
     L.rs_context_get_traversal.argtypes = [vp, vp, ip, ip, ip]
     L.rs_get_timing_totals.argtypes = [vp, ctypes.POINTER(PassTimes), ctypes.POINTER(u32), i32]
+    L.rs_scene_update_positions.argtypes = [vp, fp, fp]
     _lib = L
     return L
 
@@ -135,6 +136,24 @@ class Scene:
         renderer._check(renderer.lib.rs_scene_info(handle, ctypes.byref(n_tris), ctypes.byref(n_emis),
                                                    ctypes.byref(n_nodes), ctypes.byref(ms)))
         self.n_tris, self.n_emissive, self.n_nodes, self.build_ms = n_tris.value, n_emis.value, n_nodes.value, ms.value
+
+    def update_positions(self, positions, normals=None):
+        """Move the geometry (rs_scene_update_positions): (T, 9) float32 positions in the scene's triangle
+        order, optional (T, 9) normals; rebuilds the light CDF and the BVH."""
+        pos = np.ascontiguousarray(positions, np.float32).reshape(-1)
+        if pos.size != 9 * self.n_tris:
+            raise ValueError(f"expected {self.n_tris} x 9 positions, got {pos.size}")
+        fp = ctypes.POINTER(ctypes.c_float)
+        nrm = None if normals is None else np.ascontiguousarray(normals, np.float32).reshape(-1)
+        if nrm is not None and nrm.size != pos.size:
+            raise ValueError("normals must match positions")
+        r = self.renderer
+        r._check(r.lib.rs_scene_update_positions(self.h, pos.ctypes.data_as(fp),
+                                                 nrm.ctypes.data_as(fp) if nrm is not None else None))
+        n_tris, n_emis, n_nodes, ms = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_float()
+        r._check(r.lib.rs_scene_info(self.h, ctypes.byref(n_tris), ctypes.byref(n_emis), ctypes.byref(n_nodes),
+                                     ctypes.byref(ms)))
+        self.n_nodes, self.build_ms = n_nodes.value, ms.value
 
     def close(self):
         if self.h:

@@ -349,3 +349,23 @@ def by_name(name: str) -> Scene:
     if name in ("C3", "sponza"):
         return sponza_like()
     raise KeyError(name)
+
+
+def moving_light_positions(scene: Scene, frame: int, n_frames: int = 240, amplitude: float = 0.05) -> np.ndarray:
+    """C5 "moving lights" (a build extension -- the reference cannot move geometry): every emissive quad
+    (two consecutive emissive triangles) slides along its own plane, offset = amplitude *
+    sin(2 pi frame / n_frames + phase_q) along the quad's first edge, phase_q = 2 pi frac(q * 0.618034).
+    Returns the full (T, 9) float32 position array for Scene.update_positions / the oracle."""
+    pos = np.array(scene.positions, dtype=np.float32, copy=True)
+    emis = np.nonzero(scene.emissive_mask())[0]
+    quads = emis.reshape(-1, 2) if emis.size % 2 == 0 else emis.reshape(-1, 1)
+    v = pos[quads[:, 0]].reshape(-1, 3, 3).astype(np.float64)
+    tangent = v[:, 1] - v[:, 0]
+    tangent /= np.maximum(np.linalg.norm(tangent, axis=1, keepdims=True), 1e-12)
+    q = np.arange(quads.shape[0], dtype=np.float64)
+    phase = 2.0 * np.pi * np.modf(q * 0.618034)[0]
+    off = amplitude * np.sin(2.0 * np.pi * frame / n_frames + phase)[:, None] * tangent      # (Q, 3)
+    for j in range(quads.shape[1]):
+        t = quads[:, j]
+        pos[t] = (pos[t].reshape(-1, 3, 3) + off[:, None, :]).reshape(-1, 9).astype(np.float32)
+    return pos

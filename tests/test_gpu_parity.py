@@ -191,6 +191,30 @@ def test_traversal_kinds_bit_identical(which):
         _assert_close(frames["lane"][f], o.render(os_, cam(f), prm, f), f"{which} frame {f}")
 
 
+def test_c5_moving_lights_match_oracle():
+    """C5 extension: lights moved each frame with rs_scene_update_positions (light CDF + BVH rebuilt)
+    under an orbiting camera with temporal + spatial reuse; the oracle renders each frame from a fresh
+    scene with the same positions."""
+    sc = scenes.cornell_many_lights(256)
+    prm = P.c3_params(m_area=8)
+    W, H = 64, 48
+    g = Renderer(W, H)
+    gs = g.load_scene(sc)
+    o = O.OracleRenderer(W, H)
+    n_before = gs.n_nodes
+    for f in range(3):
+        pos = scenes.moving_light_positions(sc, 20 * f, 240)
+        gs.update_positions(pos)
+        cam = scenes.orbit_camera(sc.camera, f, 240, 0.3)
+        a = g.produce_restir(gs, cam, prm, f).copy()
+        moved = scenes.Scene(pos, sc.normals, sc.tri_material, sc.materials, sc.camera)
+        b = o.render(O.OracleScene(moved), cam, prm, f)
+        _assert_close(a, b, f"C5 frame {f}")
+    assert gs.n_nodes > 0 and abs(gs.n_nodes - n_before) < n_before
+    with pytest.raises(ValueError):
+        gs.update_positions(np.zeros((3, 9), np.float32))
+
+
 def test_timing_totals_match_per_frame_times():
     """rs_get_timing_totals (no per-frame sync) sums the same rays as per-frame timed readback and
     counts every frame, across more frames than the event ring holds."""
