@@ -98,6 +98,20 @@ public:
     }
     void resetHistory() { check(rs_reset_history(ctx_), ctx_); }
 
+    // The producer loop's post block after produceRestir (pg/simpleguidx11.cpp:246-333, OIDN excluded):
+    // accumulate into the accumulator, ACES + sRGB into display_data(), accumulatorMean/Variance.
+    void postFrame() {
+        rs_post_params pp{accumulate ? 1 : 0, tonemap ? 1 : 0, gammaCorrect ? 1 : 0, maxAccCount};
+        rs_post_stats st{};
+        const float* dptr = nullptr;
+        check(rs_post_frame(ctx_, &pp, &dptr, &st), ctx_);
+        accFrameCtr = accumulate && st.acc_frames_used + 1 <= (uint32_t)maxAccCount ? st.acc_frames_used + 1 : 0;
+        accumulatorMean = st.mean;
+        accumulatorVariance = st.variance;
+        display_device_ = dptr;
+    }
+    const float* display_device_data() const { return display_device_; }   // device W*H*4 float RGBA
+
     const float* frame_data() const { return frame_.data(); }    // W*H*3, row-major, y=0 top
     int width() const { return width_; }
     int height() const { return height_; }
@@ -110,8 +124,15 @@ public:
           temporalReusePassDuration = 0, spatialReusePassDuration = 0, shadingPassDuration = 0,
           bufferCopyDuration = 0, totalFrameDuration = 0;
     uint64_t raysTraced = 0;
+    // post block (SimpleGuiDX11 accumulate / maxAccCount / accFrameCtr, RenderParams::tonemap,
+    // Raytracer::gammaCorrect, accumulatorMean / accumulatorVariance)
+    bool accumulate = false, tonemap = true, gammaCorrect = true;
+    int maxAccCount = 300000;
+    uint32_t accFrameCtr = 0;
+    double accumulatorMean = 0.0, accumulatorVariance = 0.0;
 
 private:
+    const float* display_device_ = nullptr;
     void replace_scene(rs_scene* s) {
         if (scene_) rs_scene_destroy(scene_);
         scene_ = s;

@@ -165,6 +165,33 @@ int rs_context_set_traversal(rs_context* ctx, int mode);
 int rs_context_get_traversal(const rs_context* ctx, const rs_scene* scene, int* mode, int* last_kind,
                              int* scene_choice);
 
+/* ---- post-frame: the producer loop's block after produceRestir -------------
+ * (pg/simpleguidx11.cpp:246-333, OIDN excluded):  accumulator = mix(accumulator, frame_data,
+ * 1/(accFrameCtr+1)); display = vec4(compress(aces(accumulator)), 1) per the tonemap (RenderParams,
+ * default on) and gammaCorrect (Raytracer, default on) switches; mean / variance of the
+ * accumulator's per-pixel channel mean.  Operates on the rows of the last rendered frame (a tile's
+ * band after rs_tile_finish).  Without `accumulate` accFrameCtr restarts at 0 every frame (the
+ * accumulator then equals the frame), as in the reference (:297-306).  The accumulator starts at 0. */
+typedef struct {
+    int32_t accumulate;        /* SimpleGuiDX11::accumulate (default false) */
+    int32_t tonemap;           /* RenderParams::tonemap (default true) */
+    int32_t gamma_correct;     /* Raytracer::gammaCorrect (default true) */
+    int32_t max_acc_frames;    /* maxAccCount (<= 0: the reference's 300000) */
+} rs_post_params;
+typedef struct {
+    double mean, variance;     /* accumulatorMean / accumulatorVariance over the rows processed */
+    double sum, sqr_sum;       /* the double sums behind them (combine across tiles by summing) */
+    uint64_t pixels;
+    uint32_t acc_frames_used;  /* accFrameCtr this frame was blended with */
+    uint32_t reserved;
+} rs_post_stats;
+/* display_rgba_dptr (optional) receives the device pointer of the W*H float4 display buffer;
+ * stats (optional) synchronises the stream. */
+int rs_post_frame(rs_context* ctx, const rs_post_params* params, const float** display_rgba_dptr,
+                  rs_post_stats* stats);
+/* accFrameCtr = 0 (the next rs_post_frame overwrites the accumulator with the frame). */
+int rs_post_reset(rs_context* ctx);
+
 /* ---- state dumps for golden parity ------------------------------------------------------- */
 /* G-buffer of the last rendered frame (prev=0) or the one before (prev=1): W*H*19 floats per pixel
  * pos3 normal3 kd3 ks3 Le3 shininess depth type 1/I_M.  Reservoirs shaded last frame: W*H*12

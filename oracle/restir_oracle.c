@@ -1321,3 +1321,52 @@ void or_set_num_threads(int n) {
     (void)n;
 #endif
 }
+
+/* ------------------------------------------------------------------ post-frame */
+/* The producer loop's per-frame post block (pg/simpleguidx11.cpp:246-333):
+ *   accumulator = glm::mix(accumulator, frame, 1/(accFrameCtr+1))          (:246-253; glm
+ *                 compute_mix_scalar: x*(1-a) + y*a)
+ *   pix = accumulator; if tonemap: Utils::aces (pg/utils.cpp:191-198); if gammaCorrect:
+ *   Utils::compress per channel (pg/utils.cpp:219-229, the float compared with the double 0.0031308);
+ *   display = vec4(pix, 1)                                                    (:266-294; denoise off)
+ *   mean / variance of the accumulator's per-pixel channel mean, float mean, double sums (:304-327).
+ * Rows [y0, y1) of a W-wide image; `sum` / `sqr_sum` return the double sums over those rows. */
+static inline float post_aces(float x) {
+    const float a = 2.51f, b = 0.03f, c = 2.43f, d = 0.59f, e = 0.14f;
+    float v = (x * (a * x + b)) / (x * (c * x + d) + e);
+    return gmin(gmax(v, 0.0f), 1.0f);          /* glm::clamp = min(max(x, lo), hi), select forms */
+}
+static inline float post_compress(float u) {
+    if (u <= 0.0f) return 0.0f;
+    if (u >= 1.0f) return 1.0f;
+    if ((double)u <= 0.0031308) return u * 12.92f;
+    return 1.055f * powf(u, 1.0f / 2.4f) - 0.055f;
+}
+void or_post_apply(int W, int y0, int y1, const float* frame, float* acc, int acc_frames, int tonemap,
+                   int gamma_correct, float* display_rgba, double* sum, double* sqr_sum) {
+    const float a = 1.0f / (float)(acc_frames + 1);
+    double s = 0.0, q = 0.0;
+    for (int y = y0; y < y1; ++y) {
+        for (int x = 0; x < W; ++x) {
+            size_t p = (size_t)y * W + x;
+            float px[3];
+            for (int k = 0; k < 3; ++k) {
+                float m = acc[3 * p + k] * (1.0f - a) + frame[3 * p + k] * a;
+                acc[3 * p + k] = m;
+                float v = m;
+                if (tonemap) v = post_aces(v);
+                if (gamma_correct) v = post_compress(v);
+                px[k] = v;
+            }
+            if (display_rgba) {
+                display_rgba[4 * p] = px[0]; display_rgba[4 * p + 1] = px[1];
+                display_rgba[4 * p + 2] = px[2]; display_rgba[4 * p + 3] = 1.0f;
+            }
+            float mean = (acc[3 * p] + acc[3 * p + 1] + acc[3 * p + 2]) / 3.0f;
+            s += mean;
+            q += (double)(mean * mean);
+        }
+    }
+    if (sum) *sum = s;
+    if (sqr_sum) *sqr_sum = q;
+}

@@ -5,6 +5,7 @@
 // (pg/Scene.cpp:8-16, pg/ModelLoader.cpp:218-321, pg/TriangleCDF.cpp:8-34), computes the camera
 // (pg/camera.cpp:12-84) and sequences the passes of produceRestir (pg/simpleguidx11.cpp:359-487).
 #include "rs_passes.h"
+#include "rs_post.h"
 #include "../../include/restir_c.h"
 
 #include <cmath>
@@ -90,6 +91,13 @@ struct rs_context {
     int trav_mode = RS_TRAVERSAL_AUTO;
     int trav = TRAV_LOCKSTEP;
     bool tuning = false;
+    // post-frame (rs_post_frame): accumulator (float3, like the reference's glm::vec3 accumulator),
+    // display (float4 RGBA), per-workgroup statistic partials, accFrameCtr
+    float* acc = nullptr;
+    float4* display = nullptr;
+    double2* post_part = nullptr;
+    double2* post_out = nullptr;
+    uint32_t acc_frames = 0;
 };
 
 // --------------------------------------------------------------------------- helpers
@@ -255,6 +263,8 @@ extern "C" void rs_context_destroy(rs_context* c) {
     if (c->fb) hipFree(c->fb);
     if (c->d_cnt) hipFree(c->d_cnt);
     if (c->d_tot) hipFree(c->d_tot);
+    void* post[] = {c->acc, c->display, c->post_part, c->post_out};
+    for (void* p : post) if (p) hipFree(p);
     if (c->d_part) hipFree(c->d_part);
     if (c->h_cnt) hipHostFree(c->h_cnt);
     for (auto& slot : c->evr)
@@ -815,6 +825,59 @@ extern "C" int rs_dump_reservoirs(rs_context* c, float* out) {
         o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = b.x; o[4] = b.y; o[5] = b.z;
         o[6] = d.x; o[7] = d.y; o[8] = d.z; o[9] = a.w; o[10] = b.w; o[11] = (float)conf;
     }
+    return RS_OK;
+}
+
+// --------------------------------------------------------------------------- post-frame (§8f-1)
+extern "C" int rs_post_frame(rs_context* c, const rs_post_params* pp, const float** display_rgba_dptr,
+                             rs_post_stats* stats) {
+    if (!c || !pp) return fail(c, RS_E_INVALID, "rs_post_frame: null argument");
+    if (c->active) return fail(c, RS_E_INVALID, "rs_post_frame: a frame is in flight (finish it first)");
+    HIPCHK(c, enter(c));
+    const size_t npx = (size_t)c->W * c->H;
+    const int nblk_max = (int)((npx + 255) / 256);
+    if (!c->acc) {
+        HIPCHK(c, hipMalloc(&c->acc, npx * 3 * sizeof(float)));
+        HIPCHK(c, hipMemsetAsync(c->acc, 0, npx * 3 * sizeof(float), c->stream));   // zeroed accumulator
+        HIPCHK(c, hipMalloc(&c->display, npx * sizeof(float4)));
+        HIPCHK(c, hipMemsetAsync(c->display, 0, npx * sizeof(float4), c->stream));
+        HIPCHK(c, hipMalloc(&c->post_part, (size_t)nblk_max * sizeof(double2)));
+        HIPCHK(c, hipMalloc(&c->post_out, sizeof(double2)));
+    }
+    // rows of the last rendered frame / band (rs_render_frame: all rows)
+    const int y0 = c->frames ? c->F.y0 : 0, y1 = c->frames ? c->F.y1 : c->H;
+    PostConst P{c->W, y0, y1, 1.0f / (float)(c->acc_frames + 1), pp->tonemap ? 1 : 0, pp->gamma_correct ? 1 : 0};
+    const size_t n = (size_t)(y1 - y0) * c->W;
+    const int nblk = (int)((n + 255) / 256);
+    if (nblk > 0) {
+        k_post<<<nblk, 256, 0, c->stream>>>(c->fb, c->acc, c->display, P, c->post_part);
+        HIPCHK(c, hipGetLastError());
+        k_post_reduce<<<1, 256, 0, c->stream>>>(c->post_part, nblk, c->post_out);
+        HIPCHK(c, hipGetLastError());
+    }
+    // accFrameCtr bookkeeping (pg/simpleguidx11.cpp:297-306)
+    const uint32_t used = c->acc_frames;
+    c->acc_frames++;
+    const uint32_t max_acc = pp->max_acc_frames > 0 ? (uint32_t)pp->max_acc_frames : 300000u;
+    const bool accumulate = pp->accumulate && c->acc_frames <= max_acc;
+    if (!accumulate) c->acc_frames = 0;
+    if (display_rgba_dptr) *display_rgba_dptr = (const float*)c->display;
+    if (stats) {
+        double2 h{0.0, 0.0};
+        if (nblk > 0) HIPCHK(c, hipMemcpyAsync(&h, c->post_out, sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        stats->sum = h.x; stats->sqr_sum = h.y; stats->pixels = n;
+        stats->mean = n ? h.x / (double)n : 0.0;
+        const double sqr_mean = n ? h.y / (double)n : 0.0;
+        stats->variance = sqr_mean - stats->mean * stats->mean;     // D(X) = E(X^2) - E(X)^2 (:324-325)
+        stats->acc_frames_used = used;
+    }
+    return RS_OK;
+}
+
+extern "C" int rs_post_reset(rs_context* c) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_post_reset: null context");
+    c->acc_frames = 0;
     return RS_OK;
 }
 

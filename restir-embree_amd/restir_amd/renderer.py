@@ -28,7 +28,8 @@ EXPORTED_SYMBOLS = [
     "rs_scene_destroy", "rs_scene_info", "rs_render_frame", "rs_get_frame_device_ptr", "rs_reset_history",
     "rs_synchronize", "rs_dump_gbuffer", "rs_dump_reservoirs", "rs_tile_begin", "rs_tile_halo_ptr",
     "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_context_set_traversal",
-    "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions",
+    "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions", "rs_post_frame",
+    "rs_post_reset",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -57,6 +58,17 @@ class PassTimes(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class PostParams(ctypes.Structure):
+    _fields_ = [("accumulate", ctypes.c_int32), ("tonemap", ctypes.c_int32), ("gamma_correct", ctypes.c_int32),
+                ("max_acc_frames", ctypes.c_int32)]
+
+
+class PostStats(ctypes.Structure):
+    _fields_ = [("mean", ctypes.c_double), ("variance", ctypes.c_double), ("sum", ctypes.c_double),
+                ("sqr_sum", ctypes.c_double), ("pixels", ctypes.c_uint64), ("acc_frames_used", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 class TileDesc(ctypes.Structure):
@@ -112,6 +124,8 @@ def load_library(path: str = LIB_PATH):
     L.rs_context_get_traversal.argtypes = [vp, vp, ip, ip, ip]
     L.rs_get_timing_totals.argtypes = [vp, ctypes.POINTER(PassTimes), ctypes.POINTER(u32), i32]
     L.rs_scene_update_positions.argtypes = [vp, fp, fp]
+    L.rs_post_frame.argtypes = [vp, ctypes.POINTER(PostParams), ctypes.POINTER(vp), ctypes.POINTER(PostStats)]
+    L.rs_post_reset.argtypes = [vp]
     _lib = L
     return L
 
@@ -250,6 +264,35 @@ class Renderer:
 
     def synchronize(self):
         self._check(self.lib.rs_synchronize(self.h))
+
+    def post_frame(self, accumulate: bool = False, tonemap: bool = True, gamma_correct: bool = True,
+                   max_acc_frames: int = 0, stats: bool = True):
+        """Post-frame block of the reference's producer loop (rs_post_frame): accumulate, ACES + sRGB
+        display, accumulator mean/variance.  Returns (display device pointer, PostStats or None)."""
+        p = PostParams(int(accumulate), int(tonemap), int(gamma_correct), int(max_acc_frames))
+        dptr, st = ctypes.c_void_p(), PostStats()
+        self._check(self.lib.rs_post_frame(self.h, ctypes.byref(p), ctypes.byref(dptr),
+                                           ctypes.byref(st) if stats else None))
+        self._display_ptr = int(dptr.value or 0)
+        return self._display_ptr, (st if stats else None)
+
+    def post_reset(self):
+        self._check(self.lib.rs_post_reset(self.h))
+
+    def display_rgba(self) -> np.ndarray:
+        """Host copy of the (H, W, 4) float32 display buffer written by post_frame (a zero-copy torch
+        view of the device buffer, copied to the host)."""
+        import torch
+        if not getattr(self, "_display_ptr", 0):
+            raise RestirError("display_rgba: call post_frame first")
+
+        class _DeviceArray:
+            def __init__(self, ptr, n):
+                self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (ptr, False),
+                                                 "version": 2, "strides": None}
+        self.synchronize()
+        t = torch.as_tensor(_DeviceArray(self._display_ptr, self.H * self.W * 4), device="cuda")
+        return t.cpu().numpy().reshape(self.H, self.W, 4)
 
     def timing_totals(self, reset: bool = False):
         """(PassTimes with ms / ray totals, n_frames) over all frames finished since creation or the last

@@ -65,12 +65,15 @@ int main(int argc, char** argv) {
             r.LoadScene(meshes, {white, light});
             r.camera_ = restir::Camera(0.0f, -3.9f, 1.0f, 0.0f, 0.0f, 1.0f, 40.0f);
         }
+        r.accumulate = true;                 // the producer loop's progressive accumulation
         for (int f = 0; f < frames; ++f) {
             r.produceRestir();
+            r.postFrame();
             std::printf("frame %d: gbuffer+initial %.3f ms, temporal %.3f ms, spatial %.3f ms, shade %.3f ms, "
-                        "total %.3f ms, rays %llu\n", f, r.gBUfferFillDuration, r.temporalReusePassDuration,
-                        r.spatialReusePassDuration, r.shadingPassDuration, r.totalFrameDuration,
-                        (unsigned long long)r.raysTraced);
+                        "total %.3f ms, rays %llu, accumulator mean %.6f var %.6f (%u frames)\n", f,
+                        r.gBUfferFillDuration, r.temporalReusePassDuration, r.spatialReusePassDuration,
+                        r.shadingPassDuration, r.totalFrameDuration, (unsigned long long)r.raysTraced,
+                        r.accumulatorMean, r.accumulatorVariance, r.accFrameCtr);
         }
         if (!out.empty()) {
             FILE* fp = std::fopen(out.c_str(), "wb");

@@ -71,8 +71,39 @@ def lib():
                                        _f32p, _i32p]
         L.or_trace_any.argtypes = [ctypes.c_void_p, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _i32p]
         L.or_num_threads.restype = ctypes.c_int
+        _f64p = ctypes.POINTER(ctypes.c_double)
+        L.or_post_apply.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, _f32p, _f64p, _f64p]
         _lib = L
     return _lib
+
+
+class OraclePost:
+    """Post-frame restatement (oracle or_post_apply) with the reference's accFrameCtr bookkeeping
+    (pg/simpleguidx11.cpp:246-333): accumulate / tonemap / gamma, mean & variance of the accumulator."""
+
+    def __init__(self, W: int, H: int):
+        self.W, self.H = W, H
+        self.acc = np.zeros((H, W, 3), np.float32)
+        self.acc_frames = 0
+
+    def apply(self, frame, accumulate=False, tonemap=True, gamma_correct=True, max_acc_frames=0):
+        L = lib()
+        frame = np.ascontiguousarray(frame, np.float32)
+        disp = np.zeros((self.H, self.W, 4), np.float32)
+        s, q = ctypes.c_double(), ctypes.c_double()
+        used = self.acc_frames
+        L.or_post_apply(self.W, 0, self.H, frame.ctypes.data_as(_f32p), self.acc.ctypes.data_as(_f32p), used,
+                        int(tonemap), int(gamma_correct), disp.ctypes.data_as(_f32p), ctypes.byref(s),
+                        ctypes.byref(q))
+        self.acc_frames += 1
+        max_acc = max_acc_frames if max_acc_frames > 0 else 300000
+        if not (accumulate and self.acc_frames <= max_acc):
+            self.acc_frames = 0
+        n = self.W * self.H
+        mean = s.value / n
+        return disp, {"mean": mean, "variance": q.value / n - mean * mean, "sum": s.value, "sqr_sum": q.value,
+                      "acc_frames_used": used}
 
 
 class OracleScene:

@@ -215,6 +215,33 @@ def test_c5_moving_lights_match_oracle():
         gs.update_positions(np.zeros((3, 9), np.float32))
 
 
+def test_post_frame_matches_oracle():
+    """rs_post_frame (accumulate + ACES + sRGB + mean/variance) against the oracle's post restatement
+    applied to the GPU's own frames: accumulator bit-exact, display within powf ulps, stats 1e-9."""
+    sc = scenes.cornell_box(8)
+    prm = P.default_params(m_area=4, do_spatial=1, do_temporal=1)
+    W, H = 64, 48
+    g = Renderer(W, H)
+    gs = g.load_scene(sc)
+    post = O.OraclePost(W, H)
+    for f in range(4):
+        frame = g.produce_restir(gs, sc.camera, prm, f).copy()
+        _, st = g.post_frame(accumulate=True, tonemap=False, gamma_correct=False)
+        disp = g.display_rgba()
+        ref_disp, ref = post.apply(frame, accumulate=True, tonemap=False, gamma_correct=False)
+        assert st.acc_frames_used == ref["acc_frames_used"] == f
+        np.testing.assert_array_equal(disp, ref_disp)                     # display == accumulator
+        assert abs(st.mean - ref["mean"]) <= 1e-9 * abs(ref["mean"]) + 1e-12
+        assert abs(st.variance - ref["variance"]) <= 1e-9 * abs(ref["variance"]) + 1e-12
+    frame = g.produce_restir(gs, sc.camera, prm, 4).copy()
+    _, st = g.post_frame(accumulate=True)                                 # tonemap + gamma (defaults)
+    ref_disp, ref = post.apply(frame, accumulate=True)
+    np.testing.assert_allclose(g.display_rgba(), ref_disp, rtol=0, atol=2e-6)
+    g.post_reset()
+    _, st = g.post_frame(accumulate=False)
+    assert st.acc_frames_used == 0
+
+
 def test_timing_totals_match_per_frame_times():
     """rs_get_timing_totals (no per-frame sync) sums the same rays as per-frame timed readback and
     counts every frame, across more frames than the event ring holds."""

@@ -220,3 +220,49 @@ def test_oracle_rejects_skybox():
 
 def test_params_struct_layout():
     assert ctypes.sizeof(P.FrameParams) == 88
+
+
+def test_post_frame_restatement():
+    """Oracle post-frame (accumulate / ACES / sRGB compress / mean-variance, pg/simpleguidx11.cpp:246-333,
+    pg/utils.cpp:191-229) against an independent numpy float32 restatement of the same formulas."""
+    from oracle_lib import OraclePost
+    rng = np.random.default_rng(3)
+    W, H = 13, 7
+    frames = [rng.uniform(-0.2, 3.0, size=(H, W, 3)).astype(np.float32) for _ in range(4)]
+    frames[0][0, 0] = [0.0, 1e-4, 0.0031]      # compress edge values / linear segment
+    post = OraclePost(W, H)
+    acc = np.zeros((H, W, 3), np.float32)
+    f32 = np.float32
+
+    def aces(x):
+        v = (x * (f32(2.51) * x + f32(0.03))) / (x * (f32(2.43) * x + f32(0.59)) + f32(0.14))
+        v = np.where(v < 0, f32(0), v)         # glm max(v, 0) select form
+        return np.where(f32(1) < v, f32(1), v)  # glm min(v, 1)
+
+    def compress(u):
+        out = np.where(u <= 0, f32(0), np.where(u >= 1, f32(1), f32(0)))
+        mid = (u > 0) & (u < 1)
+        lin = mid & (u.astype(np.float64) <= 0.0031308)
+        out = np.where(lin, u * f32(12.92), out)
+        pw = f32(1.055) * np.power(u, f32(1.0) / f32(2.4), dtype=np.float32) - f32(0.055)
+        return np.where(mid & ~lin, pw, out).astype(np.float32)
+
+    for n, fr in enumerate(frames):
+        a = f32(1.0) / f32(n + 1)
+        acc = (acc * (f32(1) - a) + fr * a).astype(np.float32)
+        disp, st = post.apply(fr, accumulate=True)
+        assert st["acc_frames_used"] == n
+        np.testing.assert_array_equal(post.acc, acc)
+        ref = compress(aces(acc))
+        np.testing.assert_allclose(disp[..., :3], ref, rtol=0, atol=2e-7)
+        assert (disp[..., 3] == 1.0).all()
+        m = ((acc[..., 0] + acc[..., 1] + acc[..., 2]) / f32(3)).astype(np.float32)
+        mean = m.astype(np.float64).sum() / (W * H)
+        var = (m * m).astype(np.float64).sum() / (W * H) - mean * mean
+        assert abs(st["mean"] - mean) <= 1e-12 * max(1.0, abs(mean)) and abs(st["variance"] - var) <= 1e-9
+    # no accumulation: accFrameCtr restarts, the accumulator becomes the frame
+    post2 = OraclePost(W, H)
+    for fr in frames[:2]:
+        _, st = post2.apply(fr, accumulate=False, tonemap=False, gamma_correct=False)
+        assert st["acc_frames_used"] == 0
+        np.testing.assert_array_equal(post2.acc, fr)
