@@ -126,21 +126,32 @@ class TiledRenderer:
     def reset_history(self):
         self.be.reset_history()
 
+    def _staged(self, t) -> bool:
+        """gloo cannot move device tensors: stage them through host memory (tests only -- RCCL refuses
+        two ranks on one GPU, so multi-process GPU tests run the real backend over gloo)."""
+        import torch.distributed as dist
+        return t is not None and t.is_cuda and dist.get_backend(self.group) == "gloo"
+
     def _exchange_halo(self):
         import torch.distributed as dist
-        ops = []
+        ops, copy_back = [], []
         up, down = self.rank - 1, self.rank + 1
-        if up >= 0:
-            s, r = self.be.halo_tensor(2), self.be.halo_tensor(0)
-            if s is not None and r is not None:
-                ops += [dist.P2POp(dist.isend, s, up, self.group), dist.P2POp(dist.irecv, r, up, self.group)]
-        if down < self.world:
-            s, r = self.be.halo_tensor(3), self.be.halo_tensor(1)
-            if s is not None and r is not None:
-                ops += [dist.P2POp(dist.isend, s, down, self.group), dist.P2POp(dist.irecv, r, down, self.group)]
+        for peer, send_which, recv_which in ((up, 2, 0), (down, 3, 1)):
+            if peer < 0 or peer >= self.world:
+                continue
+            s, r = self.be.halo_tensor(send_which), self.be.halo_tensor(recv_which)
+            if s is None or r is None:
+                continue
+            if self._staged(s):
+                rh = r.new_empty(r.shape, device="cpu")
+                copy_back.append((r, rh))
+                s, r = s.cpu(), rh
+            ops += [dist.P2POp(dist.isend, s, peer, self.group), dist.P2POp(dist.irecv, r, peer, self.group)]
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
+        for dev, host in copy_back:
+            dev.copy_(host)
 
     def render(self, scene, camera, params, frame_index: int, gather: bool = True, timed: bool = False):
         """One frame; returns the full (H, W, 3) frame on rank 0 when gather=True (else None / band)."""
@@ -170,10 +181,11 @@ class TiledRenderer:
         max_rows = max(band_rows(self.H, r, self.world)[1] - band_rows(self.H, r, self.world)[0]
                        for r in range(self.world))
         n = max_rows * self.W * 3
-        buf = torch.zeros(n, dtype=torch.float32, device=band.device)
+        dev = "cpu" if self._staged(band) else band.device
+        buf = torch.zeros(n, dtype=torch.float32, device=dev)
         buf[: band.numel()].copy_(band)
         if self.rank == 0:
-            parts = [torch.empty(n, dtype=torch.float32, device=band.device) for _ in range(self.world)]
+            parts = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(self.world)]
             dist.gather(buf, parts, dst=0, group=self.group)
             rows = []
             for r in range(self.world):
