@@ -55,6 +55,24 @@ __device__ __forceinline__ bool tri_test(float4 A, float4 B, float4 C, vec3 o, v
     return true;
 }
 
+// The same test without early returns (identical arithmetic and acceptance; with det == 0 the
+// quotients are inf/NaN and the explicit det check rejects).  Used by the lockstep walks, where the
+// triangle is shared by the wave: straight-line VALU instead of three nested exec-mask regions.
+__device__ __forceinline__ bool tri_test_nb(float4 A, float4 B, float4 C, vec3 o, vec3 d, float tnear, float tfar,
+                                            float& t, float& u, float& v) {
+    vec3 v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
+    vec3 p = cross(d, e2);
+    float det = dot(e1, p);
+    float inv = 1.0f / det;
+    vec3 sv = o - v0;
+    u = dot(sv, p) * inv;
+    vec3 q = cross(sv, e1);
+    v = dot(d, q) * inv;
+    t = dot(e2, q) * inv;
+    const bool ok_u = u >= 0.0f && u <= 1.0f, ok_v = v >= 0.0f && u + v <= 1.0f, ok_t = t >= tnear && t <= tfar;
+    return (det != 0.0f) & ok_u & ok_v & ok_t;
+}
+
 // conservative slab test (interval widened by 4 ulp-ish so no box the triangle test accepts is culled)
 __device__ __forceinline__ bool box_test(float4 a, float4 b, vec3 o, vec3 inv, float tnear, float tfar) {
     float tx0 = (a.x - o.x) * inv.x, tx1 = (b.x - o.x) * inv.x;
@@ -215,45 +233,47 @@ __device__ __forceinline__ void occluded_wave_multi(const DevScene& S, const boo
         occ[k] = false;
     }
     const uint32_t n = S.n_nodes;
+    // per-lane ray state as integer bit-sets (bit k = ray k) held in VGPRs and updated with selects:
+    // bools carried across the loop's control flow would live as SGPR lane masks re-merged with
+    // s_andn2/s_and/s_or at every join -- that bookkeeping made SALU the busiest unit.  Only
+    // wave-uniform branches remain (leaf or not, ballot tests).
+    uint32_t occb = 0u;
     uint32_t m = wave_min(full, lane_min<K>(cur));
     while (m < n) {
         const float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
-        bool hb[K];
+        uint32_t hbb = 0u;
 #pragma unroll
-        for (int k = 0; k < K; ++k) hb[k] = cur[k] == m && box_test(a, b, o, inv[k], tnear, tfar[k]);
+        for (int k = 0; k < K; ++k) hbb |= (cur[k] == m && box_test(a, b, o, inv[k], tnear, tfar[k])) ? (1u << k) : 0u;
         if (leaf >= 0) {                                      // wave-uniform
             const int first = leaf >> 3, cnt = (leaf & 7) + 1;
             for (int j = 0; j < cnt; ++j) {
-                bool want = false;
-#pragma unroll
-                for (int k = 0; k < K; ++k) want = want || (hb[k] && !occ[k]);
-                if (__ballot(want) == 0) break;
+                const uint32_t want = hbb & ~occb;
+                if (__ballot(want != 0u) == 0) break;
                 const uint32_t tri = 3u * (uint32_t)(first + j);
                 const float4 T0 = sload(S.tris, tri), T1 = sload(S.tris, tri + 1), T2 = sload(S.tris, tri + 2);
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    if (hb[k] && !occ[k]) {
+                    if (__ballot((want >> k) & 1u) != 0) {        // wave-uniform
                         float t, u, v;
-                        occ[k] = tri_test(T0, T1, T2, o, d[k], tnear, tfar[k], t, u, v);
+                        const bool hit = tri_test_nb(T0, T1, T2, o, d[k], tnear, tfar[k], t, u, v);
+                        occb |= (((want >> k) & 1u) && hit) ? (1u << k) : 0u;
                     }
                 }
             }
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (cur[k] == m) cur[k] = (hb[k] && occ[k]) ? 0xffffffffu : skip;
+                cur[k] = cur[k] == m ? (((hbb & occb) >> k) & 1u ? 0xffffffffu : skip) : cur[k];
             m = wave_min(full, lane_min<K>(cur));
         } else {
-            bool desc = false;
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                desc = desc || hb[k];
-                if (cur[k] == m) cur[k] = hb[k] ? m + 1 : skip;
-            }
-            m = next_min(full, desc, m, lane_min<K>(cur));
+            for (int k = 0; k < K; ++k) cur[k] = cur[k] == m ? ((hbb >> k) & 1u ? m + 1 : skip) : cur[k];
+            m = next_min(full, hbb != 0u, m, lane_min<K>(cur));
         }
     }
+#pragma unroll
+    for (int k = 0; k < K; ++k) occ[k] = (occb >> k) & 1u;
 }
 // one any-hit ray per lane (the K = 1 walk, written out: the leaf loop exits per lane)
 __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
@@ -261,35 +281,33 @@ __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, ve
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const uint32_t n = S.n_nodes;
     uint32_t i = active ? 0u : 0xffffffffu;
-    bool occ = false;
+    uint32_t occ = 0u;                 // integer, not a bool: see occluded_wave_multi
     uint32_t m = wave_min(full, i);
     while (m < n) {
         const float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
-        bool desc = false;
-        if (i == m) {
-            const uint32_t skip = (uint32_t)__float_as_int(a.w);
-            if (box_test(a, b, o, inv, tnear, tfar)) {
-                const int leaf = __float_as_int(b.w);
-                if (leaf >= 0) {
-                    const int first = leaf >> 3, cnt = (leaf & 7) + 1;
-                    for (int k = 0; k < cnt && !occ; ++k) {
-                        const uint32_t tri = 3u * (uint32_t)(first + k);
-                        float t, u, v;
-                        occ = tri_test(sload(S.tris, tri), sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d,
-                                       tnear, tfar, t, u, v);
-                    }
-                    i = occ ? 0xffffffffu : skip;
-                } else {
-                    i = m + 1;
-                    desc = true;
-                }
-            } else {
-                i = skip;
+        const uint32_t skip = (uint32_t)__float_as_int(a.w);
+        const int leaf = __float_as_int(b.w);
+        const bool at = i == m;
+        const bool hb = at && box_test(a, b, o, inv, tnear, tfar);
+        if (leaf >= 0) {                                      // wave-uniform
+            const int first = leaf >> 3, cnt = (leaf & 7) + 1;
+            for (int k = 0; k < cnt; ++k) {
+                const bool want = hb && occ == 0u;
+                if (__ballot(want) == 0) break;
+                const uint32_t tri = 3u * (uint32_t)(first + k);
+                float t, u, v;
+                const bool hit = tri_test_nb(sload(S.tris, tri), sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d,
+                                             tnear, tfar, t, u, v);
+                occ = (want && hit) ? 1u : occ;
             }
+            i = at ? ((hb && occ) ? 0xffffffffu : skip) : i;
+            m = wave_min(full, i);
+        } else {
+            i = at ? (hb ? m + 1 : skip) : i;
+            m = next_min(full, hb, m, i);
         }
-        m = next_min(full, desc, m, i);
     }
-    return occ;
+    return occ != 0u;
 }
 __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     const bool full = __ballot(1) == ~0ull;
@@ -300,34 +318,31 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
     uint32_t m = wave_min(full, i);
     while (m < n) {
         const float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
-        bool desc = false;
-        if (i == m) {
-            const uint32_t skip = (uint32_t)__float_as_int(a.w);
-            if (box_test(a, b, o, inv, tnear, h.t)) {
-                const int leaf = __float_as_int(b.w);
-                if (leaf >= 0) {
-                    const int first = leaf >> 3, cnt = (leaf & 7) + 1;
-                    for (int k = 0; k < cnt; ++k) {
-                        const uint32_t tri = 3u * (uint32_t)(first + k);
-                        float4 T0 = sload(S.tris, tri);
-                        float t, u, v;
-                        if (tri_test(T0, sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d, tnear, h.t, t, u, v)) {
-                            int prim = __float_as_int(T0.w);
-                            if (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim)) {
-                                h.t = t; h.u = u; h.v = v; h.prim = prim;
-                            }
-                        }
-                    }
-                    i = skip;
-                } else {
-                    i = m + 1;
-                    desc = true;
+        const uint32_t skip = (uint32_t)__float_as_int(a.w);
+        const int leaf = __float_as_int(b.w);
+        const bool at = i == m;
+        const bool hb = at && box_test(a, b, o, inv, tnear, h.t);
+        if (leaf >= 0) {                                      // wave-uniform
+            if (__ballot(hb) != 0) {
+                const int first = leaf >> 3, cnt = (leaf & 7) + 1;
+                for (int k = 0; k < cnt; ++k) {
+                    const uint32_t tri = 3u * (uint32_t)(first + k);
+                    const float4 T0 = sload(S.tris, tri);
+                    float t, u, v;
+                    const bool hit = hb && tri_test_nb(T0, sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d, tnear,
+                                                       h.t, t, u, v);
+                    const int prim = __float_as_int(T0.w);
+                    const bool better = hit && (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim));
+                    h.t = better ? t : h.t; h.u = better ? u : h.u; h.v = better ? v : h.v;
+                    h.prim = better ? prim : h.prim;
                 }
-            } else {
-                i = skip;
             }
+            i = at ? skip : i;
+            m = wave_min(full, i);
+        } else {
+            i = at ? (hb ? m + 1 : skip) : i;
+            m = next_min(full, hb, m, i);
         }
-        m = next_min(full, desc, m, i);
     }
     return h;
 }
