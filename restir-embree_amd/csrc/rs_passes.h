@@ -515,12 +515,16 @@ __device__ __forceinline__ size_t list_px(const FrameConst& F, const Rng& rng, u
     return p;
 }
 
+// neighbour-list cache entries per thread in LDS (list positions 1..k; k <= kNbrCache - 1)
+constexpr int kNbrCache = 17;
+
 // spatialReusePass (pg/ReSTIRIntegrator.cpp:316-542); shade fused when this is the last pass.
 // List loops run to the uniform bound k+1 with `i < cnt` as a predicate (convergent ray queries).
 template <int T>
 __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr,
                                                                    ResBuf Rw, int pass_idx, int fuse_shade, float* fb,
                                                                    CountSlot C) {
+    __shared__ uint32_t nbr[kNbrCache * 256];
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
@@ -536,7 +540,9 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
     }
     if (__ballot(alive) != 0) {
         Rng rng; rng.init(F.seed, F.frame, PASS_SPATIAL0 + (uint32_t)pass_idx, (uint32_t)p);
-        // neighbour selection (:334-374)
+        // neighbour selection (:334-374); the accepted list is cached in LDS when k <= kNbrCache - 1
+        // (list position i -> pixel), otherwise list_px re-derives it from the RNG slots
+        const bool cached = F.k < kNbrCache;
         uint64_t acc = 0;
         int M = 1;
         for (int i = 0; i < F.k; ++i) {
@@ -553,14 +559,19 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
                 if (dr < 1.0f - hd || dr > 1.0f + hd) continue;
             }
             acc |= 1ull << i;
+            if (cached) nbr[M * 256 + threadIdx.x] = (uint32_t)q;
             M += 1;
         }
+        auto list_q = [&](int i) -> size_t {
+            if (!cached) return list_px(F, rng, acc, i, x, y, p);
+            return (i == 0 || i >= M) ? p : (size_t)nbr[i * 256 + threadIdx.x];
+        };
         rng.n = 2u * (uint32_t)F.k;
         const int cnt = M;
         const int kk = F.k + 1;                            // uniform list bound
         int csum = 0, csum_nc = 0;                         // :379-385
         for (int i = 0; i < cnt; ++i) {
-            int c = __float_as_int(Rr.r[3 * list_px(F, rng, acc, i, x, y, p) + 2].w);
+            int c = __float_as_int(Rr.r[3 * list_q(i) + 2].w);
             csum += c;
             if (i) csum_nc += c;
         }
@@ -568,9 +579,38 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
         int sel = 0;
         float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
         vec3 f_sel = mk(0, 0, 0);
-        for (int i = 0; i < kk; ++i) {
+        if (F.mis == MIS_CONSTANT) {
+            // CONSTANT MIS (the metric point): the k+1 candidates' shadow rays all start at this pixel,
+            // so pairs share one walk (trace_any_multi); the addSample draws stay in candidate order
+            const ShadeFrame sf = make_frame(th, cam);
+            for (int i0 = 0; i0 < kk; i0 += 2) {
+                FPre pre[2];
+                Res rr[2];
+                bool act[2], occ[2];
+                vec3 dir[2];
+                float tf[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int i = i0 + k;
+                    rr[k] = Rr.load(list_q(i));
+                    pre[k] = evaluate_f_pre(F, smp_of(rr[k]), th.pos, false, sf, true, alive && i < cnt);
+                    act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
+                    rays += act[k] ? 1u : 0u;
+                }
+                trace_any_multi<T, 2>(S, act, th.pos, dir, FLT_MIN + F.tnear_off, tf, occ);
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int i = i0 + k;
+                    if (i < kk) {
+                        const vec3 f = evaluate_f_post(pre[k], occ[k]);
+                        const float rw = rcpM * length(f) * rr[k].W;
+                        if (alive && i < cnt && res_add(res, smp_of(rr[k]), rw, rr[k].conf, rng)) { sel = i; f_sel = f; }
+                    }
+                }
+            }
+        } else for (int i = 0; i < kk; ++i) {
             const bool li = alive && i < cnt;
-            size_t qi = list_px(F, rng, acc, i, x, y, p);
+            size_t qi = list_q(i);
             Res ri = Rr.load(qi);
             Sample si = smp_of(ri);
             float mis = rcpM;
@@ -579,7 +619,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
                 mis = 0.0f;
                 for (int j = 0; j < kk; ++j) {
                     const bool lj = li && j < cnt;
-                    size_t qj = list_px(F, rng, acc, j, x, y, p);
+                    size_t qj = list_q(j);
                     int cj = __float_as_int(Rr.r[3 * qj + 2].w);
                     float ph = length(evaluate_f<T>(S, F, si, cam, G.load(qj), true, lj, rays));
                     if (lj) {
@@ -596,7 +636,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
                     float phc = length(evaluate_f<T>(S, F, si, cam, G.load(qi), true, li, rays)) * (float)ri.conf;
                     for (int j = 1; j < kk; ++j) {
                         const bool lj = li && j < cnt;
-                        size_t qj = list_px(F, rng, acc, j, x, y, p);
+                        size_t qj = list_q(j);
                         int cj = __float_as_int(Rr.r[3 * qj + 2].w);
                         float phj = length(evaluate_f<T>(S, F, si, cam, G.load(qj), true, lj, rays));
                         float den = phc + phj * (float)csum_nc;
@@ -628,18 +668,18 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
             float corr = 1.0f;
             for (int i = 0; i < kk; ++i) {
                 const bool li = alive && i < cnt;
-                size_t qi = list_px(F, rng, acc, i, x, y, p);
+                size_t qi = list_q(i);
                 bool occ = occluded<T>(S, F, li, G.pos(qi), res.p, rays);
                 if (li && !occ) Z += 1;
             }
             if (Z > 0 && M > 0) corr = (1.0f / (float)Z) / rcpM;
             res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
         } else if (F.mis == MIS_DEBIAS_CONTRIB) {          // :515-538
-            Sample ss = smp_of(Rr.load(list_px(F, rng, acc, sel, x, y, p)));
+            Sample ss = smp_of(Rr.load(list_q(sel)));
             float num = 0, den = 0, cw = 0, corr = 0;
             for (int i = 0; i < kk; ++i) {
                 const bool li = alive && i < cnt;
-                size_t qi = list_px(F, rng, acc, i, x, y, p);
+                size_t qi = list_q(i);
                 int ci = __float_as_int(Rr.r[3 * qi + 2].w);
                 float ph = length(evaluate_f<T>(S, F, ss, cam, G.load(qi), true, li, rays));
                 if (li) {
