@@ -329,7 +329,7 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
                     const uint32_t tri = 3u * (uint32_t)(first + k);
                     const float4 T0 = sload(S.tris, tri);
                     float t, u, v;
-                    const bool hit = hb && tri_test_nb(T0, sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d, tnear,
+                    const bool hit = hb & tri_test_nb(T0, sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d, tnear,
                                                        h.t, t, u, v);
                     const int prim = __float_as_int(T0.w);
                     const bool better = hit && (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim));
