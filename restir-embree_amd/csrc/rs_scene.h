@@ -95,6 +95,12 @@ __device__ __forceinline__ float4 sload(const float4* p, uint32_t i) {
     return p[i];   // host pass only type-checks device code
 #endif
 }
+// wave-uniform node load for the lockstep walks: scalar cache (default) or, with RS_NODE_VMEM, one
+// broadcast vector load through L1 (32 KB/CU) with the control words moved to SGPRs
+// (a broadcast vector load through L1 + readfirstlane was measured 10 % slower on C2)
+__device__ __forceinline__ void node_load(const float4* nodes, uint32_t m, float4& a, float4& b) {
+    a = sload(nodes, 2 * m); b = sload(nodes, 2 * m + 1);
+}
 template <bool Uniform>
 __device__ __forceinline__ float4 ld4(const float4* p, uint32_t i) {
     if (Uniform) return sload(p, i);
@@ -126,41 +132,61 @@ __device__ __forceinline__ void closest_visit(const DevScene& S, float4 a, float
 }
 
 // ---------------------------------------------------------------- per-lane walks (TRAV_LANE)
+// Branch-lean per-lane walks: uniform loop condition, select-based cursor updates, the leaf's
+// triangles in a wave-uniform loop up to the largest leaf among the lanes -- no per-lane exec-mask
+// regions (C3: +21 % over the branchy loop).
 __device__ __forceinline__ bool occluded_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-    if (!active) return false;
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    uint32_t i = 0;
     const uint32_t n = S.n_nodes;
-    while (i < n) {
-        float4 a = S.nodes[2 * i], b = S.nodes[2 * i + 1];
-        int skip = __float_as_int(a.w);
-        if (box_test(a, b, o, inv, tnear, tfar)) {
-            int leaf = __float_as_int(b.w);
-            if (leaf >= 0) {
-                int first = leaf >> 3, cnt = (leaf & 7) + 1;
-                for (int k = 0; k < cnt; ++k) {
-                    const float4* T = S.tris + 3 * (first + k);
-                    float t, u, v;
-                    if (tri_test(T[0], T[1], T[2], o, d, tnear, tfar, t, u, v)) return true;
-                }
-                i = (uint32_t)skip;
-            } else {
-                i = i + 1;
-            }
-        } else {
-            i = (uint32_t)skip;
+    uint32_t i = active ? 0u : 0xffffffffu, occ = 0u;
+    while (__ballot(i < n) != 0) {
+        const bool live = i < n;
+        const uint32_t ii = live ? i : 0u;
+        const float4 a = S.nodes[2 * ii], b = S.nodes[2 * ii + 1];
+        const uint32_t skip = (uint32_t)__float_as_int(a.w);
+        const int leaf = __float_as_int(b.w);
+        const bool hit = live & box_test(a, b, o, inv, tnear, tfar);
+        const bool in_leaf = hit & (leaf >= 0);
+        const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
+        for (int j = 0; j < 8; ++j) {
+            const bool want = (j < cnt) & (occ == 0u);
+            if (__ballot(want) == 0) break;
+            const float4* T = S.tris + 3 * (want ? first + j : 0);
+            float t, u, v;
+            const bool h = tri_test_nb(T[0], T[1], T[2], o, d, tnear, tfar, t, u, v);
+            occ = (want & h) ? 1u : occ;
         }
+        i = !live ? i : (occ ? 0xffffffffu : ((hit & (leaf < 0)) ? i + 1 : skip));
     }
-    return false;
+    return occ != 0u;
 }
 __device__ __forceinline__ Hit closest_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
     const uint32_t n = S.n_nodes;
-    uint32_t cur = active ? 0u : 0xffffffffu;
-    while (cur < n) {
-        const uint32_t i = cur;
-        closest_visit<false>(S, S.nodes[2 * i], S.nodes[2 * i + 1], i, o, d, inv, tnear, cur, h);
+    uint32_t i = active ? 0u : 0xffffffffu;
+    while (__ballot(i < n) != 0) {
+        const bool live = i < n;
+        const uint32_t ii = live ? i : 0u;
+        const float4 a = S.nodes[2 * ii], b = S.nodes[2 * ii + 1];
+        const uint32_t skip = (uint32_t)__float_as_int(a.w);
+        const int leaf = __float_as_int(b.w);
+        const bool hit = live & box_test(a, b, o, inv, tnear, h.t);
+        const bool in_leaf = hit & (leaf >= 0);
+        const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
+        for (int j = 0; j < 8; ++j) {
+            const bool want = j < cnt;
+            if (__ballot(want) == 0) break;
+            const float4* T = S.tris + 3 * (want ? first + j : 0);
+            const float4 T0 = T[0];
+            float t, u, v;
+            const bool hh = want & tri_test_nb(T0, T[1], T[2], o, d, tnear, h.t, t, u, v);
+            const int prim = __float_as_int(T0.w);
+            const bool better = hh & (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim));
+            h.t = better ? t : h.t; h.u = better ? u : h.u; h.v = better ? v : h.v;
+            h.prim = better ? prim : h.prim;
+        }
+        i = !live ? i : ((hit & (leaf < 0)) ? i + 1 : skip);
     }
     return h;
 }
@@ -240,7 +266,8 @@ __device__ __forceinline__ void occluded_wave_multi(const DevScene& S, const boo
     uint32_t occb = 0u;
     uint32_t m = wave_min(full, lane_min<K>(cur));
     while (m < n) {
-        const float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+        float4 a, b;
+        node_load(S.nodes, m, a, b);
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
         uint32_t hbb = 0u;
@@ -284,7 +311,8 @@ __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, ve
     uint32_t occ = 0u;                 // integer, not a bool: see occluded_wave_multi
     uint32_t m = wave_min(full, i);
     while (m < n) {
-        const float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+        float4 a, b;
+        node_load(S.nodes, m, a, b);
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
         const bool at = i == m;
@@ -317,7 +345,8 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
     uint32_t i = active ? 0u : 0xffffffffu;
     uint32_t m = wave_min(full, i);
     while (m < n) {
-        const float4 a = sload(S.nodes, 2 * m), b = sload(S.nodes, 2 * m + 1);
+        float4 a, b;
+        node_load(S.nodes, m, a, b);
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
         const bool at = i == m;
