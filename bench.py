@@ -33,7 +33,7 @@ WORKLOADS = {
     "C1": "Cornell box, 8 emissive quads, reference defaults (A=1 B=1, no reuse)",
     "C2": "Cornell box + 1024 emissive quads, A=32 B=1, spatial k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20",
     "C3": "Sponza-like ~250k tris, 4096 emissive triangles (2048 lamp quads), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
-    "C5": "C2 scene, 240-frame camera orbit (r=0.3) + moving lights (light CDF + BVH rebuilt every frame), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
+    "C5": "C2 scene, 240-frame camera orbit (r=0.3) + moving lights (light CDF recomputed + BVH refit on the GPU every frame), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
 }
 # algorithmic bytes per pixel of the dominant kernel k_gbuffer_initial: G-buffer record write
 # (5 x float4 = 80 B) + reservoir write (3 x float4 = 48 B); scene/BVH reads are cache-resident

@@ -121,10 +121,15 @@ int rs_scene_load_obj(rs_context* ctx, const char* obj_path, rs_scene** out);
 void rs_scene_destroy(rs_scene* scene);
 /* Animated geometry (C5 moving lights; the reference cannot move geometry -- the Embree analogue is
  * rtcUpdateGeometryBuffer + rtcCommitGeometry + rtcCommitScene): replaces all n_tris*9 vertex
- * positions (and, if normals != NULL, the vertex normals) in the scene's triangle order, then rebuilds
- * the emissive-triangle CDF and the BVH.  Materials and triangle count are unchanged.  Synchronises
- * the context's stream; no frame may be in flight. */
+ * positions (and, if normals != NULL, the vertex normals) in the scene's triangle order, recomputes
+ * the emissive-triangle CDF on the device and refits the BVH in place (same topology; every query
+ * answers bit-identically to a freshly built tree).  Materials and triangle count are unchanged.
+ * Asynchronous: stream-ordered after the frames already enqueued on the context's stream, no host
+ * synchronisation (the caller's arrays are copied before return); no tile frame may be open. */
 int rs_scene_update_positions(rs_scene* scene, const float* positions, const float* normals);
+/* Full rebuild of the CDF and a new PLOC tree from the scene's current positions -- restores tree
+ * quality after large motions, where a refit tree's boxes grow.  Synchronous. */
+int rs_scene_rebuild(rs_scene* scene);
 /* Scene statistics: n_tris, n_emissive, n_bvh_nodes, bvh build time (ms). */
 int rs_scene_info(const rs_scene* scene, uint32_t* n_tris, uint32_t* n_emissive, uint32_t* n_nodes,
                   float* build_ms);

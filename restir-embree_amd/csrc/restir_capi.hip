@@ -18,6 +18,10 @@
 namespace rs {
 int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes, float4** d_tris,
               std::string& err);
+int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int** d_order, int** d_lvl_off,
+                   std::vector<int>& lvl_off, std::string& err);
+int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
+              const std::vector<int>& lvl_off, hipStream_t st, std::string& err);
 int load_obj_file(const char* path, std::vector<float>& pos, std::vector<float>& nrm, std::vector<uint32_t>& tri_mat,
                   std::vector<rs_material_desc>& mats, std::string& err);
 }
@@ -34,10 +38,18 @@ struct rs_scene {
     float* d_cdf = nullptr;
     int* d_cdf_guide = nullptr;
     float build_ms = 0.0f;
-    // host copies for rs_scene_update_positions (rebuilds the geometry-dependent tables)
+    // host copies (rs_scene_rebuild re-derives the tables on the host)
     std::vector<float> h_nrm;
     std::vector<uint32_t> h_tri_mat;
     std::vector<rs_material_desc> h_mats;
+    // rs_scene_update_positions: emissive triangle ids, refit plan, pinned upload ring (2 slots)
+    int* d_emis_tri = nullptr;
+    int *d_refit_order = nullptr, *d_refit_lvl = nullptr;
+    std::vector<int> refit_lvl;
+    float* h_stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    int stage_i = 0;
+    float* d_nrm_stage = nullptr;
     // per-scene traversal choice (RS_TRAVERSAL_AUTO): frame times of each kind, tuning frames counted
     mutable int trav_choice = -1;
     mutable int trav_runs[2] = {0, 0};
@@ -381,10 +393,12 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     }
     hipStream_t st = c->stream;
     if (hipStreamSynchronize(st) != hipSuccess) { err = "stream sync failed"; return -1; }   // frames in flight
-    void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide};
+    void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide, s->d_emis_tri,
+                   s->d_refit_order, s->d_refit_lvl};
     for (void* p : old) if (p) hipFree(p);
     s->d_pos = nullptr; s->d_nodes = nullptr; s->d_tris = nullptr; s->d_emis = nullptr; s->d_cdf = nullptr;
-    s->d_cdf_guide = nullptr; s->n_nodes = 0;
+    s->d_cdf_guide = nullptr; s->d_emis_tri = nullptr; s->d_refit_order = nullptr; s->d_refit_lvl = nullptr;
+    s->n_nodes = 0; s->refit_lvl.clear();
     s->n_emis = ne;
     if (n) {
         if (hipMalloc(&s->d_pos, pos.size() * sizeof(float)) != hipSuccess) { err = "hipMalloc(pos) failed"; return -1; }
@@ -396,6 +410,10 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     hipMemcpyAsync(s->d_cdf, cdf.data(), cdf.size() * sizeof(float), hipMemcpyHostToDevice, st);
     if (hipMalloc(&s->d_cdf_guide, guide.size() * sizeof(int)) != hipSuccess) { err = "hipMalloc(guide) failed"; return -1; }
     hipMemcpyAsync(s->d_cdf_guide, guide.data(), guide.size() * sizeof(int), hipMemcpyHostToDevice, st);
+    if (ne) {
+        if (hipMalloc(&s->d_emis_tri, ne * sizeof(int)) != hipSuccess) { err = "hipMalloc(emis ids) failed"; return -1; }
+        hipMemcpyAsync(s->d_emis_tri, emis_tri.data(), ne * sizeof(int), hipMemcpyHostToDevice, st);
+    }
     if (hipStreamSynchronize(st) != hipSuccess) { err = "geometry upload failed"; return -1; }   // host vectors die
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
@@ -406,29 +424,134 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     if (rc == 0 && hipStreamSynchronize(st) == hipSuccess) hipEventElapsedTime(&s->build_ms, e0, e1);
     else { err = "BVH build failed: " + berr; rc = -1; }
     hipEventDestroy(e0); hipEventDestroy(e1);
+    if (rc == 0 && bvh_refit_plan(s->d_nodes, s->n_nodes, st, &s->d_refit_order, &s->d_refit_lvl, s->refit_lvl, berr) != 0) {
+        err = berr; rc = -1;
+    }
     return rc;
 }
 
+// TriangleCDF tables from the positions on the device (rs_scene_update_positions): the same float
+// operations in the same order as build_geometry's host loop -- sequential total and prefix sum in
+// one lane, everything else data-parallel -- so the tables are bit-identical to a fresh scene's.
+constexpr int kLightBlock = 1024;
+__global__ void __launch_bounds__(kLightBlock) k_light_table(const float* __restrict__ pos, const float4* __restrict__ tri_nrm,
+                                                             const float4* __restrict__ mats, const int* __restrict__ emis_tri,
+                                                             uint32_t ne, float4* em, float* cdf, int* guide) {
+    __shared__ float s_total;
+    for (uint32_t e = threadIdx.x; e < ne; e += kLightBlock) {
+        const int t = emis_tri[e];
+        const float* p = pos + 9 * (size_t)t;
+        const vec3 a = mk(p[0], p[1], p[2]), b = mk(p[3], p[4], p[5]), c = mk(p[6], p[7], p[8]);
+        const float area = 0.5f * length(cross(b - a, c - a));         // Triangle::area, pg/triangle.cpp:13-16
+        const float4 n0 = tri_nrm[3 * t], n1 = tri_nrm[3 * t + 1], n2 = tri_nrm[3 * t + 2];
+        const int m = __float_as_int(n0.w);
+        em[8 * e + 0] = make_float4(p[0], p[1], p[2], 0.0f);
+        em[8 * e + 1] = make_float4(p[3], p[4], p[5], 0.0f);
+        em[8 * e + 2] = make_float4(p[6], p[7], p[8], 0.0f);
+        em[8 * e + 3] = make_float4(n0.x, n0.y, n0.z, 0.0f);
+        em[8 * e + 4] = make_float4(n1.x, n1.y, n1.z, 0.0f);
+        em[8 * e + 5] = make_float4(n2.x, n2.y, n2.z, 0.0f);
+        em[8 * e + 6] = f4(xyz(mats[3 * m + 2]), 0.0f);
+        em[8 * e + 7] = make_float4(area, 0.0f, 0.0f, 0.0f);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {             // TriangleCDF ctor, pg/TriangleCDF.cpp:8-34: sequential sums
+        float total = 0.0f;
+#pragma unroll 16
+        for (uint32_t e = 0; e < ne; ++e) total += em[8 * e + 7].x;
+        float pred = 0.0f;
+#pragma unroll 16
+        for (uint32_t e = 0; e < ne; ++e) {
+            pred = pred + em[8 * e + 7].x / total;
+            cdf[e] = pred;
+        }
+        s_total = total;
+    }
+    __syncthreads();
+    const float total = s_total;
+    for (uint32_t e = threadIdx.x; e < ne; e += kLightBlock) {
+        const float area = em[8 * e + 7].x;
+        const float pick = e == 0 ? cdf[0] : cdf[e] - cdf[e - 1];
+        float pdf_brdf = area / total;
+        pdf_brdf *= 1.0f / area;
+        em[8 * e + 0].w = pick;
+        em[8 * e + 1].w = 1.0f / area;
+        em[8 * e + 2].w = pdf_brdf;
+    }
+    for (int j = threadIdx.x; j <= kCdfGuide; j += kLightBlock) {   // lower_bound(cdf, j / kCdfGuide)
+        const float key = (float)j / (float)kCdfGuide;
+        uint32_t lo = 0, hi = ne;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (cdf[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        guide[j] = (int)lo;
+    }
+}
+
+__global__ void k_set_normals(const float* __restrict__ nrm, uint32_t n, float4* tri_nrm) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const float* q = nrm + 9 * (size_t)t;
+    tri_nrm[3 * t] = make_float4(q[0], q[1], q[2], tri_nrm[3 * t].w);
+    tri_nrm[3 * t + 1] = make_float4(q[3], q[4], q[5], tri_nrm[3 * t + 1].w);
+    tri_nrm[3 * t + 2] = make_float4(q[6], q[7], q[8], 0.0f);
+}
+
+// Moving geometry (C5).  Stream-ordered and free of host synchronisation: the positions go through a
+// pinned two-slot ring (a slot is reused once its previous copy has completed), the light tables are
+// recomputed on the device and the BVH is refit in place (same topology; results bit-identical to a
+// fresh build, rs_bvh_build.hip).  Frames already enqueued see the old geometry, later ones the new.
 extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, const float* normals) {
     if (!s || !positions) return fail(s ? s->ctx : nullptr, RS_E_INVALID, "rs_scene_update_positions: null argument");
     rs_context* c = s->ctx;
     if (c->active) return fail(c, RS_E_INVALID, "rs_scene_update_positions: a frame is in flight");
     HIPCHK(c, enter(c));
-    std::vector<float> pos(positions, positions + 9 * (size_t)s->n_tris);
+    const size_t nf = 9 * (size_t)s->n_tris;
+    if (nf == 0) return RS_OK;
+    hipStream_t st = c->stream;
+    const int k = s->stage_i;
+    s->stage_i ^= 1;
+    if (!s->h_stage[k]) {
+        HIPCHK(c, hipHostMalloc(&s->h_stage[k], 2 * nf * sizeof(float), hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&s->stage_ev[k], hipEventDisableTiming));
+    } else {
+        HIPCHK(c, hipEventSynchronize(s->stage_ev[k]));
+    }
+    std::memcpy(s->h_stage[k], positions, nf * sizeof(float));
+    HIPCHK(c, hipMemcpyAsync(s->d_pos, s->h_stage[k], nf * sizeof(float), hipMemcpyHostToDevice, st));
     if (normals) {
-        s->h_nrm.assign(normals, normals + 9 * (size_t)s->n_tris);
-        std::vector<float4> tn(3 * (size_t)std::max(s->n_tris, 1u));
-        HIPCHK(c, hipMemcpy(tn.data(), s->d_tri_nrm, tn.size() * sizeof(float4), hipMemcpyDeviceToHost));
-        for (uint32_t t = 0; t < s->n_tris; ++t) {
-            const float* q = &s->h_nrm[9 * (size_t)t];
-            tn[3 * t] = make_float4(q[0], q[1], q[2], tn[3 * t].w);
-            tn[3 * t + 1] = make_float4(q[3], q[4], q[5], tn[3 * t + 1].w);
-            tn[3 * t + 2] = make_float4(q[6], q[7], q[8], 0.0f);
-        }
-        HIPCHK(c, hipMemcpy(s->d_tri_nrm, tn.data(), tn.size() * sizeof(float4), hipMemcpyHostToDevice));
+        s->h_nrm.assign(normals, normals + nf);
+        if (!s->d_nrm_stage) HIPCHK(c, hipMalloc(&s->d_nrm_stage, nf * sizeof(float)));
+        std::memcpy(s->h_stage[k] + nf, normals, nf * sizeof(float));
+        HIPCHK(c, hipMemcpyAsync(s->d_nrm_stage, s->h_stage[k] + nf, nf * sizeof(float), hipMemcpyHostToDevice, st));
+        k_set_normals<<<(s->n_tris + 255) / 256, 256, 0, st>>>(s->d_nrm_stage, s->n_tris, s->d_tri_nrm);
+    }
+    HIPCHK(c, hipEventRecord(s->stage_ev[k], st));
+    if (s->n_emis)
+        k_light_table<<<1, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, s->d_emis,
+                                                 s->d_cdf, s->d_cdf_guide);
+    HIPCHK(c, hipGetLastError());
+    std::string err;
+    if (bvh_refit(s->d_nodes, s->d_tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, s->refit_lvl, st, err) != 0)
+        return fail(c, RS_E_HIP, "rs_scene_update_positions: " + err);
+    return RS_OK;
+}
+
+// Full rebuild (light tables on the host + a new PLOC tree) from the scene's current device positions:
+// restores tree quality after large motions.  Synchronous.
+extern "C" int rs_scene_rebuild(rs_scene* s) {
+    if (!s) return fail(nullptr, RS_E_INVALID, "rs_scene_rebuild: null scene");
+    rs_context* c = s->ctx;
+    if (c->active) return fail(c, RS_E_INVALID, "rs_scene_rebuild: a frame is in flight");
+    HIPCHK(c, enter(c));
+    std::vector<float> pos(9 * (size_t)s->n_tris);
+    if (!pos.empty()) {
+        HIPCHK(c, hipMemcpyAsync(pos.data(), s->d_pos, pos.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     std::string err;
-    if (build_geometry(c, s, pos, err) != 0) return fail(c, RS_E_HIP, "rs_scene_update_positions: " + err);
+    if (build_geometry(c, s, pos, err) != 0) return fail(c, RS_E_HIP, "rs_scene_rebuild: " + err);
     return RS_OK;
 }
 
@@ -464,8 +587,14 @@ extern "C" int rs_scene_load_obj(rs_context* c, const char* path, rs_scene** out
 extern "C" void rs_scene_destroy(rs_scene* s) {
     if (!s) return;
     if (s->ctx) hipSetDevice(s->ctx->device);
-    void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide};
+    if (s->ctx && s->ctx->stream) hipStreamSynchronize(s->ctx->stream);
+    void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
+                    s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage};
     for (void* p : ptrs) if (p) hipFree(p);
+    for (int k = 0; k < 2; ++k) {
+        if (s->h_stage[k]) hipHostFree(s->h_stage[k]);
+        if (s->stage_ev[k]) hipEventDestroy(s->stage_ev[k]);
+    }
     delete s;
 }
 

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = [
     "rs_synchronize", "rs_dump_gbuffer", "rs_dump_reservoirs", "rs_tile_begin", "rs_tile_halo_ptr",
     "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_context_set_traversal",
     "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions", "rs_post_frame",
-    "rs_post_reset",
+    "rs_post_reset", "rs_scene_rebuild",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -126,6 +126,7 @@ def load_library(path: str = LIB_PATH):
     L.rs_scene_update_positions.argtypes = [vp, fp, fp]
     L.rs_post_frame.argtypes = [vp, ctypes.POINTER(PostParams), ctypes.POINTER(vp), ctypes.POINTER(PostStats)]
     L.rs_post_reset.argtypes = [vp]
+    L.rs_scene_rebuild.argtypes = [vp]
     _lib = L
     return L
 
@@ -153,7 +154,8 @@ class Scene:
 
     def update_positions(self, positions, normals=None):
         """Move the geometry (rs_scene_update_positions): (T, 9) float32 positions in the scene's triangle
-        order, optional (T, 9) normals; rebuilds the light CDF and the BVH."""
+        order, optional (T, 9) normals; light CDF recomputed and BVH refit on the device, asynchronously
+        (stream-ordered with the frames)."""
         pos = np.ascontiguousarray(positions, np.float32).reshape(-1)
         if pos.size != 9 * self.n_tris:
             raise ValueError(f"expected {self.n_tris} x 9 positions, got {pos.size}")
@@ -164,6 +166,11 @@ class Scene:
         r = self.renderer
         r._check(r.lib.rs_scene_update_positions(self.h, pos.ctypes.data_as(fp),
                                                  nrm.ctypes.data_as(fp) if nrm is not None else None))
+
+    def rebuild(self):
+        """Full light-CDF + BVH rebuild from the current positions (rs_scene_rebuild; synchronous)."""
+        r = self.renderer
+        r._check(r.lib.rs_scene_rebuild(self.h))
         n_tris, n_emis, n_nodes, ms = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_float()
         r._check(r.lib.rs_scene_info(self.h, ctypes.byref(n_tris), ctypes.byref(n_emis), ctypes.byref(n_nodes),
                                      ctypes.byref(ms)))
