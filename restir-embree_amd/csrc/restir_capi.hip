@@ -6,6 +6,7 @@
 // (pg/camera.cpp:12-84) and sequences the passes of produceRestir (pg/simpleguidx11.cpp:359-487).
 #include "rs_passes.h"
 #include "rs_post.h"
+#include "rs_refit.h"
 #include "../../include/restir_c.h"
 
 #include <cmath>
@@ -21,7 +22,7 @@ int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, 
 int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int** d_order, int** d_lvl_off,
                    std::vector<int>& lvl_off, std::string& err);
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
-              const std::vector<int>& lvl_off, hipStream_t st, std::string& err);
+              const std::vector<int>& lvl_off, hipStream_t st, int* tail, std::string& err);
 int load_obj_file(const char* path, std::vector<float>& pos, std::vector<float>& nrm, std::vector<uint32_t>& tri_mat,
                   std::vector<rs_material_desc>& mats, std::string& err);
 }
@@ -79,6 +80,7 @@ struct rs_context {
     uint2* d_part = nullptr;               // per-wave ray-count slots of this frame's launches
     size_t part_cap = 0, part_used = 0;
     Counters* d_tot = nullptr;             // running totals over frames (rs_get_timing_totals)
+    ulonglong2* d_red = nullptr;           // k_reduce_counts_part partials
     // pass timing without a per-frame host sync: every frame records into its own slot of an event
     // ring; slots are folded into the running totals lazily (when reused, or on rs_get_timing_totals)
     static constexpr int kEvRing = 64;
@@ -233,6 +235,7 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
     if (hipMalloc(&c->d_cnt, sizeof(Counters)) != hipSuccess) return bail("hipMalloc(counters) failed");
     if (hipHostMalloc(&c->h_cnt, sizeof(Counters), hipHostMallocDefault) != hipSuccess) return bail("hipHostMalloc failed");
     if (hipMalloc(&c->d_tot, sizeof(Counters)) != hipSuccess) return bail("hipMalloc(totals) failed");
+    if (hipMalloc(&c->d_red, kReduceBlocks * sizeof(ulonglong2)) != hipSuccess) return bail("hipMalloc(partials) failed");
     hipMemsetAsync(c->d_tot, 0, sizeof(Counters), c->stream);
     for (auto& slot : c->evr)
         for (auto& e : slot)
@@ -275,6 +278,7 @@ extern "C" void rs_context_destroy(rs_context* c) {
     if (c->fb) hipFree(c->fb);
     if (c->d_cnt) hipFree(c->d_cnt);
     if (c->d_tot) hipFree(c->d_tot);
+    if (c->d_red) hipFree(c->d_red);
     void* post[] = {c->acc, c->display, c->post_part, c->post_out};
     for (void* p : post) if (p) hipFree(p);
     if (c->d_part) hipFree(c->d_part);
@@ -433,11 +437,12 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
 // TriangleCDF tables from the positions on the device (rs_scene_update_positions): the same float
 // operations in the same order as build_geometry's host loop -- sequential total and prefix sum in
 // one lane, everything else data-parallel -- so the tables are bit-identical to a fresh scene's.
-constexpr int kLightBlock = 1024;
-__global__ void __launch_bounds__(kLightBlock) k_light_table(const float* __restrict__ pos, const float4* __restrict__ tri_nrm,
-                                                             const float4* __restrict__ mats, const int* __restrict__ emis_tri,
-                                                             uint32_t ne, float4* em, float* cdf, int* guide) {
+constexpr int kLightBlock = 1024, kLightChunk = 8192;
+__device__ __forceinline__ void light_table(const float* __restrict__ pos, const float4* __restrict__ tri_nrm,
+                                            const float4* __restrict__ mats, const int* __restrict__ emis_tri,
+                                            uint32_t ne, float4* em, float* cdf, int* guide) {
     __shared__ float s_total;
+    __shared__ float s_a[kLightChunk];
     for (uint32_t e = threadIdx.x; e < ne; e += kLightBlock) {
         const int t = emis_tri[e];
         const float* p = pos + 9 * (size_t)t;
@@ -455,20 +460,35 @@ __global__ void __launch_bounds__(kLightBlock) k_light_table(const float* __rest
         em[8 * e + 7] = make_float4(area, 0.0f, 0.0f, 0.0f);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {             // TriangleCDF ctor, pg/TriangleCDF.cpp:8-34: sequential sums
-        float total = 0.0f;
+    // TriangleCDF ctor, pg/TriangleCDF.cpp:8-34: the total and the prefix sum are sequential float
+    // sums (host order); one lane runs each chain out of LDS, the loads and divisions are parallel
+    float total = 0.0f;
+    for (uint32_t c0 = 0; c0 < ne; c0 += kLightChunk) {
+        const uint32_t m = min(ne - c0, (uint32_t)kLightChunk);
+        for (uint32_t j = threadIdx.x; j < m; j += kLightBlock) s_a[j] = em[8 * (c0 + j) + 7].x;
+        __syncthreads();
+        if (threadIdx.x == 0) {
 #pragma unroll 16
-        for (uint32_t e = 0; e < ne; ++e) total += em[8 * e + 7].x;
-        float pred = 0.0f;
-#pragma unroll 16
-        for (uint32_t e = 0; e < ne; ++e) {
-            pred = pred + em[8 * e + 7].x / total;
-            cdf[e] = pred;
+            for (uint32_t j = 0; j < m; ++j) total += s_a[j];
         }
-        s_total = total;
+        __syncthreads();
     }
+    if (threadIdx.x == 0) s_total = total;
     __syncthreads();
-    const float total = s_total;
+    total = s_total;
+    float pred = 0.0f;
+    for (uint32_t c0 = 0; c0 < ne; c0 += kLightChunk) {
+        const uint32_t m = min(ne - c0, (uint32_t)kLightChunk);
+        for (uint32_t j = threadIdx.x; j < m; j += kLightBlock) s_a[j] = em[8 * (c0 + j) + 7].x / total;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+#pragma unroll 16
+            for (uint32_t j = 0; j < m; ++j) { pred = pred + s_a[j]; s_a[j] = pred; }
+        }
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < m; j += kLightBlock) cdf[c0 + j] = s_a[j];
+        __syncthreads();
+    }
     for (uint32_t e = threadIdx.x; e < ne; e += kLightBlock) {
         const float area = em[8 * e + 7].x;
         const float pick = e == 0 ? cdf[0] : cdf[e] - cdf[e - 1];
@@ -486,6 +506,20 @@ __global__ void __launch_bounds__(kLightBlock) k_light_table(const float* __rest
             if (cdf[mid] < key) lo = mid + 1; else hi = mid;
         }
         guide[j] = (int)lo;
+    }
+}
+
+// one launch for the two independent single-workgroup jobs of an update: workgroup 0 the light
+// tables, workgroup 1 the last (small-level) refit batch
+struct RefitArgs { float4* nodes; float4* tris; const float* pos; const int* order; const int* lvl_off; int l0, l1; };
+__global__ void __launch_bounds__(kLightBlock) k_scene_update(const float* __restrict__ pos, const float4* __restrict__ tri_nrm,
+                                                              const float4* __restrict__ mats, const int* __restrict__ emis_tri,
+                                                              uint32_t ne, float4* em, float* cdf, int* guide, RefitArgs R) {
+    static_assert(kLightBlock == kRefitBlock, "one workgroup size for both jobs");
+    if (blockIdx.x == 0) {
+        if (ne) light_table(pos, tri_nrm, mats, emis_tri, ne, em, cdf, guide);
+    } else {
+        refit_levels(R.nodes, R.tris, R.pos, R.order, R.lvl_off, R.l0, R.l1, 0, 1);
     }
 }
 
@@ -528,13 +562,14 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
         k_set_normals<<<(s->n_tris + 255) / 256, 256, 0, st>>>(s->d_nrm_stage, s->n_tris, s->d_tri_nrm);
     }
     HIPCHK(c, hipEventRecord(s->stage_ev[k], st));
-    if (s->n_emis)
-        k_light_table<<<1, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, s->d_emis,
-                                                 s->d_cdf, s->d_cdf_guide);
-    HIPCHK(c, hipGetLastError());
     std::string err;
-    if (bvh_refit(s->d_nodes, s->d_tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, s->refit_lvl, st, err) != 0)
+    int tail[2];
+    if (bvh_refit(s->d_nodes, s->d_tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, s->refit_lvl, st, tail, err) != 0)
         return fail(c, RS_E_HIP, "rs_scene_update_positions: " + err);
+    RefitArgs R{s->d_nodes, s->d_tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, tail[0], tail[1]};
+    k_scene_update<<<2, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, s->d_emis,
+                                              s->d_cdf, s->d_cdf_guide, R);
+    HIPCHK(c, hipGetLastError());
     return RS_OK;
 }
 
@@ -834,7 +869,8 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
     }
     HIPCHK(c, hipEventRecord(c->ev[EV_SHADE], c->stream));
     c->ev_pending[c->slot] = true;
-    k_reduce_counts<<<1, 1024, 0, c->stream>>>(c->d_part, c->part_used, c->d_cnt, c->d_tot);
+    k_reduce_counts_part<<<kReduceBlocks, 1024, 0, c->stream>>>(c->d_part, c->part_used, c->d_red);
+    k_reduce_counts<<<1, kReduceBlocks, 0, c->stream>>>(c->d_red, c->d_cnt, c->d_tot);
     HIPCHK(c, hipGetLastError());
     record_traversal_time(c);
     c->r_last = c->rcur;   // reservoirsLastFrame = final buffer (pointer swap, :477)

@@ -24,6 +24,7 @@
 #include <utility>
 #include <cstring>
 #include <algorithm>
+#include "rs_refit.h"
 
 namespace rs {
 
@@ -562,63 +563,12 @@ fail: {
     return *d_nodes || n == 0 ? 0 : -1;
 }
 
-// ============================================================================================
-// In-place refit for moving geometry (rs_scene_update_positions; C5).  The topology stays; every
-// node's box is recomputed from the new vertex positions exactly as the builders compute it (per-
-// triangle min/max of the three vertices, unions by fminf/fmaxf -- order independent), and the leaf
-// triangles are rewritten from the new positions with the same operations as k_ploc_emit.  Since the
-// box test is conservative and the closest-hit tie rule does not depend on visit order, a refit tree
-// answers every query bit-identically to a freshly built one (tests/test_gpu_parity.py).
-//
-// Nodes are processed deepest level first; an interior node's children (i + 1 and the left child's
-// skip) sit exactly one level deeper.  The plan (node ids grouped by depth) is computed once per
-// topology on the host; large levels get a multi-workgroup launch each, runs of small levels share
-// one single-workgroup launch with a workgroup barrier between levels (one CU: global writes are
-// visible to the workgroup after the barrier).
-// ============================================================================================
-constexpr int kRefitBlock = 1024;
-constexpr int kRefitSmall = 4 * kRefitBlock;     // levels up to this many nodes go to the 1-block batch
-
-__device__ __forceinline__ void refit_node(float4* nodes, float4* tris, const float* __restrict__ pos, int i) {
-    const float4 a = nodes[2 * i], b = nodes[2 * i + 1];
-    const int leaf = __float_as_int(b.w);
-    float l[3], h[3];
-    if (leaf >= 0) {
-        const int first = leaf >> 3, cnt = (leaf & 7) + 1;
-        l[0] = l[1] = l[2] = INFINITY; h[0] = h[1] = h[2] = -INFINITY;
-        for (int j = 0; j < cnt; ++j) {
-            const int k = first + j;
-            const int prim = __float_as_int(tris[3 * k].w);
-            const float* p = pos + 9 * (size_t)prim;
-            for (int ax = 0; ax < 3; ++ax) {
-                l[ax] = fminf(l[ax], fminf(fminf(p[ax], p[3 + ax]), p[6 + ax]));
-                h[ax] = fmaxf(h[ax], fmaxf(fmaxf(p[ax], p[3 + ax]), p[6 + ax]));
-            }
-            const float v0x = p[0], v0y = p[1], v0z = p[2];
-            tris[3 * k] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
-            tris[3 * k + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
-            tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
-        }
-    } else {
-        const int L = i + 1, R = __float_as_int(nodes[2 * L].w);
-        const float4 al = nodes[2 * L], ah = nodes[2 * L + 1], bl = nodes[2 * R], bh = nodes[2 * R + 1];
-        l[0] = fminf(al.x, bl.x); l[1] = fminf(al.y, bl.y); l[2] = fminf(al.z, bl.z);
-        h[0] = fmaxf(ah.x, bh.x); h[1] = fmaxf(ah.y, bh.y); h[2] = fmaxf(ah.z, bh.z);
-    }
-    nodes[2 * i] = make_float4(l[0], l[1], l[2], a.w);
-    nodes[2 * i + 1] = make_float4(h[0], h[1], h[2], b.w);
-}
-
-// levels [l0, l1) of the plan; multi-block launches always get l1 == l0 + 1
+// ---------------------------------------------------------------- in-place refit (rs_refit.h)
+// multi-workgroup launches always get l1 == l0 + 1
 __global__ void __launch_bounds__(kRefitBlock) k_refit(float4* nodes, float4* tris, const float* __restrict__ pos,
                                                        const int* __restrict__ order, const int* __restrict__ lvl_off,
                                                        int l0, int l1) {
-    for (int lv = l0; lv < l1; ++lv) {
-        const int b = lvl_off[lv], e = lvl_off[lv + 1];
-        for (int q = b + blockIdx.x * kRefitBlock + threadIdx.x; q < e; q += gridDim.x * kRefitBlock)
-            refit_node(nodes, tris, pos, order[q]);
-        if (lv + 1 < l1) __syncthreads();
-    }
+    refit_levels(nodes, tris, pos, order, lvl_off, l0, l1, blockIdx.x, gridDim.x);
 }
 
 // node ids grouped by depth, deepest level first (host, once per topology)
@@ -653,23 +603,16 @@ int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int*
     return 0;
 }
 
-// stream-ordered refit; no host synchronisation
+// stream-ordered refit; no host synchronisation.  With *tail != nullptr a final single-workgroup
+// batch is not launched but returned (levels [tail[0], tail[1])) for the caller to fuse.
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
-              const std::vector<int>& lvl_off, hipStream_t st, std::string& err) {
-    const int nl = (int)lvl_off.size() - 1;
-    int l = 0;
-    while (l < nl) {
-        const int n = lvl_off[l + 1] - lvl_off[l];
-        if (n > kRefitSmall) {
-            k_refit<<<(n + kRefitBlock - 1) / kRefitBlock, kRefitBlock, 0, st>>>(d_nodes, d_tris, d_pos, d_order,
-                                                                                 d_lvl_off, l, l + 1);
-            ++l;
-        } else {
-            int e = l + 1;
-            while (e < nl && lvl_off[e + 1] - lvl_off[e] <= kRefitSmall) ++e;
-            k_refit<<<1, kRefitBlock, 0, st>>>(d_nodes, d_tris, d_pos, d_order, d_lvl_off, l, e);
-            l = e;
-        }
+              const std::vector<int>& lvl_off, hipStream_t st, int* tail, std::string& err) {
+    const std::vector<RefitBatch> bs = refit_batches(lvl_off);
+    if (tail) tail[0] = tail[1] = 0;
+    for (size_t i = 0; i < bs.size(); ++i) {
+        const RefitBatch& r = bs[i];
+        if (tail && i + 1 == bs.size() && r.blocks == 1) { tail[0] = r.l0; tail[1] = r.l1; break; }
+        k_refit<<<r.blocks, kRefitBlock, 0, st>>>(d_nodes, d_tris, d_pos, d_order, d_lvl_off, r.l0, r.l1);
     }
     if (hipGetLastError() != hipSuccess) { err = "refit launch failed"; return -1; }
     return 0;

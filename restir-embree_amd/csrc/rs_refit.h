@@ -1,0 +1,89 @@
+// rs_refit.h -- in-place BVH refit for moving geometry (device code shared by rs_bvh_build.hip and
+// the fused update launch in restir_capi.hip).
+//
+// The topology stays; every node's box is recomputed from the new vertex positions exactly as the
+// builders compute it (per-triangle min/max of the three vertices, unions by fminf/fmaxf -- order
+// independent), and the leaf triangles are rewritten from the new positions with the same operations
+// as k_ploc_emit.  Since the box test is conservative and the closest-hit tie rule does not depend on
+// visit order, a refit tree answers every query bit-identically to a freshly built one
+// (tests/test_gpu_parity.py::test_update_positions_refit_matches_fresh_scene).
+//
+// Nodes are processed deepest level first; an interior node's children (i + 1 and the left child's
+// skip) sit exactly one level deeper.  The plan (node ids grouped by depth) is computed once per
+// topology on the host (bvh_refit_plan); large levels get a multi-workgroup launch each, runs of small
+// levels share one single-workgroup launch with a workgroup barrier between levels (one CU: global
+// writes are visible to the workgroup after the barrier).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <vector>
+
+namespace rs {
+
+constexpr int kRefitBlock = 1024;
+constexpr int kRefitSmall = 4 * kRefitBlock;     // levels up to this many nodes go to the 1-block batch
+
+__device__ __forceinline__ void refit_node(float4* nodes, float4* tris, const float* __restrict__ pos, int i) {
+    const float4 a = nodes[2 * i], b = nodes[2 * i + 1];
+    const int leaf = __float_as_int(b.w);
+    float l[3], h[3];
+    if (leaf >= 0) {
+        const int first = leaf >> 3, cnt = (leaf & 7) + 1;
+        l[0] = l[1] = l[2] = INFINITY; h[0] = h[1] = h[2] = -INFINITY;
+        for (int j = 0; j < cnt; ++j) {
+            const int k = first + j;
+            const int prim = __float_as_int(tris[3 * k].w);
+            const float* p = pos + 9 * (size_t)prim;
+            for (int ax = 0; ax < 3; ++ax) {
+                l[ax] = fminf(l[ax], fminf(fminf(p[ax], p[3 + ax]), p[6 + ax]));
+                h[ax] = fmaxf(h[ax], fmaxf(fmaxf(p[ax], p[3 + ax]), p[6 + ax]));
+            }
+            const float v0x = p[0], v0y = p[1], v0z = p[2];
+            tris[3 * k] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
+            tris[3 * k + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
+            tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
+        }
+    } else {
+        const int L = i + 1, R = __float_as_int(nodes[2 * L].w);
+        const float4 al = nodes[2 * L], ah = nodes[2 * L + 1], bl = nodes[2 * R], bh = nodes[2 * R + 1];
+        l[0] = fminf(al.x, bl.x); l[1] = fminf(al.y, bl.y); l[2] = fminf(al.z, bl.z);
+        h[0] = fmaxf(ah.x, bh.x); h[1] = fmaxf(ah.y, bh.y); h[2] = fmaxf(ah.z, bh.z);
+    }
+    nodes[2 * i] = make_float4(l[0], l[1], l[2], a.w);
+    nodes[2 * i + 1] = make_float4(h[0], h[1], h[2], b.w);
+}
+
+// levels [l0, l1) of the plan (one workgroup walks them with barriers in between)
+__device__ __forceinline__ void refit_levels(float4* nodes, float4* tris, const float* __restrict__ pos,
+                                             const int* __restrict__ order, const int* __restrict__ lvl_off,
+                                             int l0, int l1, int block, int nblocks) {
+    for (int lv = l0; lv < l1; ++lv) {
+        const int b = lvl_off[lv], e = lvl_off[lv + 1];
+        for (int q = b + block * kRefitBlock + threadIdx.x; q < e; q += nblocks * kRefitBlock)
+            refit_node(nodes, tris, pos, order[q]);
+        if (lv + 1 < l1) __syncthreads();
+    }
+}
+// launch batches: a level with more than kRefitSmall nodes gets its own multi-workgroup launch, runs
+// of small levels share one single-workgroup launch
+struct RefitBatch { int l0, l1, blocks; };
+inline std::vector<RefitBatch> refit_batches(const std::vector<int>& lvl_off) {
+    std::vector<RefitBatch> out;
+    const int nl = (int)lvl_off.size() - 1;
+    int l = 0;
+    while (l < nl) {
+        const int n = lvl_off[l + 1] - lvl_off[l];
+        if (n > kRefitSmall) {
+            out.push_back({l, l + 1, (n + kRefitBlock - 1) / kRefitBlock});
+            ++l;
+        } else {
+            int e = l + 1;
+            while (e < nl && lvl_off[e + 1] - lvl_off[e] <= kRefitSmall) ++e;
+            out.push_back({l, e, 1});
+            l = e;
+        }
+    }
+    return out;
+}
+
+}  // namespace rs
