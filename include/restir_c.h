@@ -143,6 +143,18 @@ int rs_scene_info(const rs_scene* scene, uint32_t* n_tris, uint32_t* n_emissive,
 int rs_render_frame(rs_context* ctx, const rs_scene* scene, const rs_camera* camera,
                     const rs_frame_params* params, uint32_t frame_index, float* frame_rgb_host,
                     rs_pass_times* times);
+/* ---- MIS direct-light ground truth ------------------------------------------ */
+/* SimpleGuiDX11::produceStandard + NEEPathIntegrator (pg/NEEPathIntegrator.cpp:72-131) with calcDI on,
+ * calcGI off and DirectMISIntegrator (pg/DirectMISIntegrator.cpp:10-143: one BRDF sample + one light
+ * sample, power heuristic) as the direct integrator: an unbiased estimate of the direct illumination
+ * ReSTIR DI converges to.  spp samples per pixel (averaged) into the framebuffer; accumulate frames
+ * with rs_post_frame for a converged reference.  Leaves the ReSTIR history untouched.  times (optional)
+ * reports the launch in shade_ms/total_ms and the rays traced; synchronises if times or
+ * frame_rgb_host is given. */
+int rs_render_direct_mis(rs_context* ctx, const rs_scene* scene, const rs_camera* camera,
+                         const rs_frame_params* params, uint32_t frame_index, uint32_t spp,
+                         float* frame_rgb_host, rs_pass_times* times);
+
 /* Pass times and rays summed over every frame finished since context creation (or the last reset),
  * without a host sync per frame: each frame records into its own slot of an event ring and the rays
  * are summed on the device.  Synchronises the stream; sum->*_ms are totals (divide by *n_frames).

@@ -1238,6 +1238,168 @@ int or_render_frame(or_ctx* c, const or_scene* s, const float* cam7, const or_pa
     return or_tile_finish(c, out_rgb, rays_out);
 }
 
+/* ------------------------------------------------------------------ MIS direct-light ground truth
+ * SimpleGuiDX11::produceStandard (pg/simpleguidx11.cpp:336-357) with Raytracer::get_pixel
+ * (pg/raytracer.cpp:40-45) and NEEPathIntegrator::integrateImpl2 (pg/NEEPathIntegrator.cpp:72-131)
+ * at calcDI = on, calcGI = off (direct illumination only: the quantity ReSTIR DI estimates) and
+ * DirectMISIntegrator as the direct integrator (pg/DirectMISIntegrator.cpp:10-143): one BRDF sample,
+ * then one light sample, power heuristic.  The material calls are the HitInfo variants --
+ * MaterialLambert (pg/MaterialLambert.cpp:10-31) and MaterialPhong (pg/MaterialPhong.cpp:18-119), with
+ * Phong for PHONG/DIELECTRIC and Lambert for every other type (the ReSTIR path's BRDF model,
+ * pg/ReSTIRIntegrator.h:32-41, so both converge to the same image).  CenterSampler primary ray
+ * (pixel corner).  RNG: pass PASS_MIS, draws sequential per pixel over the spp samples. */
+#define PASS_MIS 64u
+typedef struct { v3 pos, n, dir, kd, ks, wr; float shin, i_m, maxD, maxS, pf; int phong; } mis_surf;
+
+static inline float mis_power(float pdf, float other) {   /* DirectMISIntegrator::powerHeuristic (:10-15) */
+    float a = pdf * pdf, b = other * other;
+    return a / (b + a);
+}
+static inline v3 dvs(v3 v, float s) { return V(v.x / s, v.y / s, v.z / s); }   /* glm vec3 / scalar */
+static inline float cos_pdf(v3 n, v3 wi) { return gmax(dot(n, wi), 0.0f) * OR_ONE_OVER_PI; }  /* pg/Distribution.h:33-35 */
+static inline float lobe_pdf(v3 wi, v3 wr, float g) {      /* CosineLobeDistribution::getPdf (pg/Distribution.h:65-67) */
+    return (g + 1.0f) * OR_ONE_OVER_2PI * powf(gmax(0.0f, dot(wi, wr)), g);
+}
+/* getPdfForSample (pg/MaterialLambert.cpp:20-23, pg/MaterialPhong.cpp:94-119) */
+static float mis_pdf_for(const mis_surf* h, v3 wi) {
+    if (!h->phong) return cos_pdf(h->n, wi);
+    float pdf = cos_pdf(h->n, wi) * h->pf;
+    pdf += lobe_pdf(wi, h->wr, h->shin) * (1.0f - h->pf);
+    return pdf;
+}
+/* evaluateBRDF (pg/MaterialLambert.cpp:25-31, pg/MaterialPhong.cpp:69-92) */
+static v3 mis_brdf(const mis_surf* h, v3 wi) {
+    v3 f = scl(h->kd, OR_ONE_OVER_PI);
+    if (!h->phong) return f;
+    return add(f, scl(scl(h->ks, h->i_m), powf(gmax(dot(wi, h->wr), 0.0f), h->shin)));
+}
+/* evaluateLightingGI (pg/MaterialLambert.cpp:10-18, pg/MaterialPhong.cpp:18-67) */
+static v3 mis_sample(const mis_surf* h, rng_t* rng, v3* f_r, float* pdf) {
+    if (!h->phong) {
+        v3 wi = cosine_sample(h->n, rng);
+        *pdf = cos_pdf(h->n, wi);
+        *f_r = dvs(h->kd, OR_PI);
+        return wi;
+    }
+    float r0 = rnd(rng, 0.0f, h->maxD + h->maxS);
+    v3 wi;
+    if (r0 < h->maxD) {
+        wi = cosine_sample(h->n, rng);
+        *f_r = scl(h->kd, OR_ONE_OVER_PI);
+    } else {
+        wi = lobe_sample(h->wr, h->shin, rng);
+        *f_r = scl(scl(h->ks, h->i_m), powf(gmax(dot(wi, h->wr), 0.0f), h->shin));
+    }
+    float pd = cos_pdf(h->n, wi) * h->pf;
+    float ps = lobe_pdf(wi, h->wr, h->shin) * (1.0f - h->pf);
+    *pdf = pd + ps;
+    if (dot(h->n, wi) < 0) *f_r = V(0, 0, 0);
+    return wi;
+}
+/* DirectMISIntegrator::evaluateBRDFSample (pg/DirectMISIntegrator.cpp:94-144) */
+static v3 mis_brdf_part(const fctx* F, const mis_surf* h, rng_t* rng, uint64_t* rays) {
+    const or_scene* s = F->s; const or_params* P = F->P;
+    v3 f_r; float pdf;
+    v3 wi = mis_sample(h, rng, &f_r, &pdf);
+    hitinfo b = intersect(F, add(h->pos, scl(h->n, P->normal_offset)), wi, FLT_MIN + P->tnear_offset, rays);
+    if (!b.hit) return V(0, 0, 0);
+    const or_mat* m = &s->mats[s->mat[b.prim]];
+    if (!(m->le.x + m->le.y + m->le.z > 0)) return V(0, 0, 0);
+    v3 ld = sub(b.point, h->pos);
+    float r2 = dot(ld, ld);
+    ld = nrmz(ld);
+    float cI = gmax(dot(ld, h->n), 0.0f);
+    float cY = gmax(dot(neg(ld), b.normal), 0.0f);
+    float amf = cY / r2;
+    int32_t e = s->emis_id[b.prim];
+    float pdf_light = s->area[e] / s->total_area;       /* TriangleCDF::getPDFForTriangle (pg/TriangleCDF.h:25-31) */
+    pdf_light *= 1.0f / s->area[e];
+    float w = mis_power(pdf * amf, pdf_light);
+    return dvs(scl(mul(scl(m->le, w), f_r), cI), pdf);
+}
+/* DirectMISIntegrator::evaluateLightSample (pg/DirectMISIntegrator.cpp:38-92) */
+static v3 mis_light_part(const fctx* F, const mis_surf* h, rng_t* rng, uint64_t* rays) {
+    const or_scene* s = F->s;
+    if (s->n_emis == 0) return V(0, 0, 0);                /* TriangleCDF::isValid */
+    float ksi = rnd(rng, 0.0f, 1.0f);                      /* TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54) */
+    uint32_t lo = 0, n = s->n_emis;
+    while (n > 0) { uint32_t k = n / 2; if (s->cdf[lo + k] < ksi) { lo = lo + k + 1; n = n - k - 1; } else n = k; }
+    uint32_t idx = lo < s->n_emis ? lo : s->n_emis - 1;
+    uint32_t t = s->emis_tri[idx];
+    float r1 = rnd(rng, 0, 1), r2 = rnd(rng, 0, 1);          /* Sampling::sampleTriangle (pg/Sampling.cpp:63-76) */
+    float x = 1.0f - sqrtf(r1), y = sqrtf(r1) * (1.0f - r2), z = sqrtf(r1) * r2;
+    v3 pt = add(add(scl(s->p0[t], x), scl(s->p1[t], y)), scl(s->p2[t], z));
+    v3 nn = nrmz(add(add(scl(s->n0[t], x), scl(s->n1[t], y)), scl(s->n2[t], z)));
+    float light_pdf = s->pick_pdf[idx] * (1.0f / s->area[idx]);
+    if (light_pdf == 0) return V(0, 0, 0);
+    v3 ld = sub(pt, h->pos);
+    float r_sqr = dot(ld, ld);
+    ld = nrmz(ld);
+    if (r_sqr == 0) return V(0, 0, 0);
+    float cI = gmax(dot(ld, h->n), 0.0f);
+    float cY = gmax(dot(neg(ld), nn), 0.0f);
+    float amf = cY / r_sqr;
+    if (!(cI > 0 && cY > 0) || occluded(F, h->pos, pt, rays)) return V(0, 0, 0);
+    float pba = mis_pdf_for(h, ld) * amf;
+    v3 le = s->mats[s->mat[t]].le;
+    float w = mis_power(light_pdf, pba);
+    if (!(w > 0.0f)) return V(0, 0, 0);
+    float G = cI * cY / r_sqr;
+    return dvs(scl(mul(scl(le, w), mis_brdf(h, ld)), G), light_pdf);
+}
+
+/* out_rgb: W*H*3 floats; spp samples per pixel averaged (sum / spp) -- frame-to-frame accumulation
+ * is or_post_apply's running mean, as the reference's accumulator */
+int or_render_direct_mis(or_ctx* c, const or_scene* s, const float* cam7, const or_params* P, uint32_t frame_index,
+                         int spp, float* out_rgb, uint64_t* rays_out) {
+    if (P->use_skybox) return -2;
+    if (spp < 1) return -1;
+    int W = c->W, H = c->H;
+    or_cam cam = make_cam(cam7, W, H);
+    fctx F; memset(&F, 0, sizeof F);
+    F.s = s; F.c = c; F.P = P; F.frame = frame_index;
+    uint64_t rc = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+:rc)
+    for (int y = 0; y < H; ++y) {
+        for (int x = 0; x < W; ++x) {
+            size_t p = (size_t)y * W + x;
+            v3 d = primary_dir(&cam, x, y, W, H);
+            hitinfo hi = intersect(&F, cam.eye, d, FLT_MIN + 0.01f, &rc);
+            v3 px;
+            if (!hi.hit) {
+                px = V(P->bg_color[0], P->bg_color[1], P->bg_color[2]);
+            } else {
+                const or_mat* m = &s->mats[s->mat[hi.prim]];
+                if (nonzero_pos(m->le)) {                  /* Material::isEmitter, camera vertex */
+                    px = m->le;
+                } else {
+                    mis_surf h;
+                    h.pos = hi.point; h.n = hi.normal; h.dir = d;
+                    h.kd = m->kd; h.ks = m->ks; h.shin = m->shin;
+                    h.phong = m->type == MT_PHONG || m->type == MT_DIELECTRIC;
+                    h.maxD = maxc(h.kd); h.maxS = maxc(h.ks);
+                    h.pf = h.maxD / (h.maxD + h.maxS);
+                    h.wr = nrmz(reflect(d, h.n));
+                    h.i_m = h.phong ? 1.0f / or_calc_I_M(dot(neg(d), h.n), h.shin) : 0.0f;
+                    rng_t rng = rng_init(P->seed, frame_index, PASS_MIS, (uint32_t)p);
+                    v3 acc = V(0, 0, 0);
+                    for (int k = 0; k < spp; ++k) {
+                        v3 L = add(V(0, 0, 0), mis_brdf_part(&F, &h, &rng, &rc));
+                        L = add(L, mis_light_part(&F, &h, &rng, &rc));
+                        L = sanitize(L);
+                        acc = add(acc, add(V(0, 0, 0), L));    /* L_i_indirect (0) + L_i_direct */
+                    }
+                    px = dvs(acc, (float)spp);
+                }
+            }
+            px = sanitize(px);
+            out_rgb[3 * p] = px.x; out_rgb[3 * p + 1] = px.y; out_rgb[3 * p + 2] = px.z;
+        }
+    }
+    if (rays_out) *rays_out = rc;
+    return 0;
+}
+
 /* ------------------------------------------------------------------ dumps / KAT hooks */
 /* G-buffer dump: 19 floats per pixel: pos3 nrm3 kd3 ks3 le3 shin depth type inv_IM */
 int or_get_gbuffer(const or_ctx* c, int prev, float* out) {

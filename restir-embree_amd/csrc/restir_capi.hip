@@ -5,6 +5,7 @@
 // (pg/Scene.cpp:8-16, pg/ModelLoader.cpp:218-321, pg/TriangleCDF.cpp:8-34), computes the camera
 // (pg/camera.cpp:12-84) and sequences the passes of produceRestir (pg/simpleguidx11.cpp:359-487).
 #include "rs_passes.h"
+#include "rs_mis.h"
 #include "rs_post.h"
 #include "rs_refit.h"
 #include "../../include/restir_c.h"
@@ -91,6 +92,7 @@ struct rs_context {
     double tot_ms[6] = {};                 // gbuffer_initial, visibility, temporal, spatial, shade, total
     uint64_t tot_frames = 0;
     hipEvent_t ev[EV_COUNT] = {};          // the frame in flight's slot
+    hipEvent_t ev_gt[2] = {};              // rs_render_direct_mis launch
     uint64_t frames = 0;
     std::string err;
     // frame / tile in flight
@@ -240,6 +242,8 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
     for (auto& slot : c->evr)
         for (auto& e : slot)
             if (hipEventCreate(&e) != hipSuccess) return bail("hipEventCreate failed");
+    for (auto& e : c->ev_gt)
+        if (hipEventCreate(&e) != hipSuccess) return bail("hipEventCreate failed");
     for (int i = 0; i < EV_COUNT; ++i) c->ev[i] = c->evr[0][i];
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail("context init failed");
     if (const char* t = std::getenv("RESTIR_TRAVERSAL")) {     // auto (default) | lockstep | lane
@@ -285,6 +289,7 @@ extern "C" void rs_context_destroy(rs_context* c) {
     if (c->h_cnt) hipHostFree(c->h_cnt);
     for (auto& slot : c->evr)
         for (auto& e : slot) if (e) hipEventDestroy(e);
+    for (auto& e : c->ev_gt) if (e) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -930,6 +935,61 @@ extern "C" int rs_render_frame(rs_context* c, const rs_scene* s, const rs_camera
         HIPCHK(c, hipMemcpyAsync(frame_rgb_host, c->fb, (size_t)c->W * c->H * 3 * sizeof(float), hipMemcpyDeviceToHost,
                                  c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return RS_OK;
+}
+
+// MIS direct-light ground truth (rs_mis.h) into the framebuffer: one launch, spp
+// samples per pixel.  Does not touch the ReSTIR history (G-buffers, reservoirs, frame counter).
+extern "C" int rs_render_direct_mis(rs_context* c, const rs_scene* s, const rs_camera* cam, const rs_frame_params* P,
+                                    uint32_t frame_index, uint32_t spp, float* frame_rgb_host, rs_pass_times* t) {
+    if (!c || !s || !cam || !P) return fail(c, RS_E_INVALID, "rs_render_direct_mis: null argument");
+    if (s->ctx != c) return fail(c, RS_E_INVALID, "rs_render_direct_mis: scene belongs to another context");
+    if (c->active) return fail(c, RS_E_INVALID, "rs_render_direct_mis: a tile frame is in flight");
+    if (P->use_skybox) return fail(c, RS_E_UNSUPPORTED, "useSkybox: the reference's sky HDR (data/env/forest.hdr) is a missing blob");
+    if (spp < 1 || spp > 65536) return fail(c, RS_E_INVALID, "rs_render_direct_mis: spp must be in [1, 65536]");
+    HIPCHK(c, enter(c));
+    FrameConst F = {};
+    F.bg = vec3{P->bg_color[0], P->bg_color[1], P->bg_color[2]};
+    F.tnear_off = P->tnear_offset; F.tfar_off = P->tfar_offset; F.normal_off = P->normal_offset;
+    F.seed = P->seed; F.frame = frame_index;
+    F.W = c->W; F.H = c->H; F.y0 = 0; F.y1 = c->H; F.gy0 = 0; F.gy1 = c->H;
+    GCam gc;
+    make_camera(cam, c->H, gc, F.inv_view);
+    F.cam = gc; F.camp = gc;
+    const DevScene S = s->dev();
+    const dim3 g = grid_rows(c->W, 0, c->H);
+    c->part_used = 0;
+    if (c->part_cap < grid_waves(g)) {
+        if (c->d_part) HIPCHK(c, hipFree(c->d_part));
+        c->d_part = nullptr; c->part_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_part, grid_waves(g) * sizeof(uint2)));
+        c->part_cap = grid_waves(g);
+    }
+    HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->stream));
+    hipEvent_t e0 = c->ev_gt[0], e1 = c->ev_gt[1];
+    HIPCHK(c, hipEventRecord(e0, c->stream));
+    pick_traversal(c, s);
+    c->tuning = false;               // the ReSTIR frames own the per-scene traversal tuning
+    LAUNCH_TRAV(c, k_direct_mis, g, S, F, (int)spp, c->fb, count_slot(c, g));
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(e1, c->stream));
+    k_reduce_counts_part<<<kReduceBlocks, 1024, 0, c->stream>>>(c->d_part, c->part_used, c->d_red);
+    k_reduce_counts<<<1, kReduceBlocks, 0, c->stream>>>(c->d_red, c->d_cnt, c->d_tot);
+    HIPCHK(c, hipGetLastError());
+    if (t || frame_rgb_host) {
+        if (frame_rgb_host)
+            HIPCHK(c, hipMemcpyAsync(frame_rgb_host, c->fb, (size_t)c->W * c->H * 3 * sizeof(float), hipMemcpyDeviceToHost,
+                                     c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->d_cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (t) {
+            float ms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            *t = rs_pass_times{};
+            t->shade_ms = ms; t->total_ms = ms;
+            t->rays = c->h_cnt->rays; t->primary_rays = c->h_cnt->primary;
+        }
     }
     return RS_OK;
 }

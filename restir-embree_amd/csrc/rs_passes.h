@@ -215,13 +215,10 @@ __device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameCons
     return g;
 }
 
-// areaSampleLight (pg/ReSTIRIntegrator.cpp:89-124), TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54),
-// Sampling::sampleTriangle (pg/Sampling.cpp:63-76)
-__device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
-                                              Rng& rng, float& W_out, float& mis_out) {
-    float ksi = rng.range(0.0f, 1.0f);
-    // std::lower_bound(cdf2, ksi), narrowed by the guide table: ksi*kCdfGuide is exact (ksi = k*2^-24),
-    // and lower_bound(j/G) <= lower_bound(ksi) <= lower_bound((j+1)/G) for j = floor(ksi*G)
+// TriangleCDF::getTriangle's index (pg/TriangleCDF.cpp:36-54): std::lower_bound(cdf2, ksi), narrowed
+// by the guide table: ksi*kCdfGuide is exact (ksi = k*2^-24), and lower_bound(j/G) <= lower_bound(ksi)
+// <= lower_bound((j+1)/G) for j = floor(ksi*G)
+__device__ __forceinline__ uint32_t light_index(const DevScene& S, float ksi) {
     uint32_t j = (uint32_t)(ksi * (float)kCdfGuide);
     uint32_t lo = (uint32_t)S.cdf_guide[j], n = (uint32_t)S.cdf_guide[j + 1] + 1u - lo;
     if (lo + n > S.n_emis) n = S.n_emis - lo;
@@ -229,7 +226,15 @@ __device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameCons
         uint32_t h = n >> 1;
         if (S.cdf[lo + h] < ksi) { lo = lo + h + 1; n = n - h - 1; } else n = h;
     }
-    uint32_t idx = lo < S.n_emis ? lo : S.n_emis - 1;
+    return lo < S.n_emis ? lo : S.n_emis - 1;
+}
+
+// areaSampleLight (pg/ReSTIRIntegrator.cpp:89-124), TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54),
+// Sampling::sampleTriangle (pg/Sampling.cpp:63-76)
+__device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
+                                              Rng& rng, float& W_out, float& mis_out) {
+    float ksi = rng.range(0.0f, 1.0f);
+    const uint32_t idx = light_index(S, ksi);
     const float4* E = S.emis + 8 * idx;
     float4 P0 = E[0], P1 = E[1], P2 = E[2];
     float r1 = rng.range(0, 1), r2 = rng.range(0, 1);

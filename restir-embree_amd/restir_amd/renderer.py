@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = [
     "rs_synchronize", "rs_dump_gbuffer", "rs_dump_reservoirs", "rs_tile_begin", "rs_tile_halo_ptr",
     "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_context_set_traversal",
     "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions", "rs_post_frame",
-    "rs_post_reset", "rs_scene_rebuild",
+    "rs_post_reset", "rs_scene_rebuild", "rs_render_direct_mis",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -127,6 +127,8 @@ def load_library(path: str = LIB_PATH):
     L.rs_post_frame.argtypes = [vp, ctypes.POINTER(PostParams), ctypes.POINTER(vp), ctypes.POINTER(PostStats)]
     L.rs_post_reset.argtypes = [vp]
     L.rs_scene_rebuild.argtypes = [vp]
+    L.rs_render_direct_mis.argtypes = [vp, vp, ctypes.POINTER(CameraDesc), ctypes.POINTER(FrameParams), u32, u32, fp,
+                                       ctypes.POINTER(PassTimes)]
     _lib = L
     return L
 
@@ -335,6 +337,18 @@ class Renderer:
         out = np.zeros((self.H, self.W, 12), np.float32)
         self._check(self.lib.rs_dump_reservoirs(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
         return out
+
+    def render_direct_mis(self, scene: Scene, camera, params: FrameParams, frame_index: int = 0, spp: int = 1,
+                          copy_out: bool = True, timed: bool = False) -> np.ndarray | None:
+        """MIS direct-light ground truth (rs_render_direct_mis; DirectMISIntegrator, calcGI off): spp
+        samples per pixel into the framebuffer.  Accumulate frames with post_frame(accumulate=True) for a
+        converged reference.  timed=True fills last_times (shade_ms = the launch, rays)."""
+        cam = camera_desc(camera)
+        out = self.frame_data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) if copy_out else None
+        self._check(self.lib.rs_render_direct_mis(self.h, scene.h, ctypes.byref(cam), ctypes.byref(params),
+                                                  int(frame_index), int(spp), out,
+                                                  ctypes.byref(self.last_times) if timed else None))
+        return self.frame_data if copy_out else None
 
     def debug_trace(self, scene: Scene, o, d, tnear, tfar, any_hit: bool, lockstep: bool = True,
                     stats: bool = False):

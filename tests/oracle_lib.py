@@ -53,6 +53,9 @@ def lib():
         L.or_render_frame.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _f32p, ctypes.POINTER(FrameParams),
                                       ctypes.c_uint32, _f32p, ctypes.POINTER(ctypes.c_uint64)]
         L.or_get_gbuffer.argtypes = [ctypes.c_void_p, ctypes.c_int, _f32p]
+        L.or_render_direct_mis.restype = ctypes.c_int
+        L.or_render_direct_mis.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _f32p, ctypes.POINTER(FrameParams),
+                                           ctypes.c_uint32, ctypes.c_int, _f32p, ctypes.POINTER(ctypes.c_uint64)]
         L.or_get_reservoirs.argtypes = [ctypes.c_void_p, _f32p]
         L.or_calc_I_M.restype = ctypes.c_float
         L.or_calc_I_M.argtypes = [ctypes.c_float, ctypes.c_float]
@@ -178,6 +181,18 @@ class OracleRenderer:
                                    ctypes.byref(rays))
         if rc != 0:
             raise RuntimeError(f"or_render_frame failed: {rc}")
+        self.rays = int(rays.value)
+        return out
+
+    def render_direct_mis(self, oscene, camera, params, frame_index=0, spp=1):
+        """MIS direct-light ground truth (or_render_direct_mis): one frame of spp samples per pixel."""
+        cam = camera.as_array() if hasattr(camera, "as_array") else np.asarray(camera, np.float32)
+        out = np.zeros((self.H, self.W, 3), np.float32)
+        rays = ctypes.c_uint64()
+        rc = lib().or_render_direct_mis(self.h, oscene.h, _ptr(cam), ctypes.byref(params), frame_index, spp,
+                                        _ptr(out), ctypes.byref(rays))
+        if rc != 0:
+            raise RuntimeError(f"or_render_direct_mis failed: {rc}")
         self.rays = int(rays.value)
         return out
 

@@ -251,6 +251,60 @@ def test_update_positions_refit_matches_fresh_scene(which):
         fresh.close()
 
 
+@pytest.mark.parametrize("which", ["c1", "phong"])
+def test_direct_mis_matches_oracle(which):
+    """§8f-3 MIS direct-light ground truth (rs_render_direct_mis) against or_render_direct_mis on the
+    same seeds (frame tolerance: 1/I_M and powf are ocml vs glibc); the two traversal kinds give
+    bit-identical frames."""
+    if which == "c1":
+        sc, prm, W, H, spp = scenes.cornell_box(8), P.default_params(), 64, 48, 4
+    else:
+        sc, prm, W, H, spp = scenes.sponza_like(target_tris=30_000, n_lamps=128), P.c3_params(), 64, 36, 2
+    o, os_ = O.OracleRenderer(W, H), O.OracleScene(sc)
+    out = {}
+    for mode in ("lockstep", "lane"):
+        g = Renderer(W, H)
+        g.set_traversal(mode)
+        gs = g.load_scene(sc)
+        out[mode] = [g.render_direct_mis(gs, sc.camera, prm, f, spp, timed=True).copy() for f in range(2)]
+        assert g.last_times.rays >= W * H
+    for f in range(2):
+        assert np.array_equal(out["lockstep"][f], out["lane"][f])
+        _assert_close(out["lane"][f], o.render_direct_mis(os_, sc.camera, prm, f, spp), f"MIS {which} frame {f}")
+
+
+def test_direct_mis_leaves_restir_history_and_converges():
+    """A ground-truth launch between two ReSTIR frames does not change the second (temporal) frame;
+    ReSTIR's RIS (initial pass, unbiased) accumulated with rs_post_frame converges to the MIS image on
+    the C2 scene (surfaces facing the emitters' back faces excluded, see tests/test_oracle.py)."""
+    sc = scenes.cornell_many_lights(1024)
+    W, H = 96, 54
+    prm_t = P.c3_params(m_area=8)
+    ref, g = Renderer(W, H), Renderer(W, H)
+    rs, gs = ref.load_scene(sc), g.load_scene(sc)
+    a0 = ref.produce_restir(rs, sc.camera, prm_t, 0).copy()
+    a1 = ref.produce_restir(rs, sc.camera, prm_t, 1).copy()
+    b0 = g.produce_restir(gs, sc.camera, prm_t, 0).copy()
+    g.render_direct_mis(gs, sc.camera, prm_t, 7, 3)
+    b1 = g.produce_restir(gs, sc.camera, prm_t, 1).copy()
+    assert np.array_equal(a0, b0) and np.array_equal(a1, b1)
+
+    prm = P.metric_params(do_spatial=0)
+    gt = g.render_direct_mis(gs, sc.camera, prm, 0, 512).astype(np.float64)
+    g.post_reset()
+    n = 64
+    for f in range(n):
+        g.produce_restir(gs, sc.camera, prm, f, copy_out=False)
+        _, st = g.post_frame(accumulate=True, tonemap=False, gamma_correct=False, stats=(f == n - 1))
+    assert st.acc_frames_used == n - 1           # accFrameCtr the last frame was blended with
+    acc = g.display_rgba()[..., :3].astype(np.float64)          # display = accumulator (no tonemap/gamma)
+    gb = g.gbuffer()
+    mask = (gb[..., 12:15].sum(-1) == 0) & (gb[..., 5] > -0.5) & (gt.sum(-1) > 0)
+    assert mask.sum() > 0.4 * W * H
+    ratio = acc.sum(-1)[mask].sum() / gt.sum(-1)[mask].sum()
+    assert abs(ratio - 1.0) <= 0.02, ratio
+
+
 def test_post_frame_matches_oracle():
     """rs_post_frame (accumulate + ACES + sRGB + mean/variance) against the oracle's post restatement
     applied to the GPU's own frames: accumulator bit-exact, display within powf ulps, stats 1e-9."""
