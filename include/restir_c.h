@@ -30,7 +30,7 @@ extern "C" {
 #define RS_OK 0
 #define RS_E_INVALID (-1)     /* bad argument / shape */
 #define RS_E_HIP (-2)         /* HIP runtime error */
-#define RS_E_UNSUPPORTED (-3) /* feature the reference has but this build does not (e.g. sky map) */
+#define RS_E_UNSUPPORTED (-3) /* feature the reference has but this build does not (e.g. JPEG textures) */
 #define RS_E_IO (-4)          /* file not found / parse error (scene loader) */
 
 typedef struct rs_context rs_context;
@@ -43,7 +43,23 @@ typedef struct {
     const float* positions;   /* n_tris * 9 floats: v0.xyz v1.xyz v2.xyz */
     const float* normals;     /* n_tris * 9 floats: n0.xyz n1.xyz n2.xyz */
     uint32_t material;        /* index into the material array (Surface::get_material, :213,243) */
+    const float* texcoords;   /* n_tris * 6 floats (uv per vertex; attribute slot 1, :284-285) or NULL = 0 */
+    const float* tangents;    /* n_tris * 9 floats (attribute slot 3, :287-289) or NULL = 0; normal maps only */
 } rs_mesh_desc;
+
+/* Decoded texture (Texture, pg/Texture.cpp:9-57): top row first, rows tightly packed, channels in
+ * R,G,B(,A) order.  Lookups are bilinear (Texture::getTexelBilinear, :170-194): REPEAT for material
+ * maps (ModelLoader::TextureProxy, pg/ModelLoader.cpp:28), CLAMP_TO_EDGE for the sky (Texture.h:27). */
+#define RS_TEX_U8 0           /* 8-bit LDR (PNG/JPG...): texel = byte / 255 */
+#define RS_TEX_F32 1          /* float HDR (.hdr/.exr/.pfm): texel = value; 3 or 4 channels */
+typedef struct {
+    uint32_t width, height;
+    uint32_t channels;        /* 1, 3 or 4 (1-channel 8-bit maps keep the reference's 3-byte read quirk) */
+    int32_t format;           /* RS_TEX_U8 or RS_TEX_F32 */
+    const void* data;         /* width * height * channels elements */
+    int32_t srgb_expand;      /* Texture::expand at load (8-bit; pg/Texture.cpp:141-160): ModelLoader sets it
+                                 for map_Kd / map_Ks when Raytracer::gammaCorrect (pg/ModelLoader.cpp:127,135) */
+} rs_texture_desc;
 
 /* Material record as the ReSTIR statics read it (pg/material.cpp:105-134, pg/material.h:105-115).
  * Colours are linear (the loader's sRGB expansion, pg/ModelLoader.cpp:80-97, already applied). */
@@ -53,6 +69,9 @@ typedef struct {
     float emission[3];        /* Ke -- emissive iff Ke.x+Ke.y+Ke.z > 0 (pg/material.h:135-137) */
     float shininess;          /* Ns */
     int32_t type;             /* MaterialType (pg/enums.h:3-11): 1 LAMBERT, 2 PHONG, 4 DIELECTRIC, ... */
+    /* texture slots (Material::kDiffuseMapSlot..., pg/material.cpp:105-134; Intersection.h:26-39):
+       1-based index into the textures passed to rs_scene_create_textured, 0 = none */
+    int32_t diffuse_map, specular_map, shininess_map, normal_map;
 } rs_material_desc;
 
 /* Camera(width, height, fov_y, view_from, view_at), Z-up (pg/camera.cpp:12-18, pg/camera.h:68). */
@@ -79,7 +98,7 @@ typedef struct {
     int32_t reject_dissimilar;
     int32_t spatial_mis;           /* SpatialWeightCalculation: 0 CONSTANT, 1 DEBIAS_CONTRIB,
                                       2 DEBIAS_Z_TERM, 3 BALANCE_HEURISTIC, 4 PAIRWISE_MIS */
-    int32_t use_skybox;            /* must be 0: the reference's sky HDR is a missing blob */
+    int32_t use_skybox;            /* primary misses read the scene's sky (rs_scene_set_sky); else bg_color */
     float bg_color[3];
     float tnear_offset;
     float tfar_offset;
@@ -115,9 +134,29 @@ const char* rs_last_error(const rs_context* ctx);   /* ctx may be NULL: last glo
  * Replaces rtcNewScene/rtcCommitScene (pg/Scene.cpp:10,15). */
 int rs_scene_create(rs_context* ctx, const rs_mesh_desc* meshes, uint32_t n_meshes,
                     const rs_material_desc* materials, uint32_t n_materials, rs_scene** out);
-/* OBJ/MTL loader honouring Pc (material class), Kd/Ks (sRGB-expanded), Ke, Ns
- * (pg/ModelLoader.cpp:41-153 conventions), then rs_scene_create.  Textures are not supported. */
+/* OBJ/MTL loader honouring Pc (material class), Kd/Ks (sRGB-expanded), Ke, Ns, vt texture
+ * coordinates and map_Kd / map_Ks / map_Ns / norm textures (PNG, .hdr, .pfm, .ppm; pg/ModelLoader.cpp:
+ * 41-153 conventions; tangents per triangle from the uv derivatives), then rs_scene_create_textured. */
 int rs_scene_load_obj(rs_context* ctx, const char* obj_path, rs_scene** out);
+/* rs_scene_create with material textures: diffuse / specular maps replace Kd / Ks, a shininess map gives
+ * Ns = 2 / r^2 - 2 (Material::getShininess, pg/material.cpp:123-134), a normal map replaces the
+ * (ray-facing) shading normal by TBN * (2 t - 1), unnormalised (pg/Intersection.h:26-39).  Textures are
+ * copied to the device; the descriptors may be freed after the call. */
+int rs_scene_create_textured(rs_context* ctx, const rs_mesh_desc* meshes, uint32_t n_meshes,
+                             const rs_material_desc* materials, uint32_t n_materials,
+                             const rs_texture_desc* textures, uint32_t n_textures, rs_scene** out);
+/* Equirectangular sky for rs_frame_params.use_skybox (Scene::loadSkybox + SphericalMap,
+ * pg/Scene.cpp:46-50, pg/SphericalMap.cpp:10-14): primary-ray misses read it (G-buffer emission,
+ * pg/ReSTIRIntegrator.cpp:231; NEE miss, pg/NEEPathIntegrator.cpp:131).  NULL removes it. */
+int rs_scene_set_sky(rs_scene* scene, const rs_texture_desc* equirect);
+/* Loads the sky from a file (Raytracer::LoadScene's forest.hdr, pg/raytracer.cpp:34-38): Radiance
+ * .hdr, .pfm, binary .ppm or PNG (8-bit gray/RGB/RGBA). */
+int rs_scene_load_sky(rs_scene* scene, const char* path);
+/* The scene loader's image decoder on its own (no device; tests and tools): with out == NULL only
+ * width/height/channels/format are returned; else out receives width*height*channels bytes (RS_TEX_U8)
+ * or floats (RS_TEX_F32), top row first -- RS_E_INVALID if out_bytes is too small. */
+int rs_image_decode(const char* path, uint32_t* width, uint32_t* height, uint32_t* channels, int32_t* format,
+                    void* out, size_t out_bytes);
 void rs_scene_destroy(rs_scene* scene);
 /* Animated geometry (C5 moving lights; the reference cannot move geometry -- the Embree analogue is
  * rtcUpdateGeometryBuffer + rtcCommitGeometry + rtcCommitScene): replaces all n_tris*9 vertex

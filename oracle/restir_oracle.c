@@ -254,7 +254,16 @@ typedef struct {
     float total_area;
     /* BVH */
     or_node* nodes; int n_nodes; uint32_t* tri_index;
+    /* textures: per-material map slots (0-based, -1 none: diffuse, specular,
+       shininess, normal), per-triangle uv (6) / tangents (9), textures in FreeImage layout, sky */
+    int32_t* maps; float* uv; float* tan;
+    struct or_tex* tex; int n_tex; int sky;
 } or_scene;
+
+/* Texture after FreeImage_ConvertToRawBits (pg/Texture.cpp:46-50): rows top first, pitch padded to
+   4 bytes, 8-bit texels B,G,R(,A), float texels R,G,B(,A); `bytes` has 16 zero guard bytes at the end */
+typedef struct or_tex { int w, h, pitch, px; uint8_t* bytes; } or_tex;
+typedef struct { uint32_t width, height, channels; int32_t format; const void* data; int32_t srgb_expand; } or_texdesc;
 
 /* Triangle::Triangle area = 0.5 * |cross(v1-v0, v2-v0)|  (pg/triangle.cpp:13-16) */
 static float tri_area(v3 a, v3 b, v3 c) { return 0.5f * len(cross(sub(b, a), sub(c, a))); }
@@ -341,7 +350,7 @@ void or_scene_destroy(or_scene* s);
 or_scene* or_scene_create(uint32_t n_tris, const float* pos, const float* nrm, const uint32_t* tri_mat,
                           uint32_t n_mat, const float* mat_f, const int32_t* mat_type) {
     or_scene* s = (or_scene*)calloc(1, sizeof(or_scene));
-    s->n_tris = n_tris; s->n_mat = n_mat;
+    s->n_tris = n_tris; s->n_mat = n_mat; s->sky = -1;
     s->p0 = malloc(n_tris * sizeof(v3)); s->p1 = malloc(n_tris * sizeof(v3)); s->p2 = malloc(n_tris * sizeof(v3));
     s->n0 = malloc(n_tris * sizeof(v3)); s->n1 = malloc(n_tris * sizeof(v3)); s->n2 = malloc(n_tris * sizeof(v3));
     s->mat = malloc(n_tris * sizeof(uint32_t)); s->emis_id = malloc(n_tris * sizeof(int32_t));
@@ -405,7 +414,136 @@ void or_scene_destroy(or_scene* s) {
     if (!s) return;
     free(s->p0); free(s->p1); free(s->p2); free(s->n0); free(s->n1); free(s->n2);
     free(s->mat); free(s->emis_id); free(s->mats); free(s->emis_tri); free(s->cdf);
-    free(s->pick_pdf); free(s->area); free(s->nodes); free(s->tri_index); free(s);
+    free(s->pick_pdf); free(s->area); free(s->nodes); free(s->tri_index);
+    for (int i = 0; i < s->n_tex; ++i) free(s->tex[i].bytes);
+    free(s->tex); free(s->maps); free(s->uv); free(s->tan); free(s);
+}
+
+/* ------------------------------------------------------------------ textures */
+/* Utils::expand (pg/utils.cpp:209-218) */
+static float srgb_expand1(float u) {
+    if (u <= 0.0f) return 0.0f;
+    if (u >= 1.0f) return 1.0f;
+    if (u <= 0.04045f) return u / 12.92f;
+    return powf((u + 0.055f) / 1.055f, 2.4f);
+}
+/* Texture ctor (pg/Texture.cpp:9-57) + Texture::expand applied n_expand times (:141-160) */
+static int tex_load(or_tex* t, const or_texdesc* d, int n_expand) {
+    if (!d->data || d->width < 1 || d->height < 1) return -1;
+    if (d->format == 0) { if (d->channels != 1 && d->channels != 3 && d->channels != 4) return -1; t->px = (int)d->channels; }
+    else if (d->format == 1) { if (d->channels != 3 && d->channels != 4) return -1; t->px = 4 * (int)d->channels; }
+    else return -1;
+    t->w = (int)d->width; t->h = (int)d->height;
+    t->pitch = (t->w * t->px + 3) & ~3;
+    t->bytes = calloc((size_t)t->pitch * t->h + 16, 1);
+    size_t rowlen = (size_t)t->w * d->channels;
+    for (int y = 0; y < t->h; ++y) {
+        uint8_t* dst = t->bytes + (size_t)y * t->pitch;
+        if (d->format == 1) { memcpy(dst, (const float*)d->data + (size_t)y * rowlen, rowlen * sizeof(float)); continue; }
+        const uint8_t* src = (const uint8_t*)d->data + (size_t)y * rowlen;
+        for (int x = 0; x < t->w; ++x) {
+            const uint8_t* q = src + (size_t)x * d->channels;
+            uint8_t* o = dst + (size_t)x * t->px;
+            if (d->channels == 1) { o[0] = q[0]; continue; }
+            o[0] = q[2]; o[1] = q[1]; o[2] = q[0];
+            if (d->channels == 4) o[3] = q[3];
+        }
+        for (int k = 0; k < n_expand; ++k)
+            for (int x = 0; x < t->w * t->px; ++x) {
+                float f = (float)dst[x] / 255.0f;
+                f = srgb_expand1(f);
+                dst[x] = (uint8_t)(f * 255.0f);
+            }
+    }
+    return 0;
+}
+/* mat_maps: n_mat x 4 one-based texture indices (0 none); uv: T x 6 or NULL; tan: T x 9 or NULL.
+   A colour texture is expanded once per diffuse/specular slot referencing it (ModelLoader expands the
+   TextureProxy-shared texture for every such slot, pg/ModelLoader.cpp:124-137). */
+int or_scene_set_textures(or_scene* s, const int32_t* mat_maps, const float* uv, const float* tan, uint32_t n_tex,
+                          const or_texdesc* descs) {
+    int* count = calloc(n_tex ? n_tex : 1, sizeof(int));
+    s->maps = malloc((s->n_mat ? s->n_mat : 1) * 4 * sizeof(int32_t));
+    for (uint32_t m = 0; m < s->n_mat; ++m)
+        for (int k = 0; k < 4; ++k) {
+            int32_t v = mat_maps[4 * m + k];
+            if (v < 0 || (uint32_t)v > n_tex) { free(count); return -1; }
+            s->maps[4 * m + k] = v - 1;
+            if (k < 2 && v > 0 && descs[v - 1].srgb_expand) count[v - 1]++;
+        }
+    s->tex = calloc(n_tex + 1, sizeof(or_tex));
+    for (uint32_t i = 0; i < n_tex; ++i)
+        if (tex_load(&s->tex[i], &descs[i], count[i])) { free(count); return -1; }
+    s->n_tex = (int)n_tex;
+    free(count);
+    s->uv = calloc((size_t)(s->n_tris ? s->n_tris : 1) * 6, sizeof(float));
+    s->tan = calloc((size_t)(s->n_tris ? s->n_tris : 1) * 9, sizeof(float));
+    if (uv) memcpy(s->uv, uv, (size_t)s->n_tris * 6 * sizeof(float));
+    if (tan) memcpy(s->tan, tan, (size_t)s->n_tris * 9 * sizeof(float));
+    return 0;
+}
+/* Scene::loadSkybox (pg/Scene.cpp:46-50): the sky texture is stored after the material maps */
+int or_scene_set_sky(or_scene* s, const or_texdesc* d) {
+    if (s->sky >= 0) { free(s->tex[s->sky].bytes); s->n_tex--; s->sky = -1; }
+    if (!d) return 0;
+    s->tex = realloc(s->tex, (size_t)(s->n_tex + 1) * sizeof(or_tex));
+    if (tex_load(&s->tex[s->n_tex], d, 0)) return -1;
+    s->sky = s->n_tex++;
+    return 0;
+}
+/* Texture::get_texel(int x, int y) (pg/Texture.cpp:72-107) */
+static v3 tex_texel(const or_tex* t, int x, int y, int repeat) {
+    int cx, cy;
+    if (repeat) { cx = abs(x % t->w); cy = abs(y % t->h); }
+    else { cx = x < 0 ? 0 : (x > t->w - 1 ? t->w - 1 : x); cy = y < 0 ? 0 : (y > t->h - 1 ? t->h - 1 : y); }
+    const uint8_t* p = t->bytes + (size_t)cy * t->pitch + (size_t)cx * t->px;
+    if (t->px > 4) { float f[3]; memcpy(f, p, sizeof f); return V(f[0], f[1], f[2]); }
+    return V((float)p[2] / 255.0f, (float)p[1] / 255.0f, (float)p[0] / 255.0f);
+}
+/* Texture::getTexelBilinear (pg/Texture.cpp:170-194); glm::mix(x, y, a) = x*(1-a) + y*a */
+static v3 tex_bilinear(const or_tex* t, float u, float v, int repeat) {
+    float pxc = u * (float)t->w, pyc = (1.0f - v) * (float)t->h;
+    float fx = floorf(pxc), fy = floorf(pyc);
+    float tx = pxc - fx, ty = pyc - fy;
+    v3 q00 = tex_texel(t, (int)fx, (int)fy, repeat), q10 = tex_texel(t, (int)(fx + 1.0f), (int)fy, repeat);
+    v3 q01 = tex_texel(t, (int)fx, (int)(fy + 1.0f), repeat), q11 = tex_texel(t, (int)(fx + 1.0f), (int)(fy + 1.0f), repeat);
+    v3 x1 = add(scl(q00, 1.0f - tx), scl(q10, tx));
+    v3 x2 = add(scl(q01, 1.0f - tx), scl(q11, tx));
+    return add(scl(x1, 1.0f - ty), scl(x2, ty));
+}
+/* SphericalMap::getTexel (pg/SphericalMap.cpp:10-14), INVPI = 1.0 / M_PI (double); sky texture is
+   BILINEAR + CLAMP_TO_EDGE (pg/Texture.h:27) */
+static v3 sky_texel(const or_scene* s, v3 dir) {
+    const double invpi = 1.0 / 3.14159265358979323846;
+    const float x = (float)(0.5f + (double)(0.5f * atan2f(dir.y, dir.x)) * invpi);
+    const float y = (float)(1.0f - (double)acosf(dir.z) * invpi);
+    return tex_bilinear(&s->tex[s->sky], x, y, 0);
+}
+/* Material::getDiffuseColor / getSpecularColor / getShininess (pg/material.cpp:105-134) at the
+   interpolated uv and the normal map (pg/Intersection.h:26-39); normal_only: BRDF-sampled emitter hits */
+static void apply_maps(const or_scene* s, uint32_t prim, float u, float v, uint32_t m, v3* kd, v3* ks, float* shin,
+                       v3* n, int normal_only) {
+    if (!s->maps) return;
+    const int32_t* mp = s->maps + 4 * m;
+    if (mp[0] < 0 && mp[1] < 0 && mp[2] < 0 && mp[3] < 0) return;
+    const float* q = s->uv + 6 * (size_t)prim;
+    float w = 1.0f - u - v;
+    float tu = (q[0] * w + q[2] * u) + q[4] * v, tv = (q[1] * w + q[3] * u) + q[5] * v;
+    if (!normal_only) {
+        if (mp[0] >= 0) *kd = tex_bilinear(&s->tex[mp[0]], tu, tv, 1);
+        if (mp[1] >= 0) *ks = tex_bilinear(&s->tex[mp[1]], tu, tv, 1);
+        if (mp[2] >= 0) { v3 r = tex_bilinear(&s->tex[mp[2]], tu, tv, 1); *shin = 2.0f / (r.x * r.x) - 2.0f; }
+    }
+    if (mp[3] >= 0) {
+        const float* g = s->tan + 9 * (size_t)prim;
+        v3 T = add(add(scl(V(g[0], g[1], g[2]), w), scl(V(g[3], g[4], g[5]), u)), scl(V(g[6], g[7], g[8]), v));
+        T = sub(T, scl(*n, dot(T, *n)));
+        T = nrmz(T);
+        v3 B = nrmz(cross(*n, T));
+        v3 N = sub(scl(tex_bilinear(&s->tex[mp[3]], tu, tv, 1), 2.0f), V(1.0f, 1.0f, 1.0f));
+        v3 nn = *n;
+        *n = V(T.x * N.x + B.x * N.y + nn.x * N.z, T.y * N.x + B.y * N.y + nn.y * N.z, T.z * N.x + B.z * N.y + nn.z * N.z);
+    }
 }
 
 /* ------------------------------------------------------------------ ray queries */
@@ -587,9 +725,10 @@ static int occluded(const fctx* F, v3 from, v3 to, uint64_t* rays) {
 }
 
 /* Intersection::intersectEmbree + getGeometryAttributes (pg/Intersection.h:8-41,85-113) */
-typedef struct { int hit; v3 point, normal; uint32_t prim; float t; } hitinfo;
+typedef struct { int hit; v3 point, normal; uint32_t prim; float t, u, v; } hitinfo;
 static hitinfo intersect(const fctx* F, v3 o, v3 d, float tnear, uint64_t* rays) {
     hitinfo hi; hi.hit = 0; hi.prim = 0xffffffffu; hi.t = FLT_MAX; hi.point = V(0, 0, 0); hi.normal = V(0, 0, 0);
+    hi.u = 0.0f; hi.v = 0.0f;
     (*rays)++;
     or_hit h = closest_hit(F->s, o, d, tnear, FLT_MAX);
     if (!h.hit) return hi;
@@ -599,7 +738,7 @@ static hitinfo intersect(const fctx* F, v3 o, v3 d, float tnear, uint64_t* rays)
     v3 n = add(add(scl(s->n0[t], w), scl(s->n1[t], h.u)), scl(s->n2[t], h.v));
     n = nrmz(n);
     if (dot(neg(d), n) <= 0.0f) n = scl(n, -1.0f);
-    hi.hit = 1; hi.normal = n; hi.prim = t; hi.t = h.t;
+    hi.hit = 1; hi.normal = n; hi.prim = t; hi.t = h.t; hi.u = h.u; hi.v = h.v;
     hi.point = add(o, scl(d, h.t));
     return hi;
 }
@@ -760,12 +899,13 @@ static void pass_gbuffer(fctx* F, const or_cam* cam, or_gbe* G, float* im, int y
                 e.pos = h.point; e.nrm = h.normal;
                 e.depth = len(sub(h.point, cam->eye));
                 e.type = m->type; e.kd = m->kd; e.ks = m->ks; e.le = m->le; e.shin = m->shin;
+                apply_maps(s, h.prim, h.u, h.v, s->mat[h.prim], &e.kd, &e.ks, &e.shin, &e.nrm, 0);
                 if (e.type == MT_PHONG || e.type == MT_DIELECTRIC) {
                     v3 Vv = nrmz(sub(cam->eye, e.pos));
                     imv = 1.0f / or_calc_I_M(dot(Vv, e.nrm), e.shin);
                 }
             } else {
-                e.le = P->use_skybox ? V(0, 0, 0) : V(P->bg_color[0], P->bg_color[1], P->bg_color[2]);
+                e.le = P->use_skybox ? sky_texel(s, d) : V(P->bg_color[0], P->bg_color[1], P->bg_color[2]);
             }
             G[(size_t)y * W + x] = e;
             im[(size_t)y * W + x] = imv;
@@ -820,6 +960,8 @@ static sample_t brdf_sample(const fctx* F, const or_gbe* g, v3 cam, rng_t* rng, 
     if (h.hit) {
         const or_mat* m = &s->mats[s->mat[h.prim]];
         if (m->le.x + m->le.y + m->le.z > 0) {
+            v3 kd_, ks_; float sh_;
+            apply_maps(s, h.prim, h.u, h.v, s->mat[h.prim], &kd_, &ks_, &sh_, &h.normal, 1);   /* normal map */
             v3 ld = sub(h.point, g->pos);
             float r2s = dot(ld, ld);
             ld = nrmz(ld);
@@ -1142,9 +1284,8 @@ static void tile_release(or_ctx* c) { free(c->tile); c->tile = NULL; }
 int or_tile_begin(or_ctx* c, const or_scene* s, const float* cam7, const or_params* P, uint32_t frame_index,
                   int y0, int y1, int margin, int halo) {
     int W = c->W, H = c->H;
-    /* useSkybox needs the equirect sky (pg/SphericalMap.cpp:10-14), whose HDR is a missing
-       blob in the reference checkout: only the background-colour miss path is restated. */
-    if (P->use_skybox) return -2;
+    /* useSkybox reads the scene's equirect sky (pg/SphericalMap.cpp:10-14) */
+    if (P->use_skybox && s->sky < 0) return -2;
     if (y0 < 0 || y1 > H || y0 >= y1 || margin < 0 || halo < 0 || halo > margin) return -1;
     or_tile_state* T = tile_of(c);
     if (!T) return -1;
@@ -1305,6 +1446,8 @@ static v3 mis_brdf_part(const fctx* F, const mis_surf* h, rng_t* rng, uint64_t* 
     if (!b.hit) return V(0, 0, 0);
     const or_mat* m = &s->mats[s->mat[b.prim]];
     if (!(m->le.x + m->le.y + m->le.z > 0)) return V(0, 0, 0);
+    v3 kd_, ks_; float sh_;
+    apply_maps(s, b.prim, b.u, b.v, s->mat[b.prim], &kd_, &ks_, &sh_, &b.normal, 1);
     v3 ld = sub(b.point, h->pos);
     float r2 = dot(ld, ld);
     ld = nrmz(ld);
@@ -1352,7 +1495,7 @@ static v3 mis_light_part(const fctx* F, const mis_surf* h, rng_t* rng, uint64_t*
  * is or_post_apply's running mean, as the reference's accumulator */
 int or_render_direct_mis(or_ctx* c, const or_scene* s, const float* cam7, const or_params* P, uint32_t frame_index,
                          int spp, float* out_rgb, uint64_t* rays_out) {
-    if (P->use_skybox) return -2;
+    if (P->use_skybox && s->sky < 0) return -2;
     if (spp < 1) return -1;
     int W = c->W, H = c->H;
     or_cam cam = make_cam(cam7, W, H);
@@ -1367,15 +1510,17 @@ int or_render_direct_mis(or_ctx* c, const or_scene* s, const float* cam7, const 
             hitinfo hi = intersect(&F, cam.eye, d, FLT_MIN + 0.01f, &rc);
             v3 px;
             if (!hi.hit) {
-                px = V(P->bg_color[0], P->bg_color[1], P->bg_color[2]);
+                px = P->use_skybox ? sky_texel(s, d) : V(P->bg_color[0], P->bg_color[1], P->bg_color[2]);
             } else {
                 const or_mat* m = &s->mats[s->mat[hi.prim]];
+                v3 kd = m->kd, ks = m->ks, hn = hi.normal; float shin = m->shin;
+                apply_maps(s, hi.prim, hi.u, hi.v, s->mat[hi.prim], &kd, &ks, &shin, &hn, 0);
                 if (nonzero_pos(m->le)) {                  /* Material::isEmitter, camera vertex */
                     px = m->le;
                 } else {
                     mis_surf h;
-                    h.pos = hi.point; h.n = hi.normal; h.dir = d;
-                    h.kd = m->kd; h.ks = m->ks; h.shin = m->shin;
+                    h.pos = hi.point; h.n = hn; h.dir = d;
+                    h.kd = kd; h.ks = ks; h.shin = shin;
                     h.phong = m->type == MT_PHONG || m->type == MT_DIELECTRIC;
                     h.maxD = maxc(h.kd); h.maxS = maxc(h.ks);
                     h.pf = h.maxD / (h.maxD + h.maxS);

@@ -9,6 +9,7 @@
 #include "rs_post.h"
 #include "rs_refit.h"
 #include "../../include/restir_c.h"
+#include "rs_image.h"
 
 #include <cmath>
 #include <cstdio>
@@ -24,8 +25,6 @@ int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int*
                    std::vector<int>& lvl_off, std::string& err);
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
               const std::vector<int>& lvl_off, hipStream_t st, int* tail, std::string& err);
-int load_obj_file(const char* path, std::vector<float>& pos, std::vector<float>& nrm, std::vector<uint32_t>& tri_mat,
-                  std::vector<rs_material_desc>& mats, std::string& err);
 }
 
 using namespace rs;
@@ -52,6 +51,13 @@ struct rs_scene {
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     int stage_i = 0;
     float* d_nrm_stage = nullptr;
+    // textures (rs_texture.h): host copies in device layout (re-packed when the sky changes)
+    struct HostTex { std::vector<uint8_t> bytes; int w = 0, h = 0, pitch = 0, px = 0; };
+    std::vector<HostTex> h_tex;            // material maps, then the sky (if any) last
+    int sky = -1;
+    uint8_t* d_tex = nullptr;
+    int4* d_texd = nullptr;
+    float4 *d_uv = nullptr, *d_tan = nullptr;
     // per-scene traversal choice (RS_TRAVERSAL_AUTO): frame times of each kind, tuning frames counted
     mutable int trav_choice = -1;
     mutable int trav_runs[2] = {0, 0};
@@ -60,6 +66,7 @@ struct rs_scene {
         DevScene S;
         S.nodes = d_nodes; S.tris = d_tris; S.tri_nrm = d_tri_nrm; S.mats = d_mats; S.emis = d_emis; S.cdf = d_cdf; S.cdf_guide = d_cdf_guide;
         S.n_nodes = n_nodes; S.n_tris = n_tris; S.n_emis = n_emis; S.n_mats = n_mats;
+        S.tri_uv = d_uv; S.tri_tan = d_tan; S.tex = d_tex; S.texd = d_texd; S.sky = sky;
         return S;
     }
 };
@@ -300,23 +307,120 @@ extern "C" const char* rs_last_error(const rs_context* c) {
 
 // --------------------------------------------------------------------------- scene
 static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& pos, std::string& err);
+// Utils::expand (pg/utils.cpp:209-218)
+static float srgb_expand1(float u) {
+    if (u <= 0.0f) return 0.0f;
+    if (u >= 1.0f) return 1.0f;
+    if (u <= 0.04045f) return u / 12.92f;
+    return powf((u + 0.055f) / 1.055f, 2.4f);
+}
+
+// A texture in the layout the reference's Texture holds after FreeImage_ConvertToRawBits
+// (pg/Texture.cpp:46-50): rows top first, pitch padded to 4 bytes, 8-bit texels as B,G,R(,A); float
+// texels as R,G,B(,A).  srgb_expand times Texture::expand (pg/Texture.cpp:141-160; every byte of the
+// pixel, quantised back to a byte each time).
+static bool prepare_texture(const rs_texture_desc& d, int srgb_expand, rs_scene::HostTex& t, std::string& err) {
+    if (!d.data || d.width < 1 || d.height < 1 || d.width > 65536 || d.height > 65536) { err = "bad texture size"; return false; }
+    if (d.format == RS_TEX_U8) {
+        if (d.channels != 1 && d.channels != 3 && d.channels != 4) { err = "8-bit textures need 1, 3 or 4 channels"; return false; }
+        t.px = (int)d.channels;
+    } else if (d.format == RS_TEX_F32) {
+        if (d.channels != 3 && d.channels != 4) { err = "float textures need 3 or 4 channels"; return false; }
+        t.px = 4 * (int)d.channels;
+    } else { err = "bad texture format"; return false; }
+    t.w = (int)d.width; t.h = (int)d.height;
+    t.pitch = (t.w * t.px + 3) & ~3;                                   // FreeImage_GetPitch
+    t.bytes.assign((size_t)t.pitch * t.h, 0);
+    const size_t rowlen = (size_t)t.w * d.channels;
+    for (int y = 0; y < t.h; ++y) {
+        uint8_t* dst = t.bytes.data() + (size_t)y * t.pitch;
+        if (d.format == RS_TEX_F32) {
+            std::memcpy(dst, (const float*)d.data + (size_t)y * rowlen, rowlen * sizeof(float));
+            continue;
+        }
+        const uint8_t* src = (const uint8_t*)d.data + (size_t)y * rowlen;
+        for (int x = 0; x < t.w; ++x) {
+            const uint8_t* q = src + (size_t)x * d.channels;
+            uint8_t* o = dst + (size_t)x * t.px;
+            if (d.channels == 1) { o[0] = q[0]; continue; }
+            o[0] = q[2]; o[1] = q[1]; o[2] = q[0];
+            if (d.channels == 4) o[3] = q[3];
+        }
+        for (int k = 0; k < srgb_expand; ++k)
+            for (int x = 0; x < t.w * t.px; ++x) {
+                float f = (float)dst[x] / 255.0f;
+                f = srgb_expand1(f);
+                dst[x] = (uint8_t)(f * 255.0f);
+            }
+    }
+    return true;
+}
+
+// (re-)upload every texture of the scene: one byte buffer (16-byte aligned offsets, 16 zero guard bytes
+// after each texture for the 1-byte texel quirk) + descriptors
+static int upload_textures(rs_context* c, rs_scene* s, std::string& err) {
+    if (s->d_tex) { hipFree(s->d_tex); s->d_tex = nullptr; }
+    if (s->d_texd) { hipFree(s->d_texd); s->d_texd = nullptr; }
+    if (s->h_tex.empty()) return 0;
+    std::vector<int4> desc;
+    size_t total = 0;
+    for (const auto& t : s->h_tex) {
+        desc.push_back(make_int4((int)total, t.w, t.h, t.pitch));
+        desc.push_back(make_int4(t.px, t.px > 4 ? RS_TEX_F32 : RS_TEX_U8, 0, 0));
+        total += (t.bytes.size() + 16 + 15) & ~(size_t)15;
+    }
+    if (total >= (size_t)INT32_MAX) { err = "textures exceed 2 GiB"; return -1; }
+    std::vector<uint8_t> all(total, 0);
+    for (size_t i = 0; i < s->h_tex.size(); ++i)
+        std::memcpy(all.data() + desc[2 * i].x, s->h_tex[i].bytes.data(), s->h_tex[i].bytes.size());
+    hipStream_t st = c->stream;
+    if (hipMalloc(&s->d_tex, total) != hipSuccess || hipMalloc(&s->d_texd, desc.size() * sizeof(int4)) != hipSuccess) {
+        err = "hipMalloc(textures) failed"; return -1;
+    }
+    if (hipMemcpyAsync(s->d_tex, all.data(), total, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(s->d_texd, desc.data(), desc.size() * sizeof(int4), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) { err = "texture upload failed"; return -1; }
+    return 0;
+}
+
 static int scene_from_arrays(rs_context* c, const std::vector<float>& pos, const std::vector<float>& nrm,
                              const std::vector<uint32_t>& tri_mat, const rs_material_desc* mats, uint32_t n_mats,
-                             rs_scene** out) {
+                             const std::vector<float>& uv, const std::vector<float>& tan,
+                             const rs_texture_desc* textures, uint32_t n_tex, rs_scene** out) {
     const uint32_t n = (uint32_t)tri_mat.size();
     for (uint32_t t = 0; t < n; ++t)
         if (tri_mat[t] >= n_mats) return fail(c, RS_E_INVALID, "rs_scene_create: material index out of range");
-    for (uint32_t m = 0; m < n_mats; ++m)
-        if (mats[m].type < 0 || mats[m].type > 6) return fail(c, RS_E_INVALID, "rs_scene_create: bad material type");
+    if (n_tex && !textures) return fail(c, RS_E_INVALID, "rs_scene_create_textured: null textures");
+    bool any_map = false, any_normal_map = false;
+    std::vector<int> expand_count(n_tex, 0);
+    for (uint32_t m = 0; m < n_mats; ++m) {
+        const rs_material_desc& d = mats[m];
+        if (d.type < 0 || d.type > 6) return fail(c, RS_E_INVALID, "rs_scene_create: bad material type");
+        const int32_t maps[4] = {d.diffuse_map, d.specular_map, d.shininess_map, d.normal_map};
+        for (int k = 0; k < 4; ++k) {
+            if (maps[k] < 0 || (uint32_t)maps[k] > n_tex)
+                return fail(c, RS_E_INVALID, "rs_scene_create: texture index out of range");
+            any_map |= maps[k] > 0;
+        }
+        any_normal_map |= d.normal_map > 0;
+    }
     // materials (pg/material.h:105-115) + emissive list in triangle order (triIdCtr, pg/ModelLoader.cpp:291-305)
-    std::vector<float4> hm(3 * (size_t)std::max(n_mats, 1u));
+    std::vector<float4> hm(kMatStride * (size_t)std::max(n_mats, 1u));
     for (uint32_t m = 0; m < n_mats; ++m) {
         const rs_material_desc& d = mats[m];
         int type = d.type;
         float tb; std::memcpy(&tb, &type, 4);
-        hm[3 * m] = make_float4(d.diffuse[0], d.diffuse[1], d.diffuse[2], d.shininess);
-        hm[3 * m + 1] = make_float4(d.specular[0], d.specular[1], d.specular[2], tb);
-        hm[3 * m + 2] = make_float4(d.emission[0], d.emission[1], d.emission[2], 0.0f);
+        const int mp[4] = {d.diffuse_map - 1, d.specular_map - 1, d.shininess_map - 1, d.normal_map - 1};
+        float mf[4]; std::memcpy(mf, mp, sizeof mf);
+        hm[kMatStride * m] = make_float4(d.diffuse[0], d.diffuse[1], d.diffuse[2], d.shininess);
+        hm[kMatStride * m + 1] = make_float4(d.specular[0], d.specular[1], d.specular[2], tb);
+        hm[kMatStride * m + 2] = make_float4(d.emission[0], d.emission[1], d.emission[2], 0.0f);
+        hm[kMatStride * m + 3] = make_float4(mf[0], mf[1], mf[2], mf[3]);
+    }
+    if (n_mats == 0) {
+        const int none[4] = {-1, -1, -1, -1};
+        float mf[4]; std::memcpy(mf, none, sizeof mf);
+        hm[3] = make_float4(mf[0], mf[1], mf[2], mf[3]);
     }
     std::vector<float4> tn(3 * (size_t)std::max(n, 1u));
     std::vector<uint32_t> emis_tri;
@@ -337,14 +441,53 @@ static int scene_from_arrays(rs_context* c, const std::vector<float>& pos, const
     rs_scene* s = new rs_scene();
     s->ctx = c; s->n_tris = n; s->n_mats = n_mats;
     s->h_nrm = nrm; s->h_tri_mat = tri_mat; s->h_mats.assign(mats, mats + n_mats);
-    auto bail = [&](const std::string& m) { rs_scene_destroy(s); return fail(c, RS_E_HIP, m); };
-    hipStream_t st = c->stream;
-    if (hipMalloc(&s->d_tri_nrm, tn.size() * sizeof(float4)) != hipSuccess) return bail("hipMalloc(nrm) failed");
-    hipMemcpyAsync(s->d_tri_nrm, tn.data(), tn.size() * sizeof(float4), hipMemcpyHostToDevice, st);
-    if (hipMalloc(&s->d_mats, hm.size() * sizeof(float4)) != hipSuccess) return bail("hipMalloc(mats) failed");
-    hipMemcpyAsync(s->d_mats, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice, st);
+    auto bail = [&](int code, const std::string& m) { rs_scene_destroy(s); return fail(c, code, m); };
     std::string err;
-    if (build_geometry(c, s, pos, err) != 0) return bail(err);
+    if (any_map) {
+        // Texture::expand count per texture: once per material diffuse/specular slot that references it
+        // (ModelLoader expands the TextureProxy-shared texture again for every such slot, :127,135)
+        for (uint32_t m = 0; m < n_mats; ++m) {
+            if (mats[m].diffuse_map > 0) expand_count[mats[m].diffuse_map - 1] += textures[mats[m].diffuse_map - 1].srgb_expand ? 1 : 0;
+            if (mats[m].specular_map > 0) expand_count[mats[m].specular_map - 1] += textures[mats[m].specular_map - 1].srgb_expand ? 1 : 0;
+        }
+        s->h_tex.resize(n_tex);
+        for (uint32_t i = 0; i < n_tex; ++i)
+            if (!prepare_texture(textures[i], expand_count[i], s->h_tex[i], err))
+                return bail(RS_E_INVALID, "texture " + std::to_string(i + 1) + ": " + err);
+        if (upload_textures(c, s, err) != 0) return bail(RS_E_HIP, err);
+        std::vector<float4> huv(2 * (size_t)std::max(n, 1u), make_float4(0, 0, 0, 0));
+        if (!uv.empty())
+            for (uint32_t t = 0; t < n; ++t) {
+                const float* q = &uv[6 * (size_t)t];
+                huv[2 * t] = make_float4(q[0], q[1], q[2], q[3]);
+                huv[2 * t + 1] = make_float4(q[4], q[5], 0.0f, 0.0f);
+            }
+        if (hipMalloc(&s->d_uv, huv.size() * sizeof(float4)) != hipSuccess) return bail(RS_E_HIP, "hipMalloc(uv) failed");
+        hipMemcpyAsync(s->d_uv, huv.data(), huv.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream);
+        if (any_normal_map) {
+            std::vector<float4> ht(3 * (size_t)std::max(n, 1u), make_float4(0, 0, 0, 0));
+            if (!tan.empty())
+                for (uint32_t t = 0; t < n; ++t)
+                    for (int j = 0; j < 3; ++j) {
+                        const float* q = &tan[9 * (size_t)t + 3 * j];
+                        ht[3 * t + j] = make_float4(q[0], q[1], q[2], 0.0f);
+                    }
+            if (hipMalloc(&s->d_tan, ht.size() * sizeof(float4)) != hipSuccess) return bail(RS_E_HIP, "hipMalloc(tangents) failed");
+            hipMemcpyAsync(s->d_tan, ht.data(), ht.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream);
+        }
+        if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(RS_E_HIP, "attribute upload failed");
+    } else if (n_tex) {
+        s->h_tex.resize(n_tex);                                        // unreferenced textures: validate only
+        for (uint32_t i = 0; i < n_tex; ++i)
+            if (!prepare_texture(textures[i], 0, s->h_tex[i], err)) return bail(RS_E_INVALID, "texture " + std::to_string(i + 1) + ": " + err);
+        s->h_tex.clear();
+    }
+    hipStream_t st = c->stream;
+    if (hipMalloc(&s->d_tri_nrm, tn.size() * sizeof(float4)) != hipSuccess) return bail(RS_E_HIP, "hipMalloc(nrm) failed");
+    hipMemcpyAsync(s->d_tri_nrm, tn.data(), tn.size() * sizeof(float4), hipMemcpyHostToDevice, st);
+    if (hipMalloc(&s->d_mats, hm.size() * sizeof(float4)) != hipSuccess) return bail(RS_E_HIP, "hipMalloc(mats) failed");
+    hipMemcpyAsync(s->d_mats, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice, st);
+    if (build_geometry(c, s, pos, err) != 0) return bail(RS_E_HIP, err);
     *out = s;
     return RS_OK;
 }
@@ -461,7 +604,7 @@ __device__ __forceinline__ void light_table(const float* __restrict__ pos, const
         em[8 * e + 3] = make_float4(n0.x, n0.y, n0.z, 0.0f);
         em[8 * e + 4] = make_float4(n1.x, n1.y, n1.z, 0.0f);
         em[8 * e + 5] = make_float4(n2.x, n2.y, n2.z, 0.0f);
-        em[8 * e + 6] = f4(xyz(mats[3 * m + 2]), 0.0f);
+        em[8 * e + 6] = f4(xyz(mats[kMatStride * m + 2]), 0.0f);
         em[8 * e + 7] = make_float4(area, 0.0f, 0.0f, 0.0f);
     }
     __syncthreads();
@@ -595,33 +738,108 @@ extern "C" int rs_scene_rebuild(rs_scene* s) {
     return RS_OK;
 }
 
-extern "C" int rs_scene_create(rs_context* c, const rs_mesh_desc* meshes, uint32_t n_meshes,
-                               const rs_material_desc* materials, uint32_t n_materials, rs_scene** out) {
+extern "C" int rs_scene_create_textured(rs_context* c, const rs_mesh_desc* meshes, uint32_t n_meshes,
+                                        const rs_material_desc* materials, uint32_t n_materials,
+                                        const rs_texture_desc* textures, uint32_t n_textures, rs_scene** out) {
     if (!c || !out || (n_meshes && !meshes) || (n_materials && !materials))
         return fail(c, RS_E_INVALID, "rs_scene_create: null argument");
     *out = nullptr;
     HIPCHK(c, enter(c));
-    std::vector<float> pos, nrm;
+    std::vector<float> pos, nrm, uv, tan;
     std::vector<uint32_t> tri_mat;
+    bool any_uv = false, any_tan = false;
+    for (uint32_t m = 0; m < n_meshes; ++m) {
+        any_uv |= meshes[m].texcoords != nullptr;
+        any_tan |= meshes[m].tangents != nullptr;
+    }
     for (uint32_t m = 0; m < n_meshes; ++m) {
         const rs_mesh_desc& d = meshes[m];
         if (d.n_tris && (!d.positions || !d.normals)) return fail(c, RS_E_INVALID, "rs_scene_create: null mesh buffer");
         pos.insert(pos.end(), d.positions, d.positions + 9 * (size_t)d.n_tris);
         nrm.insert(nrm.end(), d.normals, d.normals + 9 * (size_t)d.n_tris);
         tri_mat.insert(tri_mat.end(), d.n_tris, d.material);
+        if (any_uv) {
+            if (d.texcoords) uv.insert(uv.end(), d.texcoords, d.texcoords + 6 * (size_t)d.n_tris);
+            else uv.insert(uv.end(), 6 * (size_t)d.n_tris, 0.0f);
+        }
+        if (any_tan) {
+            if (d.tangents) tan.insert(tan.end(), d.tangents, d.tangents + 9 * (size_t)d.n_tris);
+            else tan.insert(tan.end(), 9 * (size_t)d.n_tris, 0.0f);
+        }
     }
-    return scene_from_arrays(c, pos, nrm, tri_mat, materials, n_materials, out);
+    return scene_from_arrays(c, pos, nrm, tri_mat, materials, n_materials, uv, tan, textures, n_textures, out);
+}
+
+extern "C" int rs_scene_create(rs_context* c, const rs_mesh_desc* meshes, uint32_t n_meshes,
+                               const rs_material_desc* materials, uint32_t n_materials, rs_scene** out) {
+    return rs_scene_create_textured(c, meshes, n_meshes, materials, n_materials, nullptr, 0, out);
+}
+
+static rs_texture_desc image_desc(const Image& im, int srgb) {
+    rs_texture_desc d;
+    d.width = (uint32_t)im.w; d.height = (uint32_t)im.h; d.channels = (uint32_t)im.channels;
+    d.format = im.is_float ? RS_TEX_F32 : RS_TEX_U8;
+    d.data = im.is_float ? (const void*)im.f32.data() : (const void*)im.u8.data();
+    d.srgb_expand = srgb;
+    return d;
 }
 
 extern "C" int rs_scene_load_obj(rs_context* c, const char* path, rs_scene** out) {
     if (!c || !path || !out) return fail(c, RS_E_INVALID, "rs_scene_load_obj: null argument");
     HIPCHK(c, enter(c));
-    std::vector<float> pos, nrm;
-    std::vector<uint32_t> tri_mat;
-    std::vector<rs_material_desc> mats;
+    ObjScene o;
     std::string err;
-    if (load_obj_file(path, pos, nrm, tri_mat, mats, err) != 0) return fail(c, RS_E_IO, err);
-    return scene_from_arrays(c, pos, nrm, tri_mat, mats.data(), (uint32_t)mats.size(), out);
+    int rc = load_obj_file(path, o, err);
+    if (rc) return fail(c, rc == -3 ? RS_E_UNSUPPORTED : RS_E_IO, err);
+    std::vector<rs_texture_desc> tex;
+    for (size_t i = 0; i < o.images.size(); ++i) tex.push_back(image_desc(o.images[i], o.srgb[i]));
+    const bool textured = !tex.empty();
+    static const std::vector<float> none;
+    return scene_from_arrays(c, o.pos, o.nrm, o.tri_mat, o.mats.data(), (uint32_t)o.mats.size(), textured ? o.uv : none,
+                             textured ? o.tan : none, tex.data(), (uint32_t)tex.size(), out);
+}
+
+// Scene::loadSkybox / SphericalMap (pg/Scene.cpp:46-50, pg/SphericalMap.h:8-10): the sky is kept as the
+// last texture of the scene's buffer (material map indices are unaffected)
+extern "C" int rs_scene_set_sky(rs_scene* s, const rs_texture_desc* d) {
+    if (!s) return fail(nullptr, RS_E_INVALID, "rs_scene_set_sky: null scene");
+    rs_context* c = s->ctx;
+    if (c->active) return fail(c, RS_E_INVALID, "rs_scene_set_sky: a frame is in flight");
+    HIPCHK(c, enter(c));
+    HIPCHK(c, hipStreamSynchronize(c->stream));        // enqueued frames may still read the texture buffer
+    rs_scene::HostTex t;
+    std::string err;
+    if (d && !prepare_texture(*d, 0, t, err)) return fail(c, RS_E_INVALID, "rs_scene_set_sky: " + err);
+    if (s->sky >= 0) { s->h_tex.pop_back(); s->sky = -1; }
+    if (d) { s->h_tex.push_back(std::move(t)); s->sky = (int)s->h_tex.size() - 1; }
+    if (upload_textures(c, s, err) != 0) return fail(c, RS_E_HIP, "rs_scene_set_sky: " + err);
+    return RS_OK;
+}
+
+extern "C" int rs_scene_load_sky(rs_scene* s, const char* path) {
+    if (!s || !path) return fail(s ? s->ctx : nullptr, RS_E_INVALID, "rs_scene_load_sky: null argument");
+    Image im;
+    std::string err;
+    int rc = load_image(path, im, err);
+    if (rc) return fail(s->ctx, rc == -3 ? RS_E_UNSUPPORTED : RS_E_IO, err);
+    const rs_texture_desc d = image_desc(im, 0);
+    return rs_scene_set_sky(s, &d);
+}
+
+extern "C" int rs_image_decode(const char* path, uint32_t* w, uint32_t* h, uint32_t* ch, int32_t* fmt, void* out,
+                               size_t out_bytes) {
+    if (!path || !w || !h || !ch || !fmt) return fail(nullptr, RS_E_INVALID, "rs_image_decode: null argument");
+    Image im;
+    std::string err;
+    int rc = load_image(path, im, err);
+    if (rc) return fail(nullptr, rc == -3 ? RS_E_UNSUPPORTED : RS_E_IO, err);
+    *w = (uint32_t)im.w; *h = (uint32_t)im.h; *ch = (uint32_t)im.channels;
+    *fmt = im.is_float ? RS_TEX_F32 : RS_TEX_U8;
+    if (!out) return RS_OK;
+    const size_t need = im.is_float ? im.f32.size() * sizeof(float) : im.u8.size();
+    if (out_bytes < need) return fail(nullptr, RS_E_INVALID, "rs_image_decode: output buffer too small");
+    std::memcpy(out, im.is_float ? (const void*)im.f32.data() : (const void*)im.u8.data(), need);
+    return RS_OK;
 }
 
 extern "C" void rs_scene_destroy(rs_scene* s) {
@@ -629,7 +847,8 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     if (s->ctx) hipSetDevice(s->ctx->device);
     if (s->ctx && s->ctx->stream) hipStreamSynchronize(s->ctx->stream);
     void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
-                    s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage};
+                    s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage, s->d_tex, s->d_texd, s->d_uv,
+                    s->d_tan};
     for (void* p : ptrs) if (p) hipFree(p);
     for (int k = 0; k < 2; ++k) {
         if (s->h_stage[k]) hipHostFree(s->h_stage[k]);
@@ -736,7 +955,8 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
                              uint32_t frame_index, const rs_tile_desc* tile) {
     if (!c || !s || !cam || !P || !tile) return fail(c, RS_E_INVALID, "rs_tile_begin: null argument");
     if (s->ctx != c) return fail(c, RS_E_INVALID, "rs_tile_begin: scene belongs to another context");
-    if (P->use_skybox) return fail(c, RS_E_UNSUPPORTED, "useSkybox: the reference's sky HDR (data/env/forest.hdr) is a missing blob");
+    if (P->use_skybox && s->sky < 0)
+        return fail(c, RS_E_UNSUPPORTED, "use_skybox: the scene has no sky map (rs_scene_set_sky / rs_scene_load_sky)");
     if (P->m_area < 0 || P->m_brdf < 0 || P->spatial_passes < 0 || P->confidence_cap < 0)
         return fail(c, RS_E_INVALID, "rs_frame_params: negative count");
     if (P->do_spatial && (P->spatial_neighbors < 0 || P->spatial_neighbors > 64))
@@ -754,6 +974,7 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     F.do_vis_pass = P->do_visibility_pass; F.reject = P->reject_dissimilar; F.mis = P->spatial_mis;
     F.bg = vec3{P->bg_color[0], P->bg_color[1], P->bg_color[2]};
     F.tnear_off = P->tnear_offset; F.tfar_off = P->tfar_offset; F.normal_off = P->normal_offset;
+    F.use_sky = P->use_skybox ? 1 : 0;
     F.seed = P->seed; F.frame = frame_index;
     F.W = c->W; F.H = c->H;
     F.y0 = tile->y0; F.y1 = tile->y1;
@@ -946,12 +1167,14 @@ extern "C" int rs_render_direct_mis(rs_context* c, const rs_scene* s, const rs_c
     if (!c || !s || !cam || !P) return fail(c, RS_E_INVALID, "rs_render_direct_mis: null argument");
     if (s->ctx != c) return fail(c, RS_E_INVALID, "rs_render_direct_mis: scene belongs to another context");
     if (c->active) return fail(c, RS_E_INVALID, "rs_render_direct_mis: a tile frame is in flight");
-    if (P->use_skybox) return fail(c, RS_E_UNSUPPORTED, "useSkybox: the reference's sky HDR (data/env/forest.hdr) is a missing blob");
+    if (P->use_skybox && s->sky < 0)
+        return fail(c, RS_E_UNSUPPORTED, "use_skybox: the scene has no sky map (rs_scene_set_sky / rs_scene_load_sky)");
     if (spp < 1 || spp > 65536) return fail(c, RS_E_INVALID, "rs_render_direct_mis: spp must be in [1, 65536]");
     HIPCHK(c, enter(c));
     FrameConst F = {};
     F.bg = vec3{P->bg_color[0], P->bg_color[1], P->bg_color[2]};
     F.tnear_off = P->tnear_offset; F.tfar_off = P->tfar_offset; F.normal_off = P->normal_offset;
+    F.use_sky = P->use_skybox ? 1 : 0;
     F.seed = P->seed; F.frame = frame_index;
     F.W = c->W; F.H = c->H; F.y0 = 0; F.y1 = c->H; F.gy0 = 0; F.gy1 = c->H;
     GCam gc;

@@ -80,11 +80,13 @@ __device__ __forceinline__ vec3 mis_brdf_part(const DevScene& S, const FrameCons
     if (!b.hit) return mk(0, 0, 0);
     MatRec m = load_mat(S, b.mat);
     if (!(m.le.x + m.le.y + m.le.z > 0)) return mk(0, 0, 0);      // Material::isEmissive
+    vec3 bn = b.normal;
+    if (S.texd) apply_maps(S, b, m, bn, true);
     vec3 ld = b.point - h.pos;
     float r2 = dot(ld, ld);
     ld = normalize(ld);
     float cI = gmax(dot(ld, h.n), 0.0f);
-    float cY = gmax(dot(-ld, b.normal), 0.0f);
+    float cY = gmax(dot(-ld, bn), 0.0f);
     float amf = cY / r2;
     float pdf_light = S.emis[8 * b.emis_id + 2].w;                 // TriangleCDF::getPDFForTriangle
     float w = mis_power(pdf * amf, pdf_light);
@@ -134,10 +136,12 @@ __global__ void __launch_bounds__(256) k_direct_mis(DevScene S, FrameConst F, in
                           m[2] * dc.x + m[5] * dc.y + m[8] * dc.z));
     SurfHit hi = intersect<T>(S, in, F.cam.pos, d, FLT_MIN + 0.01f);
     MatRec mr = load_mat(S, hi.mat);
+    vec3 hn = hi.normal;
+    if (S.texd && hi.hit) apply_maps(S, hi, mr, hn, false);
     const bool surf = in && hi.hit && !any_pos(mr.le);               // Material::isEmitter: camera vertex -> Le
-    vec3 px = hi.hit ? mr.le : F.bg;
+    vec3 px = hi.hit ? mr.le : (F.use_sky ? sky_texel(S, d) : F.bg);  // miss: sky or bgColor (:131)
     MisSurf h;
-    h.pos = hi.point; h.n = hi.normal; h.kd = mr.kd; h.ks = mr.ks; h.shin = mr.shin;
+    h.pos = hi.point; h.n = hn; h.kd = mr.kd; h.ks = mr.ks; h.shin = mr.shin;
     h.phong = is_phong(mr.type);
     h.maxD = maxc(h.kd); h.maxS = maxc(h.ks);
     h.pf = h.maxD / (h.maxD + h.maxS);

@@ -18,6 +18,7 @@
 // outside the image work on a clamped pixel and store nothing.
 #pragma once
 #include "rs_scene.h"
+#include "rs_texture.h"
 
 // waves per SIMD the ray-tracing kernels are register-budgeted for (launch_bounds 2nd argument)
 #ifndef RS_INITIAL_WAVES
@@ -39,6 +40,7 @@ struct FrameConst {
     float radius, min_normal_sim, max_depth_diff;
     int do_spatial, do_temporal, do_vis_pass, reject, mis;
     vec3 bg; float tnear_off, tfar_off, normal_off;
+    int use_sky;          // useSkybox with a scene sky (rs_texture.h sky_texel)
     uint32_t seed, frame;
     int W, H;             // full frame
     int y0, y1;           // band this context renders
@@ -199,7 +201,9 @@ __device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameCons
     g.shin = 0; g.depth = 0; g.type = 0; g.inv_im = 0;
     if (h.hit) {
         MatRec mr = load_mat(S, h.mat);
-        g.pos = h.point; g.nrm = h.normal; g.depth = length(h.point - F.cam.pos);
+        vec3 nrm = h.normal;
+        if (S.texd) apply_maps(S, h, mr, nrm, false);                // textured scenes only (uniform)
+        g.pos = h.point; g.nrm = nrm; g.depth = length(h.point - F.cam.pos);
         g.type = mr.type; g.kd = mr.kd; g.ks = mr.ks; g.le = mr.le; g.shin = mr.shin;
         if (g.type == MT_PHONG || g.type == MT_DIELECTRIC) {
             vec3 V = normalize(F.cam.pos - g.pos);
@@ -210,7 +214,7 @@ __device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameCons
 #endif
         }
     } else {
-        g.le = F.bg;      // useSkybox=false path: renderParams.bgColor (:231)
+        g.le = F.use_sky ? sky_texel(S, dw) : F.bg;      // useSkybox ? sky : renderParams.bgColor (:231)
     }
     return g;
 }
@@ -270,16 +274,18 @@ __device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameCons
     if (h.hit) {
         MatRec mr = load_mat(S, h.mat);
         if (mr.le.x + mr.le.y + mr.le.z > 0) {      // Material::isEmissive (pg/material.h:135-137)
+            vec3 hn = h.normal;
+            if (S.texd) apply_maps(S, h, mr, hn, true);                // a normal-mapped emitter
             vec3 ld = h.point - pos;
             float r2s = dot(ld, ld);
             ld = normalize(ld);
-            float cY = gmax(dot(-ld, h.normal), 0.0f);
+            float cY = gmax(dot(-ld, hn), 0.0f);
             float amf = cY / r2s;
             float pdf_area = S.emis[8 * h.emis_id + 2].w;   // getPDFForTriangle (pg/TriangleCDF.h:25-31)
             float bpa = pdf * amf;
             W_out = 1.0f / bpa;
             mis_out = m_brdf(F, bpa, pdf_area);
-            return Sample{h.point, h.normal, mr.le};
+            return Sample{h.point, hn, mr.le};
         }
     }
     return smp_invalid();

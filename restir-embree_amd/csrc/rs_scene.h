@@ -24,12 +24,19 @@ struct DevScene {
     const float4* nodes;      // 2 per node
     const float4* tris;       // 3 per leaf-ordered triangle
     const float4* tri_nrm;    // 3 per prim: n0 (w = material id bits), n1 (w = emissive id bits), n2
-    const float4* mats;       // 3 per material: (kd, shin), (ks, type bits), (le, 0)
+    const float4* mats;       // 4 per material: (kd, shin), (ks, type bits), (le, 0), map ids (int bits, -1 none:
+                              //   diffuse, specular, shininess, normal)
     const float4* emis;       // 8 per emissive triangle: p0,p1,p2 (w: pick_pdf, inv_area, pdf_brdf_area),
                               //   n0, n1, n2, le, (area, 0, 0, 0)
     const float* cdf;         // cumulative normalised area (TriangleCDF::cdf2)
     const int* cdf_guide;     // kCdfGuide+1 entries: lower_bound(cdf, j / kCdfGuide)
     uint32_t n_nodes, n_tris, n_emis, n_mats;
+    // textures (rs_texture.h); all null / -1 for untextured scenes
+    const float4* tri_uv;     // 2 per prim: (uv0, uv1), (uv2, 0, 0)
+    const float4* tri_tan;    // 3 per prim: tangent t0, t1, t2 (normal-mapped scenes only)
+    const uint8_t* tex;       // texel bytes of every texture
+    const int4* texd;         // 2 per texture: (byte offset, width, height, pitch), (pixel bytes, format, 0, 0)
+    int sky;                  // texture index of the equirect sky, -1 none
 };
 constexpr int kCdfGuide = 1024;
 
@@ -401,18 +408,24 @@ __device__ __forceinline__ Hit trace_closest(const DevScene& S, bool active, vec
 
 // Material record (pg/material.h:105-115)
 struct MatRec { vec3 kd; float shin; vec3 ks; int type; vec3 le; };
+constexpr int kMatStride = 4;
 __device__ __forceinline__ MatRec load_mat(const DevScene& S, uint32_t m) {
-    float4 a = S.mats[3 * m], b = S.mats[3 * m + 1], c = S.mats[3 * m + 2];
+    float4 a = S.mats[kMatStride * m], b = S.mats[kMatStride * m + 1], c = S.mats[kMatStride * m + 2];
     return MatRec{xyz(a), a.w, xyz(b), __float_as_int(b.w), xyz(c)};
+}
+__device__ __forceinline__ int4 load_maps(const DevScene& S, uint32_t m) {
+    float4 q = S.mats[kMatStride * m + 3];
+    return make_int4(__float_as_int(q.x), __float_as_int(q.y), __float_as_int(q.z), __float_as_int(q.w));
 }
 
 // Intersection::intersectEmbree + getGeometryAttributes (pg/Intersection.h:8-41,85-113):
 // hit point = org + dir*t, interpolated normal (1-u-v)n0 + u n1 + v n2, normalised, flipped to face
 // the ray; material; emissive id (vertex-0 attribute, :103-110).
-struct SurfHit { bool hit; vec3 point, normal; uint32_t mat; int emis_id; };
+struct SurfHit { bool hit; vec3 point, normal; uint32_t mat; int emis_id; int prim; float u, v; };
 template <int T>
 __device__ __forceinline__ SurfHit intersect(const DevScene& S, bool active, vec3 o, vec3 d, float tnear) {
     SurfHit r; r.hit = false; r.mat = 0; r.emis_id = -1; r.point = mk(0, 0, 0); r.normal = mk(0, 0, 0);
+    r.prim = -1; r.u = 0.0f; r.v = 0.0f;
     Hit h = trace_closest<T>(S, active, o, d, tnear, FLT_MAX);
     if (h.prim < 0) return r;
     const float4* N = S.tri_nrm + 3 * h.prim;
@@ -423,6 +436,7 @@ __device__ __forceinline__ SurfHit intersect(const DevScene& S, bool active, vec
     if (dot(-d, n) <= 0.0f) n = n * -1.0f;
     r.hit = true; r.normal = n; r.point = o + d * h.t;
     r.mat = (uint32_t)__float_as_int(n0.w); r.emis_id = __float_as_int(n1.w);
+    r.prim = h.prim; r.u = h.u; r.v = h.v;
     return r;
 }
 

@@ -29,7 +29,8 @@ EXPORTED_SYMBOLS = [
     "rs_synchronize", "rs_dump_gbuffer", "rs_dump_reservoirs", "rs_tile_begin", "rs_tile_halo_ptr",
     "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_context_set_traversal",
     "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions", "rs_post_frame",
-    "rs_post_reset", "rs_scene_rebuild", "rs_render_direct_mis",
+    "rs_post_reset", "rs_scene_rebuild", "rs_render_direct_mis", "rs_scene_create_textured", "rs_scene_set_sky",
+    "rs_scene_load_sky", "rs_image_decode",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -39,12 +40,38 @@ TRAVERSAL_NAMES = {"auto": TRAVERSAL_AUTO, "lockstep": TRAVERSAL_LOCKSTEP, "lane
 
 class MeshDesc(ctypes.Structure):
     _fields_ = [("n_tris", ctypes.c_uint32), ("positions", ctypes.POINTER(ctypes.c_float)),
-                ("normals", ctypes.POINTER(ctypes.c_float)), ("material", ctypes.c_uint32)]
+                ("normals", ctypes.POINTER(ctypes.c_float)), ("material", ctypes.c_uint32),
+                ("texcoords", ctypes.POINTER(ctypes.c_float)), ("tangents", ctypes.POINTER(ctypes.c_float))]
 
 
 class MaterialDesc(ctypes.Structure):
     _fields_ = [("diffuse", ctypes.c_float * 3), ("specular", ctypes.c_float * 3), ("emission", ctypes.c_float * 3),
-                ("shininess", ctypes.c_float), ("type", ctypes.c_int32)]
+                ("shininess", ctypes.c_float), ("type", ctypes.c_int32), ("diffuse_map", ctypes.c_int32),
+                ("specular_map", ctypes.c_int32), ("shininess_map", ctypes.c_int32), ("normal_map", ctypes.c_int32)]
+
+
+TEX_U8, TEX_F32 = 0, 1
+
+
+class TextureDesc(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("channels", ctypes.c_uint32),
+                ("format", ctypes.c_int32), ("data", ctypes.c_void_p), ("srgb_expand", ctypes.c_int32)]
+
+
+def texture_desc(tex):
+    """(TextureDesc, keep-alive array) for a scenes.Texture or an (H, W, C) array."""
+    arr = tex.data if hasattr(tex, "data") and not isinstance(tex, np.ndarray) else tex
+    arr = np.asarray(arr)
+    if arr.ndim == 2:
+        arr = arr[:, :, None]
+    if arr.dtype == np.uint8:
+        fmt = TEX_U8
+    else:
+        arr, fmt = arr.astype(np.float32), TEX_F32
+    arr = np.ascontiguousarray(arr)
+    d = TextureDesc(arr.shape[1], arr.shape[0], arr.shape[2], fmt, arr.ctypes.data,
+                    int(getattr(tex, "srgb_expand", 0)))
+    return d, arr
 
 
 class CameraDesc(ctypes.Structure):
@@ -127,10 +154,32 @@ def load_library(path: str = LIB_PATH):
     L.rs_post_frame.argtypes = [vp, ctypes.POINTER(PostParams), ctypes.POINTER(vp), ctypes.POINTER(PostStats)]
     L.rs_post_reset.argtypes = [vp]
     L.rs_scene_rebuild.argtypes = [vp]
+    L.rs_scene_create_textured.argtypes = [vp, ctypes.POINTER(MeshDesc), u32, ctypes.POINTER(MaterialDesc), u32,
+                                           ctypes.POINTER(TextureDesc), u32, ctypes.POINTER(vp)]
+    L.rs_scene_set_sky.argtypes = [vp, ctypes.POINTER(TextureDesc)]
+    L.rs_scene_load_sky.argtypes = [vp, ctypes.c_char_p]
+    L.rs_image_decode.argtypes = [ctypes.c_char_p, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32),
+                                  ctypes.POINTER(i32), vp, ctypes.c_size_t]
     L.rs_render_direct_mis.argtypes = [vp, vp, ctypes.POINTER(CameraDesc), ctypes.POINTER(FrameParams), u32, u32, fp,
                                        ctypes.POINTER(PassTimes)]
     _lib = L
     return L
+
+
+def decode_image(path) -> np.ndarray:
+    """The scene loader's image decoder (rs_image_decode; no GPU needed): (H, W, C) uint8 or float32."""
+    L = load_library()
+    w, h, c, f = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int32()
+    p = os.fsencode(path)
+    rc = L.rs_image_decode(p, ctypes.byref(w), ctypes.byref(h), ctypes.byref(c), ctypes.byref(f), None, 0)
+    if rc != RS_OK:
+        raise RestirError(f"rs_image_decode({path}): {L.rs_last_error(None).decode()}")
+    out = np.zeros((h.value, w.value, c.value), np.uint8 if f.value == TEX_U8 else np.float32)
+    rc = L.rs_image_decode(p, ctypes.byref(w), ctypes.byref(h), ctypes.byref(c), ctypes.byref(f), out.ctypes.data,
+                           out.nbytes)
+    if rc != RS_OK:
+        raise RestirError(f"rs_image_decode({path}): {L.rs_last_error(None).decode()}")
+    return out
 
 
 def camera_desc(camera) -> CameraDesc:
@@ -168,6 +217,21 @@ class Scene:
         r = self.renderer
         r._check(r.lib.rs_scene_update_positions(self.h, pos.ctypes.data_as(fp),
                                                  nrm.ctypes.data_as(fp) if nrm is not None else None))
+
+    def set_sky(self, texture):
+        """Equirect sky for params.use_skybox (rs_scene_set_sky); None removes it."""
+        r = self.renderer
+        if texture is None:
+            r._check(r.lib.rs_scene_set_sky(self.h, None))
+            return
+        d, keep = texture_desc(texture)
+        r._check(r.lib.rs_scene_set_sky(self.h, ctypes.byref(d)))
+        del keep
+
+    def load_sky(self, path):
+        """Sky from a .hdr / .pfm / .ppm / .png file (rs_scene_load_sky)."""
+        r = self.renderer
+        r._check(r.lib.rs_scene_load_sky(self.h, os.fsencode(path)))
 
     def rebuild(self):
         """Full light-CDF + BVH rebuild from the current positions (rs_scene_rebuild; synchronous)."""
@@ -239,11 +303,19 @@ class Renderer:
         ends = np.concatenate([cuts, [tm.shape[0]]]).astype(np.int64)
         meshes = (MeshDesc * max(1, len(starts)))()
         fp = ctypes.POINTER(ctypes.c_float)
+        uv = getattr(scene, "texcoords", None)
+        tg = getattr(scene, "tangents", None)
+        uv = None if uv is None else np.ascontiguousarray(uv, np.float32).reshape(-1, 6)
+        tg = None if tg is None else np.ascontiguousarray(tg, np.float32).reshape(-1, 9)
         for i, (a, b) in enumerate(zip(starts, ends)):
             meshes[i].n_tris = int(b - a)
             meshes[i].positions = pos[a:b].ctypes.data_as(fp)
             meshes[i].normals = nrm[a:b].ctypes.data_as(fp)
             meshes[i].material = int(tm[a]) if b > a else 0
+            if uv is not None:
+                meshes[i].texcoords = uv[a:b].ctypes.data_as(fp)
+            if tg is not None:
+                meshes[i].tangents = tg[a:b].ctypes.data_as(fp)
         mats = (MaterialDesc * max(1, len(scene.materials)))()
         for i, m in enumerate(scene.materials):
             for j in range(3):
@@ -252,10 +324,19 @@ class Renderer:
                 mats[i].emission[j] = m.le[j]
             mats[i].shininess = m.shininess
             mats[i].type = m.type
+            for k in ("diffuse_map", "specular_map", "shininess_map", "normal_map"):
+                setattr(mats[i], k, int(getattr(m, k, 0)))
         out = ctypes.c_void_p()
         n_mesh = len(starts) if tm.shape[0] else 0
-        self._check(self.lib.rs_scene_create(self.h, meshes, n_mesh, mats, len(scene.materials), ctypes.byref(out)))
-        return Scene(self, out)
+        textures = list(getattr(scene, "textures", []) or [])
+        descs = [texture_desc(t) for t in textures]
+        tex_arr = (TextureDesc * max(1, len(descs)))(*[d for d, _ in descs])
+        self._check(self.lib.rs_scene_create_textured(self.h, meshes, n_mesh, mats, len(scene.materials), tex_arr,
+                                                      len(descs), ctypes.byref(out)))
+        sc = Scene(self, out)
+        if getattr(scene, "sky", None) is not None:
+            sc.set_sky(scene.sky)
+        return sc
 
     # ---- render(frame) ------------------------------------------------------------------
     def produce_restir(self, scene: Scene, camera, params: FrameParams, frame_index: int = 0,

@@ -28,6 +28,20 @@ class Material:
     le: tuple = (0.0, 0.0, 0.0)
     shininess: float = 1.0
     type: int = LAMBERT
+    # texture slots (pg/material.cpp:105-134, pg/Intersection.h:26-39): 1-based index into Scene.textures
+    diffuse_map: int = 0
+    specular_map: int = 0
+    shininess_map: int = 0
+    normal_map: int = 0
+
+
+@dataclass
+class Texture:
+    """Decoded texture (include/restir_c.h rs_texture_desc): (H, W, C) uint8 (texel = byte/255) or
+    float32, top row first, C in {1, 3, 4} (float: 3 or 4).  srgb_expand: Texture::expand at load for
+    colour maps (the OBJ loader sets it for map_Kd / map_Ks)."""
+    data: np.ndarray
+    srgb_expand: int = 0
 
 
 @dataclass
@@ -49,6 +63,10 @@ class Scene:
     materials: list = field(default_factory=list)
     camera: Camera | None = None
     name: str = ""
+    texcoords: np.ndarray | None = None   # (T, 6) float32 uv per vertex (attribute slot 1)
+    tangents: np.ndarray | None = None    # (T, 9) float32 (attribute slot 3; normal maps)
+    textures: list = field(default_factory=list)
+    sky: Texture | None = None            # equirect sky (useSkybox)
 
     @property
     def n_tris(self) -> int:
@@ -186,6 +204,46 @@ def cornell_box(n_lights: int = 8) -> Scene:
             k += 1
     b.quads(np.array(corners), np.array(normals), light)
     return b.build(CORNELL_CAMERA, f"cornell_{n_lights}")
+
+
+def textured_cornell(n_lights: int = 8, seed: int = 5, sky: bool = True) -> Scene:
+    """§8f-2 test scene: C1 with material textures and an equirect sky (synthetic texels, seeded).
+    Exercises every texture path of the reference: 8-bit RGB and RGBA diffuse maps (sRGB-expanded; the
+    RGB map is shared by two materials, so it is expanded twice -- ModelLoader's TextureProxy quirk), a
+    1-channel roughness map (the 3-byte read quirk, Ns = 2/r^2 - 2), a specular map, a normal map with
+    tangents, planar uvs spanning negative values (REPEAT's abs(x % w)), a float RGB sky seen through the
+    open front of the box."""
+    sc = cornell_box(n_lights)
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:48, 0:64]
+    checker = np.where(((xx // 8) + (yy // 8)) % 2 == 0, 220, 60).astype(np.uint8)
+    checker = np.stack([checker, (xx * 4).astype(np.uint8), (255 - yy * 5).astype(np.uint8)], -1)
+    rgba = rng.integers(0, 256, size=(32, 32, 4), dtype=np.uint8)
+    rough = rng.integers(40, 200, size=(16, 24), dtype=np.uint8)[:, :, None]
+    spec = rng.integers(0, 40, size=(20, 20, 3), dtype=np.uint8)
+    ny, nx = np.mgrid[0:32, 0:32] / 32.0
+    n = np.stack([0.3 * np.sin(6.28 * nx), 0.3 * np.cos(6.28 * ny), np.ones_like(nx)], -1)
+    n /= np.linalg.norm(n, axis=-1, keepdims=True)
+    nmap = np.clip((n * 0.5 + 0.5) * 255.0, 0, 255).astype(np.uint8)
+    sc.textures = [Texture(checker, 1), Texture(rgba, 1), Texture(rough, 0), Texture(nmap, 0), Texture(spec, 1)]
+    mats = [Material(**vars(m)) for m in sc.materials]
+    mats[0].diffuse_map, mats[0].normal_map = 1, 4          # white: checker + normal map
+    mats[1].diffuse_map = 2                                  # red: RGBA
+    mats[2].diffuse_map = 1                                  # green: the checker again (expanded twice)
+    mats[3].specular_map, mats[3].shininess_map = 5, 3      # glossy Phong block
+    sc.materials = mats
+    P = sc.positions.reshape(-1, 3, 3).astype(np.float64)
+    u = 0.7 * (P[..., 0] + P[..., 1]) + 0.13
+    v = 0.6 * P[..., 2] - 0.4
+    sc.texcoords = np.stack([u, v], -1).reshape(-1, 6).astype(np.float32)
+    t = np.tile(np.array([1.0, 1.0, 0.2]), (P.shape[0], 3, 1)) + rng.normal(0, 0.05, size=(P.shape[0], 3, 3))
+    t /= np.linalg.norm(t, axis=-1, keepdims=True)
+    sc.tangents = t.reshape(-1, 9).astype(np.float32)
+    if sky:
+        sy, sx = np.mgrid[0:16, 0:32]
+        sc.sky = Texture(np.stack([0.2 + sx / 32.0, 0.5 + 0.5 * np.sin(sy / 3.0), 1.5 - sy / 16.0], -1).astype(np.float32))
+    sc.name = f"textured_cornell_{n_lights}"
+    return sc
 
 
 def cornell_many_lights(n_lights: int = 1024, seed: int = 7, size: float = 0.03) -> Scene:

@@ -53,6 +53,10 @@ def lib():
         L.or_render_frame.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _f32p, ctypes.POINTER(FrameParams),
                                       ctypes.c_uint32, _f32p, ctypes.POINTER(ctypes.c_uint64)]
         L.or_get_gbuffer.argtypes = [ctypes.c_void_p, ctypes.c_int, _f32p]
+        L.or_scene_set_textures.restype = ctypes.c_int
+        L.or_scene_set_textures.argtypes = [ctypes.c_void_p, _i32p, _f32p, _f32p, ctypes.c_uint32, ctypes.c_void_p]
+        L.or_scene_set_sky.restype = ctypes.c_int
+        L.or_scene_set_sky.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.or_render_direct_mis.restype = ctypes.c_int
         L.or_render_direct_mis.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _f32p, ctypes.POINTER(FrameParams),
                                            ctypes.c_uint32, ctypes.c_int, _f32p, ctypes.POINTER(ctypes.c_uint64)]
@@ -109,6 +113,25 @@ class OraclePost:
                       "acc_frames_used": used}
 
 
+class _TexDesc(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("channels", ctypes.c_uint32),
+                ("format", ctypes.c_int32), ("data", ctypes.c_void_p), ("srgb_expand", ctypes.c_int32)]
+
+
+def _texdescs(textures):
+    """or_texdesc array (+ the arrays it points into) for scenes.Texture objects."""
+    keep, arr = [], (_TexDesc * max(1, len(textures)))()
+    for i, t in enumerate(textures):
+        a = np.asarray(t.data)
+        if a.ndim == 2:
+            a = a[:, :, None]
+        fmt = 0 if a.dtype == np.uint8 else 1
+        a = np.ascontiguousarray(a if fmt == 0 else a.astype(np.float32))
+        keep.append(a)
+        arr[i] = _TexDesc(a.shape[1], a.shape[0], a.shape[2], fmt, a.ctypes.data, int(t.srgb_expand))
+    return arr, keep
+
+
 class OracleScene:
     def __init__(self, scene):
         L = lib()
@@ -120,6 +143,24 @@ class OracleScene:
         self._mf, self._mt = np.ascontiguousarray(mf), np.ascontiguousarray(mt)
         self.h = L.or_scene_create(scene.n_tris, _ptr(self._pos), _ptr(self._nrm), _ptr(self._mat, _u32p),
                                    len(scene.materials), _ptr(self._mf), _ptr(self._mt, _i32p))
+        textures = list(getattr(scene, "textures", []) or [])
+        maps = np.array([[getattr(m, k, 0) for k in ("diffuse_map", "specular_map", "shininess_map", "normal_map")]
+                         for m in scene.materials] or [[0, 0, 0, 0]], np.int32)
+        if textures or maps.any():
+            descs, keep = _texdescs(textures)
+            uv = getattr(scene, "texcoords", None)
+            tg = getattr(scene, "tangents", None)
+            self._uv = None if uv is None else np.ascontiguousarray(uv, np.float32)
+            self._tg = None if tg is None else np.ascontiguousarray(tg, np.float32)
+            rc = L.or_scene_set_textures(self.h, _ptr(maps, _i32p), _ptr(self._uv) if self._uv is not None else None,
+                                         _ptr(self._tg) if self._tg is not None else None, len(textures),
+                                         ctypes.cast(descs, ctypes.c_void_p))
+            if rc != 0:
+                raise RuntimeError("or_scene_set_textures failed")
+        if getattr(scene, "sky", None) is not None:
+            descs, keep = _texdescs([scene.sky])
+            if L.or_scene_set_sky(self.h, ctypes.cast(descs, ctypes.c_void_p)) != 0:
+                raise RuntimeError("or_scene_set_sky failed")
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:

@@ -1,0 +1,134 @@
+"""GPU parity for textures and the sky against the oracle's restatement of
+Texture / SphericalMap / Material::get* / the normal map (oracle/restir_oracle.c apply_maps, sky_texel).
+
+Tolerances: G-buffer positions, normals (incl. normal-mapped), diffuse/specular/shininess from maps are
+bit-exact (same bilinear arithmetic, same FreeImage byte layout, same sRGB expansion); 1/I_M as in
+test_gpu_parity (ocml vs glibc); sky texels within 1e-5 relative (atan2f / acosf differ by an ulp
+between ocml and glibc, which moves the bilinear weights).  Frames: the frame tolerance of test_gpu_parity.
+"""
+import numpy as np
+import pytest
+from PIL import Image
+
+import oracle_lib as O
+from restir_amd import params as P
+from restir_amd import scenes
+from restir_amd.renderer import Renderer
+from test_gpu_parity import _assert_close
+from test_image_io import _rgbe_encode, _write_hdr
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_gbuffer(a, b):
+    hit = b[..., 16] > 0                                  # depth > 0: primary hit
+    assert hit.any() and (~hit).any()
+    assert np.array_equal(a[hit][:, :12], b[hit][:, :12])            # pos, normal, kd, ks
+    assert np.array_equal(a[hit][:, 12:18], b[hit][:, 12:18])        # le, shininess, depth, type
+    np.testing.assert_allclose(a[hit][:, 18], b[hit][:, 18], rtol=1e-5, atol=0)
+    np.testing.assert_allclose(a[~hit][:, 12:15], b[~hit][:, 12:15], rtol=1e-5, atol=1e-7)   # sky
+
+
+def test_textured_gbuffer_matches_oracle():
+    sc = scenes.textured_cornell()
+    W, H = 96, 72
+    prm = P.default_params(use_skybox=1)
+    g = Renderer(W, H)
+    gs = g.load_scene(sc)
+    g.produce_restir(gs, sc.camera, prm, 0)
+    o = O.OracleRenderer(W, H)
+    o.render(O.OracleScene(sc), sc.camera, prm, 0)
+    a, b = g.gbuffer(), o.gbuffer()
+    _check_gbuffer(a, b)
+    plain = Renderer(W, H)
+    plain.produce_restir(plain.load_scene(scenes.cornell_box(8)), sc.camera, P.default_params(), 0)
+    c = plain.gbuffer()
+    assert (a[..., 6:9] != c[..., 6:9]).any(-1).mean() > 0.3          # the maps are in effect
+    assert (a[..., 3:6] != c[..., 3:6]).any(-1).mean() > 0.2          # normal map
+
+
+def test_textured_frames_match_oracle():
+    sc = scenes.textured_cornell()
+    W, H = 64, 48
+    o_s = O.OracleScene(sc)
+    for prm, frames in ((P.default_params(use_skybox=1), 1),
+                        (P.c3_params(m_area=8, use_skybox=1), 3)):
+        g, o = Renderer(W, H), O.OracleRenderer(W, H)
+        gs = g.load_scene(sc)
+        for f in range(frames):
+            cam = scenes.orbit_camera(sc.camera, f, 48, 0.3)
+            _assert_close(g.produce_restir(gs, cam, prm, f).copy(), o.render(o_s, cam, prm, f), f"textured frame {f}")
+    g = Renderer(W, H)
+    gs = g.load_scene(sc)
+    prm = P.default_params(use_skybox=1)
+    o = O.OracleRenderer(W, H)
+    _assert_close(g.render_direct_mis(gs, sc.camera, prm, 0, 4).copy(), o.render_direct_mis(o_s, sc.camera, prm, 0, 4),
+                  "textured MIS")
+
+
+def test_sky_requires_a_sky_map():
+    sc = scenes.textured_cornell(sky=False)
+    g = Renderer(16, 16)
+    gs = g.load_scene(sc)
+    with pytest.raises(Exception, match="sky"):
+        g.produce_restir(gs, sc.camera, P.default_params(use_skybox=1), 0)
+    gs.set_sky(scenes.Texture(np.ones((4, 8, 3), np.float32)))
+    g.produce_restir(gs, sc.camera, P.default_params(use_skybox=1), 0)
+    gs.set_sky(None)
+    with pytest.raises(Exception, match="sky"):
+        g.produce_restir(gs, sc.camera, P.default_params(use_skybox=1), 0)
+
+
+def _write_obj(tmp, sc):
+    """The textured scene as OBJ + MTL + PNG maps (PIL) + an RLE .hdr sky; no normal map (the loader
+    derives tangents itself)."""
+    files = {1: "checker.png", 2: "rgba.png", 3: "rough.png", 5: "spec.png"}
+    for k, name in files.items():
+        d = sc.textures[k - 1].data
+        Image.fromarray(d[..., 0] if d.shape[-1] == 1 else d).save(tmp / name)
+    lines = []
+    for i, m in enumerate(sc.materials):
+        lines += [f"newmtl m{i}", f"Kd {m.kd[0]:g} {m.kd[1]:g} {m.kd[2]:g}", "Ks 0 0 0", f"Ke {m.le[0]:.9g} {m.le[1]:.9g} {m.le[2]:.9g}",
+                  f"Ns {m.shininess:.9g}", f"Pc {m.type}"]
+        for key, slot in (("map_Kd", m.diffuse_map), ("map_Ks", m.specular_map), ("map_Ns", m.shininess_map)):
+            if slot:
+                lines.append(f"{key} {files[slot]}")
+    (tmp / "scene.mtl").write_text("\n".join(lines) + "\n")
+    pos, nrm, uv = sc.positions.reshape(-1, 3), sc.normals.reshape(-1, 3), sc.texcoords.reshape(-1, 2)
+    out = ["mtllib scene.mtl"]
+    out += [f"v {p[0]:.9g} {p[1]:.9g} {p[2]:.9g}" for p in pos]
+    out += [f"vt {t[0]:.9g} {t[1]:.9g}" for t in uv]
+    out += [f"vn {n[0]:.9g} {n[1]:.9g} {n[2]:.9g}" for n in nrm]
+    cur = None
+    for t in range(sc.n_tris):
+        if sc.tri_material[t] != cur:
+            cur = sc.tri_material[t]
+            out.append(f"usemtl m{cur}")
+        i = 3 * t + 1
+        out.append(f"f {i}/{i}/{i} {i + 1}/{i + 1}/{i + 1} {i + 2}/{i + 2}/{i + 2}")
+    (tmp / "scene.obj").write_text("\n".join(out) + "\n")
+    rgbe, sky = _rgbe_encode(sc.sky.data)
+    _write_hdr(tmp / "sky.hdr", rgbe, rle=True)
+    return tmp / "scene.obj", tmp / "sky.hdr", sky
+
+
+def test_obj_textures_and_hdr_sky_end_to_end(tmp_path):
+    sc = scenes.textured_cornell()
+    for m in sc.materials:                               # constants the loader's sRGB expansion keeps
+        m.normal_map = 0
+        if not any(m.le):
+            m.kd = (1.0, 1.0, 1.0)
+        m.ks = (0.0, 0.0, 0.0)
+    obj, hdr, sky = _write_obj(tmp_path, sc)
+    ref = scenes.Scene(sc.positions, sc.normals, sc.tri_material, sc.materials, sc.camera, "ref", sc.texcoords,
+                       None, sc.textures, scenes.Texture(sky))
+    W, H = 80, 60
+    prm = P.default_params(use_skybox=1)
+    g = Renderer(W, H)
+    gs = g.load_scene(str(obj))
+    gs.load_sky(str(hdr))
+    assert gs.n_tris == sc.n_tris
+    g.produce_restir(gs, sc.camera, prm, 0)
+    o = O.OracleRenderer(W, H)
+    o.render(O.OracleScene(ref), sc.camera, prm, 0)
+    _check_gbuffer(g.gbuffer(), o.gbuffer())

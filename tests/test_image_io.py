@@ -1,0 +1,142 @@
+"""Scene-loader image decoders (rs_image_decode) -- CPU only, no device needed.
+
+The reference decodes textures with FreeImage (pg/Texture.cpp:9-57), which is not available here.  The
+decoders are pinned against PIL (an independent PNG decoder) and against numpy restatements of the
+Radiance RGBE / PFM / PNM formats written by this test: bit-exact texels.
+"""
+import os
+import struct
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from restir_amd.renderer import RestirError, decode_image
+
+
+def _rgbe_encode(img):
+    """float32 (H, W, 3) -> RGBE bytes (Ward's float2rgbe) and the floats a decoder must return."""
+    v = img.max(-1).astype(np.float64)
+    m, e = np.frexp(v)
+    scale = np.where(v > 1e-32, m * 256.0 / np.where(v > 0, v, 1), 0.0)
+    rgb = np.clip(np.floor(img * scale[..., None]), 0, 255).astype(np.uint8)
+    ex = np.where(v > 1e-32, e + 128, 0).astype(np.uint8)
+    rgbe = np.concatenate([rgb, ex[..., None]], -1)
+    f = np.where(rgbe[..., 3:4] > 0, np.ldexp(1.0, rgbe[..., 3:4].astype(np.int32) - 136), 0.0)
+    dec = (rgbe[..., :3].astype(np.float64) * f).astype(np.float32)
+    return rgbe, dec
+
+
+def _rle_channel(a):
+    out, i, n = bytearray(), 0, len(a)
+    while i < n:
+        j = i
+        while j < n and j - i < 127 and a[j] == a[i]:
+            j += 1
+        if j - i >= 3:
+            out += bytes([128 + (j - i), a[i]])
+            i = j
+            continue
+        j = i
+        while j < n and j - i < 128 and not (j + 2 < n and a[j] == a[j + 1] == a[j + 2]):
+            j += 1
+        out += bytes([j - i]) + bytes(a[i:j])
+        i = j
+    return out
+
+
+def _write_hdr(path, rgbe, rle):
+    H, W, _ = rgbe.shape
+    with open(path, "wb") as f:
+        f.write(b"#?RADIANCE\nFORMAT=32-bit_rle_rgbe\nEXPOSURE=1.0\n\n")
+        f.write(f"-Y {H} +X {W}\n".encode())
+        for y in range(H):
+            if rle:
+                f.write(bytes([2, 2, W >> 8, W & 255]))
+                for c in range(4):
+                    f.write(_rle_channel(rgbe[y, :, c].tolist()))
+            else:
+                f.write(rgbe[y].tobytes())
+
+
+@pytest.mark.parametrize("mode", ["RGB", "RGBA", "L", "LA", "P", "PT"])
+def test_png_matches_pil(tmp_path, mode):
+    rng = np.random.default_rng(3)
+    H, W = 37, 53                                 # odd sizes: row padding, every filter type
+    base = rng.integers(0, 256, size=(H, W, 4), dtype=np.uint8)
+    base[:, : W // 2] //= 16                     # smooth + noisy halves so the encoder picks mixed filters
+    if mode in ("P", "PT"):
+        im = Image.fromarray(base[..., :3]).quantize(colors=40)
+        if mode == "PT":
+            im.info["transparency"] = bytes(range(0, 240, 6))
+    else:
+        arr = {"RGB": base[..., :3], "RGBA": base, "L": base[..., 0], "LA": base[..., :2]}[mode]
+        im = Image.fromarray(arr, mode=mode)
+    p = tmp_path / f"t_{mode}.png"
+    im.save(p, optimize=True)
+    got = decode_image(p)
+    ref_im = Image.open(p)
+    if mode == "PT":
+        want = np.asarray(ref_im.convert("RGBA"))
+    elif mode == "P":
+        want = np.asarray(ref_im.convert("RGB"))
+    elif mode == "LA":                             # FreeImage loads gray+alpha as 32-bit RGBA
+        want = np.asarray(ref_im.convert("RGBA"))
+    else:
+        want = np.asarray(ref_im)
+    if want.ndim == 2:
+        want = want[:, :, None]
+    assert got.dtype == np.uint8 and got.shape == want.shape
+    assert np.array_equal(got, want)
+
+
+def test_png_unsupported_variants(tmp_path):
+    p16 = tmp_path / "d16.png"
+    Image.fromarray(np.arange(64, dtype=np.uint16).reshape(8, 8) * 900).save(p16)
+    with pytest.raises(RestirError, match="8-bit"):
+        decode_image(p16)
+    jpg = tmp_path / "t.jpg"
+    Image.fromarray(np.zeros((8, 8, 3), np.uint8)).save(jpg)
+    with pytest.raises(RestirError, match="JPEG"):
+        decode_image(jpg)
+    with pytest.raises(RestirError):
+        decode_image(tmp_path / "missing.png")
+
+
+@pytest.mark.parametrize("rle", [False, True])
+def test_radiance_hdr(tmp_path, rle):
+    rng = np.random.default_rng(9)
+    img = (rng.lognormal(0, 2, size=(13, 40, 3))).astype(np.float32)
+    img[3, 5:30] = img[3, 5]                      # long runs for the RLE path
+    img[7] = 0.0
+    rgbe, want = _rgbe_encode(img)
+    p = tmp_path / f"sky_{int(rle)}.hdr"
+    _write_hdr(p, rgbe, rle)
+    got = decode_image(p)
+    assert got.dtype == np.float32 and got.shape == (13, 40, 3)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("little,color", [(True, True), (False, True), (True, False)])
+def test_pfm(tmp_path, little, color):
+    rng = np.random.default_rng(4)
+    C = 3 if color else 1
+    img = rng.normal(size=(9, 11, C)).astype(np.float32)
+    p = tmp_path / "t.pfm"
+    with open(p, "wb") as f:
+        f.write(f"{'PF' if color else 'Pf'}\n11 9\n{-1.0 if little else 1.0}\n".encode())
+        f.write(np.ascontiguousarray(img[::-1]).astype("<f4" if little else ">f4").tobytes())   # bottom row first
+    got = decode_image(p)
+    want = img if color else np.repeat(img, 3, -1)
+    assert np.array_equal(got, want)
+
+
+def test_pnm(tmp_path):
+    rng = np.random.default_rng(5)
+    rgb = rng.integers(0, 256, size=(6, 7, 3), dtype=np.uint8)
+    gray = rng.integers(0, 256, size=(6, 7), dtype=np.uint8)
+    p6, p5 = tmp_path / "t.ppm", tmp_path / "t.pgm"
+    p6.write_bytes(b"P6\n# comment\n7 6\n255\n" + rgb.tobytes())
+    p5.write_bytes(b"P5 7 6 255\n" + gray.tobytes())
+    assert np.array_equal(decode_image(p6), rgb)
+    assert np.array_equal(decode_image(p5), gray[:, :, None])
