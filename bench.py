@@ -10,9 +10,13 @@ N=1: one GPU renders the whole frame.  N>1 (torchrun): the frame is split into N
 (strong scaling, one process per GPU); reservoir halo rows are exchanged over RCCL before each
 spatial pass and the band framebuffers are gathered to rank 0 (restir_amd/distributed.py).
 
+Frames are pipelined by the library (run-ahead lanes, up to 3 frames in flight; RESTIR_RUNAHEAD=0
+renders strictly one frame after the other); every frame is still rendered completely.
+
 Output: one JSON line (rank 0) with value = whole-job frames/s, plus mrays_per_s, roofline of the
-dominant kernel (k_gbuffer_initial, algorithmic bytes, HIP-event timed) and cpu_baseline (the oracle
-restatement on this host's cores, N=1 only).
+dominant kernel (k_gbuffer_initial, algorithmic bytes, HIP-event timed on its stream), the whole-frame
+roofline at the job's frame rate, and cpu_baseline (the oracle restatement on this host's cores, N=1
+only).
 """
 import argparse
 import json
@@ -39,6 +43,22 @@ WORKLOADS = {
 # (5 x float4 = 80 B) + reservoir write (3 x float4 = 48 B); scene/BVH reads are cache-resident
 # shared data, not per-pixel traffic.  DESIGN.md "Roofline".
 DOMINANT_BYTES_PER_PX = 80 + 48
+
+
+def frame_bytes_per_px(prm) -> int:
+    """Compulsory HBM bytes per pixel of one whole frame in this build's layout (each per-pixel record
+    read / written once per pass; neighbour and reprojected reads are the same records): initial
+    G + R write 128; temporal G cur + G prev + R cur + R prev read, R write 304; each spatial pass G + R
+    read, R write 176; framebuffer write 12 (fused into the last pass; a separate shade pass reads
+    G + R: +128).  SURVEY.md §8(d) prices the reference's unfused passes (480 B at C2)."""
+    b = 128
+    if prm.do_temporal:
+        b += 304
+    if prm.do_spatial and prm.spatial_passes > 0:
+        b += 176 * prm.spatial_passes + 12
+    else:
+        b += 128 + 12
+    return b
 
 
 def parse():
@@ -128,7 +148,8 @@ def main():
         eng = r
     else:
         from restir_amd.distributed import TiledRenderer
-        tr = TiledRenderer(W, H, rank, world, device=local, stream=stream)
+        # async gather: frame f's band framebuffers travel to rank 0 while frame f+1 renders
+        tr = TiledRenderer(W, H, rank, world, device=local, stream=stream, async_gather=True)
         gs = tr.load_scene(sc)
         render = lambda f: tr.render(gs, camera(f) if camera else sc.camera, prm, f, gather=True, timed=False)
         eng = tr
@@ -146,6 +167,10 @@ def main():
     # BVH walk kinds over a scene's first 4 frames, then the history is reset
     for f in range(4):
         step(f)
+    if world > 1:   # cost-balanced bands from 2 frames' per-row wave times (all ranks agree; resets history)
+        bands = tr.rebalance(step, n_frames=2)
+        if rank == 0:
+            print(f"bands: {bands}", file=sys.stderr)
     eng.reset_history()
     for f in range(args.warmup):
         step(f)
@@ -191,6 +216,7 @@ def main():
                 valu = pmc.get("k_gbuffer_initial_valu_per_launch")
         except Exception:
             traffic = valu = None
+    inflight = 1 + int(os.environ.get("RESTIR_RUNAHEAD", "2"))
     trav_name = None
     if world == 1:
         _, last_kind, _ = r.traversal(gs)
@@ -214,7 +240,7 @@ def main():
             "data": f"synthetic (procedural scene, BASELINE.json configs[{ {'C1': 0, 'C2': 1, 'C3': 2, 'C5': 4}[args.scene]}])",
             "config": {"workload": f"{args.scene}: {WORKLOADS[args.scene]}, {W}x{H}",
                        "width": W, "height": H, "parallelism": f"row-bands x{world}" if world > 1 else "1 GPU",
-                       "traversal": trav_name},
+                       "traversal": trav_name, "frames_in_flight": inflight},
             "mrays_per_s": round(mrays, 2),
             "rays_per_frame": rays // max(1, args.steps),
             "pass_ms": {k: round(v / args.steps, 4) for k, v in acc.items()},
@@ -225,6 +251,13 @@ def main():
             # the kernel's real limiter is instruction issue / latency, not HBM: VALU wave-instructions
             # per launch (PMC SQ_INSTS_VALU, profiles/pmc_traffic.json) over the live kernel time, against
             # 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU op (MI355X_MICROARCH.md)
+            # the whole frame (all passes) at the job's frame rate -- with frames in flight on the
+            # library's lanes the kernels overlap, so per-kernel launch durations (above) include the
+            # time they share the GPU with other frames' kernels; this is the pipeline's figure
+            "frame_roofline": {"bound": "hbm", "bytes_per_px": frame_bytes_per_px(prm), "unit": "GB/s",
+                               "achieved": round(frame_bytes_per_px(prm) * W * H / (ms_per_step * 1e-3) / 1e9, 2),
+                               "peak": HBM_PEAK_GBS,
+                               "frac": round(frame_bytes_per_px(prm) * W * H / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)},
             "valu_issue": None if not valu or k_ms <= 0 else {
                 "achieved": round(valu / (k_ms * 1e-3) / 1e9, 2), "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
                 "frac": round(valu / (k_ms * 1e-3) / 1e9 / VALU_PEAK_GIPS, 4), "valu_per_launch": valu},

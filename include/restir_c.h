@@ -199,7 +199,8 @@ int rs_render_direct_mis(rs_context* ctx, const rs_scene* scene, const rs_camera
  * are summed on the device.  Synchronises the stream; sum->*_ms are totals (divide by *n_frames).
  * Replaces reading the per-pass std::chrono members every frame (pg/simpleguidx11.h:120-127). */
 int rs_get_timing_totals(rs_context* ctx, rs_pass_times* sum, uint32_t* n_frames, int reset);
-/* Device pointer to the framebuffer (frame_data): W*H*3 floats, valid until the next render. */
+/* Device pointer to the framebuffer (frame_data): W*H*3 floats, valid until the next render (with a
+ * frame ring of 2: until the render after next). */
 int rs_get_frame_device_ptr(rs_context* ctx, const float** dptr);
 /* Forget the previous frame (frameCtr = 0): the next frame skips temporal reuse. */
 int rs_reset_history(rs_context* ctx);
@@ -220,6 +221,37 @@ int rs_context_set_traversal(rs_context* ctx, int mode);
  * settled on for `scene` (-1 while still timing; scene may be NULL). */
 int rs_context_get_traversal(const rs_context* ctx, const rs_scene* scene, int* mode, int* last_kind,
                              int* scene_choice);
+
+/* ---- candidate-split initial pass (no reference counterpart: a launch-shape choice) ------------
+ * ON: the initial pass spreads a pixel's A+B candidates over 4 waves of one 8x8-tile workgroup
+ * (fills the GPU when a rank renders a small band); OFF: one thread carries all candidates of its
+ * pixel; AUTO (default; env RESTIR_SPLIT=on|off overrides at context creation): ON when the launch
+ * has fewer than ~3 rounds of one-thread-per-pixel waves for the device.  Needs A+B <= 64 and B <= 2
+ * (OFF otherwise).  Frames are bit-identical either way. */
+#define RS_SPLIT_AUTO (-1)
+#define RS_SPLIT_OFF 0
+#define RS_SPLIT_ON 1
+int rs_context_set_initial_split(rs_context* ctx, int mode);
+/* mode: the requested mode; last: whether the last frame's initial pass ran split (0/1) */
+int rs_context_get_initial_split(const rs_context* ctx, int* mode, int* last);
+/* Frame pipelining (no reference counterpart): with depth D (0..2, default 2; env RESTIR_RUNAHEAD=D at
+ * context creation) frames rotate over D+1 internal streams, so a frame's G-buffer + initial pass
+ * (which reads nothing of earlier frames) runs while up to D earlier frames still run their later
+ * passes; only the temporal pass waits for the previous frame.  The context's stream waits for every
+ * frame, so its semantics are unchanged; a frame's framebuffer pointer (rs_tile_finish,
+ * rs_get_frame_device_ptr) stays valid for D+1 frames.  Work enqueued on the context's stream between
+ * frames (geometry updates) is waited for by the next frame.  Frames are bit-identical for every D. */
+int rs_context_set_run_ahead(rs_context* ctx, int depth);
+/* Framebuffer ring (no reference counterpart): n = 1 (default, one frame_data buffer, like
+ * pg/simpleguidx11.h:152) or 2 -- consecutive frames alternate between two buffers, so a consumer
+ * (the multi-GPU gather, an async copy) may still read frame f while frame f+1 renders. */
+int rs_context_set_frame_ring(rs_context* ctx, int n);
+/* Load-balancing record for tile sharding (no reference counterpart): while enabled, every pass
+ * kernel's waves add their lifetime (100 MHz ticks) to the image row at the top of their tile, for rows
+ * inside the context's band.  rs_get_row_costs copies the H per-row sums to `costs` (host, H floats;
+ * synchronises the stream) and optionally zeroes them. */
+int rs_context_track_row_costs(rs_context* ctx, int enable);
+int rs_get_row_costs(rs_context* ctx, float* costs, int reset);
 
 /* ---- post-frame: the producer loop's block after produceRestir -------------
  * (pg/simpleguidx11.cpp:246-333, OIDN excluded):  accumulator = mix(accumulator, frame_data,
@@ -277,6 +309,10 @@ int rs_tile_begin(rs_context* ctx, const rs_scene* scene, const rs_camera* camer
  *        2 = rows [y0, y0+halo) (send up), 3 = rows [y1-halo, y1) (send down).
  * *bytes = rows * width * 48; NULL pointer when the rows fall outside the frame. */
 int rs_tile_halo_ptr(rs_context* ctx, int which, void** dptr, size_t* bytes);
+/* The stream the frame in flight runs on (a run-ahead lane, or the context's stream at depth 0) and its
+ * lane index: a multi-GPU driver issues the frame's halo exchange and gather on it, so frames of
+ * different lanes communicate independently. */
+int rs_tile_stream(rs_context* ctx, void** stream, int* lane);
 int rs_tile_temporal(rs_context* ctx);
 int rs_tile_spatial(rs_context* ctx, int pass_index);
 int rs_tile_finish(rs_context* ctx, const float** band_rgb_dptr, rs_pass_times* times);

@@ -71,24 +71,51 @@ struct rs_scene {
     }
 };
 
-enum { EV_BEGIN, EV_INIT, EV_VIS, EV_TEMPORAL, EV_SPATIAL, EV_SHADE, EV_COUNT };
+enum { EV_BEGIN, EV_INIT, EV_VIS, EV_TEMPORAL, EV_SPATIAL, EV_SHADE, EV_DONE, EV_COUNT };
 
+// Frame pipelining ("run-ahead", depth D <= kMaxAhead): frames rotate over D+1 internal "lane"
+// streams, frame f running entirely on lane f mod (D+1), so up to D+1 consecutive frames are in flight
+// at once: one frame's G-buffer + initial pass (which reads nothing of earlier frames) overlaps the
+// previous frames' later passes, halo exchanges and gathers, and the tails of their kernels.  Only the
+// temporal pass depends on the previous frame (its final reservoirs and G-buffer): it waits for that
+// frame's completion event.  Each lane owns its framebuffer, ray-count slots and counters; the G ring
+// holds D+2 buffers (frames f-D-1..f), the reservoir ring 3D+2 (the buffers frames f-D..f-1 touch stay
+// apart from the two frame f writes).  The context's stream waits for every frame's completion, so
+// its semantics are those of a sequential renderer.  D = 0 runs everything on the context's stream.
+// Work enqueued on the context's stream between frames (geometry updates, MIS frames, sky changes)
+// makes the next frame's lane wait for it.
+constexpr int kMaxAhead = 2, kLanes = kMaxAhead + 1, kGRing = kMaxAhead + 2, kRRing = 3 * kMaxAhead + 2;
 struct rs_context {
     int device = 0, W = 0, H = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    GBuf G[2] = {};
-    GCam gcam[2] = {};
-    int gcur = 0;
-    float4* R[3] = {nullptr, nullptr, nullptr};
+    hipStream_t lane[kLanes] = {};         // frame streams (run-ahead); frame f on lane f mod (D+1)
+    int ahead = kMaxAhead;                 // run-ahead depth D (rs_context_set_run_ahead)
+    hipStream_t fs = nullptr;              // stream of the frame in flight (a lane, or `stream` when D = 0)
+    int li = 0;                            // its lane index (0 when D = 0)
+    bool join_next = true;                 // the next frame waits for the context's stream
+    GBuf G[kGRing] = {};
+    GCam gcam[kGRing] = {};
+    int gcur = 0, gprev = 0;
+    float4* R[kRRing] = {};
     int r_last = 2;
-    float* fb = nullptr;
-    Counters* d_cnt = nullptr;
+    int rhist[kMaxAhead][3];               // {ra, rb, last} of the previous frames (most recent first)
+    float* fb = nullptr;                   // the framebuffer of the frame in flight / last frame
+    float* fbs[kLanes] = {};               // per-lane framebuffers (fbs[0] allocated at create, others on demand)
+    int fb_ring = 1;
+    float* d_rowcost = nullptr;            // per-row wave time while tracking (rs_context_track_row_costs)
+    bool track_rows = false;
+    Counters* d_cnt = nullptr;             // = cnts[li]
+    Counters* cnts[kLanes] = {};
     Counters* h_cnt = nullptr;
-    uint2* d_part = nullptr;               // per-wave ray-count slots of this frame's launches
+    uint2* d_part = nullptr;               // per-wave ray-count slots of this frame's launches (= parts[pk])
     size_t part_cap = 0, part_used = 0;
+    uint2* parts[kLanes] = {};             // per-lane slot buffers
+    size_t part_caps[kLanes] = {};
+    int pk = 0;
     Counters* d_tot = nullptr;             // running totals over frames (rs_get_timing_totals)
-    ulonglong2* d_red = nullptr;           // k_reduce_counts_part partials
+    ulonglong2* d_red = nullptr;           // k_reduce_counts_part partials (= reds[li])
+    ulonglong2* reds[kLanes] = {};
     // pass timing without a per-frame host sync: every frame records into its own slot of an event
     // ring; slots are folded into the running totals lazily (when reused, or on rs_get_timing_totals)
     static constexpr int kEvRing = 64;
@@ -112,8 +139,16 @@ struct rs_context {
     bool temporal_ran = false, spatial_ran = false, shade_fused = false, ev_temporal = false;
     // traversal kind (rs_scene.h Trav): requested mode, kind of the frame in flight, tuning frame flag
     int trav_mode = RS_TRAVERSAL_AUTO;
+    hipEvent_t last_done = nullptr;        // completion event of the last finished frame
+    hipEvent_t prev_done = nullptr;        // ... of the frame before the one in flight (temporal waits)
+    hipEvent_t prev_begin = nullptr;       // start event of the last frame begun
+    hipEvent_t lane_wait[kLanes] = {};     // a lane's last frame ran on the context's stream: its done event
     int trav = TRAV_LOCKSTEP;
     bool tuning = false;
+    // candidate-split initial pass (rs_passes.h k_gbuffer_initial_split): requested mode, last frame's
+    int split_mode = RS_SPLIT_AUTO;
+    bool split = false;
+    int wave_slots = 0;                    // resident wave capacity of the device at the initial pass's budget
     // post-frame (rs_post_frame): accumulator (float3, like the reference's glm::vec3 accumulator),
     // display (float4 RGBA), per-workgroup statistic partials, accFrameCtr
     float* acc = nullptr;
@@ -141,6 +176,11 @@ static int fail(rs_context* c, int code, const std::string& msg) {
 static hipError_t enter(rs_context* c) {
     (void)hipGetLastError();
     return hipSetDevice(c->device);
+}
+// the context's stream and the run-ahead side streams
+static void sync_all(rs_context* c) {
+    hipStreamSynchronize(c->stream);
+    for (auto st : c->lane) if (st) hipStreamSynchronize(st);
 }
 
 // glm-semantics host maths for the camera (pg/camera.cpp:44-58, glm/ext/matrix_transform.inl:99-119,
@@ -227,24 +267,33 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail("hipStreamCreate failed");
         c->own_stream = true;
     }
+    for (auto& st : c->lane)
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return bail("hipStreamCreate failed");
+    for (auto& h : c->rhist) h[0] = h[1] = h[2] = -1;
     size_t n = (size_t)width * height;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kGRing; ++i) {
         float4** f[5] = {&c->G[i].g0, &c->G[i].g1, &c->G[i].g2, &c->G[i].g3, &c->G[i].g4};
         for (auto* p : f) {
             if (hipMalloc(p, n * sizeof(float4)) != hipSuccess) return bail("hipMalloc(G-buffer) failed");
             hipMemsetAsync(*p, 0, n * sizeof(float4), c->stream);
         }
     }
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < kRRing; ++i) {
         if (hipMalloc(&c->R[i], n * 3 * sizeof(float4)) != hipSuccess) return bail("hipMalloc(reservoirs) failed");
         hipMemsetAsync(c->R[i], 0, n * 3 * sizeof(float4), c->stream);
     }
-    if (hipMalloc(&c->fb, n * 3 * sizeof(float)) != hipSuccess) return bail("hipMalloc(frame) failed");
-    hipMemsetAsync(c->fb, 0, n * 3 * sizeof(float), c->stream);
-    if (hipMalloc(&c->d_cnt, sizeof(Counters)) != hipSuccess) return bail("hipMalloc(counters) failed");
+    if (hipMalloc(&c->fbs[0], n * 3 * sizeof(float)) != hipSuccess) return bail("hipMalloc(frame) failed");
+    hipMemsetAsync(c->fbs[0], 0, n * 3 * sizeof(float), c->stream);
+    c->fb = c->fbs[0];
+    for (int i = 0; i < kLanes; ++i) {
+        if (hipMalloc(&c->cnts[i], sizeof(Counters)) != hipSuccess) return bail("hipMalloc(counters) failed");
+        if (hipMalloc(&c->reds[i], kReduceBlocks * sizeof(ulonglong2)) != hipSuccess) return bail("hipMalloc(partials) failed");
+        hipMemsetAsync(c->cnts[i], 0, sizeof(Counters), c->stream);
+    }
+    c->d_cnt = c->cnts[0]; c->d_red = c->reds[0];
+    c->fs = c->stream;
     if (hipHostMalloc(&c->h_cnt, sizeof(Counters), hipHostMallocDefault) != hipSuccess) return bail("hipHostMalloc failed");
     if (hipMalloc(&c->d_tot, sizeof(Counters)) != hipSuccess) return bail("hipMalloc(totals) failed");
-    if (hipMalloc(&c->d_red, kReduceBlocks * sizeof(ulonglong2)) != hipSuccess) return bail("hipMalloc(partials) failed");
     hipMemsetAsync(c->d_tot, 0, sizeof(Counters), c->stream);
     for (auto& slot : c->evr)
         for (auto& e : slot)
@@ -257,6 +306,17 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "lockstep")) c->trav_mode = RS_TRAVERSAL_LOCKSTEP;
         else if (!std::strcmp(t, "lane")) c->trav_mode = RS_TRAVERSAL_LANE;
     }
+    if (const char* t = std::getenv("RESTIR_SPLIT")) {         // auto (default) | on | off
+        if (!std::strcmp(t, "on")) c->split_mode = RS_SPLIT_ON;
+        else if (!std::strcmp(t, "off")) c->split_mode = RS_SPLIT_OFF;
+    }
+    if (const char* t = std::getenv("RESTIR_RUNAHEAD"))        // run-ahead depth 0..kMaxAhead
+        c->ahead = std::max(0, std::min(kMaxAhead, std::atoi(t)));
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0) cus = 256;
+        c->wave_slots = cus * 4 * RS_INITIAL_WAVES;
+    }
     *out = c;
     return RS_OK;
 }
@@ -266,6 +326,59 @@ extern "C" int rs_context_set_traversal(rs_context* c, int mode) {
     if (mode != RS_TRAVERSAL_AUTO && mode != RS_TRAVERSAL_LOCKSTEP && mode != RS_TRAVERSAL_LANE)
         return fail(c, RS_E_INVALID, "rs_context_set_traversal: mode must be RS_TRAVERSAL_AUTO/LOCKSTEP/LANE");
     c->trav_mode = mode;
+    return RS_OK;
+}
+extern "C" int rs_context_set_initial_split(rs_context* c, int mode) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_context_set_initial_split: null context");
+    if (mode != RS_SPLIT_AUTO && mode != RS_SPLIT_OFF && mode != RS_SPLIT_ON)
+        return fail(c, RS_E_INVALID, "rs_context_set_initial_split: mode must be RS_SPLIT_AUTO/OFF/ON");
+    c->split_mode = mode;
+    return RS_OK;
+}
+extern "C" int rs_context_set_run_ahead(rs_context* c, int depth) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_context_set_run_ahead: null context");
+    if (c->active) return fail(c, RS_E_INVALID, "rs_context_set_run_ahead: a frame is in flight");
+    HIPCHK(c, enter(c));
+    sync_all(c);                                 // frames in flight keep the buffers of the old depth
+    if (depth < 0 || depth > kMaxAhead) return fail(c, RS_E_INVALID, "rs_context_set_run_ahead: depth must be 0..2");
+    c->ahead = depth;
+    c->join_next = true;
+    return RS_OK;
+}
+extern "C" int rs_context_set_frame_ring(rs_context* c, int n) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_context_set_frame_ring: null context");
+    if (n != 1 && n != 2) return fail(c, RS_E_INVALID, "rs_context_set_frame_ring: n must be 1 or 2");
+    if (c->active) return fail(c, RS_E_INVALID, "rs_context_set_frame_ring: a frame is in flight");
+    HIPCHK(c, enter(c));
+    c->fb_ring = n;
+    return RS_OK;
+}
+extern "C" int rs_context_track_row_costs(rs_context* c, int enable) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_context_track_row_costs: null context");
+    if (c->active) return fail(c, RS_E_INVALID, "rs_context_track_row_costs: a frame is in flight");
+    HIPCHK(c, enter(c));
+    if (enable && !c->d_rowcost) {
+        HIPCHK(c, hipMalloc(&c->d_rowcost, (size_t)c->H * sizeof(float)));
+        HIPCHK(c, hipMemsetAsync(c->d_rowcost, 0, (size_t)c->H * sizeof(float), c->stream));
+    }
+    c->track_rows = enable != 0;
+    return RS_OK;
+}
+extern "C" int rs_get_row_costs(rs_context* c, float* costs, int reset) {
+    if (!c || !costs) return fail(c, RS_E_INVALID, "rs_get_row_costs: null argument");
+    if (c->active) return fail(c, RS_E_INVALID, "rs_get_row_costs: a frame is in flight");
+    HIPCHK(c, enter(c));
+    const size_t bytes = (size_t)c->H * sizeof(float);
+    if (!c->d_rowcost) { std::memset(costs, 0, bytes); return RS_OK; }
+    HIPCHK(c, hipMemcpyAsync(costs, c->d_rowcost, bytes, hipMemcpyDeviceToHost, c->stream));
+    if (reset) HIPCHK(c, hipMemsetAsync(c->d_rowcost, 0, bytes, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RS_OK;
+}
+extern "C" int rs_context_get_initial_split(const rs_context* c, int* mode, int* last) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_context_get_initial_split: null context");
+    if (mode) *mode = c->split_mode;
+    if (last) *last = c->split ? 1 : 0;
     return RS_OK;
 }
 extern "C" int rs_context_get_traversal(const rs_context* c, const rs_scene* s, int* mode, int* last_kind,
@@ -281,22 +394,25 @@ extern "C" void rs_context_destroy(rs_context* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    for (auto st : c->lane) if (st) hipStreamSynchronize(st);
     for (auto& g : c->G) {
         float4* f[5] = {g.g0, g.g1, g.g2, g.g3, g.g4};
         for (auto* p : f) if (p) hipFree(p);
     }
     for (auto* r : c->R) if (r) hipFree(r);
-    if (c->fb) hipFree(c->fb);
-    if (c->d_cnt) hipFree(c->d_cnt);
+    for (float* f : c->fbs) if (f) hipFree(f);
+    if (c->d_rowcost) hipFree(c->d_rowcost);
+    for (auto* p : c->cnts) if (p) hipFree(p);
+    for (auto* p : c->reds) if (p) hipFree(p);
     if (c->d_tot) hipFree(c->d_tot);
-    if (c->d_red) hipFree(c->d_red);
     void* post[] = {c->acc, c->display, c->post_part, c->post_out};
     for (void* p : post) if (p) hipFree(p);
-    if (c->d_part) hipFree(c->d_part);
+    for (uint2* p : c->parts) if (p) hipFree(p);
     if (c->h_cnt) hipHostFree(c->h_cnt);
     for (auto& slot : c->evr)
         for (auto& e : slot) if (e) hipEventDestroy(e);
     for (auto& e : c->ev_gt) if (e) hipEventDestroy(e);
+    for (auto st : c->lane) if (st) hipStreamDestroy(st);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -544,6 +660,7 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
         guide[j] = (int)(std::lower_bound(cdf.begin(), cdf.begin() + ne, key) - cdf.begin());
     }
     hipStream_t st = c->stream;
+    c->join_next = true;
     if (hipStreamSynchronize(st) != hipSuccess) { err = "stream sync failed"; return -1; }   // frames in flight
     void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide, s->d_emis_tri,
                    s->d_refit_order, s->d_refit_lvl};
@@ -691,6 +808,7 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
     HIPCHK(c, enter(c));
     const size_t nf = 9 * (size_t)s->n_tris;
     if (nf == 0) return RS_OK;
+    c->join_next = true;            // the next frame's initial pass must see the new geometry
     hipStream_t st = c->stream;
     const int k = s->stage_i;
     s->stage_i ^= 1;
@@ -807,6 +925,7 @@ extern "C" int rs_scene_set_sky(rs_scene* s, const rs_texture_desc* d) {
     if (c->active) return fail(c, RS_E_INVALID, "rs_scene_set_sky: a frame is in flight");
     HIPCHK(c, enter(c));
     HIPCHK(c, hipStreamSynchronize(c->stream));        // enqueued frames may still read the texture buffer
+    c->join_next = true;
     rs_scene::HostTex t;
     std::string err;
     if (d && !prepare_texture(*d, 0, t, err)) return fail(c, RS_E_INVALID, "rs_scene_set_sky: " + err);
@@ -846,6 +965,7 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     if (!s) return;
     if (s->ctx) hipSetDevice(s->ctx->device);
     if (s->ctx && s->ctx->stream) hipStreamSynchronize(s->ctx->stream);
+    if (s->ctx) sync_all(s->ctx);
     void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
                     s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage, s->d_tex, s->d_texd, s->d_uv,
                     s->d_tan};
@@ -871,11 +991,12 @@ extern "C" int rs_scene_info(const rs_scene* s, uint32_t* n_tris, uint32_t* n_em
 static dim3 grid_rows(int W, int ya, int yb) { return dim3((W + 15) / 16, (yb - ya + 15) / 16); }
 
 // launch kernel<Trav> for the frame's traversal kind
-#define LAUNCH_TRAV(c, kernel, grid, ...)                                                      \
+#define LAUNCH_TRAV_ON(c, st, kernel, grid, ...)                                               \
     do {                                                                                       \
-        if ((c)->trav == TRAV_LANE) kernel<TRAV_LANE><<<(grid), 256, 0, (c)->stream>>>(__VA_ARGS__); \
-        else kernel<TRAV_LOCKSTEP><<<(grid), 256, 0, (c)->stream>>>(__VA_ARGS__);           \
+        if ((c)->trav == TRAV_LANE) kernel<TRAV_LANE><<<(grid), 256, 0, (st)>>>(__VA_ARGS__);   \
+        else kernel<TRAV_LOCKSTEP><<<(grid), 256, 0, (st)>>>(__VA_ARGS__);                     \
     } while (0)
+#define LAUNCH_TRAV(c, kernel, grid, ...) LAUNCH_TRAV_ON(c, (c)->fs, kernel, grid, __VA_ARGS__)
 
 // fold a finished frame's pass times (event-ring slot s) into the running totals
 static void fold_slot(rs_context* c, int s) {
@@ -919,36 +1040,55 @@ static void record_traversal_time(rs_context* c) {
 }
 static size_t grid_waves(dim3 g) { return (size_t)g.x * g.y * 4; }
 
+// the ray-count slot buffer k (of two: consecutive frames can be in flight) with >= need slots; the
+// frame's launches then take consecutive slices of it (count_slot)
+static bool use_parts(rs_context* c, int k, size_t need) {
+    c->pk = k;
+    c->part_used = 0;
+    if (need > c->part_caps[k]) {
+        sync_all(c);
+        if (c->parts[k]) hipFree(c->parts[k]);
+        c->parts[k] = nullptr; c->part_caps[k] = 0;
+        if (hipMalloc(&c->parts[k], need * sizeof(uint2)) != hipSuccess) { c->d_part = nullptr; c->part_cap = 0; return false; }
+        c->part_caps[k] = need;
+    }
+    c->d_part = c->parts[k]; c->part_cap = c->part_caps[k];
+    return true;
+}
 // ray-count slots for one launch (rs_passes.h CountSlot); capacity is reserved in rs_tile_begin
 static CountSlot count_slot(rs_context* c, dim3 grid) {
     const size_t n = grid_waves(grid);
     if (c->part_used + n > c->part_cap) {       // more launches than reserved (a pass re-run): grow, keep slots
         const size_t cap = 2 * (c->part_used + n);
         uint2* np = nullptr;
-        hipStreamSynchronize(c->stream);
+        sync_all(c);
         if (hipMalloc(&np, cap * sizeof(uint2)) == hipSuccess) {
             if (c->part_used) hipMemcpy(np, c->d_part, c->part_used * sizeof(uint2), hipMemcpyDeviceToDevice);
             hipFree(c->d_part);
-            c->d_part = np; c->part_cap = cap;
+            c->d_part = c->parts[c->pk] = np; c->part_cap = c->part_caps[c->pk] = cap;
         } else {
             c->part_used = 0;                   // out of memory: recount from slot 0 (totals undercount)
         }
     }
-    CountSlot s{c->d_part + c->part_used, &c->d_cnt->reproj_outside};
+    CountSlot s{c->d_part + c->part_used, &c->d_cnt->reproj_outside, c->track_rows ? c->d_rowcost : nullptr,
+                c->F.y0, c->F.y1};
     c->part_used += n;
     return s;
 }
 // reserve slots for every launch of a frame: initial + visibility + temporal + P spatial + shade
-static bool reserve_count_slots(rs_context* c, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
-    size_t need = grid_waves(grid_rows(c->W, gy0, gy1)) +
+static dim3 grid_split(int W, int ya, int yb) { return dim3((W + 7) / 8, (yb - ya + 7) / 8); }
+// the initial pass runs candidate-split when asked, or (AUTO) when one thread per pixel would give the
+// launch fewer than 3 rounds of the device's resident waves (a rank's band of a multi-GPU frame)
+static bool want_split(const rs_context* c, const rs_frame_params* P, int gy0, int gy1) {
+    if (P->m_area + P->m_brdf > kSplitMaxCand || P->m_brdf > kSplitMaxBrdf) return false;
+    if (c->split_mode == RS_SPLIT_ON) return true;
+    if (c->split_mode == RS_SPLIT_OFF) return false;
+    return grid_waves(grid_rows(c->W, gy0, gy1)) < (size_t)3 * c->wave_slots;
+}
+static bool reserve_count_slots(rs_context* c, int k, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
+    size_t need = grid_waves(c->split ? grid_split(c->W, gy0, gy1) : grid_rows(c->W, gy0, gy1)) +
                   grid_waves(grid_rows(c->W, y0, y1)) * (4 + (size_t)std::max(0, P->spatial_passes));
-    c->part_used = 0;
-    if (need <= c->part_cap) return true;
-    if (c->d_part) hipFree(c->d_part);
-    c->d_part = nullptr; c->part_cap = 0;
-    if (hipMalloc(&c->d_part, need * sizeof(uint2)) != hipSuccess) return false;
-    c->part_cap = need;
-    return true;
+    return use_parts(c, k, need);
 }
 
 extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* cam, const rs_frame_params* P,
@@ -979,37 +1119,98 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     F.W = c->W; F.H = c->H;
     F.y0 = tile->y0; F.y1 = tile->y1;
     F.gy0 = std::max(0, tile->y0 - tile->margin); F.gy1 = std::min(c->H, tile->y1 + tile->margin);
-    // G-buffer ping-pong (replaces gBufferLastFrame.setDataFrom, pg/simpleguidx11.cpp:480)
-    int gnew = c->gcur ^ 1;
+    // G-buffer ring (replaces gBufferLastFrame.setDataFrom, pg/simpleguidx11.cpp:480): this frame
+    // writes the slot after the current one; G[gcur] becomes the previous frame's
+    int gnew = (c->gcur + 1) % kGRing;
     make_camera(cam, c->H, c->gcam[gnew], F.inv_view);
     F.cam = c->gcam[gnew];
     F.camp = c->gcam[c->gcur];
+    // the frame's stream: lane seq mod (D+1) (run-ahead), else the context's stream
+    const int D = c->ahead;
+    c->li = D > 0 ? (int)(c->seq % (uint64_t)(D + 1)) : (c->fb_ring == 2 ? (int)(c->seq & 1) : 0);
+    // a frame that must follow work enqueued on the context's stream since the last frame (geometry
+    // updates, ...) simply runs on that stream (it is ordered after every earlier frame there); the next
+    // frame on its lane then waits for it
+    const bool on_ctx = D == 0 || c->join_next;
+    c->fs = on_ctx ? c->stream : c->lane[c->li];
+    if (!c->fbs[c->li]) {                       // a lane's framebuffer, on first use
+        const size_t bytes = (size_t)c->W * c->H * 3 * sizeof(float);
+        HIPCHK(c, hipMalloc(&c->fbs[c->li], bytes));
+        HIPCHK(c, hipMemsetAsync(c->fbs[c->li], 0, bytes, c->stream));
+        c->join_next = true;
+    }
+    c->fb = c->fbs[c->li];
+    c->d_cnt = c->cnts[c->li]; c->d_red = c->reds[c->li];
+    // reservoir ring: `last` = the previous frame's final buffer (reservoirsLastFrame, a pointer swap,
+    // :477); this frame writes two buffers none of the D frames before it touches (they may still run)
     c->last = c->r_last;
-    c->ra = (c->last + 1) % 3; c->rb = (c->last + 2) % 3; c->rcur = c->ra;
+    {
+        auto used = [&](int i) {
+            if (i == c->last) return true;
+            for (int g = 0; g < D; ++g)
+                if (i == c->rhist[g][0] || i == c->rhist[g][1] || i == c->rhist[g][2]) return true;
+            return false;
+        };
+        c->ra = 0;
+        while (used(c->ra)) ++c->ra;
+        c->rb = c->ra + 1;
+        while (used(c->rb)) ++c->rb;            // < kRRing: D frames touch <= 3D buffers, `last` among them
+        for (int g = kMaxAhead - 1; g > 0; --g)
+            for (int j = 0; j < 3; ++j) c->rhist[g][j] = c->rhist[g - 1][j];
+        c->rhist[0][0] = c->ra; c->rhist[0][1] = c->rb; c->rhist[0][2] = c->last;
+    }
+    c->rcur = c->ra;
     const bool temporal = P->do_temporal && c->frames > 0;
     const bool spatial = P->do_spatial && P->spatial_passes > 0;
     c->shade_fused = !P->do_visibility_pass && !temporal && !spatial;
     c->temporal_ran = c->spatial_ran = c->ev_temporal = false;
     const DevScene S = s->dev();
-    if (!reserve_count_slots(c, P, F.gy0, F.gy1, F.y0, F.y1)) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
-    HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->stream));
+    c->split = want_split(c, P, F.gy0, F.gy1);
+    if (!reserve_count_slots(c, c->li, P, F.gy0, F.gy1, F.y0, F.y1)) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
+    if (c->fs != c->stream && c->lane_wait[c->li]) {   // this lane's previous frame ran on the context's stream
+        HIPCHK(c, hipStreamWaitEvent(c->fs, c->lane_wait[c->li], 0));
+    }
+    c->lane_wait[c->li] = nullptr;
+    // frames start in order (the previous frame has started -- so every frame up to f-D-1 has finished:
+    // the one on this lane by stream order, earlier ones by induction): frames f-D..f-1 are the only
+    // ones that can still run beside this frame
+    if (c->fs != c->stream && c->prev_begin) HIPCHK(c, hipStreamWaitEvent(c->fs, c->prev_begin, 0));
+    c->join_next = false;
+    HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->fs));
     c->slot = (int)(c->seq++ % rs_context::kEvRing);
     fold_slot(c, c->slot);                      // the slot's previous frame (kEvRing frames ago)
     for (int i = 0; i < EV_COUNT; ++i) c->ev[i] = c->evr[c->slot][i];
-    HIPCHK(c, hipEventRecord(c->ev[EV_BEGIN], c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[EV_BEGIN], c->fs));
+    c->prev_begin = c->ev[EV_BEGIN];
     pick_traversal(c, s);
     const dim3 gg = grid_rows(c->W, F.gy0, F.gy1), gb = grid_rows(c->W, F.y0, F.y1);
-    LAUNCH_TRAV(c, k_gbuffer_initial, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
-                count_slot(c, gg));
+    if (c->split) {
+        const dim3 gs = grid_split(c->W, F.gy0, F.gy1);
+        LAUNCH_TRAV(c, k_gbuffer_initial_split, gs, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
+                    c->shade_fused ? 1 : 0, count_slot(c, gs));
+    } else {
+        LAUNCH_TRAV(c, k_gbuffer_initial, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
+                    count_slot(c, gg));
+    }
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->ev[EV_INIT], c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[EV_INIT], c->fs));
     if (P->do_visibility_pass) {
         LAUNCH_TRAV(c, k_visibility, gb, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
     }
-    HIPCHK(c, hipEventRecord(c->ev[EV_VIS], c->stream));
-    c->gcur = gnew;       // G[gcur] = this frame, G[gcur^1] = previous frame
+    HIPCHK(c, hipEventRecord(c->ev[EV_VIS], c->fs));
+    c->gprev = c->gcur;
+    c->gcur = gnew;       // G[gcur] = this frame, G[gprev] = previous frame
+    c->prev_done = c->last_done;
     c->active = true;
+    return RS_OK;
+}
+
+extern "C" int rs_tile_stream(rs_context* c, void** stream, int* lane) {
+    if (!c || !stream) return fail(c, RS_E_INVALID, "rs_tile_stream: null argument");
+    if (!c->active) return fail(c, RS_E_INVALID, "rs_tile_stream: no frame in flight");
+    *stream = (void*)c->fs;
+    if (lane) *lane = c->li;
     return RS_OK;
 }
 
@@ -1036,14 +1237,16 @@ extern "C" int rs_tile_temporal(rs_context* c) {
     if (c->P.do_temporal && c->frames > 0 && !c->temporal_ran) {
         const DevScene S = c->scene->dev();
         const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
-        LAUNCH_TRAV(c, k_temporal, gb, S, c->F, c->G[c->gcur], c->G[c->gcur ^ 1], ResBuf{c->R[c->rcur]},
+        // the previous frame's final reservoirs and G-buffer (another lane may still be finishing it)
+        if (c->prev_done && c->fs != c->stream) HIPCHK(c, hipStreamWaitEvent(c->fs, c->prev_done, 0));
+        LAUNCH_TRAV(c, k_temporal, gb, S, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]},
                     ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
         c->rcur = c->rb;
         c->temporal_ran = true;
     }
     if (!c->ev_temporal) {
-        HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->stream));
+        HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->fs));
         c->ev_temporal = true;
     }
     return RS_OK;
@@ -1058,7 +1261,7 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
         if (rc) return rc;
     }
     if (!c->ev_temporal) {
-        HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->stream));
+        HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->fs));
         c->ev_temporal = true;
     }
     const DevScene S = c->scene->dev();
@@ -1071,7 +1274,7 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
     c->rcur = dst;
     if (fuse) c->shade_fused = true;
     c->spatial_ran = true;
-    HIPCHK(c, hipEventRecord(c->ev[EV_SPATIAL], c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[EV_SPATIAL], c->fs));
     return RS_OK;
 }
 
@@ -1083,29 +1286,33 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
         if (rc) return rc;
     }
     if (!c->ev_temporal) {
-        HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->stream));
+        HIPCHK(c, hipEventRecord(c->ev[EV_TEMPORAL], c->fs));
         c->ev_temporal = true;
     }
-    if (!c->spatial_ran) HIPCHK(c, hipEventRecord(c->ev[EV_SPATIAL], c->stream));
+    if (!c->spatial_ran) HIPCHK(c, hipEventRecord(c->ev[EV_SPATIAL], c->fs));
     if (!c->shade_fused) {
         const DevScene S = c->scene->dev();
         const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
         LAUNCH_TRAV(c, k_shade, gb, S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]}, c->fb, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
     }
-    HIPCHK(c, hipEventRecord(c->ev[EV_SHADE], c->stream));
+    HIPCHK(c, hipEventRecord(c->ev[EV_SHADE], c->fs));
     c->ev_pending[c->slot] = true;
-    k_reduce_counts_part<<<kReduceBlocks, 1024, 0, c->stream>>>(c->d_part, c->part_used, c->d_red);
-    k_reduce_counts<<<1, kReduceBlocks, 0, c->stream>>>(c->d_red, c->d_cnt, c->d_tot);
+    k_reduce_counts_part<<<kReduceBlocks, 1024, 0, c->fs>>>(c->d_part, c->part_used, c->d_red);
+    k_reduce_counts<<<1, kReduceBlocks, 0, c->fs>>>(c->d_red, c->d_cnt, c->d_tot);
     HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev[EV_DONE], c->fs));
+    c->last_done = c->ev[EV_DONE];
+    if (c->fs == c->stream && c->ahead > 0) c->lane_wait[c->li] = c->ev[EV_DONE];
+    if (c->fs != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev[EV_DONE], 0));   // sequential semantics
     record_traversal_time(c);
     c->r_last = c->rcur;   // reservoirsLastFrame = final buffer (pointer swap, :477)
     c->frames++;
     c->active = false;
     if (band_rgb) *band_rgb = c->fb + 3 * (size_t)c->F.y0 * c->W;
     if (t) {
-        HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->d_cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->d_cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->fs));
+        HIPCHK(c, hipStreamSynchronize(c->fs));
         float a = 0, b = 0, d = 0, e = 0, f = 0, tot = 0;
         hipEventElapsedTime(&a, c->ev[EV_BEGIN], c->ev[EV_INIT]);
         hipEventElapsedTime(&b, c->ev[EV_INIT], c->ev[EV_VIS]);
@@ -1182,13 +1389,11 @@ extern "C" int rs_render_direct_mis(rs_context* c, const rs_scene* s, const rs_c
     F.cam = gc; F.camp = gc;
     const DevScene S = s->dev();
     const dim3 g = grid_rows(c->W, 0, c->H);
-    c->part_used = 0;
-    if (c->part_cap < grid_waves(g)) {
-        if (c->d_part) HIPCHK(c, hipFree(c->d_part));
-        c->d_part = nullptr; c->part_cap = 0;
-        HIPCHK(c, hipMalloc(&c->d_part, grid_waves(g) * sizeof(uint2)));
-        c->part_cap = grid_waves(g);
-    }
+    c->fs = c->stream; c->li = 0;                 // the context's stream (after every frame enqueued so far)
+    c->d_cnt = c->cnts[0]; c->d_red = c->reds[0];
+    sync_all(c);                                  // lane 0's slots may still be in use
+    if (!use_parts(c, 0, grid_waves(g))) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
+    c->join_next = true;
     HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->stream));
     hipEvent_t e0 = c->ev_gt[0], e1 = c->ev_gt[1];
     HIPCHK(c, hipEventRecord(e0, c->stream));
@@ -1240,7 +1445,7 @@ extern "C" int rs_dump_gbuffer(rs_context* c, int prev, float* out) {
     if (!c || !out) return fail(c, RS_E_INVALID, "rs_dump_gbuffer: null argument");
     HIPCHK(c, enter(c));
     size_t n = (size_t)c->W * c->H;
-    const GBuf& g = c->G[prev ? (c->gcur ^ 1) : c->gcur];
+    const GBuf& g = c->G[prev ? c->gprev : c->gcur];
     std::vector<float4> a(n), b(n), d(n), e(n), f(n);
     HIPCHK(c, hipMemcpyAsync(a.data(), g.g0, n * 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(b.data(), g.g1, n * 16, hipMemcpyDeviceToHost, c->stream));

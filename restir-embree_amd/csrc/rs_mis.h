@@ -128,6 +128,7 @@ template <int T>
 __global__ void __launch_bounds__(256) k_direct_mis(DevScene S, FrameConst F, int spp, float* fb, CountSlot C) {
     int x, y;
     const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const uint64_t t0 = wave_clock();
     const uint32_t pix = (uint32_t)y * (uint32_t)F.W + (uint32_t)x;
     uint32_t rays = in ? 1u : 0u;
     vec3 dc = mk((float)x - (float)F.W / 2.0f, (float)F.H / 2.0f - (float)y, -F.cam.focal);
@@ -157,7 +158,7 @@ __global__ void __launch_bounds__(256) k_direct_mis(DevScene S, FrameConst F, in
     if (surf) px = dvs(acc, (float)spp);
     px = sanitize(px);
     if (in) store_rgb(fb, pix, px);
-    count_rays(C, rays, in ? 1u : 0u);
+    count_rays(C, rays, in ? 1u : 0u, t0, y);
 }
 
 }  // namespace rs

@@ -58,16 +58,27 @@ struct Counters { unsigned long long rays, primary, reproj_outside; };   // per-
 struct CountSlot {
     uint2* part;                         // gridDim.x * gridDim.y * 4 entries (4 waves per workgroup)
     unsigned long long* outside;         // Counters::reproj_outside (rare: tile-edge reprojections)
+    float* row_cost;                     // per-image-row wave time (rs_context_track_row_costs), or null
+    int y0, y1;                          // rows whose cost is recorded (the rank's band)
 };
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-__device__ __forceinline__ void count_rays(CountSlot C, uint32_t rays, uint32_t primary) {
+// constant-rate (100 MHz) clock at a wave's start, for the optional per-row cost record
+__device__ __forceinline__ uint64_t wave_clock() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void count_rays(CountSlot C, uint32_t rays, uint32_t primary, uint64_t t0, int y) {
     uint32_t r = wave_sum(rays), p = wave_sum(primary);
     if ((threadIdx.x & 63) == 0)
         C.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)] = make_uint2(r, p);
+    // load-balancing record (TiledRenderer.rebalance): the wave's lifetime, charged to its top row.
+    // Row-spread same-address atomics, only while tracking is on (calibration frames).
+    if (C.row_cost) {
+        const int yt = __builtin_amdgcn_readfirstlane(y);
+        if ((threadIdx.x & 63) == 0 && yt >= C.y0 && yt < C.y1)
+            atomicAdd(C.row_cost + yt, (float)(wave_clock() - t0));
+    }
 }
 
 // sum n slot pairs into the frame totals (and the context's running totals): kReduceBlocks
@@ -96,7 +107,7 @@ __global__ void __launch_bounds__(kReduceBlocks) k_reduce_counts(const ulonglong
     block_sum2(r, p);
     if (threadIdx.x == 0) {
         out->rays = r; out->primary = p;
-        tot->rays += r; tot->primary += p;
+        atomicAdd(&tot->rays, r); atomicAdd(&tot->primary, p);   // frames of several lanes may finish together
     }
 }
 
@@ -297,19 +308,18 @@ __device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameCons
 // in load() keeps LICM from hoisting the reads back out of the candidate loop).  256 threads x 80 B =
 // 20 KB per workgroup.
 struct FrameSlot {
-    float4* base;   // __shared__ float4[5 * 256]
+    float4* base;   // __shared__ float4[5 * n] (+ n more for the split kernel's (pos, alive))
+    int t, n;       // this thread's entry, entries per component (compile-time at every use)
     __device__ __forceinline__ void store(const ShadeFrame& s) const {
-        const int t = threadIdx.x;
         base[t] = f4(s.nrm, s.pf);
-        base[256 + t] = f4(s.wr, s.omp);
-        base[512 + t] = f4(s.kd_pi, s.shin);
-        base[768 + t] = f4(s.ks_im, s.a);
-        base[1024 + t] = make_float4(s.maxD, s.maxS, __int_as_float(s.type), 0.0f);
+        base[n + t] = f4(s.wr, s.omp);
+        base[2 * n + t] = f4(s.kd_pi, s.shin);
+        base[3 * n + t] = f4(s.ks_im, s.a);
+        base[4 * n + t] = make_float4(s.maxD, s.maxS, __int_as_float(s.type), 0.0f);
     }
     __device__ __forceinline__ ShadeFrame load() const {
         asm volatile("" ::: "memory");
-        const int t = threadIdx.x;
-        const float4 a = base[t], b = base[256 + t], c = base[512 + t], d = base[768 + t], e = base[1024 + t];
+        const float4 a = base[t], b = base[n + t], c = base[2 * n + t], d = base[3 * n + t], e = base[4 * n + t];
         ShadeFrame s;
         s.nrm = xyz(a); s.pf = a.w; s.wr = xyz(b); s.omp = b.w; s.kd_pi = xyz(c); s.shin = c.w;
         s.ks_im = xyz(d); s.a = d.w; s.maxD = e.x; s.maxS = e.y; s.type = __float_as_int(e.z);
@@ -405,12 +415,13 @@ template <int T>
 __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G,
                                                                             ResBuf Rw, float* fb, int fuse_shade,
                                                                             CountSlot C) {
+    const uint64_t t0 = wave_clock();
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.gy0, F.gy1, F.W, x, y);
     const size_t p = (size_t)y * F.W + x;
     __shared__ float4 frame_lds[5 * 256];
-    const FrameSlot fs{frame_lds};
+    const FrameSlot fs{frame_lds, (int)threadIdx.x, 256};
     GElem g = gbuffer_fill<T>(S, F, x, y, in);
     if (in) G.store(p, g);
     fs.store(make_frame(g, F.cam.pos));
@@ -421,12 +432,157 @@ __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevSc
         Rw.store(p, r);
         if (fuse_shade) store_rgb(fb, p, shade_px(r, f, g.le));
     }
-    count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u);
+    count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u, t0, y);
 }
+// ---------------------------------------------------------------- candidate-split initial pass
+// The same G-buffer + initialRenderPass with the candidates of a pixel spread over kSplit waves: a
+// workgroup is ONE 8x8 tile, wave g evaluates candidate group g of its 64 pixels.  A pixel's
+// candidates are independent until the reservoir stream (every candidate owns its RNG slots, and
+// the shadow ray / p-hat / w of a candidate do not depend on the others), so the groups only
+// exchange each candidate's weight w_c through LDS; wave 0 then runs the reference's sequential
+// addSample stream over w_0..w_{A+B-1} (the same float additions in the same order, the same U per
+// candidate) and re-draws the selected area sample.  Results are bit-identical to k_gbuffer_initial.
+// Why: a one-thread-per-pixel launch over a small band (a rank's 1/8 of 1080p: ~4k waves for 5k wave
+// slots) runs as ONE round whose time is the slowest tile's; 4x the waves with 1/4 the work each
+// fill the chip and average the tiles out.
+// A selected candidate always has w > 0, hence p-hat > 0, hence an unoccluded f: its f is the
+// evaluate_f_pre L of the re-drawn sample, no shadow ray needed.  BRDF candidates cannot be re-drawn
+// without their closest-hit ray, so their sample and f go through LDS too.
+constexpr int kSplit = 4;                 // waves (candidate groups) per 8x8 tile
+constexpr int kSplitMaxCand = 64;         // A + B the split kernel keeps in LDS
+constexpr int kSplitMaxBrdf = 2;          // B the split kernel keeps in LDS
+struct SplitLds {
+    float4 frame[6 * 64];                 // FrameSlot (5 x 64) + (pos, alive) per pixel
+    float w[kSplitMaxCand * 64];          // w_c of candidate c, pixel lane
+    float4 brdf[kSplitMaxBrdf * 3 * 64];  // BRDF candidate i: (p, f.x) (n, f.y) (li, f.z)
+};
+// candidate range [lo, hi) of group g over the combined list (area 0..A-1, then BRDF A..A+B-1)
+__device__ __forceinline__ void split_range(int n, int g, int& lo, int& hi) {
+    lo = (g * n) / kSplit; hi = ((g + 1) * n) / kSplit;
+}
+
+template <int T>
+__global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial_split(DevScene S, FrameConst F, GBuf G,
+                                                                                  ResBuf Rw, float* fb, int fuse_shade,
+                                                                                  CountSlot C) {
+    const uint64_t t0 = wave_clock();
+    __shared__ SplitLds L;
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    int x = blockIdx.x * 8 + (lane & 7), y = F.gy0 + blockIdx.y * 8 + (lane >> 3);
+    const bool in = x < F.W && y < F.gy1;
+    x = x < F.W ? x : F.W - 1;
+    y = y < F.gy1 ? y : F.gy1 - 1;
+    const size_t p = (size_t)y * F.W + x;
+    const bool ris = in && y >= F.y0 && y < F.y1;
+    const FrameSlot fs{L.frame, lane, 64};
+    uint32_t rays = 0;
+    vec3 le = mk(0, 0, 0);
+    if (g == 0) {                                                       // wave-uniform
+        GElem gel = gbuffer_fill<T>(S, F, x, y, in);
+        if (in) G.store(p, gel);
+        fs.store(make_frame(gel, F.cam.pos));
+        const bool alive = ris && !any_pos(gel.le) && S.n_emis > 0;    // :238-244
+        L.frame[5 * 64 + lane] = f4(gel.pos, alive ? 1.0f : 0.0f);
+        le = gel.le;
+    }
+    __syncthreads();
+    const float4 pa = L.frame[5 * 64 + lane];
+    const vec3 pos = xyz(pa);
+    const bool alive = pa.w != 0.0f;
+    const int A = F.m_area, B = F.m_brdf, n = A + B;
+    const bool tv = !F.do_vis_pass;
+    int lo, hi;
+    split_range(n, g, lo, hi);
+    if (__ballot(alive) != 0) {                                         // wave-uniform
+        Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, (uint32_t)p);
+        const int ahi = hi < A ? hi : A;
+        for (int c0 = lo; c0 < ahi; c0 += RS_RIS_BATCH) {               // area candidates (:246-266)
+            FPre pre[RS_RIS_BATCH];
+            float Wc[RS_RIS_BATCH], mis[RS_RIS_BATCH];
+            bool act[RS_RIS_BATCH], occ[RS_RIS_BATCH];
+            vec3 dir[RS_RIS_BATCH];
+            float tf[RS_RIS_BATCH];
+            const ShadeFrame sf = fs.load();
+#pragma unroll
+            for (int k = 0; k < RS_RIS_BATCH; ++k) {
+                const bool inb = c0 + k < ahi;
+                rng.n = cand_slot(c0 + k);
+                Sample s = area_sample(S, F, pos, sf, rng, Wc[k], mis[k]);
+                pre[k] = evaluate_f_pre(F, s, pos, false, sf, tv, alive && inb);
+                act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
+                rays += act[k] ? 1u : 0u;
+            }
+            if (tv) trace_any_multi<T, RS_RIS_BATCH>(S, act, pos, dir, FLT_MIN + F.tnear_off, tf, occ);
+#pragma unroll
+            for (int k = 0; k < RS_RIS_BATCH; ++k) {
+                if (c0 + k < ahi) {
+                    const float ph = length(evaluate_f_post(pre[k], occ[k]));
+                    L.w[(c0 + k) * 64 + lane] = B > 0 ? mis[k] * ph * Wc[k] : (1.0f / (float)A) * ph * Wc[k];
+                }
+            }
+        }
+        for (int c = lo > A ? lo : A; c < hi; ++c) {                     // BRDF candidates (:268-286)
+            float Wc, mis;
+            rng.n = cand_slot(c);
+            const ShadeFrame sf = fs.load();
+            Sample s = brdf_sample<T>(S, F, pos, sf, alive, rng, Wc, mis, rays);
+            const vec3 f = evaluate_f<T>(S, F, s, pos, false, sf, tv, alive, rays);
+            L.w[c * 64 + lane] = A > 0 ? mis * length(f) * Wc : (1.0f / (float)B) * length(f) * Wc;
+            float4* q = L.brdf + (c - A) * 3 * 64;
+            q[lane] = f4(s.p, f.x); q[64 + lane] = f4(s.n, f.y); q[128 + lane] = f4(s.li, f.z);
+        }
+    }
+    __syncthreads();
+    if (g != 0) { count_rays(C, rays, 0, t0, y); return; }
+    // wave 0: the reservoir stream in candidate order (Reservoir::addSample, pg/Reservoir.h:33-47)
+    Res r = res_empty();
+    vec3 f_sel = mk(0, 0, 0);
+    float best_phat = 0.0f;
+    if (__ballot(alive) != 0) {
+        Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, (uint32_t)p);
+        int sel = -1;
+        for (int c = 0; c < A; ++c) {
+            rng.n = cand_slot(c) + 3u;
+            if (alive && res_add_w(r, L.w[c * 64 + lane], 1, rng)) sel = c;
+        }
+        if (sel >= 0) {                                                 // re-draw the selected area sample
+            float Wc, mis;
+            rng.n = cand_slot(sel);
+            const ShadeFrame sf = fs.load();
+            Sample s = area_sample(S, F, pos, sf, rng, Wc, mis);
+            f_sel = evaluate_f_pre(F, s, pos, false, sf, tv, true).L;
+            best_phat = length(f_sel);
+            r.p = s.p; r.n = s.n; r.li = s.li;
+        }
+        for (int c = A; c < n; ++c) {
+            rng.n = cand_slot(c) + 3u;
+            if (alive && res_add_w(r, L.w[c * 64 + lane], 1, rng)) {
+                const float4* q = L.brdf + (c - A) * 3 * 64;
+                const float4 a = q[lane], b = q[64 + lane], d = q[128 + lane];
+                r.p = xyz(a); r.n = xyz(b); r.li = xyz(d);
+                f_sel = mk(a.w, b.w, d.w);
+                best_phat = length(f_sel);
+            }
+        }
+    }
+    if (!alive) { f_sel = mk(0, 0, 0); r = res_empty(); }
+    else {
+        const float ph = smp_valid(smp_of(r)) ? best_phat : 0.0f;
+        r.W = ph > 0.0f ? 1.0f / ph * r.wsum : 0.0f;
+        res_cap(r, F.cap);
+    }
+    if (ris) {
+        Rw.store(p, r);
+        if (fuse_shade) store_rgb(fb, p, shade_px(r, f_sel, le));
+    }
+    count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u, t0, y);
+}
+
 // visibilityPass (pg/ReSTIRIntegrator.cpp:302-312).  Invalid samples always carry W == 0 already,
 // so their (meaningless) ray is not traced.
 template <int T>
 __global__ void __launch_bounds__(256) k_visibility(DevScene S, FrameConst F, GBuf G, ResBuf R, CountSlot C) {
+    const uint64_t t0 = wave_clock();
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
@@ -434,7 +590,7 @@ __global__ void __launch_bounds__(256) k_visibility(DevScene S, FrameConst F, GB
     Res r = R.load(p);
     const bool need = in && smp_valid(smp_of(r));
     if (occluded<T>(S, F, need, G.pos(p), r.p, rays) && need) R.r[3 * p + 1].w = 0.0f;
-    count_rays(C, rays, 0);
+    count_rays(C, rays, 0, t0, y);
 }
 
 // reprojectBackward / reprojectForward (pg/ReSTIRIntegrator.cpp:544-587)
@@ -459,6 +615,7 @@ __device__ __forceinline__ bool reproject(const GCam& c, vec3 ws, int W, int H, 
 template <int T>
 __global__ void __launch_bounds__(256) k_temporal(DevScene S, FrameConst F, GBuf G, GBuf Gp, ResBuf Rr, ResBuf Rl,
                                                   ResBuf Rw, CountSlot C) {
+    const uint64_t t0 = wave_clock();
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
@@ -513,7 +670,7 @@ __global__ void __launch_bounds__(256) k_temporal(DevScene S, FrameConst F, GBuf
         }
     }
     if (in) Rw.store(p, out);
-    count_rays(C, rays, 0);
+    count_rays(C, rays, 0, t0, y);
 }
 
 // Sampling::sampleDiskUniform (pg/Sampling.cpp:78-87) -> glm::vec<2,int> (truncation), clamped to
@@ -552,6 +709,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
                                                                    ResBuf Rw, int pass_idx, int fuse_shade, float* fb,
                                                                    CountSlot C) {
     __shared__ uint32_t nbr[kNbrCache * 256];
+    const uint64_t t0 = wave_clock();
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
@@ -724,12 +882,13 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
             if (fuse_shade) store_rgb(fb, p, shade_px(res, f_sel, th.le));
         }
     }
-    count_rays(C, rays, 0);
+    count_rays(C, rays, 0, t0, y);
 }
 
 // shade loop (pg/simpleguidx11.cpp:447-472)
 template <int T>
 __global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G, ResBuf Rr, float* fb, CountSlot C) {
+    const uint64_t t0 = wave_clock();
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
@@ -738,7 +897,7 @@ __global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G,
     GElem g = G.load(p);
     vec3 f = evaluate_f<T>(S, F, smp_of(r), F.cam.pos, g, true, in && r.wsum > 0.0f, rays);
     if (in) store_rgb(fb, p, shade_px(r, f, g.le));
-    count_rays(C, rays, 0);
+    count_rays(C, rays, 0, t0, y);
 }
 
 }  // namespace rs

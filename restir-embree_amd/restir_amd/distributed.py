@@ -14,7 +14,18 @@ full scene replica (the GPU LBVH build is deterministic, so the trees are identi
                               pg/Sampling.cpp:78-87 + truncation pg/ReSTIRIntegrator.cpp:338)
                rs_tile_spatial(p)
            rs_tile_finish  shade -> band framebuffer
-  gather:  band framebuffers (12 B/px) -> rank 0 (each peer sends over its own xGMI link)
+  gather:  band framebuffers (12 B/px) -> rank 0 (each peer sends over its own xGMI link): one
+           batched point-to-point group straight into rank 0's full-frame buffer (no staging copy);
+           with async_gather the next frames render while it is in flight
+
+Frames in flight: the library runs consecutive frames on rotating "lane" streams (run-ahead,
+rs_context_set_run_ahead); each frame's halo exchange and gather are issued on its lane's stream
+through that lane's own process group, so a frame's communication overlaps other frames' compute.
+
+Load balance: bands start equal; ``rebalance`` moves the boundaries so every rank's measured cost
+(per-row wave time recorded by the pass kernels, rs_context_track_row_costs) is equal -- the rows of a
+Cornell box's ceiling (cheap emissive pixels) and floor (every light visible) differ ~2x in cost.
+Band placement never changes the frame (tests), only which GPU computes which rows.
 
 The per-pixel counter RNG is keyed by the full-frame pixel index, so the gathered frame is bit-identical
 to a single-GPU frame (tests/test_distributed.py, tests/test_gpu_tiles.py).  Temporal reprojection
@@ -52,28 +63,59 @@ class GpuTileBackend:
 
     def __init__(self, renderer):
         self.r = renderer
+        self._views = {}
+        self._streams = {}
+        self._lane_stream = None
 
     def _sync_if_foreign_stream(self):
-        """Tensor views are consumed on torch's current stream; if the context renders on a stream of
-        its own, wait for it (the bench creates contexts on torch's stream, so this is a no-op there)."""
+        """Tensor views are consumed on torch's current stream; unless that is the frame's own stream
+        (TiledRenderer runs each frame's communication on it) or the context's, wait for the context."""
         import torch
-        if self.r.stream is None or self.r.stream != torch.cuda.current_stream().cuda_stream:
+        cur = torch.cuda.current_stream().cuda_stream
+        if self.r.stream is None or cur not in (self.r.stream, self._lane_stream):
             self.r.synchronize()
+
+    def frame_stream(self):
+        """(torch stream of the frame in flight, its lane) -- the frame's run-ahead lane (rs_tile_stream)."""
+        import torch
+        ptr, lane = self.r.tile_stream()
+        st = self._streams.get(ptr)
+        if st is None:
+            st = self._streams[ptr] = torch.cuda.ExternalStream(ptr)
+        self._lane_stream = ptr
+        return st, lane
+
+    def _view(self, ptr, nbytes, typestr="|u1", itemsize=1):
+        """Cached zero-copy tensor over device memory (the buffers live as long as the context)."""
+        import torch
+        key = (ptr, nbytes, typestr)
+        t = self._views.get(key)
+        if t is None:
+            t = self._views[key] = torch.as_tensor(_CudaBuf(ptr, nbytes, typestr, itemsize), device="cuda")
+        return t
 
     def load_scene(self, scene):
         return self.r.load_scene(scene)
+
+    def set_frame_ring(self, n):
+        self.r.set_frame_ring(n)
+
+    def track_row_costs(self, enable=True):
+        self.r.track_row_costs(enable)
+
+    def row_costs(self, reset=True):
+        return self.r.row_costs(reset)
 
     def begin(self, scene, camera, params, frame, y0, y1, margin, halo):
         self.y0, self.y1 = y0, y1
         self.r.tile_begin(scene, camera, params, frame, y0, y1, margin, halo)
 
     def halo_tensor(self, which: int):
-        import torch
         self._sync_if_foreign_stream()
         ptr, n = self.r.tile_halo_ptr(which)
         if not ptr:
             return None
-        return torch.as_tensor(_CudaBuf(ptr, n), device="cuda")
+        return self._view(ptr, n)
 
     def temporal(self):
         self.r.tile_temporal()
@@ -82,11 +124,10 @@ class GpuTileBackend:
         self.r.tile_spatial(p)
 
     def finish(self, timed=False):
-        import torch
         ptr = self.r.tile_finish(timed)
         self._sync_if_foreign_stream()
         n = (self.y1 - self.y0) * self.r.W * 3
-        return torch.as_tensor(_CudaBuf(ptr, n * 4, "<f4", 4), device="cuda")
+        return self._view(ptr, n * 4, "<f4", 4)
 
     @property
     def last_times(self):
@@ -99,18 +140,76 @@ class GpuTileBackend:
         self.r.reset_history()
 
 
+def _torch_stream(st):
+    import torch
+    return torch.cuda.stream(st)
+
+
+def balanced_bands(costs, world: int, min_rows: int = 1):
+    """Contiguous row bands [(y0, y1)] * world with (as nearly as rows allow) equal summed cost.
+    Deterministic (every rank computes the same split from the same all-reduced costs); every band
+    keeps >= min_rows rows (the spatial halo must fit inside a neighbour's band)."""
+    c = np.asarray(costs, np.float64)
+    H = c.shape[0]
+    if world * min_rows > H:
+        raise ValueError(f"{world} bands of >= {min_rows} rows do not fit in {H} rows")
+    c = np.where(np.isfinite(c) & (c > 0), c, 0.0)
+    if c.sum() <= 0:
+        return [band_rows(H, r, world) for r in range(world)]
+    c = c + c.sum() * 1e-6 / H                      # no zero-cost plateaus: boundaries stay put
+    cum = np.concatenate([[0.0], np.cumsum(c)])
+    bounds = [0]
+    for r in range(1, world):
+        y = int(np.searchsorted(cum, cum[-1] * r / world))
+        y = max(bounds[-1] + min_rows, min(y, H - (world - r) * min_rows))
+        bounds.append(y)
+    bounds.append(H)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+LANES = 3   # run-ahead lanes of a context (kMaxAhead + 1 in restir_capi.hip)
+
+
 class TiledRenderer:
     def __init__(self, W: int, H: int, rank: int, world: int, device: int = 0, stream=None, backend=None,
-                 temporal_margin: int = 64, group=None):
+                 temporal_margin: int = 64, group=None, async_gather: bool = False):
         self.W, self.H, self.rank, self.world = W, H, rank, world
-        self.y0, self.y1 = band_rows(H, rank, world)
+        self.bands = [band_rows(H, r, world) for r in range(world)]
         self.temporal_margin = temporal_margin
         self.group = group
+        # one process group per run-ahead lane: frames in flight on different lanes exchange halos and
+        # gather through independent communicators (one group's collectives run in issue order)
+        self.lane_groups = [group] * LANES
+        if world > 1:
+            import torch.distributed as dist
+            ranks = list(range(world)) if group is None else dist.get_process_group_ranks(group)
+            self.lane_groups = [group] + [dist.new_group(ranks=ranks) for _ in range(LANES - 1)]
         if backend is None:
             from .renderer import Renderer
             backend = GpuTileBackend(Renderer(W, H, device=device, stream=stream))
         self.be = backend
         self.frame = None
+        self.async_gather = async_gather and world > 1
+        if self.async_gather:
+            self.be.set_frame_ring(2)
+        self._inflight = [[] for _ in range(LANES)]   # gather works per lane (its framebuffer)
+        self._out = [None] * LANES                    # rank 0's full-frame buffers, per lane
+
+    @property
+    def y0(self):
+        return self.bands[self.rank][0]
+
+    @property
+    def y1(self):
+        return self.bands[self.rank][1]
+
+    def set_bands(self, bands):
+        bands = [(int(a), int(b)) for a, b in bands]
+        if len(bands) != self.world or bands[0][0] != 0 or bands[-1][1] != self.H or \
+                any(a >= b for a, b in bands) or any(bands[i][1] != bands[i + 1][0] for i in range(self.world - 1)):
+            raise ValueError(f"bands must tile [0, {self.H}) contiguously, one per rank: {bands}")
+        self.wait()
+        self.bands = bands
 
     def load_scene(self, scene):
         return self.be.load_scene(scene)
@@ -126,14 +225,46 @@ class TiledRenderer:
     def reset_history(self):
         self.be.reset_history()
 
+    def wait(self):
+        """Order every in-flight gather before later work on the current stream."""
+        for slot in self._inflight:
+            for w in slot:
+                w.wait()
+            slot.clear()
+
+    def rebalance(self, render_frame, n_frames: int = 2, min_rows: int | None = None):
+        """Measure per-row cost over ``n_frames`` calls of ``render_frame(i)`` (this renderer's frames,
+        any content), all-reduce the rows' costs, move the band boundaries to equalise them, reset the
+        history (the previous G-buffer rows of a moved band belong to another rank).  Returns the bands."""
+        import torch
+        import torch.distributed as dist
+        if self.world == 1:
+            return self.bands
+        self.be.track_row_costs(True)
+        self.be.row_costs(reset=True)
+        for i in range(n_frames):
+            render_frame(i)
+        self.wait()
+        costs = self.be.row_costs(reset=True)
+        self.be.track_row_costs(False)
+        dev = "cpu" if dist.get_backend(self.group) == "gloo" else "cuda"
+        t = torch.as_tensor(costs.astype(np.float64), device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        total = t.cpu().numpy()
+        h = max(1, min_rows if min_rows is not None else 8)
+        self.set_bands(balanced_bands(total, self.world, h))
+        self.reset_history()
+        return self.bands
+
     def _staged(self, t) -> bool:
         """gloo cannot move device tensors: stage them through host memory (tests only -- RCCL refuses
         two ranks on one GPU, so multi-process GPU tests run the real backend over gloo)."""
         import torch.distributed as dist
         return t is not None and t.is_cuda and dist.get_backend(self.group) == "gloo"
 
-    def _exchange_halo(self):
+    def _exchange_halo(self, group=None):
         import torch.distributed as dist
+        group = self.group if group is None else group
         ops, copy_back = [], []
         up, down = self.rank - 1, self.rank + 1
         for peer, send_which, recv_which in ((up, 2, 0), (down, 3, 1)):
@@ -146,7 +277,7 @@ class TiledRenderer:
                 rh = r.new_empty(r.shape, device="cpu")
                 copy_back.append((r, rh))
                 s, r = s.cpu(), rh
-            ops += [dist.P2POp(dist.isend, s, peer, self.group), dist.P2POp(dist.irecv, r, peer, self.group)]
+            ops += [dist.P2POp(dist.isend, s, peer, group), dist.P2POp(dist.irecv, r, peer, group)]
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
@@ -154,44 +285,58 @@ class TiledRenderer:
             dev.copy_(host)
 
     def render(self, scene, camera, params, frame_index: int, gather: bool = True, timed: bool = False):
-        """One frame; returns the full (H, W, 3) frame on rank 0 when gather=True (else None / band)."""
+        """One frame; returns the full (H, W, 3) frame on rank 0 when gather=True (else None / band).
+        With async_gather the returned frame is complete once the stream (or ``wait()``) is synchronised."""
         halo = halo_rows(params) if self.world > 1 else 0
-        if halo and (self.H // self.world) < halo:
-            raise ValueError(f"band height {self.H // self.world} < spatial halo {halo}: too many ranks for H={self.H}")
+        if halo and min(b - a for a, b in self.bands) < halo:
+            raise ValueError(f"a band is thinner than the spatial halo {halo}: too many ranks for H={self.H}")
         margin = max(halo, self.temporal_margin if params.do_temporal else 0) if self.world > 1 else 0
         be = self.be
         be.begin(scene, camera, params, frame_index, self.y0, self.y1, margin, halo)
-        be.temporal()
-        if params.do_spatial:
-            for p in range(params.spatial_passes):
-                if self.world > 1:
-                    self._exchange_halo()
-                be.spatial(p)
-        band = be.finish(timed)
-        if not gather:
-            return band
-        return self._gather(band)
+        st, k = be.frame_stream() if hasattr(be, "frame_stream") else (None, 0)
+        import contextlib
+        with (contextlib.nullcontext() if st is None else _torch_stream(st)):
+            for w in self._inflight[k]:        # the gather that last read this lane's framebuffer
+                w.wait()
+            self._inflight[k].clear()
+            be.temporal()
+            if params.do_spatial:
+                for p in range(params.spatial_passes):
+                    if self.world > 1:
+                        self._exchange_halo(self.lane_groups[k])
+                    be.spatial(p)
+            band = be.finish(timed)
+            if not gather:
+                return band
+            return self._gather(band, k)
 
-    def _gather(self, band):
+    def _gather(self, band, k=0):
+        """Band framebuffers -> rank 0's full frame: rank r > 0 sends its band, rank 0 receives every
+        band straight into its rows of the frame (one batched P2P group; sizes may differ per rank)."""
         import torch
         import torch.distributed as dist
         if self.world == 1:
             self.frame = band.reshape(self.H, self.W, 3)
             return self.frame
-        max_rows = max(band_rows(self.H, r, self.world)[1] - band_rows(self.H, r, self.world)[0]
-                       for r in range(self.world))
-        n = max_rows * self.W * 3
-        dev = "cpu" if self._staged(band) else band.device
-        buf = torch.zeros(n, dtype=torch.float32, device=dev)
-        buf[: band.numel()].copy_(band)
+        staged = self._staged(band)
+        src = band.cpu() if staged else band
+        row = self.W * 3
         if self.rank == 0:
-            parts = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(self.world)]
-            dist.gather(buf, parts, dst=0, group=self.group)
-            rows = []
-            for r in range(self.world):
-                a, b = band_rows(self.H, r, self.world)
-                rows.append(parts[r][: (b - a) * self.W * 3].reshape(b - a, self.W, 3))
-            self.frame = torch.cat(rows, 0)
-            return self.frame
-        dist.gather(buf, None, dst=0, group=self.group)
-        return None
+            out = self._out[k]
+            if out is None or out.device != src.device:
+                out = self._out[k] = torch.empty(self.H * row, dtype=torch.float32, device=src.device)
+            grp = self.lane_groups[k]
+            ops = [dist.P2POp(dist.irecv, out[a * row:b * row], r, grp)
+                   for r, (a, b) in enumerate(self.bands) if r != 0]
+            out[self.y0 * row:self.y1 * row].copy_(src)
+            works = dist.batch_isend_irecv(ops) if ops else []
+            self.frame = out.reshape(self.H, self.W, 3)
+        else:
+            works = dist.batch_isend_irecv([dist.P2POp(dist.isend, src, 0, self.lane_groups[k])])
+            self.frame = None
+        if self.async_gather and not staged:
+            self._inflight[k].extend(works)
+        else:
+            for w in works:
+                w.wait()
+        return self.frame

@@ -30,12 +30,16 @@ EXPORTED_SYMBOLS = [
     "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_context_set_traversal",
     "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions", "rs_post_frame",
     "rs_post_reset", "rs_scene_rebuild", "rs_render_direct_mis", "rs_scene_create_textured", "rs_scene_set_sky",
-    "rs_scene_load_sky", "rs_image_decode",
+    "rs_scene_load_sky", "rs_image_decode", "rs_context_set_initial_split", "rs_context_get_initial_split",
+    "rs_context_set_frame_ring", "rs_context_set_run_ahead", "rs_tile_stream", "rs_context_track_row_costs", "rs_get_row_costs",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
 TRAVERSAL_AUTO, TRAVERSAL_LOCKSTEP, TRAVERSAL_LANE = -1, 0, 1
 TRAVERSAL_NAMES = {"auto": TRAVERSAL_AUTO, "lockstep": TRAVERSAL_LOCKSTEP, "lane": TRAVERSAL_LANE}
+# candidate-split initial pass (include/restir_c.h RS_SPLIT_*)
+SPLIT_AUTO, SPLIT_OFF, SPLIT_ON = -1, 0, 1
+SPLIT_NAMES = {"auto": SPLIT_AUTO, "off": SPLIT_OFF, "on": SPLIT_ON}
 
 
 class MeshDesc(ctypes.Structure):
@@ -149,6 +153,13 @@ def load_library(path: str = LIB_PATH):
     L.rs_context_set_traversal.argtypes = [vp, i32]
     ip = ctypes.POINTER(ctypes.c_int32)
     L.rs_context_get_traversal.argtypes = [vp, vp, ip, ip, ip]
+    L.rs_context_set_initial_split.argtypes = [vp, i32]
+    L.rs_context_get_initial_split.argtypes = [vp, ip, ip]
+    L.rs_context_set_frame_ring.argtypes = [vp, i32]
+    L.rs_context_set_run_ahead.argtypes = [vp, i32]
+    L.rs_tile_stream.argtypes = [vp, ctypes.POINTER(vp), ip]
+    L.rs_context_track_row_costs.argtypes = [vp, i32]
+    L.rs_get_row_costs.argtypes = [vp, fp, i32]
     L.rs_get_timing_totals.argtypes = [vp, ctypes.POINTER(PassTimes), ctypes.POINTER(u32), i32]
     L.rs_scene_update_positions.argtypes = [vp, fp, fp]
     L.rs_post_frame.argtypes = [vp, ctypes.POINTER(PostParams), ctypes.POINTER(vp), ctypes.POINTER(PostStats)]
@@ -396,6 +407,36 @@ class Renderer:
         m = TRAVERSAL_NAMES[mode] if isinstance(mode, str) else int(mode)
         self._check(self.lib.rs_context_set_traversal(self.h, m))
 
+    def set_initial_split(self, mode):
+        """Candidate-split initial pass: "auto" (default), "off" or "on" (or the SPLIT_* ints)."""
+        m = SPLIT_NAMES[mode] if isinstance(mode, str) else int(mode)
+        self._check(self.lib.rs_context_set_initial_split(self.h, m))
+
+    def set_run_ahead(self, depth: int):
+        """Frame pipelining depth 0..2: a frame's initial pass overlaps up to `depth` earlier frames."""
+        self._check(self.lib.rs_context_set_run_ahead(self.h, int(depth)))
+
+    def set_frame_ring(self, n: int):
+        """1 (default) or 2 framebuffers alternating per frame (a reader may lag one frame)."""
+        self._check(self.lib.rs_context_set_frame_ring(self.h, int(n)))
+
+    def track_row_costs(self, enable: bool = True):
+        """Record per-row wave time in every pass (load balancing of tile-sharded frames)."""
+        self._check(self.lib.rs_context_track_row_costs(self.h, 1 if enable else 0))
+
+    def row_costs(self, reset: bool = True) -> np.ndarray:
+        """(H,) float32 per-row wave time accumulated since the last reset (synchronises)."""
+        out = np.zeros(self.H, np.float32)
+        self._check(self.lib.rs_get_row_costs(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                              1 if reset else 0))
+        return out
+
+    def initial_split(self):
+        """(requested mode, whether the last frame's initial pass ran split)."""
+        m, last = ctypes.c_int32(), ctypes.c_int32()
+        self._check(self.lib.rs_context_get_initial_split(self.h, ctypes.byref(m), ctypes.byref(last)))
+        return m.value, bool(last.value)
+
     def traversal(self, scene: "Scene | None" = None):
         """(requested mode, kind the last frame ran with, kind AUTO settled on for `scene` or -1)."""
         m, k, s = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
@@ -467,6 +508,12 @@ class Renderer:
         p, n = ctypes.c_void_p(), ctypes.c_size_t()
         self._check(self.lib.rs_tile_halo_ptr(self.h, which, ctypes.byref(p), ctypes.byref(n)))
         return int(p.value or 0), int(n.value)
+
+    def tile_stream(self):
+        """(stream handle, lane index) of the frame in flight."""
+        p, lane = ctypes.c_void_p(), ctypes.c_int32()
+        self._check(self.lib.rs_tile_stream(self.h, ctypes.byref(p), ctypes.byref(lane)))
+        return int(p.value or 0), lane.value
 
     def tile_temporal(self):
         self._check(self.lib.rs_tile_temporal(self.h))

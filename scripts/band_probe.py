@@ -1,0 +1,96 @@
+"""Diagnostic (GPU box, 1 GPU): what one rank of an N-GPU row-band frame costs, without the
+communication -- the compute + host-overhead floor of bench.py --gpus N.  For N in (1, 2, 4, 8) it renders
+the middle band of the frame (rank N//2, margin/halo as TiledRenderer sets them) K times through the
+tile ABI and reports wall ms/frame, GPU ms/frame (event ring) and host ms per render() call.
+Usage: python scripts/band_probe.py [--scene C2|C3|C5] [--steps K]"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "restir-embree_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="C2")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--split", default="auto", help="initial-pass candidate split: auto|on|off")
+    ap.add_argument("--balanced", action="store_true", help="cost-balanced bands (row costs of a full frame)")
+    ap.add_argument("--inflight", type=int, default=1, help="frames in flight (contexts on separate streams)")
+    ap.add_argument("--ahead", type=int, default=-1, help="run-ahead depth (default: the library's)")
+    ap.add_argument("--only-n", type=int, default=0, help="only this N (rank N//2)")
+    ap.add_argument("--all-ranks", type=int, default=0, help="time every rank of this N instead")
+    a = ap.parse_args()
+    import torch
+    from restir_amd import Renderer, scenes
+    from restir_amd.params import metric_params, c3_params
+    from restir_amd.distributed import band_rows, halo_rows, balanced_bands
+
+    sc = scenes.sponza_like() if a.scene == "C3" else scenes.cornell_many_lights(1024)
+    prm = metric_params() if a.scene == "C2" else c3_params()
+    W, H = a.width, a.height
+    streams = [torch.cuda.Stream() for _ in range(a.inflight)]
+    rs = [Renderer(W, H, device=0, stream=st.cuda_stream) for st in streams]
+    for x in rs:
+        x.set_initial_split(a.split)
+        if a.ahead >= 0:
+            x.set_run_ahead(a.ahead)
+    gss = [x.load_scene(sc) for x in rs]
+    r, gs = rs[0], gss[0]
+    costs = None
+    if a.balanced:
+        r.track_row_costs(True)
+        for f in range(3):
+            r.produce_restir(gs, sc.camera, prm, f, copy_out=False, timed=False)
+        costs = r.row_costs(reset=True)
+        r.track_row_costs(False)
+        r.reset_history()
+    cases = [(N, N // 2) for N in (1, 2, 4, 8)]
+    if a.only_n:
+        cases = [(a.only_n, a.only_n // 2)]
+    if a.all_ranks:
+        cases = [(a.all_ranks, k) for k in range(a.all_ranks)]
+    for N, rank in cases:
+        y0, y1 = balanced_bands(costs, N, 8)[rank] if costs is not None else band_rows(H, rank, N)
+        halo = halo_rows(prm) if N > 1 else 0
+        margin = max(halo, 64 if prm.do_temporal else 0) if N > 1 else 0
+
+        def frame(f):
+            r, gs = rs[f % len(rs)], gss[f % len(rs)]
+            r.tile_begin(gs, sc.camera, prm, f, y0, y1, margin, halo)
+            r.tile_temporal()
+            for p in range(prm.spatial_passes if prm.do_spatial else 0):
+                r.tile_halo_ptr(0)
+                r.tile_spatial(p)
+            r.tile_finish(False)
+
+        for f in range(6):
+            frame(f)
+        for x in rs:
+            x.reset_history()
+        for f in range(3):
+            frame(f)
+        torch.cuda.synchronize()
+        for x in rs:
+            x.timing_totals(reset=True)
+        host = 0.0
+        t0 = time.perf_counter()
+        for f in range(a.steps):
+            h0 = time.perf_counter()
+            frame(3 + f)
+            host += time.perf_counter() - h0
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        tot, n = r.timing_totals()
+        print(f"{a.scene} ahead={a.ahead} inflight={a.inflight} split={a.split}:{int(r.initial_split()[1])} N={N} rank={rank} rows={y1 - y0} margin={margin}: wall {dt / a.steps * 1e3:.4f} ms/frame, "
+              f"gpu {tot.total_ms / n:.4f} ms (initial {tot.gbuffer_initial_ms / n:.4f}, spatial {tot.spatial_ms / n:.4f}, "
+              f"temporal {tot.temporal_ms / n:.4f}), host {host / a.steps * 1e3:.4f} ms/call; "
+              f"ideal (N=1 / N) -> efficiency bound", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -268,6 +268,20 @@ class OracleTileBackend:
     def load_scene(self, scene):
         return OracleScene(scene)
 
+    # load-balancing hooks: the oracle records no wave times; a synthetic per-row cost (rising toward
+    # the bottom rows, only for this rank's band) drives TiledRenderer.rebalance to unequal bands
+    def track_row_costs(self, enable=True):
+        self._track = enable
+
+    def reset_history(self):
+        self.r.reset_history()
+
+    def row_costs(self, reset=True):
+        c = np.zeros(self.H, np.float32)
+        y0, y1 = getattr(self, "y0", 0), getattr(self, "y1", 0)
+        c[y0:y1] = (np.arange(y0, y1, dtype=np.float32) + 1.0) ** 2
+        return c
+
     def begin(self, scene, camera, params, frame, y0, y1, margin, halo):
         self.y0, self.y1 = y0, y1
         self._params = params

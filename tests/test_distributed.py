@@ -26,7 +26,7 @@ def _cfg():
     return sc, prm, cams
 
 
-def _worker(rank, world, port, W, H, out_path):
+def _worker(rank, world, port, W, H, out_path, rebalance=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "restir-embree_amd"), os.path.join(root, "tests")]
@@ -39,6 +39,9 @@ def _worker(rank, world, port, W, H, out_path):
     sc, prm, cams = _cfg()
     tr = TiledRenderer(W, H, rank, world, backend=O.OracleTileBackend(W, H), temporal_margin=H)
     s = tr.load_scene(sc)
+    if rebalance:
+        bands = tr.rebalance(lambda i: tr.render(s, cams[0], prm, i), n_frames=1, min_rows=6)
+        assert bands != [(r * H // world, (r + 1) * H // world) for r in range(world)], bands
     frames = []
     for f, cam in enumerate(cams):
         fr = tr.render(s, cam, prm, f)
@@ -50,12 +53,13 @@ def _worker(rank, world, port, W, H, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_tiled_frames_match_full_frame(world, tmp_path):
+@pytest.mark.parametrize("world,rebalance", [(2, False), (3, False), (3, True)])
+def test_tiled_frames_match_full_frame(world, rebalance, tmp_path):
+    """Equal bands and cost-balanced (unequal) bands both gather the full frame bit for bit."""
     import oracle_lib as O
     W, H = 40, 36
     out = str(tmp_path / "frames.npy")
-    mp.spawn(_worker, args=(world, _free_port(), W, H, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), W, H, out, rebalance), nprocs=world, join=True)
     got = np.load(out)
     sc, prm, cams = _cfg()
     r = O.OracleRenderer(W, H)
@@ -63,6 +67,18 @@ def test_tiled_frames_match_full_frame(world, tmp_path):
     for f, cam in enumerate(cams):
         ref = r.render(s, cam, prm, f)
         assert np.array_equal(got[f], ref), f"frame {f}: max diff {np.abs(got[f] - ref).max()}"
+
+
+def test_balanced_bands():
+    from restir_amd.distributed import balanced_bands
+    assert balanced_bands(np.ones(100), 4) == [(0, 25), (25, 50), (50, 75), (75, 100)]
+    b = balanced_bands(np.r_[np.ones(50), 3 * np.ones(50)], 2)
+    assert b == [(0, 67), (67, 100)], b                     # 50 + 17*3 = 101 vs 99
+    assert balanced_bands(np.zeros(10), 2) == [(0, 5), (5, 10)]  # no costs: equal bands
+    b = balanced_bands(np.r_[np.zeros(90), np.ones(10)], 4, min_rows=5)
+    assert all(y1 - y0 >= 5 for y0, y1 in b) and b[0][0] == 0 and b[-1][1] == 100
+    with pytest.raises(ValueError):
+        balanced_bands(np.ones(10), 4, min_rows=3)
 
 
 def test_halo_rows_and_bands():

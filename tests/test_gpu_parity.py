@@ -191,6 +191,86 @@ def test_traversal_kinds_bit_identical(which):
         _assert_close(frames["lane"][f], o.render(os_, cam(f), prm, f), f"{which} frame {f}")
 
 
+@pytest.mark.parametrize("which", ["c2", "c3", "brdf2", "odd"])
+def test_initial_split_bit_identical(which):
+    """The candidate-split initial pass (a pixel's candidates over 4 waves, LDS weight exchange) renders
+    frames bit-identical to the one-thread-per-pixel pass for both traversal kinds, incl. B=2 BRDF
+    candidates, no area candidates, odd candidate counts and a ragged image; AUTO picks split for a
+    small launch."""
+    W, H = 64, 40
+    cam = lambda f: sc.camera
+    if which == "c2":
+        sc, prm = scenes.cornell_many_lights(1024), P.metric_params()
+    elif which == "c3":
+        sc, prm = scenes.sponza_like(target_tris=30_000, n_lamps=128), P.c3_params(m_area=7)
+        cam = lambda f: scenes.orbit_camera(sc.camera, f, 240, 0.3)
+    elif which == "brdf2":
+        sc, prm = scenes.cornell_box(8), P.default_params(m_area=5, m_brdf=2, do_temporal=1, do_spatial=1)
+    else:
+        sc, prm, W, H = scenes.cornell_box(8), P.default_params(m_area=0, m_brdf=1), 45, 27
+    out = {}
+    for trav in ("lockstep", "lane"):
+        for split in ("off", "on", "auto"):
+            g = Renderer(W, H)
+            g.set_traversal(trav)
+            g.set_initial_split(split)
+            gs = g.load_scene(sc)
+            out[trav, split] = [g.produce_restir(gs, cam(f), prm, f).copy() for f in range(3)]
+            if split == "auto":
+                assert g.initial_split() == (-1, True)
+            elif split == "on":
+                assert g.initial_split() == (1, True)
+    ref = out["lockstep", "off"]
+    for k, v in out.items():
+        for f in range(3):
+            assert np.array_equal(ref[f], v[f]), f"{which} {k} frame {f}"
+    o, os_ = O.OracleRenderer(W, H), O.OracleScene(sc)
+    _assert_close(out["lane", "on"][0], o.render(os_, cam(0), prm, 0), f"{which} split vs oracle")
+
+
+@pytest.mark.parametrize("which", ["c2", "c3", "c5", "fused"])
+def test_run_ahead_bit_identical(which):
+    """Frame pipelining (initial pass of frame f+1 on the side stream, overlapping frame f's later
+    passes) renders the same frames as strictly sequential frames, with temporal reuse, moving
+    geometry (rs_scene_update_positions between frames) and a fused-shade configuration; frames are
+    read back only at the end (from the frame ring) so the overlap really happens."""
+    W, H = 96, 64
+    upd = None
+    cam = lambda f: scenes.orbit_camera(sc.camera, f, 48, 0.2)
+    if which == "c2":
+        sc, prm = scenes.cornell_many_lights(1024), P.metric_params()
+    elif which == "c3":
+        sc, prm = scenes.sponza_like(target_tris=30_000, n_lamps=128), P.c3_params(m_area=6)
+    elif which == "c5":
+        sc, prm = scenes.cornell_many_lights(256), P.c3_params(m_area=6)
+        upd = lambda f: scenes.moving_light_positions(sc, f, 48)
+    else:
+        sc, prm = scenes.cornell_box(8), P.default_params(m_area=4)
+    import torch
+    from restir_amd.distributed import _CudaBuf
+    torch.cuda.set_stream(torch.cuda.Stream())       # the clones below are ordered on the frames' stream
+    st = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for ra in (0, 1, 2):
+        g = Renderer(W, H, stream=st)
+        g.set_run_ahead(ra)
+        gs = g.load_scene(sc)
+        frames = []
+        for f in range(6):
+            if upd:
+                gs.update_positions(upd(f))
+            g.produce_restir(gs, cam(f), prm, f, copy_out=False, timed=False)
+            frames.append(torch.as_tensor(_CudaBuf(g.frame_device_ptr(), W * H * 12, "<f4", 4), device="cuda").clone())
+        out[ra] = [t.cpu().numpy().reshape(H, W, 3) for t in frames]
+    for f in range(6):
+        for ra in (1, 2):
+            assert np.array_equal(out[0][f], out[ra][f]), f"{which} depth {ra} frame {f}"
+    if which != "c5":
+        o, os_ = O.OracleRenderer(W, H), O.OracleScene(sc)
+        for f in range(2):
+            _assert_close(out[2][f], o.render(os_, cam(f), prm, f), f"{which} run-ahead frame {f}")
+
+
 def test_c5_moving_lights_match_oracle():
     """C5 extension: lights moved each frame with rs_scene_update_positions (light CDF + BVH rebuilt)
     under an orbiting camera with temporal + spatial reuse; the oracle renders each frame from a fresh

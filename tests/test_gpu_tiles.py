@@ -69,7 +69,7 @@ def test_metric_point_tiles():
 
 
 # ---------------------------------------------------------------- real processes, real GPU contexts
-def _gpu_worker(rank, world, port, W, H, out_path):
+def _gpu_worker(rank, world, port, W, H, out_path, rebalance):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "restir-embree_amd"), os.path.join(root, "tests")]
@@ -86,6 +86,9 @@ def _gpu_worker(rank, world, port, W, H, out_path):
     tr = TiledRenderer(W, H, rank, world, device=0, stream=torch.cuda.current_stream().cuda_stream,
                        temporal_margin=H)
     s = tr.load_scene(sc)
+    if rebalance:   # bands from the GPU's own per-row wave times (unequal in general)
+        bands = tr.rebalance(lambda i: tr.render(s, sc.camera, prm, i), n_frames=2, min_rows=6)
+        assert bands[0][0] == 0 and bands[-1][1] == H and len(bands) == world
     frames = []
     for f in range(3):
         fr = tr.render(s, scenes.orbit_camera(sc.camera, f, 24, 0.25), prm, f)
@@ -97,7 +100,8 @@ def _gpu_worker(rank, world, port, W, H, out_path):
     dist.destroy_process_group()
 
 
-def test_multiprocess_tiles_on_gpu_match_full_frame(tmp_path):
+@pytest.mark.parametrize("world,rebalance", [(2, False), (3, True)])
+def test_multiprocess_tiles_on_gpu_match_full_frame(world, rebalance, tmp_path):
     """TiledRenderer + GpuTileBackend in 2 real processes (one HIP context each on the same GPU; halo
     exchange and gather over gloo, staged through host memory because RCCL refuses two ranks on one
     device): the gathered frames equal a single-context full frame bit for bit."""
@@ -110,7 +114,7 @@ def test_multiprocess_tiles_on_gpu_match_full_frame(tmp_path):
     s.close()
     W, H = 48, 40
     out = str(tmp_path / "frames.npy")
-    mp.spawn(_gpu_worker, args=(2, port, W, H, out), nprocs=2, join=True)
+    mp.spawn(_gpu_worker, args=(world, port, W, H, out, rebalance), nprocs=world, join=True)
     got = np.load(out)
     sc = scenes.cornell_many_lights(256)
     prm = P.c3_params(m_area=8, spatial_passes=2)
