@@ -280,6 +280,21 @@ int rs_post_frame(rs_context* ctx, const rs_post_params* params, const float** d
 /* accFrameCtr = 0 (the next rs_post_frame overwrites the accumulator with the frame). */
 int rs_post_reset(rs_context* ctx);
 
+/* ---- image export (SimpleGuiDX11::exportImage, pg/simpleguidx11.cpp:607-650) ------
+ * Writes the display buffer of the last rs_post_frame as an 8-bit RGBA PNG -- every channel
+ * (uint8_t)(display * 255.0f), as the reference's glm::vec<4,uint8_t>(display_data[i] * 255.0f) -- and,
+ * with write_sidecar, "<path>.txt" with the reference's fields: iteration count (accFrameCtr), area /
+ * BRDF samples, spatial reuse (pass count, neighbour count, radius), temporal reuse, render time,
+ * image mean / variance (of the last rs_post_frame) and the last frame's camera.  Synchronises. */
+typedef struct {
+    float render_time_s;       /* the `time` argument of exportImage (the caller's clock) */
+    int32_t write_sidecar;
+} rs_export_params;
+int rs_export_png(rs_context* ctx, const char* path, const rs_export_params* params);
+/* Utility: encode `channels` (1..4) interleaved 8-bit samples, top row first, as a PNG file. */
+int rs_image_encode_png(const char* path, uint32_t width, uint32_t height, uint32_t channels,
+                        const uint8_t* pixels);
+
 /* ---- state dumps for golden parity ------------------------------------------------------- */
 /* G-buffer of the last rendered frame (prev=0) or the one before (prev=1): W*H*19 floats per pixel
  * pos3 normal3 kd3 ks3 Le3 shininess depth type 1/I_M.  Reservoirs shaded last frame: W*H*12

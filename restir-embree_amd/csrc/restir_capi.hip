@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <sstream>
 #include <string>
 #include <vector>
 #include <algorithm>
@@ -156,6 +157,8 @@ struct rs_context {
     double2* post_part = nullptr;
     double2* post_out = nullptr;
     uint32_t acc_frames = 0;
+    uint64_t post_px = 0;                  // pixels the last rs_post_frame's statistics cover
+    rs_camera cam_last = {};               // camera of the last frame (rs_export_png's sidecar)
 };
 
 // --------------------------------------------------------------------------- helpers
@@ -1106,7 +1109,7 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
         tile->halo > tile->margin)
         return fail(c, RS_E_INVALID, "rs_tile_begin: bad tile (need 0<=y0<y1<=H, 0<=halo<=margin)");
     HIPCHK(c, enter(c));
-    c->scene = s; c->P = *P; c->tile = *tile;
+    c->scene = s; c->P = *P; c->tile = *tile; c->cam_last = *cam;
     FrameConst& F = c->F;
     F.m_area = P->m_area; F.m_brdf = P->m_brdf; F.k = P->spatial_neighbors; F.spatial_passes = P->spatial_passes;
     F.cap = P->confidence_cap; F.radius = P->spatial_radius; F.min_normal_sim = P->min_normal_similarity;
@@ -1508,6 +1511,7 @@ extern "C" int rs_post_frame(rs_context* c, const rs_post_params* pp, const floa
         k_post_reduce<<<1, 256, 0, c->stream>>>(c->post_part, nblk, c->post_out);
         HIPCHK(c, hipGetLastError());
     }
+    c->post_px = nblk > 0 ? n : 0;
     // accFrameCtr bookkeeping (pg/simpleguidx11.cpp:297-306)
     const uint32_t used = c->acc_frames;
     c->acc_frames++;
@@ -1525,6 +1529,68 @@ extern "C" int rs_post_frame(rs_context* c, const rs_post_params* pp, const floa
         stats->variance = sqr_mean - stats->mean * stats->mean;     // D(X) = E(X^2) - E(X)^2 (:324-325)
         stats->acc_frames_used = used;
     }
+    return RS_OK;
+}
+
+// glm::to_string(vec3): "vec3(x, y, z)" with %f
+static std::string glm_vec3(const float* v) {
+    char b[160];
+    std::snprintf(b, sizeof b, "vec3(%f, %f, %f)", v[0], v[1], v[2]);
+    return b;
+}
+extern "C" int rs_export_png(rs_context* c, const char* path, const rs_export_params* ep) {
+    if (!c || !path) return fail(c, RS_E_INVALID, "rs_export_png: null argument");
+    if (!c->display) return fail(c, RS_E_INVALID, "rs_export_png: no display buffer (call rs_post_frame first)");
+    HIPCHK(c, enter(c));
+    const size_t npx = (size_t)c->W * c->H;
+    std::vector<float4> disp(npx);
+    double2 st{0.0, 0.0};
+    HIPCHK(c, hipMemcpyAsync(disp.data(), c->display, npx * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    if (c->post_px) HIPCHK(c, hipMemcpyAsync(&st, c->post_out, sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<uint8_t> px(npx * 4);
+    for (size_t i = 0; i < npx; ++i) {          // glm::vec<4,uint8_t>(display_data[i] * 255.0f), :617-619
+        const float v[4] = {disp[i].x, disp[i].y, disp[i].z, disp[i].w};
+        for (int k = 0; k < 4; ++k) {
+            const float f = v[k] * 255.0f;
+            px[4 * i + k] = (f > 0.0f) ? (uint8_t)(f < 255.0f ? f : 255.0f) : (uint8_t)0;   // out-of-range: clamp
+        }
+    }
+    std::string err;
+    if (write_png(path, c->W, c->H, 4, px.data(), err) != 0) return fail(c, RS_E_IO, "rs_export_png: " + err);
+    if (ep && ep->write_sidecar) {              // :628-650
+        const double n = (double)c->post_px;
+        const double mean = n > 0 ? st.x / n : 0.0, var = n > 0 ? st.y / n - mean * mean : 0.0;
+        std::FILE* f = std::fopen((std::string(path) + ".txt").c_str(), "w");
+        if (!f) return fail(c, RS_E_IO, std::string("rs_export_png: cannot write ") + path + ".txt");
+        const rs_frame_params& P = c->P;
+        std::ostringstream o;
+        o << "Image name: " << path << "\n\n";
+        o << "Iteration count: " << c->acc_frames << "\n";
+        o << "Area samples: " << P.m_area << "\n";
+        o << "BRDF samples: " << P.m_brdf << "\n\n";
+        o << "Spatial reuse: " << (P.do_spatial ? "True" : "False") << "\n";
+        o << "\tPass count: " << P.spatial_passes << "\n";
+        o << "\tNeighbor count: " << P.spatial_neighbors << "\n";
+        o << "\tReuse radius: " << P.spatial_radius << "\n\n";
+        o << "Temporal reuse: " << (P.do_temporal ? "True" : "False") << "\n\n";
+        o << "Render time: " << (ep ? ep->render_time_s : 0.0f) << " s" << "\n";
+        o << "Image mean: " << mean << "\n";
+        o << "Image variance: " << var << "\n\n";
+        o << "Camera position: " << glm_vec3(c->cam_last.eye) << "\n";
+        o << "Camera view at: " << glm_vec3(c->cam_last.at) << "\n";
+        o << "Camera vertical FOV: " << c->cam_last.fov_y_deg << std::endl;
+        const std::string t = o.str();
+        const bool ok = std::fwrite(t.data(), 1, t.size(), f) == t.size();
+        std::fclose(f);
+        if (!ok) return fail(c, RS_E_IO, "rs_export_png: sidecar write failed");
+    }
+    return RS_OK;
+}
+extern "C" int rs_image_encode_png(const char* path, uint32_t w, uint32_t h, uint32_t ch, const uint8_t* px) {
+    if (!path || !px || !w || !h || ch < 1 || ch > 4) return fail(nullptr, RS_E_INVALID, "rs_image_encode_png: bad arguments");
+    std::string err;
+    if (write_png(path, (int)w, (int)h, (int)ch, px, err) != 0) return fail(nullptr, RS_E_IO, err);
     return RS_OK;
 }
 

@@ -26,6 +26,43 @@ static bool read_file(const std::string& path, std::vector<uint8_t>& out) {
 static uint32_t be32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
 
 // ---------------------------------------------------------------- PNG (ISO/IEC 15948)
+static void put_be32(std::vector<uint8_t>& o, uint32_t v) {
+    o.push_back((uint8_t)(v >> 24)); o.push_back((uint8_t)(v >> 16)); o.push_back((uint8_t)(v >> 8)); o.push_back((uint8_t)v);
+}
+static void put_chunk(std::vector<uint8_t>& o, const char* type, const uint8_t* d, size_t n) {
+    put_be32(o, (uint32_t)n);
+    const size_t t = o.size();
+    o.insert(o.end(), type, type + 4);
+    o.insert(o.end(), d, d + n);
+    put_be32(o, (uint32_t)crc32(0L, o.data() + t, (uInt)(n + 4)));
+}
+int write_png(const std::string& path, int w, int h, int channels, const uint8_t* px, std::string& err) {
+    if (w <= 0 || h <= 0 || channels < 1 || channels > 4 || !px) { err = "write_png: bad image"; return -1; }
+    static const uint8_t ctypes[5] = {0, 0, 4, 2, 6};          // gray, gray+alpha, RGB, RGBA
+    const size_t row = (size_t)w * channels;
+    std::vector<uint8_t> raw((row + 1) * h);
+    for (int y = 0; y < h; ++y) {                               // filter type 0 (None) per scanline
+        raw[(row + 1) * y] = 0;
+        std::memcpy(&raw[(row + 1) * y + 1], px + row * y, row);
+    }
+    uLongf zn = compressBound((uLong)raw.size());
+    std::vector<uint8_t> z(zn);
+    if (compress2(z.data(), &zn, raw.data(), (uLong)raw.size(), 6) != Z_OK) { err = "write_png: deflate failed"; return -1; }
+    std::vector<uint8_t> o = {137, 80, 78, 71, 13, 10, 26, 10};
+    uint8_t ihdr[13];
+    ihdr[0] = (uint8_t)(w >> 24); ihdr[1] = (uint8_t)(w >> 16); ihdr[2] = (uint8_t)(w >> 8); ihdr[3] = (uint8_t)w;
+    ihdr[4] = (uint8_t)(h >> 24); ihdr[5] = (uint8_t)(h >> 16); ihdr[6] = (uint8_t)(h >> 8); ihdr[7] = (uint8_t)h;
+    ihdr[8] = 8; ihdr[9] = ctypes[channels]; ihdr[10] = 0; ihdr[11] = 0; ihdr[12] = 0;
+    put_chunk(o, "IHDR", ihdr, 13);
+    put_chunk(o, "IDAT", z.data(), zn);
+    put_chunk(o, "IEND", nullptr, 0);
+    std::ofstream f(path, std::ios::binary);
+    if (!f) { err = "cannot open " + path + " for writing"; return -1; }
+    f.write((const char*)o.data(), (std::streamsize)o.size());
+    if (!f) { err = "write failed: " + path; return -1; }
+    return 0;
+}
+
 static int decode_png(const std::vector<uint8_t>& f, Image& img, std::string& err) {
     static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
     if (f.size() < 8 || std::memcmp(f.data(), sig, 8) != 0) { err = "not a PNG file"; return -1; }

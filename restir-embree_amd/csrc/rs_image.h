@@ -20,6 +20,10 @@ struct Image {
 // 0 on success; -1 I/O or format error, -3 unsupported variant (JPEG, 16-bit / interlaced PNG)
 int load_image(const std::string& path, Image& img, std::string& err);
 
+// 8-bit PNG writer (stbi_write_png's role in SimpleGuiDX11::exportImage, pg/simpleguidx11.cpp:607-627):
+// `channels` = 1..4 interleaved bytes, top row first; 0 on success, -1 I/O error
+int write_png(const std::string& path, int w, int h, int channels, const uint8_t* px, std::string& err);
+
 // OBJ/MTL scene (rs_obj_loader.cpp): de-indexed triangles in file order, materials with 1-based map
 // slots into `images`; srgb[i] = texture i is a colour map (Texture::expand per referencing slot)
 struct ObjScene {

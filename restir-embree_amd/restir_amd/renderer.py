@@ -31,7 +31,8 @@ EXPORTED_SYMBOLS = [
     "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions", "rs_post_frame",
     "rs_post_reset", "rs_scene_rebuild", "rs_render_direct_mis", "rs_scene_create_textured", "rs_scene_set_sky",
     "rs_scene_load_sky", "rs_image_decode", "rs_context_set_initial_split", "rs_context_get_initial_split",
-    "rs_context_set_frame_ring", "rs_context_set_run_ahead", "rs_tile_stream", "rs_context_track_row_costs", "rs_get_row_costs",
+    "rs_context_set_frame_ring", "rs_context_set_run_ahead", "rs_tile_stream", "rs_export_png",
+    "rs_image_encode_png", "rs_context_track_row_costs", "rs_get_row_costs",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -102,6 +103,10 @@ class PostStats(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+class ExportParams(ctypes.Structure):
+    _fields_ = [("render_time_s", ctypes.c_float), ("write_sidecar", ctypes.c_int32)]
+
+
 class TileDesc(ctypes.Structure):
     _fields_ = [("y0", ctypes.c_int32), ("y1", ctypes.c_int32), ("margin", ctypes.c_int32), ("halo", ctypes.c_int32)]
 
@@ -158,6 +163,8 @@ def load_library(path: str = LIB_PATH):
     L.rs_context_set_frame_ring.argtypes = [vp, i32]
     L.rs_context_set_run_ahead.argtypes = [vp, i32]
     L.rs_tile_stream.argtypes = [vp, ctypes.POINTER(vp), ip]
+    L.rs_export_png.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ExportParams)]
+    L.rs_image_encode_png.argtypes = [ctypes.c_char_p, u32, u32, u32, ctypes.POINTER(ctypes.c_uint8)]
     L.rs_context_track_row_costs.argtypes = [vp, i32]
     L.rs_get_row_costs.argtypes = [vp, fp, i32]
     L.rs_get_timing_totals.argtypes = [vp, ctypes.POINTER(PassTimes), ctypes.POINTER(u32), i32]
@@ -191,6 +198,17 @@ def decode_image(path) -> np.ndarray:
     if rc != RS_OK:
         raise RestirError(f"rs_image_decode({path}): {L.rs_last_error(None).decode()}")
     return out
+
+
+def encode_png(path, pixels) -> None:
+    """Write (H, W[, C]) uint8 pixels (C = 1..4) as a PNG (rs_image_encode_png)."""
+    a = np.ascontiguousarray(pixels, np.uint8)
+    if a.ndim == 2:
+        a = a[:, :, None]
+    lib = load_library()
+    if lib.rs_image_encode_png(os.fsencode(path), a.shape[1], a.shape[0], a.shape[2],
+                               a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))) != RS_OK:
+        raise RestirError(lib.rs_last_error(None).decode())
 
 
 def camera_desc(camera) -> CameraDesc:
@@ -376,6 +394,11 @@ class Renderer:
                                            ctypes.byref(st) if stats else None))
         self._display_ptr = int(dptr.value or 0)
         return self._display_ptr, (st if stats else None)
+
+    def export_png(self, path, render_time_s: float = 0.0, sidecar: bool = True):
+        """SimpleGuiDX11::exportImage: the last post_frame's display as RGBA8 PNG (+ <path>.txt)."""
+        p = ExportParams(float(render_time_s), 1 if sidecar else 0)
+        self._check(self.lib.rs_export_png(self.h, os.fsencode(path), ctypes.byref(p)))
 
     def post_reset(self):
         self._check(self.lib.rs_post_reset(self.h))

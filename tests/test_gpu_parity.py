@@ -412,6 +412,32 @@ def test_post_frame_matches_oracle():
     assert st.acc_frames_used == 0
 
 
+def test_export_png_and_sidecar(tmp_path):
+    """SimpleGuiDX11::exportImage (pg/simpleguidx11.cpp:607-650): the display buffer as RGBA8 with
+    (uint8)(v * 255) truncation, and the sidecar's fields (params, mean/variance, camera)."""
+    from PIL import Image
+    sc, prm = scenes.cornell_box(8), P.default_params(m_area=4, do_spatial=1, spatial_passes=2)
+    g = Renderer(48, 32)
+    gs = g.load_scene(sc)
+    for f in range(3):
+        g.produce_restir(gs, sc.camera, prm, f)
+        _, st = g.post_frame(accumulate=True)
+    disp = g.display_rgba()
+    p = tmp_path / "shot.png"
+    g.export_png(p, render_time_s=1.25)
+    got = np.asarray(Image.open(p))
+    want = (disp * np.float32(255.0)).astype(np.uint8)
+    assert got.shape == (32, 48, 4) and np.array_equal(got, want)
+    txt = open(str(p) + ".txt").read()
+    assert f"Image name: {p}" in txt and "Area samples: 4" in txt and "BRDF samples: 1" in txt
+    assert "Spatial reuse: True" in txt and "\tPass count: 2" in txt and "Temporal reuse: False" in txt
+    assert "Render time: 1.25 s" in txt and "Iteration count: 3" in txt
+    mean = float(txt.split("Image mean: ")[1].split()[0])
+    assert abs(mean - st.mean) <= 1e-5 * abs(st.mean)
+    e = sc.camera.eye
+    assert f"Camera position: vec3({e[0]:f}, {e[1]:f}, {e[2]:f})" in txt
+
+
 def test_timing_totals_match_per_frame_times():
     """rs_get_timing_totals (no per-frame sync) sums the same rays as per-frame timed readback and
     counts every frame, across more frames than the event ring holds."""

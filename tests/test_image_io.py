@@ -140,3 +140,21 @@ def test_pnm(tmp_path):
     p5.write_bytes(b"P5 7 6 255\n" + gray.tobytes())
     assert np.array_equal(decode_image(p6), rgb)
     assert np.array_equal(decode_image(p5), gray[:, :, None])
+
+
+@pytest.mark.parametrize("channels", [1, 2, 3, 4])
+def test_png_encoder_roundtrip(tmp_path, channels):
+    """rs_image_encode_png (the exportImage writer) -> PIL and our decoder read back the same bytes."""
+    from PIL import Image
+    from restir_amd.renderer import encode_png
+    rng = np.random.default_rng(channels)
+    px = rng.integers(0, 256, (23, 37, channels), dtype=np.uint8)
+    p = tmp_path / "e.png"
+    encode_png(p, px)
+    got = np.asarray(Image.open(p))
+    assert np.array_equal(got.reshape(px.shape), px)
+    dec = decode_image(p)
+    if channels == 2:                     # the decoder expands gray+alpha to RGBA (g, g, g, a)
+        assert np.array_equal(dec[..., 0], px[..., 0]) and np.array_equal(dec[..., 3], px[..., 1])
+    else:
+        assert np.array_equal(dec.reshape(px.shape), px)
