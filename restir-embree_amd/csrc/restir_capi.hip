@@ -1271,8 +1271,19 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
     int dst = (c->rcur == c->ra) ? c->rb : c->ra;
     int fuse = (pass_index == c->P.spatial_passes - 1) ? 1 : 0;
     const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
-    LAUNCH_TRAV(c, k_spatial, gb, S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]}, ResBuf{c->R[dst]}, pass_index, fuse,
-                c->fb, count_slot(c, gb));
+    {
+        const CountSlot cs = count_slot(c, gb);
+        const GBuf& G = c->G[c->gcur];
+        const ResBuf Rr{c->R[c->rcur]}, Rw{c->R[dst]};
+        const bool cm = c->F.mis == MIS_CONSTANT;
+        if (c->trav == TRAV_LANE) {
+            if (cm) k_spatial<TRAV_LANE, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+            else k_spatial<TRAV_LANE, 0><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+        } else {
+            if (cm) k_spatial<TRAV_LOCKSTEP, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+            else k_spatial<TRAV_LOCKSTEP, 0><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+        }
+    }
     HIPCHK(c, hipGetLastError());
     c->rcur = dst;
     if (fuse) c->shade_fused = true;

@@ -27,9 +27,27 @@
 #ifndef RS_SPATIAL_WAVES
 #define RS_SPATIAL_WAVES 4
 #endif
+// ... for the per-lane traversal kind (incoherent scenes: the walk loop needs more registers)
+#ifndef RS_INITIAL_WAVES_LANE
+#define RS_INITIAL_WAVES_LANE RS_INITIAL_WAVES
+#endif
+#ifndef RS_SPATIAL_WAVES_LANE
+#define RS_SPATIAL_WAVES_LANE RS_SPATIAL_WAVES
+#endif
+#ifndef RS_TEMPORAL_WAVES
+#define RS_TEMPORAL_WAVES 4
+#endif
+#ifndef RS_TEMPORAL_WAVES_LANE
+#define RS_TEMPORAL_WAVES_LANE RS_TEMPORAL_WAVES
+#endif
+#define RS_WAVES(T, lockstep, lane) ((T) == TRAV_LANE ? (lane) : (lockstep))
 // area candidates whose shadow rays share one lockstep traversal (occluded_wave_multi)
 #ifndef RS_RIS_BATCH
 #define RS_RIS_BATCH 2
+#endif
+// ... and for the per-lane walk (occluded_lane_seq: a lane's rays run back to back in one loop)
+#ifndef RS_RIS_BATCH_LANE
+#define RS_RIS_BATCH_LANE 2
 #endif
 
 namespace rs {
@@ -339,6 +357,7 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
     if (__ballot(alive) == 0) return r;                                 // wave-uniform exit
     Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, pix);
     const bool tv = !F.do_vis_pass;
+    constexpr int kB = T == TRAV_LANE ? RS_RIS_BATCH_LANE : RS_RIS_BATCH;
     float best_phat = 0.0f;
     if (F.m_area > 0) {
         // area candidates in batches of RS_RIS_BATCH: sample + unoccluded f for the batch, ONE lockstep
@@ -346,15 +365,15 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
         // sample is re-drawn from its slots once at the end instead of being carried per candidate.
         float inv_ma = 1.0f / (float)F.m_area;
         int sel = -1;
-        for (int c0 = 0; c0 < F.m_area; c0 += RS_RIS_BATCH) {
-            FPre pre[RS_RIS_BATCH];
-            float Wc[RS_RIS_BATCH], mis[RS_RIS_BATCH];
-            bool act[RS_RIS_BATCH], occ[RS_RIS_BATCH];
-            vec3 dir[RS_RIS_BATCH];
-            float tf[RS_RIS_BATCH];
+        for (int c0 = 0; c0 < F.m_area; c0 += kB) {
+            FPre pre[kB];
+            float Wc[kB], mis[kB];
+            bool act[kB], occ[kB];
+            vec3 dir[kB];
+            float tf[kB];
             const ShadeFrame sf = fs.load();
 #pragma unroll
-            for (int k = 0; k < RS_RIS_BATCH; ++k) {
+            for (int k = 0; k < kB; ++k) {
                 const bool inb = c0 + k < F.m_area;
                 rng.n = cand_slot(c0 + k);
                 Sample s = area_sample(S, F, pos, sf, rng, Wc[k], mis[k]);
@@ -362,9 +381,9 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
                 act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
                 rays += act[k] ? 1u : 0u;
             }
-            if (tv) trace_any_multi<T, RS_RIS_BATCH>(S, act, pos, dir, FLT_MIN + F.tnear_off, tf, occ);
+            if (tv) trace_any_multi<T, kB>(S, act, pos, dir, FLT_MIN + F.tnear_off, tf, occ);
 #pragma unroll
-            for (int k = 0; k < RS_RIS_BATCH; ++k) {
+            for (int k = 0; k < kB; ++k) {
                 if (c0 + k < F.m_area) {
                     vec3 f = evaluate_f_post(pre[k], occ[k]);
                     float ph = length(f);
@@ -412,7 +431,7 @@ __device__ __forceinline__ void store_rgb(float* fb, size_t p, vec3 c) {
 }
 
 template <int T>
-__global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G,
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_WAVES_LANE)) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G,
                                                                             ResBuf Rw, float* fb, int fuse_shade,
                                                                             CountSlot C) {
     const uint64_t t0 = wave_clock();
@@ -462,7 +481,7 @@ __device__ __forceinline__ void split_range(int n, int g, int& lo, int& hi) {
 }
 
 template <int T>
-__global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial_split(DevScene S, FrameConst F, GBuf G,
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_WAVES_LANE)) k_gbuffer_initial_split(DevScene S, FrameConst F, GBuf G,
                                                                                   ResBuf Rw, float* fb, int fuse_shade,
                                                                                   CountSlot C) {
     const uint64_t t0 = wave_clock();
@@ -491,20 +510,21 @@ __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial_split
     const bool alive = pa.w != 0.0f;
     const int A = F.m_area, B = F.m_brdf, n = A + B;
     const bool tv = !F.do_vis_pass;
+    constexpr int kB = T == TRAV_LANE ? RS_RIS_BATCH_LANE : RS_RIS_BATCH;
     int lo, hi;
     split_range(n, g, lo, hi);
     if (__ballot(alive) != 0) {                                         // wave-uniform
         Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, (uint32_t)p);
         const int ahi = hi < A ? hi : A;
-        for (int c0 = lo; c0 < ahi; c0 += RS_RIS_BATCH) {               // area candidates (:246-266)
-            FPre pre[RS_RIS_BATCH];
-            float Wc[RS_RIS_BATCH], mis[RS_RIS_BATCH];
-            bool act[RS_RIS_BATCH], occ[RS_RIS_BATCH];
-            vec3 dir[RS_RIS_BATCH];
-            float tf[RS_RIS_BATCH];
+        for (int c0 = lo; c0 < ahi; c0 += kB) {               // area candidates (:246-266)
+            FPre pre[kB];
+            float Wc[kB], mis[kB];
+            bool act[kB], occ[kB];
+            vec3 dir[kB];
+            float tf[kB];
             const ShadeFrame sf = fs.load();
 #pragma unroll
-            for (int k = 0; k < RS_RIS_BATCH; ++k) {
+            for (int k = 0; k < kB; ++k) {
                 const bool inb = c0 + k < ahi;
                 rng.n = cand_slot(c0 + k);
                 Sample s = area_sample(S, F, pos, sf, rng, Wc[k], mis[k]);
@@ -512,9 +532,9 @@ __global__ void __launch_bounds__(256, RS_INITIAL_WAVES) k_gbuffer_initial_split
                 act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
                 rays += act[k] ? 1u : 0u;
             }
-            if (tv) trace_any_multi<T, RS_RIS_BATCH>(S, act, pos, dir, FLT_MIN + F.tnear_off, tf, occ);
+            if (tv) trace_any_multi<T, kB>(S, act, pos, dir, FLT_MIN + F.tnear_off, tf, occ);
 #pragma unroll
-            for (int k = 0; k < RS_RIS_BATCH; ++k) {
+            for (int k = 0; k < kB; ++k) {
                 if (c0 + k < ahi) {
                     const float ph = length(evaluate_f_post(pre[k], occ[k]));
                     L.w[(c0 + k) * 64 + lane] = B > 0 ? mis[k] * ph * Wc[k] : (1.0f / (float)A) * ph * Wc[k];
@@ -613,7 +633,7 @@ __device__ __forceinline__ bool reproject(const GCam& c, vec3 ws, int W, int H, 
 // temporalReusePass (pg/ReSTIRIntegrator.cpp:625-732).  The previous reservoir is read at the
 // CURRENT pixel (:641), the previous G-buffer at the reprojected pixel (:652).
 template <int T>
-__global__ void __launch_bounds__(256) k_temporal(DevScene S, FrameConst F, GBuf G, GBuf Gp, ResBuf Rr, ResBuf Rl,
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORAL_WAVES_LANE)) k_temporal(DevScene S, FrameConst F, GBuf G, GBuf Gp, ResBuf Rr, ResBuf Rl,
                                                   ResBuf Rw, CountSlot C) {
     const uint64_t t0 = wave_clock();
     int x, y;
@@ -704,10 +724,12 @@ constexpr int kNbrCache = 17;
 
 // spatialReusePass (pg/ReSTIRIntegrator.cpp:316-542); shade fused when this is the last pass.
 // List loops run to the uniform bound k+1 with `i < cnt` as a predicate (convergent ray queries).
-template <int T>
-__global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr,
-                                                                   ResBuf Rw, int pass_idx, int fuse_shade, float* fb,
-                                                                   CountSlot C) {
+// CM = 1: the CONSTANT-MIS instantiation (the metric point), compiled without the other modes' code
+// and register pressure; CM = 0 handles every mode.
+template <int T, int CM>
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_SPATIAL_WAVES, RS_SPATIAL_WAVES_LANE))
+k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, int fuse_shade, float* fb, CountSlot C) {
+    const int mis = CM ? MIS_CONSTANT : F.mis;
     __shared__ uint32_t nbr[kNbrCache * 256];
     const uint64_t t0 = wave_clock();
     int x, y;
@@ -764,7 +786,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
         int sel = 0;
         float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
         vec3 f_sel = mk(0, 0, 0);
-        if (F.mis == MIS_CONSTANT) {
+        if (mis == MIS_CONSTANT) {
             // CONSTANT MIS (the metric point): the k+1 candidates' shadow rays all start at this pixel,
             // so pairs share one walk (trace_any_multi); the addSample draws stay in candidate order
             const ShadeFrame sf = make_frame(th, cam);
@@ -799,7 +821,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
             Res ri = Rr.load(qi);
             Sample si = smp_of(ri);
             float mis = rcpM;
-            if (F.mis == MIS_BALANCE) {                    // :407-424
+            if (mis == MIS_BALANCE) {                    // :407-424
                 float num = 0, den = 0;
                 mis = 0.0f;
                 for (int j = 0; j < kk; ++j) {
@@ -814,7 +836,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
                 }
                 if (den > 0) mis = num / den;
             }
-            if (F.mis == MIS_PAIRWISE) {                   // :427-467
+            if (mis == MIS_PAIRWISE) {                   // :427-467
                 mis = 0.0f;
                 if (i == 0) {
                     float sum = 0.0f;
@@ -846,9 +868,9 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
             if (li && res_add(res, si, rw, ri.conf, rng)) { sel = i; f_sel = f; }
         }
         float fph = smp_valid(smp_of(res)) ? length(f_sel) : 0.0f;  // :481
-        if (F.mis == MIS_CONSTANT || F.mis == MIS_BALANCE || F.mis == MIS_PAIRWISE) {
+        if (mis == MIS_CONSTANT || mis == MIS_BALANCE || mis == MIS_PAIRWISE) {
             res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
-        } else if (F.mis == MIS_DEBIAS_Z) {                // :494-506
+        } else if (mis == MIS_DEBIAS_Z) {                // :494-506
             int Z = 0;
             float corr = 1.0f;
             for (int i = 0; i < kk; ++i) {
@@ -859,7 +881,7 @@ __global__ void __launch_bounds__(256, RS_SPATIAL_WAVES) k_spatial(DevScene S, F
             }
             if (Z > 0 && M > 0) corr = (1.0f / (float)Z) / rcpM;
             res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
-        } else if (F.mis == MIS_DEBIAS_CONTRIB) {          // :515-538
+        } else if (mis == MIS_DEBIAS_CONTRIB) {          // :515-538
             Sample ss = smp_of(Rr.load(list_q(sel)));
             float num = 0, den = 0, cw = 0, corr = 0;
             for (int i = 0; i < kk; ++i) {

@@ -7,4 +7,5 @@ F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off $2"
 /opt/rocm/bin/hipcc $F -c csrc/restir_capi.hip -o _variants/$1/capi.o
 /opt/rocm/bin/hipcc $F -c csrc/rs_bvh_build.hip -o _variants/$1/bvh.o
 /opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -c csrc/rs_obj_loader.cpp -o _variants/$1/obj.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o _variants/$1.so _variants/$1/*.o
+/opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -ffp-contract=off -c csrc/rs_image.cpp -o _variants/$1/image.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o _variants/$1.so _variants/$1/*.o -lz
