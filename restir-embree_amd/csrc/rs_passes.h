@@ -729,7 +729,7 @@ constexpr int kNbrCache = 17;
 template <int T, int CM>
 __global__ void __launch_bounds__(256, RS_WAVES(T, RS_SPATIAL_WAVES, RS_SPATIAL_WAVES_LANE))
 k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, int fuse_shade, float* fb, CountSlot C) {
-    const int mis = CM ? MIS_CONSTANT : F.mis;
+    const int mode = CM ? MIS_CONSTANT : F.mis;
     __shared__ uint32_t nbr[kNbrCache * 256];
     const uint64_t t0 = wave_clock();
     int x, y;
@@ -786,7 +786,7 @@ k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, 
         int sel = 0;
         float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
         vec3 f_sel = mk(0, 0, 0);
-        if (mis == MIS_CONSTANT) {
+        if (mode == MIS_CONSTANT) {
             // CONSTANT MIS (the metric point): the k+1 candidates' shadow rays all start at this pixel,
             // so pairs share one walk (trace_any_multi); the addSample draws stay in candidate order
             const ShadeFrame sf = make_frame(th, cam);
@@ -821,7 +821,7 @@ k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, 
             Res ri = Rr.load(qi);
             Sample si = smp_of(ri);
             float mis = rcpM;
-            if (mis == MIS_BALANCE) {                    // :407-424
+            if (mode == MIS_BALANCE) {                    // :407-424
                 float num = 0, den = 0;
                 mis = 0.0f;
                 for (int j = 0; j < kk; ++j) {
@@ -836,7 +836,7 @@ k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, 
                 }
                 if (den > 0) mis = num / den;
             }
-            if (mis == MIS_PAIRWISE) {                   // :427-467
+            if (mode == MIS_PAIRWISE) {                   // :427-467
                 mis = 0.0f;
                 if (i == 0) {
                     float sum = 0.0f;
@@ -868,9 +868,9 @@ k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, 
             if (li && res_add(res, si, rw, ri.conf, rng)) { sel = i; f_sel = f; }
         }
         float fph = smp_valid(smp_of(res)) ? length(f_sel) : 0.0f;  // :481
-        if (mis == MIS_CONSTANT || mis == MIS_BALANCE || mis == MIS_PAIRWISE) {
+        if (mode == MIS_CONSTANT || mode == MIS_BALANCE || mode == MIS_PAIRWISE) {
             res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
-        } else if (mis == MIS_DEBIAS_Z) {                // :494-506
+        } else if (mode == MIS_DEBIAS_Z) {                // :494-506
             int Z = 0;
             float corr = 1.0f;
             for (int i = 0; i < kk; ++i) {
@@ -881,7 +881,7 @@ k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, 
             }
             if (Z > 0 && M > 0) corr = (1.0f / (float)Z) / rcpM;
             res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
-        } else if (mis == MIS_DEBIAS_CONTRIB) {          // :515-538
+        } else if (mode == MIS_DEBIAS_CONTRIB) {          // :515-538
             Sample ss = smp_of(Rr.load(list_q(sel)));
             float num = 0, den = 0, cw = 0, corr = 0;
             for (int i = 0; i < kk; ++i) {
