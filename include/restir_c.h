@@ -226,7 +226,8 @@ int rs_context_get_traversal(const rs_context* ctx, const rs_scene* scene, int* 
  * ON: the initial pass spreads a pixel's A+B candidates over 4 waves of one 8x8-tile workgroup
  * (fills the GPU when a rank renders a small band); OFF: one thread carries all candidates of its
  * pixel; AUTO (default; env RESTIR_SPLIT=on|off overrides at context creation): ON when the launch
- * has fewer than ~3 rounds of one-thread-per-pixel waves for the device.  Needs A+B <= 64 and B <= 2
+ * has fewer than ~3 rounds of one-thread-per-pixel waves for the device and the frame uses the
+ * lockstep traversal.  Needs A+B <= 64 and B <= 2
  * (OFF otherwise).  Frames are bit-identical either way. */
 #define RS_SPLIT_AUTO (-1)
 #define RS_SPLIT_OFF 0

@@ -1081,12 +1081,14 @@ static CountSlot count_slot(rs_context* c, dim3 grid) {
 // reserve slots for every launch of a frame: initial + visibility + temporal + P spatial + shade
 static dim3 grid_split(int W, int ya, int yb) { return dim3((W + 7) / 8, (yb - ya + 7) / 8); }
 // the initial pass runs candidate-split when asked, or (AUTO) when one thread per pixel would give the
-// launch fewer than 3 rounds of the device's resident waves (a rank's band of a multi-GPU frame)
+// launch fewer than 3 rounds of the device's resident waves (a rank's band of a multi-GPU frame) and
+// the walks are lockstep: per-lane walks are latency-bound and need the occupancy the split kernel's
+// LDS takes away (C3 1/8 band: 5.3 ms split vs 4.2 ms one thread per pixel)
 static bool want_split(const rs_context* c, const rs_frame_params* P, int gy0, int gy1) {
     if (P->m_area + P->m_brdf > kSplitMaxCand || P->m_brdf > kSplitMaxBrdf) return false;
     if (c->split_mode == RS_SPLIT_ON) return true;
     if (c->split_mode == RS_SPLIT_OFF) return false;
-    return grid_waves(grid_rows(c->W, gy0, gy1)) < (size_t)3 * c->wave_slots;
+    return c->trav == TRAV_LOCKSTEP && grid_waves(grid_rows(c->W, gy0, gy1)) < (size_t)3 * c->wave_slots;
 }
 static bool reserve_count_slots(rs_context* c, int k, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
     size_t need = grid_waves(c->split ? grid_split(c->W, gy0, gy1) : grid_rows(c->W, gy0, gy1)) +
@@ -1168,6 +1170,7 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     c->shade_fused = !P->do_visibility_pass && !temporal && !spatial;
     c->temporal_ran = c->spatial_ran = c->ev_temporal = false;
     const DevScene S = s->dev();
+    pick_traversal(c, s);
     c->split = want_split(c, P, F.gy0, F.gy1);
     if (!reserve_count_slots(c, c->li, P, F.gy0, F.gy1, F.y0, F.y1)) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
     if (c->fs != c->stream && c->lane_wait[c->li]) {   // this lane's previous frame ran on the context's stream
@@ -1185,7 +1188,6 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     for (int i = 0; i < EV_COUNT; ++i) c->ev[i] = c->evr[c->slot][i];
     HIPCHK(c, hipEventRecord(c->ev[EV_BEGIN], c->fs));
     c->prev_begin = c->ev[EV_BEGIN];
-    pick_traversal(c, s);
     const dim3 gg = grid_rows(c->W, F.gy0, F.gy1), gb = grid_rows(c->W, F.y0, F.y1);
     if (c->split) {
         const dim3 gs = grid_split(c->W, F.gy0, F.gy1);

@@ -196,7 +196,7 @@ def test_initial_split_bit_identical(which):
     """The candidate-split initial pass (a pixel's candidates over 4 waves, LDS weight exchange) renders
     frames bit-identical to the one-thread-per-pixel pass for both traversal kinds, incl. B=2 BRDF
     candidates, no area candidates, odd candidate counts and a ragged image; AUTO picks split for a
-    small launch."""
+    small launch with lockstep walks."""
     W, H = 64, 40
     cam = lambda f: sc.camera
     if which == "c2":
@@ -216,8 +216,8 @@ def test_initial_split_bit_identical(which):
             g.set_initial_split(split)
             gs = g.load_scene(sc)
             out[trav, split] = [g.produce_restir(gs, cam(f), prm, f).copy() for f in range(3)]
-            if split == "auto":
-                assert g.initial_split() == (-1, True)
+            if split == "auto":                  # small launch: split for lockstep walks only
+                assert g.initial_split() == (-1, trav == "lockstep")
             elif split == "on":
                 assert g.initial_split() == (1, True)
     ref = out["lockstep", "off"]
