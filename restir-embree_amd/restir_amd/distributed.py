@@ -110,8 +110,9 @@ class GpuTileBackend:
         self.y0, self.y1 = y0, y1
         self.r.tile_begin(scene, camera, params, frame, y0, y1, margin, halo)
 
-    def halo_tensor(self, which: int):
-        self._sync_if_foreign_stream()
+    def halo_tensor(self, which: int, on_frame_stream: bool = False):
+        if not on_frame_stream:
+            self._sync_if_foreign_stream()
         ptr, n = self.r.tile_halo_ptr(which)
         if not ptr:
             return None
@@ -123,9 +124,10 @@ class GpuTileBackend:
     def spatial(self, p):
         self.r.tile_spatial(p)
 
-    def finish(self, timed=False):
+    def finish(self, timed=False, on_frame_stream: bool = False):
         ptr = self.r.tile_finish(timed)
-        self._sync_if_foreign_stream()
+        if not on_frame_stream:
+            self._sync_if_foreign_stream()
         n = (self.y1 - self.y0) * self.r.W * 3
         return self._view(ptr, n * 4, "<f4", 4)
 
@@ -194,6 +196,7 @@ class TiledRenderer:
             self.be.set_frame_ring(2)
         self._inflight = [[] for _ in range(LANES)]   # gather works per lane (its framebuffer)
         self._out = [None] * LANES                    # rank 0's full-frame buffers, per lane
+        self._recv_ops = {}
 
     @property
     def y0(self):
@@ -262,15 +265,16 @@ class TiledRenderer:
         import torch.distributed as dist
         return t is not None and t.is_cuda and dist.get_backend(self.group) == "gloo"
 
-    def _exchange_halo(self, group=None):
+    def _exchange_halo(self, group=None, on_frame_stream=False):
         import torch.distributed as dist
         group = self.group if group is None else group
         ops, copy_back = [], []
         up, down = self.rank - 1, self.rank + 1
+        kw = {"on_frame_stream": True} if on_frame_stream else {}
         for peer, send_which, recv_which in ((up, 2, 0), (down, 3, 1)):
             if peer < 0 or peer >= self.world:
                 continue
-            s, r = self.be.halo_tensor(send_which), self.be.halo_tensor(recv_which)
+            s, r = self.be.halo_tensor(send_which, **kw), self.be.halo_tensor(recv_which, **kw)
             if s is None or r is None:
                 continue
             if self._staged(s):
@@ -303,9 +307,9 @@ class TiledRenderer:
             if params.do_spatial:
                 for p in range(params.spatial_passes):
                     if self.world > 1:
-                        self._exchange_halo(self.lane_groups[k])
+                        self._exchange_halo(self.lane_groups[k], on_frame_stream=st is not None)
                     be.spatial(p)
-            band = be.finish(timed)
+            band = be.finish(timed, on_frame_stream=True) if st is not None else be.finish(timed)
             if not gather:
                 return band
             return self._gather(band, k)
@@ -325,9 +329,12 @@ class TiledRenderer:
             out = self._out[k]
             if out is None or out.device != src.device:
                 out = self._out[k] = torch.empty(self.H * row, dtype=torch.float32, device=src.device)
-            grp = self.lane_groups[k]
-            ops = [dist.P2POp(dist.irecv, out[a * row:b * row], r, grp)
-                   for r, (a, b) in enumerate(self.bands) if r != 0]
+            key = (k, tuple(self.bands), out.data_ptr())
+            ops = self._recv_ops.get(key)
+            if ops is None:                    # the receive descriptors of a lane's frame buffer, reused
+                grp = self.lane_groups[k]
+                ops = self._recv_ops[key] = [dist.P2POp(dist.irecv, out[a * row:b * row], r, grp)
+                                             for r, (a, b) in enumerate(self.bands) if r != 0]
             out[self.y0 * row:self.y1 * row].copy_(src)
             works = dist.batch_isend_irecv(ops) if ops else []
             self.frame = out.reshape(self.H, self.W, 3)

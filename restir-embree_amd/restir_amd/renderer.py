@@ -289,6 +289,7 @@ class Renderer:
     def __init__(self, width: int, height: int, device: int = 0, stream: int | None = None):
         self.lib = load_library()
         self.W, self.H = int(width), int(height)
+        self._tile_cache = None
         h = ctypes.c_void_p()
         rc = self.lib.rs_context_create(device, self.W, self.H, ctypes.c_void_p(stream) if stream else None,
                                         ctypes.byref(h))
@@ -522,8 +523,11 @@ class Renderer:
     # ---- tile stages (multi-GPU) ------------------------------------------------------------
     def tile_begin(self, scene: Scene, camera, params: FrameParams, frame_index: int, y0: int, y1: int,
                    margin: int, halo: int):
-        cam = camera_desc(camera)
-        t = TileDesc(y0, y1, margin, halo)
+        # per-frame host work is on the multi-GPU critical path: reuse the descriptors of a repeated
+        # camera object / band instead of rebuilding them
+        if self._tile_cache is None or self._tile_cache[0] is not camera or self._tile_cache[1] != (y0, y1, margin, halo):
+            self._tile_cache = (camera, (y0, y1, margin, halo), camera_desc(camera), TileDesc(y0, y1, margin, halo))
+        _, _, cam, t = self._tile_cache
         self._check(self.lib.rs_tile_begin(self.h, scene.h, ctypes.byref(cam), ctypes.byref(params),
                                            int(frame_index), ctypes.byref(t)))
 
