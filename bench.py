@@ -205,7 +205,7 @@ def main():
     k_ms = acc["gbuffer_initial_ms"] / args.steps
     px_band = W * math.ceil(H / world)
     achieved = DOMINANT_BYTES_PER_PX * px_band / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
-    traffic = valu = None
+    traffic = valu = frame_traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf) and world == 1:
         try:
@@ -213,9 +213,10 @@ def main():
                 pmc = json.load(f)
             if pmc.get("config") == f"{args.scene}_{W}x{H}":
                 traffic = pmc.get("k_gbuffer_initial_bytes_per_launch")
+                frame_traffic = pmc.get("frame_bytes")
                 valu = pmc.get("k_gbuffer_initial_valu_per_launch")
         except Exception:
-            traffic = valu = None
+            traffic = valu = frame_traffic = None
     inflight = 1 + int(os.environ.get("RESTIR_RUNAHEAD", "2"))
     trav_name = None
     if world == 1:
@@ -256,7 +257,7 @@ def main():
             # time they share the GPU with other frames' kernels; this is the pipeline's figure
             "frame_roofline": {"bound": "hbm", "bytes_per_px": frame_bytes_per_px(prm), "unit": "GB/s",
                                "achieved": round(frame_bytes_per_px(prm) * W * H / (ms_per_step * 1e-3) / 1e9, 2),
-                               "peak": HBM_PEAK_GBS,
+                               "peak": HBM_PEAK_GBS, "traffic": frame_traffic,
                                "frac": round(frame_bytes_per_px(prm) * W * H / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)},
             "valu_issue": None if not valu or k_ms <= 0 else {
                 "achieved": round(valu / (k_ms * 1e-3) / 1e9, 2), "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",

@@ -345,6 +345,47 @@ struct FrameSlot {
     }
 };
 
+// One batch of area candidates [c0, c0 + kB) (initialRenderPass :246-266): sample, unoccluded f, one
+// walk for the batch's shadow rays; returns each candidate's RIS weight w in w_out.  Only two weights per
+// candidate stay live across the walk -- the unoccluded one and the occluded one, (m * 0) * W -- instead
+// of the sample, f, MIS weight and W: an occluded (or invalid) candidate has f = 0 and p-hat = 0, which
+// both produce bit for bit.  (The selected candidate's f is re-derived from its re-drawn sample.)
+template <int T, int kB>
+__device__ __forceinline__ void area_batch(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
+                                           Rng& rng, int c0, int c_end, bool alive, bool tv, float* w_out,
+                                           uint32_t& rays) {
+    float wu[kB], wo[kB];
+    bool act[kB], okb[kB], occ[kB];
+    vec3 dir[kB];
+    float tf[kB];
+    const float inv_ma = 1.0f / (float)F.m_area;
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+        float Wc, mis;
+        rng.n = cand_slot(c0 + k);
+        const Sample s = area_sample(S, F, pos, sf, rng, Wc, mis);
+        const FPre p = evaluate_f_pre(F, s, pos, false, sf, tv, alive && c0 + k < c_end);
+        const float ph = length(p.L);
+        const float m = F.m_brdf > 0 ? mis : inv_ma;
+        wu[k] = m * ph * Wc;
+        wo[k] = m * 0.0f * Wc;
+        act[k] = p.need; okb[k] = p.ok; dir[k] = p.dir; tf[k] = p.tfar; occ[k] = false;
+        rays += act[k] ? 1u : 0u;
+    }
+    if (tv) trace_any_multi<T, kB>(S, act, pos, dir, FLT_MIN + F.tnear_off, tf, occ);
+#pragma unroll
+    for (int k = 0; k < kB; ++k) w_out[k] = (okb[k] && !(act[k] && occ[k])) ? wu[k] : wo[k];   // evaluate_f_post
+}
+// the selected area candidate's sample and (unoccluded) f, re-drawn from its RNG slots
+__device__ __forceinline__ Sample area_redraw(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
+                                             Rng& rng, int c, bool tv, vec3& f) {
+    float Wc, mis;
+    rng.n = cand_slot(c);
+    const Sample s = area_sample(S, F, pos, sf, rng, Wc, mis);
+    f = evaluate_f_pre(F, s, pos, false, sf, tv, true).L;
+    return s;
+}
+
 // initialRenderPass (pg/ReSTIRIntegrator.cpp:236-298) for the lanes with `in_pass`.  f_sel returns the
 // selected candidate's f (for the fused shade); the final p-hat (:289) equals the selected candidate's
 // p-hat (same arguments), so it is not re-evaluated.
@@ -360,43 +401,24 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
     constexpr int kB = T == TRAV_LANE ? RS_RIS_BATCH_LANE : RS_RIS_BATCH;
     float best_phat = 0.0f;
     if (F.m_area > 0) {
-        // area candidates in batches of RS_RIS_BATCH: sample + unoccluded f for the batch, ONE lockstep
-        // walk for the batch's shadow rays, then the reservoir updates in candidate order.  The selected
-        // sample is re-drawn from its slots once at the end instead of being carried per candidate.
-        float inv_ma = 1.0f / (float)F.m_area;
+        // area candidates in batches of kB (area_batch: one walk per batch), then the reservoir updates
+        // in candidate order.  The selected sample and its f are re-drawn from its slots once at the end
+        // instead of being carried per candidate (a selected candidate has w > 0: unoccluded, f = L).
         int sel = -1;
         for (int c0 = 0; c0 < F.m_area; c0 += kB) {
-            FPre pre[kB];
-            float Wc[kB], mis[kB];
-            bool act[kB], occ[kB];
-            vec3 dir[kB];
-            float tf[kB];
-            const ShadeFrame sf = fs.load();
-#pragma unroll
-            for (int k = 0; k < kB; ++k) {
-                const bool inb = c0 + k < F.m_area;
-                rng.n = cand_slot(c0 + k);
-                Sample s = area_sample(S, F, pos, sf, rng, Wc[k], mis[k]);
-                pre[k] = evaluate_f_pre(F, s, pos, false, sf, tv, alive && inb);
-                act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
-                rays += act[k] ? 1u : 0u;
-            }
-            if (tv) trace_any_multi<T, kB>(S, act, pos, dir, FLT_MIN + F.tnear_off, tf, occ);
+            float w[kB];
+            area_batch<T, kB>(S, F, pos, fs.load(), rng, c0, F.m_area, alive, tv, w, rays);
 #pragma unroll
             for (int k = 0; k < kB; ++k) {
                 if (c0 + k < F.m_area) {
-                    vec3 f = evaluate_f_post(pre[k], occ[k]);
-                    float ph = length(f);
-                    float w = F.m_brdf > 0 ? mis[k] * ph * Wc[k] : inv_ma * ph * Wc[k];
                     rng.n = cand_slot(c0 + k) + 3u;
-                    if (alive && res_add_w(r, w, 1, rng)) { sel = c0 + k; best_phat = ph; f_sel = f; }
+                    if (alive && res_add_w(r, w[k], 1, rng)) sel = c0 + k;
                 }
             }
         }
         if (sel >= 0) {
-            float Wc, mis;
-            rng.n = cand_slot(sel);
-            Sample s = area_sample(S, F, pos, fs.load(), rng, Wc, mis);
+            const Sample s = area_redraw(S, F, pos, fs.load(), rng, sel, tv, f_sel);
+            best_phat = length(f_sel);
             r.p = s.p; r.n = s.n; r.li = s.li;
         }
     }
@@ -517,29 +539,11 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
         Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, (uint32_t)p);
         const int ahi = hi < A ? hi : A;
         for (int c0 = lo; c0 < ahi; c0 += kB) {               // area candidates (:246-266)
-            FPre pre[kB];
-            float Wc[kB], mis[kB];
-            bool act[kB], occ[kB];
-            vec3 dir[kB];
-            float tf[kB];
-            const ShadeFrame sf = fs.load();
+            float w[kB];
+            area_batch<T, kB>(S, F, pos, fs.load(), rng, c0, ahi, alive, tv, w, rays);
 #pragma unroll
-            for (int k = 0; k < kB; ++k) {
-                const bool inb = c0 + k < ahi;
-                rng.n = cand_slot(c0 + k);
-                Sample s = area_sample(S, F, pos, sf, rng, Wc[k], mis[k]);
-                pre[k] = evaluate_f_pre(F, s, pos, false, sf, tv, alive && inb);
-                act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
-                rays += act[k] ? 1u : 0u;
-            }
-            if (tv) trace_any_multi<T, kB>(S, act, pos, dir, FLT_MIN + F.tnear_off, tf, occ);
-#pragma unroll
-            for (int k = 0; k < kB; ++k) {
-                if (c0 + k < ahi) {
-                    const float ph = length(evaluate_f_post(pre[k], occ[k]));
-                    L.w[(c0 + k) * 64 + lane] = B > 0 ? mis[k] * ph * Wc[k] : (1.0f / (float)A) * ph * Wc[k];
-                }
-            }
+            for (int k = 0; k < kB; ++k)
+                if (c0 + k < ahi) L.w[(c0 + k) * 64 + lane] = w[k];
         }
         for (int c = lo > A ? lo : A; c < hi; ++c) {                     // BRDF candidates (:268-286)
             float Wc, mis;
@@ -566,11 +570,7 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
             if (alive && res_add_w(r, L.w[c * 64 + lane], 1, rng)) sel = c;
         }
         if (sel >= 0) {                                                 // re-draw the selected area sample
-            float Wc, mis;
-            rng.n = cand_slot(sel);
-            const ShadeFrame sf = fs.load();
-            Sample s = area_sample(S, F, pos, sf, rng, Wc, mis);
-            f_sel = evaluate_f_pre(F, s, pos, false, sf, tv, true).L;
+            const Sample s = area_redraw(S, F, pos, fs.load(), rng, sel, tv, f_sel);
             best_phat = length(f_sel);
             r.p = s.p; r.n = s.n; r.li = s.li;
         }

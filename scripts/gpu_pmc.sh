@@ -2,6 +2,8 @@
 # PMC HBM-traffic passes (one counter group per run, kernel-trace only besides --pmc).  The traversal
 # kind is pinned (RESTIR_TRAVERSAL, default lockstep) so AUTO's tuning frames do not mix both kinds.
 export RESTIR_TRAVERSAL=${RESTIR_TRAVERSAL:-lockstep}
+# one frame in flight: counters are read per dispatch, and overlapping frames would add their traffic
+export RESTIR_RUNAHEAD=${RESTIR_RUNAHEAD:-0}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
 mkdir -p gpurun_out

@@ -34,6 +34,8 @@ for k, d in vals.items():
                          "bytes_per_px_corrected": round((2 * fe + wr) * 1024 / px, 2)}
 if "k_gbuffer_initial" in res["kernels"]:
     res["k_gbuffer_initial_bytes_per_launch"] = res["kernels"]["k_gbuffer_initial"]["hbm_bytes_corrected"]
+# one frame = one launch of each pass kernel (C2: initial + spatial)
+res["frame_bytes"] = sum(v["hbm_bytes_corrected"] for v in res["kernels"].values())
 # instruction-issue pass (SQ counters; SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* / SQ_WAIT_* are quad-cycles)
 sq_csv = os.path.join(src, "pmc_SQ_WAVES", "run_counter_collection.csv")
 if os.path.exists(sq_csv):
