@@ -36,6 +36,7 @@ VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2   # wave64 VALU instr/ns: 1024 SIMD-32s, 2 cy
 WORKLOADS = {
     "C1": "Cornell box, 8 emissive quads, reference defaults (A=1 B=1, no reuse)",
     "C2": "Cornell box + 1024 emissive quads, A=32 B=1, spatial k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20",
+    "C2V": "C2 with doVisibilityPass (initial candidates without shadow rays, one visibility ray per pixel)",
     "C3": "Sponza-like ~250k tris, 4096 emissive triangles (2048 lamp quads), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
     "C5": "C2 scene, 240-frame camera orbit (r=0.3) + moving lights (light CDF recomputed + BVH refit on the GPU every frame), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
 }
@@ -48,10 +49,12 @@ DOMINANT_BYTES_PER_PX = 80 + 48
 def frame_bytes_per_px(prm) -> int:
     """Compulsory HBM bytes per pixel of one whole frame in this build's layout (each per-pixel record
     read / written once per pass; neighbour and reprojected reads are the same records): initial
-    G + R write 128; temporal G cur + G prev + R cur + R prev read, R write 304; each spatial pass G + R
+    G + R write 128; visibility pass 68; temporal G cur + G prev + R cur + R prev read, R write 304; each spatial pass G + R
     read, R write 176; framebuffer write 12 (fused into the last pass; a separate shade pass reads
     G + R: +128).  SURVEY.md §8(d) prices the reference's unfused passes (480 B at C2)."""
     b = 128
+    if prm.do_visibility_pass:                 # G position + reservoir read, W write
+        b += 16 + 48 + 4
     if prm.do_temporal:
         b += 304
     if prm.do_spatial and prm.spatial_passes > 0:
@@ -68,7 +71,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--scene", default="C2", choices=["C1", "C2", "C3", "C5"])
+    ap.add_argument("--scene", default="C2", choices=["C1", "C2", "C2V", "C3", "C5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
@@ -129,6 +132,8 @@ def main():
         sc, prm = scenes.cornell_box(8), default_params()
     elif args.scene == "C2":
         sc, prm = scenes.cornell_many_lights(1024), metric_params()
+    elif args.scene == "C2V":   # doVisibilityPass variant (1 shadow ray instead of A per pixel)
+        sc, prm = scenes.cornell_many_lights(1024), metric_params(do_visibility_pass=1)
     elif args.scene == "C3":
         sc, prm = scenes.sponza_like(), c3_params()
     else:   # C5: C2's scene, 240-frame camera orbit + moving lights, temporal reuse with M-cap 20
@@ -238,7 +243,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic (procedural scene, BASELINE.json configs[{ {'C1': 0, 'C2': 1, 'C3': 2, 'C5': 4}[args.scene]}])",
+            "data": f"synthetic (procedural scene, BASELINE.json configs[{ {'C1': 0, 'C2': 1, 'C2V': 1, 'C3': 2, 'C5': 4}[args.scene]}])",
             "config": {"workload": f"{args.scene}: {WORKLOADS[args.scene]}, {W}x{H}",
                        "width": W, "height": H, "parallelism": f"row-bands x{world}" if world > 1 else "1 GPU",
                        "traversal": trav_name, "frames_in_flight": inflight},

@@ -225,9 +225,11 @@ __device__ __forceinline__ ShadeFrame make_frame(const GElem& g, vec3 cam) {
 __device__ __forceinline__ bool is_phong(int type) { return type == MT_PHONG || type == MT_DIELECTRIC; }
 // MaterialPhong::evalPdf -- the MIS pdf is always Phong's (pg/ReSTIRIntegrator.h:54-59,
 // pg/MaterialPhong.cpp:150-172)
+// Lambert surfaces (ks = 0: omp = 0) add the lobe term a * pow(..) * 0 = +0 exactly (a finite, the pow in
+// [0, 1]), so the powf is skipped for them -- the MIS pdf of every area candidate on a diffuse wall
 __device__ __forceinline__ float phong_pdf(const ShadeFrame& s, vec3 wi) {
     float pdf = gmax(dot(s.nrm, wi), 0.0f) * kOneOverPi * s.pf;
-    pdf += s.a * powf(gmax(0.0f, dot(wi, s.wr)), s.shin) * s.omp;
+    pdf += (s.omp != 0.0f || !isfinite(s.a)) ? s.a * powf(gmax(0.0f, dot(wi, s.wr)), s.shin) * s.omp : 0.0f;
     return pdf;
 }
 // BRDF eval dispatch (pg/ReSTIRIntegrator.h:32-41): Phong for PHONG/DIELECTRIC

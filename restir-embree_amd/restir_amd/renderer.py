@@ -124,6 +124,14 @@ def load_library(path: str = LIB_PATH):
     if _lib is not None:
         return _lib
     path = os.environ.get("RESTIR_LIB", path)     # A/B builds of the same ABI (scripts/ab_variants.sh)
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7 (same soname as
+    # /opt/rocm's, which this library links).  Whichever is loaded first serves both, and torch cannot
+    # initialise the device on a runtime other than its own -- so torch (when installed: it carries
+    # the multi-GPU plumbing) is imported before this library is dlopen-ed.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(path):
         raise RestirError(f"{path} not found: build it with `make -C restir-embree_amd` (hipcc, gfx950)")
     L = ctypes.CDLL(path)

@@ -271,6 +271,24 @@ def test_run_ahead_bit_identical(which):
             _assert_close(out[2][f], o.render(os_, cam(f), prm, f), f"{which} run-ahead frame {f}")
 
 
+def test_spatial_reuse_variance_matches_oracle():
+    """SURVEY.md §8(c) / north star: spatial-reuse variance -- per-pixel variance over 64 frame indices
+    (static camera, temporal off, metric point), averaged over non-emissive pixels -- within [0.95, 1.05]
+    of the oracle's."""
+    sc = scenes.cornell_many_lights(256)
+    W, H, N = 64, 40, 64
+    prm = P.metric_params()
+    g = Renderer(W, H)
+    gs = g.load_scene(sc)
+    o, os_ = O.OracleRenderer(W, H), O.OracleScene(sc)
+    gpu = np.stack([g.produce_restir(gs, sc.camera, prm, f).copy() for f in range(N)]).astype(np.float64)
+    ref = np.stack([o.render(os_, sc.camera, prm, f) for f in range(N)]).astype(np.float64)
+    emissive = g.gbuffer()[..., 12:15].max(-1) > 0
+    v_gpu = gpu.mean(-1).var(0)[~emissive].mean()
+    v_ref = ref.mean(-1).var(0)[~emissive].mean()
+    assert 0.95 <= v_gpu / v_ref <= 1.05, (v_gpu, v_ref)
+
+
 def test_c5_moving_lights_match_oracle():
     """C5 extension: lights moved each frame with rs_scene_update_positions (light CDF + BVH rebuilt)
     under an orbiting camera with temporal + spatial reuse; the oracle renders each frame from a fresh
