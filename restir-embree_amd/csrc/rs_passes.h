@@ -412,7 +412,7 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
             for (int k = 0; k < kB; ++k) {
                 if (c0 + k < F.m_area) {
                     rng.n = cand_slot(c0 + k) + 3u;
-                    if (alive && res_add_w(r, w[k], 1, rng)) sel = c0 + k;
+                    if (alive && res_add_w(r, w[k], 0, rng)) sel = c0 + k;
                 }
             }
         }
@@ -433,10 +433,13 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
             float ph = length(f);
             float w = F.m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
             rng.n = cand_slot(F.m_area + i) + 3u;
-            if (alive && res_add(r, s, w, 1, rng)) { best_phat = ph; f_sel = f; }
+            if (alive && res_add(r, s, w, 0, rng)) { best_phat = ph; f_sel = f; }
         }
     }
     if (!alive) { f_sel = mk(0, 0, 0); return res_empty(); }
+    // every candidate adds confidence 1 (Reservoir::addSample, pg/Reservoir.h:35): counted here, not
+    // carried through the candidate loops (one register less across every shadow walk)
+    r.conf = F.m_area + F.m_brdf;
     float ph = smp_valid(smp_of(r)) ? best_phat : 0.0f;
     r.W = ph > 0.0f ? 1.0f / ph * r.wsum : 0.0f;
     res_cap(r, F.cap);
