@@ -45,9 +45,10 @@
 #ifndef RS_RIS_BATCH
 #define RS_RIS_BATCH 2
 #endif
-// ... and for the per-lane walk (occluded_lane_seq: a lane's rays run back to back in one loop)
+// ... for the per-lane walk: one candidate at a time (per-lane walks gain nothing from batching, and a
+// second pending ray is register pressure inside the walk loop: C3 +1.3 %)
 #ifndef RS_RIS_BATCH_LANE
-#define RS_RIS_BATCH_LANE 2
+#define RS_RIS_BATCH_LANE 1
 #endif
 
 namespace rs {
