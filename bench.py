@@ -32,6 +32,7 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 C5_FRAMES = 240
+TUNE_FRAMES = 6                # RS_TRAVERSAL_AUTO tuning frames (2 kinds x kTuneRuns, restir_capi.hip)
 VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2   # wave64 VALU instr/ns: 1024 SIMD-32s, 2 cycles each, 2.4 GHz
 WORKLOADS = {
     "C1": "Cornell box, 8 emissive quads, reference defaults (A=1 B=1, no reuse)",
@@ -169,8 +170,8 @@ def main():
             dist.barrier()
 
     # initialisation (like the scene load, outside warm-up and timing): RS_TRAVERSAL_AUTO times the two
-    # BVH walk kinds over a scene's first 4 frames, then the history is reset
-    for f in range(4):
+    # BVH walk kinds over a scene's first 6 frames, then the history is reset
+    for f in range(TUNE_FRAMES):
         step(f)
     if world > 1:   # cost-balanced bands from 2 frames' per-row wave times (all ranks agree; resets history)
         bands = tr.rebalance(step, n_frames=2)

@@ -210,9 +210,10 @@ int rs_synchronize(rs_context* ctx);
 /* ---- BVH traversal kind (no reference counterpart: Embree picks its own kernels) ---------------
  * LOCKSTEP: a wave walks the node array together (scalar node loads) -- best for coherent rays.
  * LANE: every lane walks its own path (vector loads) -- best for incoherent rays in large scenes.
- * AUTO (default; env RESTIR_TRAVERSAL=lockstep|lane overrides at context creation): the first four
- * frames of a scene alternate the kinds and time them (the first frame of each kind is a warm-up),
- * later frames use the faster one.  Both kinds return bit-identical frames. */
+ * AUTO (default; env RESTIR_TRAVERSAL=lockstep|lane overrides at context creation): the first six
+ * frames of a scene alternate the kinds and time them (the first frame of each kind is a warm-up; a
+ * tuning frame runs alone, not beside other frames in flight, and only its kernels are timed), later
+ * frames use the faster one.  Both kinds return bit-identical frames. */
 #define RS_TRAVERSAL_AUTO (-1)
 #define RS_TRAVERSAL_LOCKSTEP 0
 #define RS_TRAVERSAL_LANE 1
@@ -226,8 +227,8 @@ int rs_context_get_traversal(const rs_context* ctx, const rs_scene* scene, int* 
  * ON: the initial pass spreads a pixel's A+B candidates over 4 waves of one 8x8-tile workgroup
  * (fills the GPU when a rank renders a small band); OFF: one thread carries all candidates of its
  * pixel; AUTO (default; env RESTIR_SPLIT=on|off overrides at context creation): ON when the launch
- * has fewer than ~3 rounds of one-thread-per-pixel waves for the device and the frame uses the
- * lockstep traversal.  Needs A+B <= 64 and B <= 2
+ * has fewer than one round (frames in flight) or 3 rounds (run-ahead depth 0) of one-thread-per-pixel
+ * waves for the device and the frame uses the lockstep traversal.  Needs A+B <= 64 and B <= 2
  * (OFF otherwise).  Frames are bit-identical either way. */
 #define RS_SPLIT_AUTO (-1)
 #define RS_SPLIT_OFF 0

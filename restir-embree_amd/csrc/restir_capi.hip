@@ -146,6 +146,8 @@ struct rs_context {
     hipEvent_t lane_wait[kLanes] = {};     // a lane's last frame ran on the context's stream: its done event
     int trav = TRAV_LOCKSTEP;
     bool tuning = false;
+    hipEvent_t tune_ev[16] = {};           // tuning frame: events around each spatial kernel (halo exchanges excluded)
+    int tune_n = 0;
     // candidate-split initial pass (rs_passes.h k_gbuffer_initial_split): requested mode, last frame's
     int split_mode = RS_SPLIT_AUTO;
     bool split = false;
@@ -415,6 +417,7 @@ extern "C" void rs_context_destroy(rs_context* c) {
     for (auto& slot : c->evr)
         for (auto& e : slot) if (e) hipEventDestroy(e);
     for (auto& e : c->ev_gt) if (e) hipEventDestroy(e);
+    for (auto& e : c->tune_ev) if (e) hipEventDestroy(e);
     for (auto st : c->lane) if (st) hipStreamDestroy(st);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -1018,24 +1021,38 @@ static void fold_slot(rs_context* c, int s) {
     c->tot_frames++;
 }
 
-// RS_TRAVERSAL_AUTO: the first frames of a scene alternate the two kinds; per kind the first run is a
-// warm-up (lazy code-object load, cold caches), the next kTuneRuns-1 are timed (EV_BEGIN..EV_SHADE).
-constexpr int kTuneRuns = 2;
+// RS_TRAVERSAL_AUTO: the first 2*kTuneRuns frames of a scene alternate the two kinds; per kind the first
+// run is a warm-up (lazy code-object load, cold caches), the next kTuneRuns-1 are timed (their kernels
+// only, each tuning frame running alone: record_traversal_time).
+constexpr int kTuneRuns = 3;
 static void pick_traversal(rs_context* c, const rs_scene* s) {
     c->tuning = false;
     if (c->trav_mode == RS_TRAVERSAL_LOCKSTEP) { c->trav = TRAV_LOCKSTEP; return; }
     if (c->trav_mode == RS_TRAVERSAL_LANE) { c->trav = TRAV_LANE; return; }
     if (s->trav_choice >= 0) { c->trav = s->trav_choice; return; }
     c->trav = s->trav_runs[TRAV_LOCKSTEP] <= s->trav_runs[TRAV_LANE] ? TRAV_LOCKSTEP : TRAV_LANE;
+    for (auto& e : c->tune_ev)
+        if (!e && hipEventCreate(&e) != hipSuccess) { e = nullptr; return; }   // untimed: stays un-tuned
+    c->tune_n = 0;
     c->tuning = true;
 }
 static void record_traversal_time(rs_context* c) {
     if (!c->tuning) return;
     c->tuning = false;
-    float ms = 0.0f;
+    // a tuning frame runs alone (rs_tile_begin: on the context's stream, and the next frame waits for
+    // it), and only its kernels are timed: begin..temporal, each spatial kernel, spatial..shade -- not
+    // the halo exchanges of a multi-GPU frame, which wait for other ranks
+    c->join_next = true;
+    float ms = 0.0f, t = 0.0f;
     if (hipEventSynchronize(c->ev[EV_SHADE]) != hipSuccess ||
-        hipEventElapsedTime(&ms, c->ev[EV_BEGIN], c->ev[EV_SHADE]) != hipSuccess)
+        hipEventElapsedTime(&ms, c->ev[EV_BEGIN], c->ev[EV_TEMPORAL]) != hipSuccess ||
+        hipEventElapsedTime(&t, c->ev[c->tune_n ? EV_SPATIAL : EV_TEMPORAL], c->ev[EV_SHADE]) != hipSuccess)
         return;
+    ms += t;
+    for (int i = 0; i + 1 < c->tune_n; i += 2) {
+        if (hipEventElapsedTime(&t, c->tune_ev[i], c->tune_ev[i + 1]) != hipSuccess) return;
+        ms += t;
+    }
     const rs_scene* s = c->scene;
     if (++s->trav_runs[c->trav] > 1) s->trav_ms[c->trav] += ms;
     if (s->trav_runs[TRAV_LOCKSTEP] >= kTuneRuns && s->trav_runs[TRAV_LANE] >= kTuneRuns)
@@ -1081,14 +1098,18 @@ static CountSlot count_slot(rs_context* c, dim3 grid) {
 // reserve slots for every launch of a frame: initial + visibility + temporal + P spatial + shade
 static dim3 grid_split(int W, int ya, int yb) { return dim3((W + 7) / 8, (yb - ya + 7) / 8); }
 // the initial pass runs candidate-split when asked, or (AUTO) when one thread per pixel would give the
-// launch fewer than 3 rounds of the device's resident waves (a rank's band of a multi-GPU frame) and
+// launch too few rounds of the device's resident waves (a rank's band of a multi-GPU frame) and
 // the walks are lockstep: per-lane walks are latency-bound and need the occupancy the split kernel's
 // LDS takes away (C3 1/8 band: 5.3 ms split vs 4.2 ms one thread per pixel)
 static bool want_split(const rs_context* c, const rs_frame_params* P, int gy0, int gy1) {
     if (P->m_area + P->m_brdf > kSplitMaxCand || P->m_brdf > kSplitMaxBrdf) return false;
     if (c->split_mode == RS_SPLIT_ON) return true;
     if (c->split_mode == RS_SPLIT_OFF) return false;
-    return c->trav == TRAV_LOCKSTEP && grid_waves(grid_rows(c->W, gy0, gy1)) < (size_t)3 * c->wave_slots;
+    // with frames in flight the neighbouring frames fill a launch's tail: split only below one round
+    // (C2 1/4 band, 1.4 rounds: 0.38 ms/frame unsplit vs 0.44 split; 1/8 band, 0.7 rounds: 0.24 split
+    // vs 0.26); one frame at a time, below 3 rounds (1/8 band 0.64 -> 0.40 ms)
+    const size_t rounds = c->ahead > 0 ? 1 : 3;
+    return c->trav == TRAV_LOCKSTEP && grid_waves(grid_rows(c->W, gy0, gy1)) < rounds * c->wave_slots;
 }
 static bool reserve_count_slots(rs_context* c, int k, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
     size_t need = grid_waves(c->split ? grid_split(c->W, gy0, gy1) : grid_rows(c->W, gy0, gy1)) +
@@ -1136,7 +1157,8 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     // a frame that must follow work enqueued on the context's stream since the last frame (geometry
     // updates, ...) simply runs on that stream (it is ordered after every earlier frame there); the next
     // frame on its lane then waits for it
-    const bool on_ctx = D == 0 || c->join_next;
+    pick_traversal(c, s);
+    const bool on_ctx = D == 0 || c->join_next || c->tuning;   // a traversal-tuning frame runs alone
     c->fs = on_ctx ? c->stream : c->lane[c->li];
     if (!c->fbs[c->li]) {                       // a lane's framebuffer, on first use
         const size_t bytes = (size_t)c->W * c->H * 3 * sizeof(float);
@@ -1170,7 +1192,6 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     c->shade_fused = !P->do_visibility_pass && !temporal && !spatial;
     c->temporal_ran = c->spatial_ran = c->ev_temporal = false;
     const DevScene S = s->dev();
-    pick_traversal(c, s);
     c->split = want_split(c, P, F.gy0, F.gy1);
     if (!reserve_count_slots(c, c->li, P, F.gy0, F.gy1, F.y0, F.y1)) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
     if (c->fs != c->stream && c->lane_wait[c->li]) {   // this lane's previous frame ran on the context's stream
@@ -1278,12 +1299,18 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
         const GBuf& G = c->G[c->gcur];
         const ResBuf Rr{c->R[c->rcur]}, Rw{c->R[dst]};
         const bool cm = c->F.mis == MIS_CONSTANT;
+        const bool tev = c->tuning && c->tune_n + 2 <= (int)(sizeof(c->tune_ev) / sizeof(c->tune_ev[0]));
+        if (tev) HIPCHK(c, hipEventRecord(c->tune_ev[c->tune_n], c->fs));
         if (c->trav == TRAV_LANE) {
             if (cm) k_spatial<TRAV_LANE, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
             else k_spatial<TRAV_LANE, 0><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
         } else {
             if (cm) k_spatial<TRAV_LOCKSTEP, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
             else k_spatial<TRAV_LOCKSTEP, 0><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+        }
+        if (tev) {
+            HIPCHK(c, hipEventRecord(c->tune_ev[c->tune_n + 1], c->fs));
+            c->tune_n += 2;
         }
     }
     HIPCHK(c, hipGetLastError());
@@ -1314,7 +1341,7 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
     }
     HIPCHK(c, hipEventRecord(c->ev[EV_SHADE], c->fs));
     c->ev_pending[c->slot] = true;
-    k_reduce_counts_part<<<kReduceBlocks, 1024, 0, c->fs>>>(c->d_part, c->part_used, c->d_red);
+    k_reduce_counts_part<<<kReduceBlocks, kReduceThreads, 0, c->fs>>>(c->d_part, c->part_used, c->d_red);
     k_reduce_counts<<<1, kReduceBlocks, 0, c->fs>>>(c->d_red, c->d_cnt, c->d_tot);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[EV_DONE], c->fs));
@@ -1418,7 +1445,7 @@ extern "C" int rs_render_direct_mis(rs_context* c, const rs_scene* s, const rs_c
     LAUNCH_TRAV(c, k_direct_mis, g, S, F, (int)spp, c->fb, count_slot(c, g));
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(e1, c->stream));
-    k_reduce_counts_part<<<kReduceBlocks, 1024, 0, c->stream>>>(c->d_part, c->part_used, c->d_red);
+    k_reduce_counts_part<<<kReduceBlocks, kReduceThreads, 0, c->stream>>>(c->d_part, c->part_used, c->d_red);
     k_reduce_counts<<<1, kReduceBlocks, 0, c->stream>>>(c->d_red, c->d_cnt, c->d_tot);
     HIPCHK(c, hipGetLastError());
     if (t || frame_rgb_host) {

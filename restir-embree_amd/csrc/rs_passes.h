@@ -101,9 +101,12 @@ __device__ __forceinline__ void count_rays(CountSlot C, uint32_t rays, uint32_t 
 }
 
 // sum n slot pairs into the frame totals (and the context's running totals): kReduceBlocks
-// workgroups reduce contiguous chunks into partials (integer sums: order-free), one workgroup folds
-// them (a single workgroup streaming ~1.6 MB of slots at 1080p was CU-bandwidth bound: 40 us)
-constexpr int kReduceBlocks = 128;
+// one-wave workgroups reduce contiguous chunks into partials (integer sums: order-free), one
+// workgroup folds them (a single workgroup streaming ~1.6 MB of slots at 1080p was CU-bandwidth
+// bound: 40 us).  One wave per workgroup: the reduction runs while other frames' pass kernels fill
+// the CUs, and a 1024-thread workgroup (16 free wave slots on one CU at once) waited ~150 us for a
+// CU to drain -- on the frame's critical path (a rank's band: 0.36 ms initial + 0.15 ms waiting).
+constexpr int kReduceBlocks = 128, kReduceThreads = 64;
 __device__ __forceinline__ void block_sum2(unsigned long long& r, unsigned long long& p) {
     __shared__ unsigned long long sr[16], sp[16];
     for (int o = 32; o > 0; o >>= 1) { r += __shfl_xor(r, o, 64); p += __shfl_xor(p, o, 64); }
@@ -114,10 +117,10 @@ __device__ __forceinline__ void block_sum2(unsigned long long& r, unsigned long 
     if (threadIdx.x == 0)
         for (int i = 0; i < nw; ++i) { r += sr[i]; p += sp[i]; }
 }
-__global__ void __launch_bounds__(1024) k_reduce_counts_part(const uint2* part, size_t n, ulonglong2* partial) {
+__global__ void __launch_bounds__(kReduceThreads) k_reduce_counts_part(const uint2* part, size_t n, ulonglong2* partial) {
     const size_t chunk = (n + gridDim.x - 1) / gridDim.x, b = blockIdx.x * chunk, e = b + chunk < n ? b + chunk : n;
     unsigned long long r = 0, p = 0;
-    for (size_t i = b + threadIdx.x; i < e; i += 1024) { uint2 v = part[i]; r += v.x; p += v.y; }
+    for (size_t i = b + threadIdx.x; i < e; i += kReduceThreads) { uint2 v = part[i]; r += v.x; p += v.y; }
     block_sum2(r, p);
     if (threadIdx.x == 0) partial[blockIdx.x] = make_ulonglong2(r, p);
 }

@@ -42,13 +42,14 @@ def main():
     gss = [x.load_scene(sc) for x in rs]
     r, gs = rs[0], gss[0]
     costs = None
-    if a.balanced:
-        r.track_row_costs(True)
-        for f in range(3):
-            r.produce_restir(gs, sc.camera, prm, f, copy_out=False, timed=False)
-        costs = r.row_costs(reset=True)
-        r.track_row_costs(False)
-        r.reset_history()
+    if a.balanced:   # row costs from full frames of a separate context (the probed scene tunes on its band)
+        rc = Renderer(W, H, device=0, stream=streams[0].cuda_stream)
+        gc = rc.load_scene(sc)
+        rc.track_row_costs(True)
+        for f in range(8):
+            rc.produce_restir(gc, sc.camera, prm, f, copy_out=False, timed=False)
+        costs = rc.row_costs(reset=True)
+        del rc, gc
     cases = [(N, N // 2) for N in (1, 2, 4, 8)]
     if a.only_n:
         cases = [(a.only_n, a.only_n // 2)]
