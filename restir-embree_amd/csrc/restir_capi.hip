@@ -1003,6 +1003,11 @@ static dim3 grid_rows(int W, int ya, int yb) { return dim3((W + 15) / 16, (yb - 
         else kernel<TRAV_LOCKSTEP><<<(grid), 256, 0, (st)>>>(__VA_ARGS__);                     \
     } while (0)
 #define LAUNCH_TRAV(c, kernel, grid, ...) LAUNCH_TRAV_ON(c, (c)->fs, kernel, grid, __VA_ARGS__)
+#define LAUNCH_TRAV_BS(c, kernel, grid, bs, ...)                                                  \
+    do {                                                                                       \
+        if ((c)->trav == TRAV_LANE) kernel<TRAV_LANE><<<(grid), (bs), 0, (c)->fs>>>(__VA_ARGS__); \
+        else kernel<TRAV_LOCKSTEP><<<(grid), (bs), 0, (c)->fs>>>(__VA_ARGS__);                   \
+    } while (0)
 
 // fold a finished frame's pass times (event-ring slot s) into the running totals
 static void fold_slot(rs_context* c, int s) {
@@ -1058,7 +1063,7 @@ static void record_traversal_time(rs_context* c) {
     if (s->trav_runs[TRAV_LOCKSTEP] >= kTuneRuns && s->trav_runs[TRAV_LANE] >= kTuneRuns)
         s->trav_choice = s->trav_ms[TRAV_LANE] < s->trav_ms[TRAV_LOCKSTEP] ? TRAV_LANE : TRAV_LOCKSTEP;
 }
-static size_t grid_waves(dim3 g) { return (size_t)g.x * g.y * 4; }
+static size_t grid_waves(dim3 g, int waves_per_block = 4) { return (size_t)g.x * g.y * waves_per_block; }
 
 // the ray-count slot buffer k (of two: consecutive frames can be in flight) with >= need slots; the
 // frame's launches then take consecutive slices of it (count_slot)
@@ -1076,8 +1081,8 @@ static bool use_parts(rs_context* c, int k, size_t need) {
     return true;
 }
 // ray-count slots for one launch (rs_passes.h CountSlot); capacity is reserved in rs_tile_begin
-static CountSlot count_slot(rs_context* c, dim3 grid) {
-    const size_t n = grid_waves(grid);
+static CountSlot count_slot(rs_context* c, dim3 grid, int waves_per_block = 4) {
+    const size_t n = grid_waves(grid, waves_per_block);
     if (c->part_used + n > c->part_cap) {       // more launches than reserved (a pass re-run): grow, keep slots
         const size_t cap = 2 * (c->part_used + n);
         uint2* np = nullptr;
@@ -1112,7 +1117,7 @@ static bool want_split(const rs_context* c, const rs_frame_params* P, int gy0, i
     return c->trav == TRAV_LOCKSTEP && grid_waves(grid_rows(c->W, gy0, gy1)) < rounds * c->wave_slots;
 }
 static bool reserve_count_slots(rs_context* c, int k, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
-    size_t need = grid_waves(c->split ? grid_split(c->W, gy0, gy1) : grid_rows(c->W, gy0, gy1)) +
+    size_t need = (c->split ? grid_waves(grid_split(c->W, gy0, gy1), kSplit) : grid_waves(grid_rows(c->W, gy0, gy1))) +
                   grid_waves(grid_rows(c->W, y0, y1)) * (4 + (size_t)std::max(0, P->spatial_passes));
     return use_parts(c, k, need);
 }
@@ -1212,8 +1217,8 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     const dim3 gg = grid_rows(c->W, F.gy0, F.gy1), gb = grid_rows(c->W, F.y0, F.y1);
     if (c->split) {
         const dim3 gs = grid_split(c->W, F.gy0, F.gy1);
-        LAUNCH_TRAV(c, k_gbuffer_initial_split, gs, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
-                    c->shade_fused ? 1 : 0, count_slot(c, gs));
+        LAUNCH_TRAV_BS(c, k_gbuffer_initial_split, gs, 64 * kSplit, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
+                    c->shade_fused ? 1 : 0, count_slot(c, gs, kSplit));
     } else {
         LAUNCH_TRAV(c, k_gbuffer_initial, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                     count_slot(c, gg));

@@ -75,7 +75,7 @@ struct Counters { unsigned long long rays, primary, reproj_outside; };   // per-
 // atomics from all 8 XCDs serialise at the memory side: one 64-bit atomicAdd per wave cost ~0.7 ms
 // per 1080p kernel, more than the G-buffer pass itself -- scripts/initial_breakdown.py.)
 struct CountSlot {
-    uint2* part;                         // gridDim.x * gridDim.y * 4 entries (4 waves per workgroup)
+    uint2* part;                         // one entry per wave of the launch
     unsigned long long* outside;         // Counters::reproj_outside (rare: tile-edge reprojections)
     float* row_cost;                     // per-image-row wave time (rs_context_track_row_costs), or null
     int y0, y1;                          // rows whose cost is recorded (the rank's band)
@@ -90,7 +90,7 @@ __device__ __forceinline__ uint64_t wave_clock() { return __builtin_amdgcn_s_mem
 __device__ __forceinline__ void count_rays(CountSlot C, uint32_t rays, uint32_t primary, uint64_t t0, int y) {
     uint32_t r = wave_sum(rays), p = wave_sum(primary);
     if ((threadIdx.x & 63) == 0)
-        C.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)] = make_uint2(r, p);
+        C.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)] = make_uint2(r, p);
     // load-balancing record (TiledRenderer.rebalance): the wave's lifetime, charged to its top row.
     // Row-spread same-address atomics, only while tracking is on (calibration frames).
     if (C.row_cost) {
@@ -496,7 +496,10 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
 // A selected candidate always has w > 0, hence p-hat > 0, hence an unoccluded f: its f is the
 // evaluate_f_pre L of the re-drawn sample, no shadow ray needed.  BRDF candidates cannot be re-drawn
 // without their closest-hit ray, so their sample and f go through LDS too.
-constexpr int kSplit = 4;                 // waves (candidate groups) per 8x8 tile
+#ifndef RS_SPLIT_WAVES
+#define RS_SPLIT_WAVES 4
+#endif
+constexpr int kSplit = RS_SPLIT_WAVES;    // waves (candidate groups) per 8x8 tile
 constexpr int kSplitMaxCand = 64;         // A + B the split kernel keeps in LDS
 constexpr int kSplitMaxBrdf = 2;          // B the split kernel keeps in LDS
 struct SplitLds {
@@ -510,7 +513,7 @@ __device__ __forceinline__ void split_range(int n, int g, int& lo, int& hi) {
 }
 
 template <int T>
-__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_WAVES_LANE)) k_gbuffer_initial_split(DevScene S, FrameConst F, GBuf G,
+__global__ void __launch_bounds__(64 * kSplit, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_WAVES_LANE)) k_gbuffer_initial_split(DevScene S, FrameConst F, GBuf G,
                                                                                   ResBuf Rw, float* fb, int fuse_shade,
                                                                                   CountSlot C) {
     const uint64_t t0 = wave_clock();
