@@ -115,7 +115,7 @@ struct rs_context {
     size_t part_caps[kLanes] = {};
     int pk = 0;
     Counters* d_tot = nullptr;             // running totals over frames (rs_get_timing_totals)
-    ulonglong2* d_red = nullptr;           // k_reduce_counts_part partials (= reds[li])
+    ulonglong2* d_red = nullptr;           // k_reduce_counts partials + ticket (= reds[li])
     ulonglong2* reds[kLanes] = {};
     // pass timing without a per-frame host sync: every frame records into its own slot of an event
     // ring; slots are folded into the running totals lazily (when reused, or on rs_get_timing_totals)
@@ -292,7 +292,8 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
     c->fb = c->fbs[0];
     for (int i = 0; i < kLanes; ++i) {
         if (hipMalloc(&c->cnts[i], sizeof(Counters)) != hipSuccess) return bail("hipMalloc(counters) failed");
-        if (hipMalloc(&c->reds[i], kReduceBlocks * sizeof(ulonglong2)) != hipSuccess) return bail("hipMalloc(partials) failed");
+        if (hipMalloc(&c->reds[i], (kReduceBlocks + 1) * sizeof(ulonglong2)) != hipSuccess) return bail("hipMalloc(partials) failed");
+        hipMemsetAsync(c->reds[i], 0, (kReduceBlocks + 1) * sizeof(ulonglong2), c->stream);   // ticket = 0
         hipMemsetAsync(c->cnts[i], 0, sizeof(Counters), c->stream);
     }
     c->d_cnt = c->cnts[0]; c->d_red = c->reds[0];
@@ -1208,7 +1209,8 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     // ones that can still run beside this frame
     if (c->fs != c->stream && c->prev_begin) HIPCHK(c, hipStreamWaitEvent(c->fs, c->prev_begin, 0));
     c->join_next = false;
-    HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->fs));
+    // (the frame's Counters need no memset: k_reduce_counts stores rays/primary, and the initial pass
+    // zeroes reproj_outside before the temporal pass can count -- one API call less per frame)
     c->slot = (int)(c->seq++ % rs_context::kEvRing);
     fold_slot(c, c->slot);                      // the slot's previous frame (kEvRing frames ago)
     for (int i = 0; i < EV_COUNT; ++i) c->ev[i] = c->evr[c->slot][i];
@@ -1346,8 +1348,8 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
     }
     HIPCHK(c, hipEventRecord(c->ev[EV_SHADE], c->fs));
     c->ev_pending[c->slot] = true;
-    k_reduce_counts_part<<<kReduceBlocks, kReduceThreads, 0, c->fs>>>(c->d_part, c->part_used, c->d_red);
-    k_reduce_counts<<<1, kReduceBlocks, 0, c->fs>>>(c->d_red, c->d_cnt, c->d_tot);
+    k_reduce_counts<<<kReduceBlocks, kReduceThreads, 0, c->fs>>>(c->d_part, c->part_used, c->d_red,
+                                                                 (unsigned*)(c->d_red + kReduceBlocks), c->d_cnt, c->d_tot);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[EV_DONE], c->fs));
     c->last_done = c->ev[EV_DONE];
@@ -1450,8 +1452,8 @@ extern "C" int rs_render_direct_mis(rs_context* c, const rs_scene* s, const rs_c
     LAUNCH_TRAV(c, k_direct_mis, g, S, F, (int)spp, c->fb, count_slot(c, g));
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(e1, c->stream));
-    k_reduce_counts_part<<<kReduceBlocks, kReduceThreads, 0, c->stream>>>(c->d_part, c->part_used, c->d_red);
-    k_reduce_counts<<<1, kReduceBlocks, 0, c->stream>>>(c->d_red, c->d_cnt, c->d_tot);
+    k_reduce_counts<<<kReduceBlocks, kReduceThreads, 0, c->stream>>>(c->d_part, c->part_used, c->d_red,
+                                                                     (unsigned*)(c->d_red + kReduceBlocks), c->d_cnt, c->d_tot);
     HIPCHK(c, hipGetLastError());
     if (t || frame_rgb_host) {
         if (frame_rgb_host)

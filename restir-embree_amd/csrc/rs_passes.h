@@ -101,9 +101,9 @@ __device__ __forceinline__ void count_rays(CountSlot C, uint32_t rays, uint32_t 
 }
 
 // sum n slot pairs into the frame totals (and the context's running totals): kReduceBlocks
-// one-wave workgroups reduce contiguous chunks into partials (integer sums: order-free), one
-// workgroup folds them (a single workgroup streaming ~1.6 MB of slots at 1080p was CU-bandwidth
-// bound: 40 us).  One wave per workgroup: the reduction runs while other frames' pass kernels fill
+// one-wave workgroups reduce contiguous chunks into partials (integer sums: order-free), the last
+// one folds them (a single workgroup streaming ~1.6 MB of slots at 1080p was CU-bandwidth bound:
+// 40 us).  One wave per workgroup: the reduction runs while other frames' pass kernels fill
 // the CUs, and a 1024-thread workgroup (16 free wave slots on one CU at once) waited ~150 us for a
 // CU to drain -- on the frame's critical path (a rank's band: 0.36 ms initial + 0.15 ms waiting).
 constexpr int kReduceBlocks = 128, kReduceThreads = 64;
@@ -117,19 +117,34 @@ __device__ __forceinline__ void block_sum2(unsigned long long& r, unsigned long 
     if (threadIdx.x == 0)
         for (int i = 0; i < nw; ++i) { r += sr[i]; p += sp[i]; }
 }
-__global__ void __launch_bounds__(kReduceThreads) k_reduce_counts_part(const uint2* part, size_t n, ulonglong2* partial) {
+// One launch: every workgroup publishes its partial, and the last one to finish (a device-scope
+// ticket; acquire/release at agent scope, since the partials come from all XCDs) folds them into the
+// frame's totals and re-arms the ticket for the lane's next frame.  (Two launches cost one more
+// ~11 us hipLaunchKernel on the host per frame.)
+__global__ void __launch_bounds__(kReduceThreads) k_reduce_counts(const uint2* part, size_t n, ulonglong2* partial,
+                                                                  unsigned* ticket, Counters* out, Counters* tot) {
     const size_t chunk = (n + gridDim.x - 1) / gridDim.x, b = blockIdx.x * chunk, e = b + chunk < n ? b + chunk : n;
     unsigned long long r = 0, p = 0;
     for (size_t i = b + threadIdx.x; i < e; i += kReduceThreads) { uint2 v = part[i]; r += v.x; p += v.y; }
     block_sum2(r, p);
-    if (threadIdx.x == 0) partial[blockIdx.x] = make_ulonglong2(r, p);
-}
-__global__ void __launch_bounds__(kReduceBlocks) k_reduce_counts(const ulonglong2* partial, Counters* out, Counters* tot) {
-    unsigned long long r = partial[threadIdx.x].x, p = partial[threadIdx.x].y;
+    __shared__ bool last;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&partial[blockIdx.x].x, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&partial[blockIdx.x].y, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    r = 0; p = 0;
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += kReduceThreads) {
+        r += __hip_atomic_load(&partial[i].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        p += __hip_atomic_load(&partial[i].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     block_sum2(r, p);
     if (threadIdx.x == 0) {
         out->rays = r; out->primary = p;
         atomicAdd(&tot->rays, r); atomicAdd(&tot->primary, p);   // frames of several lanes may finish together
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -464,6 +479,7 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
                                                                             ResBuf Rw, float* fb, int fuse_shade,
                                                                             CountSlot C) {
     const uint64_t t0 = wave_clock();
+    if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F.gy0, F.gy1, F.W, x, y);
@@ -517,6 +533,7 @@ __global__ void __launch_bounds__(64 * kSplit, RS_WAVES(T, RS_INITIAL_WAVES, RS_
                                                                                   ResBuf Rw, float* fb, int fuse_shade,
                                                                                   CountSlot C) {
     const uint64_t t0 = wave_clock();
+    if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
     __shared__ SplitLds L;
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
     int x = blockIdx.x * 8 + (lane & 7), y = F.gy0 + blockIdx.y * 8 + (lane >> 3);
