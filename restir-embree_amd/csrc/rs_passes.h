@@ -283,10 +283,15 @@ __device__ __forceinline__ uint32_t light_index(const DevScene& S, float ksi) {
 
 // areaSampleLight (pg/ReSTIRIntegrator.cpp:89-124), TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54),
 // Sampling::sampleTriangle (pg/Sampling.cpp:63-76)
-__device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
-                                              Rng& rng, float& W_out, float& mis_out) {
-    float ksi = rng.range(0.0f, 1.0f);
-    const uint32_t idx = light_index(S, ksi);
+// the emissive-triangle pick of candidate c alone (its first RNG slot): the CDF search is a chain of
+// dependent loads, so the initial pass issues the next batch's picks before the current batch's walk
+__device__ __forceinline__ uint32_t area_pick(const DevScene& S, const Rng& rng, int c) {
+    Rng q = rng;
+    q.n = cand_slot(c);
+    return light_index(S, q.range(0.0f, 1.0f));
+}
+__device__ __forceinline__ Sample area_sample_at(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
+                                                 Rng& rng, uint32_t idx, float& W_out, float& mis_out) {
     const float4* E = S.emis + 8 * idx;
     float4 P0 = E[0], P1 = E[1], P2 = E[2];
     float r1 = rng.range(0, 1), r2 = rng.range(0, 1);
@@ -304,6 +309,11 @@ __device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameCons
     mis_out = m_area(F, pdf_area, pba);
     W_out = 1.0f / pdf_area;
     return Sample{pt, nn, xyz(E[6])};
+}
+__device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
+                                              Rng& rng, float& W_out, float& mis_out) {
+    const uint32_t idx = light_index(S, rng.range(0.0f, 1.0f));
+    return area_sample_at(S, F, pos, sf, rng, idx, W_out, mis_out);
 }
 
 // brdfSampleLight (pg/ReSTIRIntegrator.cpp:126-177)
@@ -371,8 +381,8 @@ struct FrameSlot {
 // both produce bit for bit.  (The selected candidate's f is re-derived from its re-drawn sample.)
 template <int T, int kB>
 __device__ __forceinline__ void area_batch(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
-                                           Rng& rng, int c0, int c_end, bool alive, bool tv, float* w_out,
-                                           uint32_t& rays) {
+                                           Rng& rng, int c0, int c_end, bool alive, bool tv, const uint32_t* pick,
+                                           float* w_out, uint32_t& rays) {
     float wu[kB], wo[kB];
     bool act[kB], okb[kB], occ[kB];
     vec3 dir[kB];
@@ -381,8 +391,8 @@ __device__ __forceinline__ void area_batch(const DevScene& S, const FrameConst& 
 #pragma unroll
     for (int k = 0; k < kB; ++k) {
         float Wc, mis;
-        rng.n = cand_slot(c0 + k);
-        const Sample s = area_sample(S, F, pos, sf, rng, Wc, mis);
+        rng.n = cand_slot(c0 + k) + 1u;                 // slot +0 was the pick (area_pick)
+        const Sample s = area_sample_at(S, F, pos, sf, rng, pick[k], Wc, mis);
         const FPre p = evaluate_f_pre(F, s, pos, false, sf, tv, alive && c0 + k < c_end);
         const float ph = length(p.L);
         const float m = F.m_brdf > 0 ? mis : inv_ma;
@@ -424,9 +434,17 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
         // in candidate order.  The selected sample and its f are re-drawn from its slots once at the end
         // instead of being carried per candidate (a selected candidate has w > 0: unoccluded, f = L).
         int sel = -1;
+        uint32_t pick[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) pick[k] = area_pick(S, rng, k);
         for (int c0 = 0; c0 < F.m_area; c0 += kB) {
             float w[kB];
-            area_batch<T, kB>(S, F, pos, fs.load(), rng, c0, F.m_area, alive, tv, w, rays);
+            uint32_t next[kB];
+#pragma unroll
+            for (int k = 0; k < kB; ++k) next[k] = area_pick(S, rng, c0 + kB + k);   // in flight during the walk
+            area_batch<T, kB>(S, F, pos, fs.load(), rng, c0, F.m_area, alive, tv, pick, w, rays);
+#pragma unroll
+            for (int k = 0; k < kB; ++k) pick[k] = next[k];
 #pragma unroll
             for (int k = 0; k < kB; ++k) {
                 if (c0 + k < F.m_area) {
@@ -567,7 +585,10 @@ __global__ void __launch_bounds__(64 * kSplit, RS_WAVES(T, RS_INITIAL_WAVES, RS_
         const int ahi = hi < A ? hi : A;
         for (int c0 = lo; c0 < ahi; c0 += kB) {               // area candidates (:246-266)
             float w[kB];
-            area_batch<T, kB>(S, F, pos, fs.load(), rng, c0, ahi, alive, tv, w, rays);
+            uint32_t pick[kB];
+#pragma unroll
+            for (int k = 0; k < kB; ++k) pick[k] = area_pick(S, rng, c0 + k);
+            area_batch<T, kB>(S, F, pos, fs.load(), rng, c0, ahi, alive, tv, pick, w, rays);
 #pragma unroll
             for (int k = 0; k < kB; ++k)
                 if (c0 + k < ahi) L.w[(c0 + k) * 64 + lane] = w[k];
