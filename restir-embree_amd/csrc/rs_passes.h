@@ -281,8 +281,6 @@ __device__ __forceinline__ uint32_t light_index(const DevScene& S, float ksi) {
     return lo < S.n_emis ? lo : S.n_emis - 1;
 }
 
-// areaSampleLight (pg/ReSTIRIntegrator.cpp:89-124), TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54),
-// Sampling::sampleTriangle (pg/Sampling.cpp:63-76)
 // the emissive-triangle pick of candidate c alone (its first RNG slot): the CDF search is a chain of
 // dependent loads, so the initial pass issues the next batch's picks before the current batch's walk
 __device__ __forceinline__ uint32_t area_pick(const DevScene& S, const Rng& rng, int c) {
@@ -290,6 +288,8 @@ __device__ __forceinline__ uint32_t area_pick(const DevScene& S, const Rng& rng,
     q.n = cand_slot(c);
     return light_index(S, q.range(0.0f, 1.0f));
 }
+// areaSampleLight (pg/ReSTIRIntegrator.cpp:89-124), TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54),
+// Sampling::sampleTriangle (pg/Sampling.cpp:63-76)
 __device__ __forceinline__ Sample area_sample_at(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
                                                  Rng& rng, uint32_t idx, float& W_out, float& mis_out) {
     const float4* E = S.emis + 8 * idx;
