@@ -652,14 +652,16 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
         float inv_area = 1.0f / area[e];
         float pdf_brdf = area[e] / total;
         pdf_brdf *= 1.0f / area[e];
-        em[8 * e + 0] = make_float4(p[0], p[1], p[2], pick);
-        em[8 * e + 1] = make_float4(p[3], p[4], p[5], inv_area);
-        em[8 * e + 2] = make_float4(p[6], p[7], p[8], pdf_brdf);
-        em[8 * e + 3] = make_float4(q[0], q[1], q[2], 0.0f);
-        em[8 * e + 4] = make_float4(q[3], q[4], q[5], 0.0f);
-        em[8 * e + 5] = make_float4(q[6], q[7], q[8], 0.0f);
-        em[8 * e + 6] = make_float4(d.emission[0], d.emission[1], d.emission[2], 0.0f);
-        em[8 * e + 7] = make_float4(area[e], 0.0f, 0.0f, 0.0f);
+        const bool flat = std::memcmp(q, q + 3, 3 * sizeof(float)) == 0 && std::memcmp(q, q + 6, 3 * sizeof(float)) == 0;
+        const float pdf_area = pick * inv_area;           // the product areaSampleLight forms (rs_passes.h EmisRec)
+        em[8 * e + 0] = make_float4(p[0], p[1], p[2], flat ? pdf_area : -pdf_area);
+        em[8 * e + 1] = make_float4(p[3], p[4], p[5], q[0]);
+        em[8 * e + 2] = make_float4(p[6], p[7], p[8], q[1]);
+        em[8 * e + 3] = make_float4(d.emission[0], d.emission[1], d.emission[2], q[2]);
+        em[8 * e + 4] = make_float4(q[3], q[4], q[5], pick);
+        em[8 * e + 5] = make_float4(q[6], q[7], q[8], pdf_brdf);
+        em[8 * e + 6] = make_float4(area[e], inv_area, 0.0f, 0.0f);
+        em[8 * e + 7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     std::vector<int> guide(kCdfGuide + 1);     // guide[j] = lower_bound(cdf, j / kCdfGuide)
     for (int j = 0; j <= kCdfGuide; ++j) {
@@ -722,14 +724,18 @@ __device__ __forceinline__ void light_table(const float* __restrict__ pos, const
         const float area = 0.5f * length(cross(b - a, c - a));         // Triangle::area, pg/triangle.cpp:13-16
         const float4 n0 = tri_nrm[3 * t], n1 = tri_nrm[3 * t + 1], n2 = tri_nrm[3 * t + 2];
         const int m = __float_as_int(n0.w);
-        em[8 * e + 0] = make_float4(p[0], p[1], p[2], 0.0f);
-        em[8 * e + 1] = make_float4(p[3], p[4], p[5], 0.0f);
-        em[8 * e + 2] = make_float4(p[6], p[7], p[8], 0.0f);
-        em[8 * e + 3] = make_float4(n0.x, n0.y, n0.z, 0.0f);
+        // record layout: rs_passes.h EmisRec (the .w of e0/e4/e5 and e6.y are set below)
+        const bool flat = __float_as_uint(n0.x) == __float_as_uint(n1.x) && __float_as_uint(n0.y) == __float_as_uint(n1.y) &&
+                          __float_as_uint(n0.z) == __float_as_uint(n1.z) && __float_as_uint(n0.x) == __float_as_uint(n2.x) &&
+                          __float_as_uint(n0.y) == __float_as_uint(n2.y) && __float_as_uint(n0.z) == __float_as_uint(n2.z);
+        em[8 * e + 0] = make_float4(p[0], p[1], p[2], flat ? 0.0f : -0.0f);   // sign bit: normals differ
+        em[8 * e + 1] = make_float4(p[3], p[4], p[5], n0.x);
+        em[8 * e + 2] = make_float4(p[6], p[7], p[8], n0.y);
+        em[8 * e + 3] = f4(xyz(mats[kMatStride * m + 2]), n0.z);
         em[8 * e + 4] = make_float4(n1.x, n1.y, n1.z, 0.0f);
         em[8 * e + 5] = make_float4(n2.x, n2.y, n2.z, 0.0f);
-        em[8 * e + 6] = f4(xyz(mats[kMatStride * m + 2]), 0.0f);
-        em[8 * e + 7] = make_float4(area, 0.0f, 0.0f, 0.0f);
+        em[8 * e + 6] = make_float4(area, 0.0f, 0.0f, 0.0f);
+        em[8 * e + 7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     __syncthreads();
     // TriangleCDF ctor, pg/TriangleCDF.cpp:8-34: the total and the prefix sum are sequential float
@@ -737,7 +743,7 @@ __device__ __forceinline__ void light_table(const float* __restrict__ pos, const
     float total = 0.0f;
     for (uint32_t c0 = 0; c0 < ne; c0 += kLightChunk) {
         const uint32_t m = min(ne - c0, (uint32_t)kLightChunk);
-        for (uint32_t j = threadIdx.x; j < m; j += kLightBlock) s_a[j] = em[8 * (c0 + j) + 7].x;
+        for (uint32_t j = threadIdx.x; j < m; j += kLightBlock) s_a[j] = em[8 * (c0 + j) + 6].x;
         __syncthreads();
         if (threadIdx.x == 0) {
 #pragma unroll 16
@@ -751,7 +757,7 @@ __device__ __forceinline__ void light_table(const float* __restrict__ pos, const
     float pred = 0.0f;
     for (uint32_t c0 = 0; c0 < ne; c0 += kLightChunk) {
         const uint32_t m = min(ne - c0, (uint32_t)kLightChunk);
-        for (uint32_t j = threadIdx.x; j < m; j += kLightBlock) s_a[j] = em[8 * (c0 + j) + 7].x / total;
+        for (uint32_t j = threadIdx.x; j < m; j += kLightBlock) s_a[j] = em[8 * (c0 + j) + 6].x / total;
         __syncthreads();
         if (threadIdx.x == 0) {
 #pragma unroll 16
@@ -762,13 +768,15 @@ __device__ __forceinline__ void light_table(const float* __restrict__ pos, const
         __syncthreads();
     }
     for (uint32_t e = threadIdx.x; e < ne; e += kLightBlock) {
-        const float area = em[8 * e + 7].x;
+        const float area = em[8 * e + 6].x;
         const float pick = e == 0 ? cdf[0] : cdf[e] - cdf[e - 1];
         float pdf_brdf = area / total;
         pdf_brdf *= 1.0f / area;
-        em[8 * e + 0].w = pick;
-        em[8 * e + 1].w = 1.0f / area;
-        em[8 * e + 2].w = pdf_brdf;
+        const float inv_area = 1.0f / area, pdf_area = pick * inv_area;
+        em[8 * e + 0].w = (__float_as_uint(em[8 * e + 0].w) >> 31) ? -pdf_area : pdf_area;
+        em[8 * e + 4].w = pick;
+        em[8 * e + 5].w = pdf_brdf;
+        em[8 * e + 6].y = inv_area;
     }
     for (int j = threadIdx.x; j <= kCdfGuide; j += kLightBlock) {   // lower_bound(cdf, j / kCdfGuide)
         const float key = (float)j / (float)kCdfGuide;

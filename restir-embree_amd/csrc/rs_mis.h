@@ -88,7 +88,7 @@ __device__ __forceinline__ vec3 mis_brdf_part(const DevScene& S, const FrameCons
     float cI = gmax(dot(ld, h.n), 0.0f);
     float cY = gmax(dot(-ld, bn), 0.0f);
     float amf = cY / r2;
-    float pdf_light = S.emis[8 * b.emis_id + 2].w;                 // TriangleCDF::getPDFForTriangle
+    float pdf_light = emis_pdf_brdf(S, b.emis_id);                 // TriangleCDF::getPDFForTriangle
     float w = mis_power(pdf * amf, pdf_light);
     return dvs(((m.le * w) * f_r) * cI, pdf);
 }
@@ -100,14 +100,13 @@ __device__ __forceinline__ vec3 mis_light_part(const DevScene& S, const FrameCon
     if (S.n_emis == 0) return mk(0, 0, 0);                          // TriangleCDF::isValid (uniform)
     float ksi = rng.range(0.0f, 1.0f);                              // TriangleCDF::getTriangle
     const uint32_t idx = light_index(S, ksi);
-    const float4* E = S.emis + 8 * idx;
-    const float4 P0 = E[0], P1 = E[1], P2 = E[2];
+    const EmisRec E = EmisRec::load(S.emis + 8 * idx);
     float r1 = rng.range(0, 1), r2 = rng.range(0, 1);                // Sampling::sampleTriangle
     float sr = sqrtf(r1);
     float bx = 1.0f - sr, by = sr * (1.0f - r2), bz = sr * r2;
-    vec3 pt = (xyz(P0) * bx + xyz(P1) * by) + xyz(P2) * bz;
-    vec3 nn = normalize((xyz(E[3]) * bx + xyz(E[4]) * by) + xyz(E[5]) * bz);
-    float light_pdf = P0.w * P1.w;                                   // pick prob * (1 / area)
+    vec3 pt = (E.p0 * bx + E.p1 * by) + E.p2 * bz;
+    vec3 nn = normalize((E.n0 * bx + E.n1 * by) + E.n2 * bz);
+    float light_pdf = E.pdf_area;                                    // pick prob * (1 / area)
     vec3 ld = pt - h.pos;
     float r_sqr = dot(ld, ld);
     ld = normalize(ld);
@@ -121,7 +120,7 @@ __device__ __forceinline__ vec3 mis_light_part(const DevScene& S, const FrameCon
     float w = mis_power(light_pdf, pba);
     if (!(w > 0.0f)) return mk(0, 0, 0);
     float G = cI * cY / r_sqr;
-    return dvs(((xyz(E[6]) * w) * mis_brdf(h, ld)) * G, light_pdf);
+    return dvs(((E.le * w) * mis_brdf(h, ld)) * G, light_pdf);
 }
 
 template <int T>

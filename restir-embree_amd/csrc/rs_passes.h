@@ -288,18 +288,41 @@ __device__ __forceinline__ uint32_t area_pick(const DevScene& S, const Rng& rng,
     q.n = cand_slot(c);
     return light_index(S, q.range(0.0f, 1.0f));
 }
+// An emissive triangle's record, 8 float4 (one 128-B line):
+//   e0 (p0, pdf_area)  e1 (p1, n0.x)  e2 (p2, n0.y)  e3 (le, n0.z)
+//   e4 (n1, pick)      e5 (n2, pdf_brdf)  e6 (area, inv_area, 0, 0)  e7 unused
+// pdf_area = pick * inv_area (TriangleCDF pick probability x 1/area, the product areaSampleLight forms),
+// its sign bit set when the vertex normals differ.  An area sample of a flat emitter (all vertex normals
+// equal -- every quad light) reads e0..e3 only: 4 loads instead of 7 per candidate, the light-table
+// gathers being ~18 % of the C2 initial pass.  A flat emitter's n1 = n2 = n0 bit for bit, so the
+// interpolated normal is computed with the same operands either way.
+struct EmisRec {
+    vec3 p0, p1, p2, n0, n1, n2, le;
+    float pdf_area;
+    __device__ __forceinline__ static EmisRec load(const float4* E) {
+        const float4 a = E[0], b = E[1], c = E[2], d = E[3];
+        EmisRec r;
+        r.p0 = xyz(a); r.p1 = xyz(b); r.p2 = xyz(c); r.le = xyz(d);
+        r.n0 = mk(b.w, c.w, d.w);
+        r.n1 = r.n0; r.n2 = r.n0;
+        if (__float_as_uint(a.w) >> 31) { r.n1 = xyz(E[4]); r.n2 = xyz(E[5]); }
+        r.pdf_area = fabsf(a.w);
+        return r;
+    }
+};
+__device__ __forceinline__ float emis_pdf_brdf(const DevScene& S, int id) { return S.emis[8 * id + 5].w; }
+
 // areaSampleLight (pg/ReSTIRIntegrator.cpp:89-124), TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54),
 // Sampling::sampleTriangle (pg/Sampling.cpp:63-76)
 __device__ __forceinline__ Sample area_sample_at(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
                                                  Rng& rng, uint32_t idx, float& W_out, float& mis_out) {
-    const float4* E = S.emis + 8 * idx;
-    float4 P0 = E[0], P1 = E[1], P2 = E[2];
+    const EmisRec E = EmisRec::load(S.emis + 8 * idx);
     float r1 = rng.range(0, 1), r2 = rng.range(0, 1);
     float sr = sqrtf(r1);
     float bx = 1.0f - sr, by = sr * (1.0f - r2), bz = sr * r2;
-    vec3 pt = (xyz(P0) * bx + xyz(P1) * by) + xyz(P2) * bz;
-    vec3 nn = normalize((xyz(E[3]) * bx + xyz(E[4]) * by) + xyz(E[5]) * bz);
-    float pdf_area = P0.w * P1.w;           // pick prob * (1 / area)
+    vec3 pt = (E.p0 * bx + E.p1 * by) + E.p2 * bz;
+    vec3 nn = normalize((E.n0 * bx + E.n1 * by) + E.n2 * bz);
+    float pdf_area = E.pdf_area;            // pick prob * (1 / area)
     vec3 ld = pt - pos;
     float r2s = dot(ld, ld);
     ld = normalize(ld);
@@ -308,7 +331,7 @@ __device__ __forceinline__ Sample area_sample_at(const DevScene& S, const FrameC
     float pba = phong_pdf(sf, ld) * amf;
     mis_out = m_area(F, pdf_area, pba);
     W_out = 1.0f / pdf_area;
-    return Sample{pt, nn, xyz(E[6])};
+    return Sample{pt, nn, E.le};
 }
 __device__ __forceinline__ Sample area_sample(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
                                               Rng& rng, float& W_out, float& mis_out) {
@@ -339,7 +362,7 @@ __device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameCons
             ld = normalize(ld);
             float cY = gmax(dot(-ld, hn), 0.0f);
             float amf = cY / r2s;
-            float pdf_area = S.emis[8 * h.emis_id + 2].w;   // getPDFForTriangle (pg/TriangleCDF.h:25-31)
+            float pdf_area = emis_pdf_brdf(S, h.emis_id);   // getPDFForTriangle (pg/TriangleCDF.h:25-31)
             float bpa = pdf * amf;
             W_out = 1.0f / bpa;
             mis_out = m_brdf(F, bpa, pdf_area);

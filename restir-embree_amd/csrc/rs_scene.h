@@ -26,8 +26,7 @@ struct DevScene {
     const float4* tri_nrm;    // 3 per prim: n0 (w = material id bits), n1 (w = emissive id bits), n2
     const float4* mats;       // 4 per material: (kd, shin), (ks, type bits), (le, 0), map ids (int bits, -1 none:
                               //   diffuse, specular, shininess, normal)
-    const float4* emis;       // 8 per emissive triangle: p0,p1,p2 (w: pick_pdf, inv_area, pdf_brdf_area),
-                              //   n0, n1, n2, le, (area, 0, 0, 0)
+    const float4* emis;       // 8 per emissive triangle (one 128-B line; layout at EmisRec)
     const float* cdf;         // cumulative normalised area (TriangleCDF::cdf2)
     const int* cdf_guide;     // kCdfGuide+1 entries: lower_bound(cdf, j / kCdfGuide)
     uint32_t n_nodes, n_tris, n_emis, n_mats;
