@@ -1319,6 +1319,9 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
         if (c->trav == TRAV_LANE) {
             if (cm) k_spatial<TRAV_LANE, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
             else k_spatial<TRAV_LANE, 0><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+        } else if (grid_waves(gb) < (size_t)2 * c->wave_slots) {   // a small launch: RS_SPATIAL_WAVES_SMALL budget
+            if (cm) k_spatial<TRAV_LOCKSTEP, 1, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+            else k_spatial<TRAV_LOCKSTEP, 0, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
         } else {
             if (cm) k_spatial<TRAV_LOCKSTEP, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
             else k_spatial<TRAV_LOCKSTEP, 0><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);

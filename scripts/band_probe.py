@@ -45,8 +45,10 @@ def main():
     if a.balanced:   # row costs from full frames of a separate context (the probed scene tunes on its band)
         rc = Renderer(W, H, device=0, stream=streams[0].cuda_stream)
         gc = rc.load_scene(sc)
+        for f in range(6):          # traversal tuning first (bench.py order): costs of the settled kind only
+            rc.produce_restir(gc, sc.camera, prm, f, copy_out=False, timed=False)
         rc.track_row_costs(True)
-        for f in range(8):
+        for f in range(6, 10):
             rc.produce_restir(gc, sc.camera, prm, f, copy_out=False, timed=False)
         costs = rc.row_costs(reset=True)
         del rc, gc
