@@ -69,7 +69,7 @@ def test_metric_point_tiles():
 
 
 # ---------------------------------------------------------------- real processes, real GPU contexts
-def _gpu_worker(rank, world, port, W, H, out_path, rebalance):
+def _gpu_worker(rank, world, port, W, H, out_path, rebalance, async_gather=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "restir-embree_amd"), os.path.join(root, "tests")]
@@ -84,7 +84,7 @@ def _gpu_worker(rank, world, port, W, H, out_path, rebalance):
     sc = scenes.cornell_many_lights(256)
     prm = P.c3_params(m_area=8, spatial_passes=2)
     tr = TiledRenderer(W, H, rank, world, device=0, stream=torch.cuda.current_stream().cuda_stream,
-                       temporal_margin=H)
+                       temporal_margin=H, async_gather=async_gather)
     s = tr.load_scene(sc)
     if rebalance:   # bands from the GPU's own per-row wave times (unequal in general)
         bands = tr.rebalance(lambda i: tr.render(s, sc.camera, prm, i), n_frames=2, min_rows=6)
@@ -92,6 +92,7 @@ def _gpu_worker(rank, world, port, W, H, out_path, rebalance):
     frames = []
     for f in range(3):
         fr = tr.render(s, scenes.orbit_camera(sc.camera, f, 24, 0.25), prm, f)
+        tr.wait()
         if rank == 0:
             frames.append(fr.cpu().numpy().copy())
     if rank == 0:
@@ -100,11 +101,12 @@ def _gpu_worker(rank, world, port, W, H, out_path, rebalance):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rebalance", [(2, False), (3, True)])
-def test_multiprocess_tiles_on_gpu_match_full_frame(world, rebalance, tmp_path):
-    """TiledRenderer + GpuTileBackend in 2 real processes (one HIP context each on the same GPU; halo
+@pytest.mark.parametrize("world,rebalance,async_gather", [(2, False, False), (3, True, True)])
+def test_multiprocess_tiles_on_gpu_match_full_frame(world, rebalance, async_gather, tmp_path):
+    """TiledRenderer + GpuTileBackend in 2-3 real processes (one HIP context each on the same GPU; halo
     exchange and gather over gloo, staged through host memory because RCCL refuses two ranks on one
-    device): the gathered frames equal a single-context full frame bit for bit."""
+    device; the 3-rank case with bench.py's async gather: per-lane process groups and framebuffers):
+    the gathered frames equal a single-context full frame bit for bit."""
     import socket
     import torch.multiprocessing as mp
     from restir_amd import params as P, scenes
@@ -114,7 +116,7 @@ def test_multiprocess_tiles_on_gpu_match_full_frame(world, rebalance, tmp_path):
     s.close()
     W, H = 48, 40
     out = str(tmp_path / "frames.npy")
-    mp.spawn(_gpu_worker, args=(world, port, W, H, out, rebalance), nprocs=world, join=True)
+    mp.spawn(_gpu_worker, args=(world, port, W, H, out, rebalance, async_gather), nprocs=world, join=True)
     got = np.load(out)
     sc = scenes.cornell_many_lights(256)
     prm = P.c3_params(m_area=8, spatial_passes=2)
