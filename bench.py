@@ -120,11 +120,20 @@ def main():
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # RESTIR_DIST_BACKEND=gloo rehearses the N>1 flow with more ranks than GPUs (ranks share devices,
+    # halo/gather staged through host memory); the measured configuration is RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("RESTIR_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
+    red_dev = "cpu" if backend == "gloo" else "cuda"
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     W, H = args.width, args.height
     camera = None                       # per-frame camera (C5 orbit); None = the scene's static camera
@@ -197,12 +206,12 @@ def main():
     acc = {k: float(getattr(tot, k)) for k in keys}
     rays = int(tot.rays)
     if dist is not None:
-        tt = torch.tensor([dt, float(rays)], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt, float(rays)], dtype=torch.float64, device=red_dev)
         dmax = tt.clone()
         dist.all_reduce(dmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
         dt, rays = float(dmax[0]), int(tt[1])
-        acc_t = torch.tensor([acc[k] for k in acc], dtype=torch.float64, device="cuda")
+        acc_t = torch.tensor([acc[k] for k in acc], dtype=torch.float64, device=tt.device)
         dist.all_reduce(acc_t, op=dist.ReduceOp.MAX)
         acc = {k: float(v) for k, v in zip(acc, acc_t.tolist())}
     ms_per_step = dt / args.steps * 1e3
