@@ -27,8 +27,9 @@
 #ifndef RS_SPATIAL_WAVES
 #define RS_SPATIAL_WAVES 4
 #endif
-// ... for a small lockstep spatial launch (a rank's band: < 2 rounds of waves), where fewer, faster
-// waves shorten the launch's tail (C2 1/8 band: 0.244 ms/frame at 4 waves vs 0.253 at 5)
+// ... for a small lockstep spatial launch (a rank's band: < 2 rounds of waves), which runs beside the
+// other frames in flight (C2 balanced bands, 5 vs 4 waves: 1/4 band 0.373 vs 0.383 ms/frame, 1/8 band
+// 0.241 vs 0.244; a full-size launch stays at 4: 5 cost C5 3.7 %)
 #ifndef RS_SPATIAL_WAVES_SMALL
 #define RS_SPATIAL_WAVES_SMALL RS_SPATIAL_WAVES
 #endif
