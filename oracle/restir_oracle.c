@@ -695,13 +695,21 @@ static inline sample_t smp_invalid(void) { sample_t s; s.p = V(-FLT_MAX, -FLT_MA
 static inline int smp_valid(sample_t s) {
     or_res r; r.p = s.p; r.n = s.n; r.li = s.li; return sample_valid(&r);
 }
-/* Reservoir::addSample (pg/Reservoir.h:33-47) */
-static inline int res_add(or_res* r, sample_t s, float w, int conf, rng_t* rng) {
+/* Reservoir::addSample (pg/Reservoir.h:33-47), in two halves so the golden-vector hook below can
+ * replay a recorded U stream through the same code: res_update accumulates and says whether a U is
+ * drawn (not when w == 0 && w_sum == 0), res_take decides with that U. */
+static inline int res_update(or_res* r, float w, int conf) {
     r->wsum += w;
     r->conf += conf;
-    if (w == 0 && r->wsum == 0) return 0;
-    if (rng_u(rng) < w / r->wsum) { r->p = s.p; r->n = s.n; r->li = s.li; return 1; }
+    return !(w == 0 && r->wsum == 0);
+}
+static inline int res_take(or_res* r, sample_t s, float w, float u) {
+    if (u < w / r->wsum) { r->p = s.p; r->n = s.n; r->li = s.li; return 1; }
     return 0;
+}
+static inline int res_add(or_res* r, sample_t s, float w, int conf, rng_t* rng) {
+    if (!res_update(r, w, conf)) return 0;
+    return res_take(r, s, w, rng_u(rng));
 }
 /* Reservoir::capConfidence (pg/Reservoir.h:54-56) */
 static inline void res_cap(or_res* r, int cap) { r->conf = r->conf < cap ? r->conf : cap; }
@@ -743,14 +751,20 @@ static hitinfo intersect(const fctx* F, v3 o, v3 d, float tnear, uint64_t* rays)
     return hi;
 }
 
+/* CosineWeightedDistribution::getPdf (pg/Distribution.h:33-35) */
+static inline float cosine_pdf(v3 n, v3 wi) { return gmax(dot(n, wi), 0.0f) * OR_ONE_OVER_PI; }
+/* CosineLobeDistribution::getPdf (pg/Distribution.h:65-67) */
+static inline float lobe_pdf(v3 wi, v3 wr, float gamma) {
+    return (gamma + 1.0f) * OR_ONE_OVER_2PI * powf(gmax(0.0f, dot(wi, wr)), gamma);
+}
 /* pdf eval dispatch: always MaterialPhong::evalPdf (pg/ReSTIRIntegrator.h:54-59, pg/MaterialPhong.cpp:150-172) */
 static float phong_eval_pdf(const or_gbe* g, v3 cam, v3 wi) {
     float maxD = maxc(g->kd), maxS = maxc(g->ks);
     float pf = maxD / (maxD + maxS);
-    float pdf = gmax(dot(g->nrm, wi), 0.0f) * OR_ONE_OVER_PI * pf;
+    float pdf = cosine_pdf(g->nrm, wi) * pf;
     v3 wo = nrmz(sub(g->pos, cam));
     v3 wr = nrmz(reflect(wo, g->nrm));
-    pdf += (g->shin + 1.0f) * OR_ONE_OVER_2PI * powf(gmax(0.0f, dot(wi, wr)), g->shin) * (1.0f - pf);
+    pdf += lobe_pdf(wi, wr, g->shin) * (1.0f - pf);
     return pdf;
 }
 
@@ -806,22 +820,28 @@ static v3 to_world(v3 smp, v3 n) {
              o1.y * smp.x + o2.y * smp.y + n.y * smp.z,
              o1.z * smp.x + o2.z * smp.y + n.z * smp.z);
 }
-static v3 cosine_sample(v3 n, rng_t* rng) {
-    float r1 = rnd(rng, 0, 1), r2 = rnd(rng, 0, 1);
+static v3 cosine_sample_u(v3 n, float r1, float r2) {
     float ang = OR_PI * 2.0f * r1;
     float x = cosf(ang) * sqrtf(1.0f - r2);
     float y = sinf(ang) * sqrtf(1.0f - r2);
     float z = sqrtf(r2);
     return to_world(nrmz(V(x, y, z)), n);
 }
-/* CosineLobeDistribution::sample (pg/Distribution.h:37-57) */
-static v3 lobe_sample(v3 wr, float gamma, rng_t* rng) {
+static v3 cosine_sample(v3 n, rng_t* rng) {
     float r1 = rnd(rng, 0, 1), r2 = rnd(rng, 0, 1);
+    return cosine_sample_u(n, r1, r2);
+}
+/* CosineLobeDistribution::sample (pg/Distribution.h:37-57) */
+static v3 lobe_sample_u(v3 wr, float gamma, float r1, float r2) {
     float ang = 2.0f * OR_PI * r1;
     float x = cosf(ang) * sqrtf(1.0f - powf(r2, 2.0f / (gamma + 1.0f)));
     float y = sinf(ang) * sqrtf(1.0f - powf(r2, 2.0f / (gamma + 1.0f)));
     float z = powf(r2, 1.0f / (gamma + 1.0f));
     return to_world(nrmz(V(x, y, z)), wr);
+}
+static v3 lobe_sample(v3 wr, float gamma, rng_t* rng) {
+    float r1 = rnd(rng, 0, 1), r2 = rnd(rng, 0, 1);
+    return lobe_sample_u(wr, gamma, r1, r2);
 }
 
 /* BRDF sampling dispatch (pg/ReSTIRIntegrator.h:43-52): returns omega_i and pdf */
@@ -829,7 +849,7 @@ static v3 sample_brdf(const or_gbe* g, v3 cam, rng_t* rng, float* pdf_out) {
     if (g->type == MT_LAMBERT) {
         /* MaterialLambert::sampleBRDF (pg/MaterialLambert.cpp:43-53) */
         v3 wi = cosine_sample(g->nrm, rng);
-        *pdf_out = gmax(dot(g->nrm, wi), 0.0f) * OR_ONE_OVER_PI;
+        *pdf_out = cosine_pdf(g->nrm, wi);
         return wi;
     }
     /* MaterialPhong::sampleBRDF (pg/MaterialPhong.cpp:174-222) */
@@ -841,8 +861,8 @@ static v3 sample_brdf(const or_gbe* g, v3 cam, rng_t* rng, float* pdf_out) {
     v3 wi;
     if (r0 < maxD) wi = cosine_sample(g->nrm, rng);
     else wi = lobe_sample(wr, g->shin, rng);
-    float pd = gmax(dot(g->nrm, wi), 0.0f) * OR_ONE_OVER_PI * pf;
-    float ps = (g->shin + 1.0f) * OR_ONE_OVER_2PI * powf(gmax(0.0f, dot(wi, wr)), g->shin) * (1.0f - pf);
+    float pd = cosine_pdf(g->nrm, wi) * pf;
+    float ps = lobe_pdf(wi, wr, g->shin) * (1.0f - pf);
     *pdf_out = pd + ps;
     return wi;
 }
@@ -1397,14 +1417,10 @@ static inline float mis_power(float pdf, float other) {   /* DirectMISIntegrator
     return a / (b + a);
 }
 static inline v3 dvs(v3 v, float s) { return V(v.x / s, v.y / s, v.z / s); }   /* glm vec3 / scalar */
-static inline float cos_pdf(v3 n, v3 wi) { return gmax(dot(n, wi), 0.0f) * OR_ONE_OVER_PI; }  /* pg/Distribution.h:33-35 */
-static inline float lobe_pdf(v3 wi, v3 wr, float g) {      /* CosineLobeDistribution::getPdf (pg/Distribution.h:65-67) */
-    return (g + 1.0f) * OR_ONE_OVER_2PI * powf(gmax(0.0f, dot(wi, wr)), g);
-}
 /* getPdfForSample (pg/MaterialLambert.cpp:20-23, pg/MaterialPhong.cpp:94-119) */
 static float mis_pdf_for(const mis_surf* h, v3 wi) {
-    if (!h->phong) return cos_pdf(h->n, wi);
-    float pdf = cos_pdf(h->n, wi) * h->pf;
+    if (!h->phong) return cosine_pdf(h->n, wi);
+    float pdf = cosine_pdf(h->n, wi) * h->pf;
     pdf += lobe_pdf(wi, h->wr, h->shin) * (1.0f - h->pf);
     return pdf;
 }
@@ -1418,7 +1434,7 @@ static v3 mis_brdf(const mis_surf* h, v3 wi) {
 static v3 mis_sample(const mis_surf* h, rng_t* rng, v3* f_r, float* pdf) {
     if (!h->phong) {
         v3 wi = cosine_sample(h->n, rng);
-        *pdf = cos_pdf(h->n, wi);
+        *pdf = cosine_pdf(h->n, wi);
         *f_r = dvs(h->kd, OR_PI);
         return wi;
     }
@@ -1431,7 +1447,7 @@ static v3 mis_sample(const mis_surf* h, rng_t* rng, v3* f_r, float* pdf) {
         wi = lobe_sample(h->wr, h->shin, rng);
         *f_r = scl(scl(h->ks, h->i_m), powf(gmax(dot(wi, h->wr), 0.0f), h->shin));
     }
-    float pd = cos_pdf(h->n, wi) * h->pf;
+    float pd = cosine_pdf(h->n, wi) * h->pf;
     float ps = lobe_pdf(wi, h->wr, h->shin) * (1.0f - h->pf);
     *pdf = pd + ps;
     if (dot(h->n, wi) < 0) *f_r = V(0, 0, 0);
@@ -1677,3 +1693,51 @@ void or_post_apply(int W, int y0, int y1, const float* frame, float* acc, int ac
     if (sum) *sum = s;
     if (sqr_sum) *sqr_sum = q;
 }
+
+/* ------------------------------------------------------------------ golden-vector hooks (tests only) */
+/* Reference header-only code compiled by oracle/kat/gen_refheaders.cpp (tests/golden/refheaders_kat.json)
+ * replays recorded U streams; these hooks run the oracle's own functions over the same streams. */
+/* a sequence of addSample(sample_i, w[i], conf[i]) then capConfidence(cap) (pg/Reservoir.h:33-56):
+ * out_i = {chosen sample index or -1, draws consumed, confidence before cap, after cap, hasSample,
+ * bestSample.isValid}; *out_wsum = w_sum; taken[i] = 1 where addSample returned true */
+void or_kat_reservoir(const float* w, const int32_t* conf, int n, const float* u, int nu, int cap,
+                      float* out_wsum, int32_t* out_i, int32_t* taken) {
+    or_res r = res_empty();
+    int used = 0;
+    for (int i = 0; i < n; ++i) {
+        sample_t s = {V((float)i, 0.5f, -0.5f), V(0.0f, 0.0f, 1.0f), V(1.0f, 2.0f, 3.0f)};
+        taken[i] = 0;
+        if (res_update(&r, w[i], conf[i])) taken[i] = res_take(&r, s, w[i], u[used++ % nu]);
+    }
+    out_i[0] = r.p.x == -FLT_MAX ? -1 : (int)r.p.x;
+    out_i[1] = used;
+    out_i[2] = r.conf;
+    res_cap(&r, cap);
+    out_i[3] = r.conf;
+    out_i[4] = r.wsum > 0.0f;                  /* Reservoir::hasSample (pg/Reservoir.h:49-52) */
+    out_i[5] = sample_valid(&r);
+    *out_wsum = r.wsum;
+}
+int or_kat_light_sample_valid(const float* p, const float* n, const float* li) {
+    or_res r = res_empty();
+    r.p = V(p[0], p[1], p[2]); r.n = V(n[0], n[1], n[2]); r.li = V(li[0], li[1], li[2]);
+    return sample_valid(&r);
+}
+/* CosineWeightedDistribution::sample / getPdf with draws (r1, r2) (pg/Distribution.h:10-35) */
+void or_kat_cosine(const float* n, float r1, float r2, const float* other, float* out5) {
+    v3 N = V(n[0], n[1], n[2]);
+    v3 wi = cosine_sample_u(N, r1, r2);
+    out5[0] = wi.x; out5[1] = wi.y; out5[2] = wi.z;
+    out5[3] = cosine_pdf(N, wi);
+    out5[4] = cosine_pdf(N, V(other[0], other[1], other[2]));
+}
+/* CosineLobeDistribution::sample / getPdf (pg/Distribution.h:43-67) */
+void or_kat_lobe(const float* wr, float gamma, float r1, float r2, const float* other, float* out5) {
+    v3 R = V(wr[0], wr[1], wr[2]);
+    v3 wi = lobe_sample_u(R, gamma, r1, r2);
+    out5[0] = wi.x; out5[1] = wi.y; out5[2] = wi.z;
+    out5[3] = lobe_pdf(wi, R, gamma);
+    out5[4] = lobe_pdf(V(other[0], other[1], other[2]), R, gamma);
+}
+float or_kat_power_heuristic(float a, float b) { return mis_power(a, b); }
+float or_kat_max_component(const float* v) { return maxc(V(v[0], v[1], v[2])); }

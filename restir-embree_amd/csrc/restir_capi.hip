@@ -1172,14 +1172,14 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     // updates, ...) simply runs on that stream (it is ordered after every earlier frame there); the next
     // frame on its lane then waits for it
     pick_traversal(c, s);
-    const bool on_ctx = D == 0 || c->join_next || c->tuning;   // a traversal-tuning frame runs alone
-    c->fs = on_ctx ? c->stream : c->lane[c->li];
-    if (!c->fbs[c->li]) {                       // a lane's framebuffer, on first use
-        const size_t bytes = (size_t)c->W * c->H * 3 * sizeof(float);
+    if (!c->fbs[c->li]) {                       // a lane's framebuffer, on first use: cleared on the context's
+        const size_t bytes = (size_t)c->W * c->H * 3 * sizeof(float);   // stream, so this frame runs there too
         HIPCHK(c, hipMalloc(&c->fbs[c->li], bytes));
         HIPCHK(c, hipMemsetAsync(c->fbs[c->li], 0, bytes, c->stream));
         c->join_next = true;
     }
+    const bool on_ctx = D == 0 || c->join_next || c->tuning;   // a traversal-tuning frame runs alone
+    c->fs = on_ctx ? c->stream : c->lane[c->li];
     c->fb = c->fbs[c->li];
     c->d_cnt = c->cnts[c->li]; c->d_red = c->reds[c->li];
     // reservoir ring: `last` = the previous frame's final buffer (reservoirsLastFrame, a pointer swap,

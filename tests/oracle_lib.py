@@ -81,6 +81,16 @@ def lib():
         _f64p = ctypes.POINTER(ctypes.c_double)
         L.or_post_apply.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, _f32p, _f64p, _f64p]
+        L.or_kat_reservoir.argtypes = [_f32p, _i32p, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int, _f32p, _i32p,
+                                       _i32p]
+        L.or_kat_light_sample_valid.restype = ctypes.c_int
+        L.or_kat_light_sample_valid.argtypes = [_f32p, _f32p, _f32p]
+        L.or_kat_cosine.argtypes = [_f32p, ctypes.c_float, ctypes.c_float, _f32p, _f32p]
+        L.or_kat_lobe.argtypes = [_f32p, ctypes.c_float, ctypes.c_float, ctypes.c_float, _f32p, _f32p]
+        L.or_kat_power_heuristic.restype = ctypes.c_float
+        L.or_kat_power_heuristic.argtypes = [ctypes.c_float, ctypes.c_float]
+        L.or_kat_max_component.restype = ctypes.c_float
+        L.or_kat_max_component.argtypes = [_f32p]
         _lib = L
     return _lib
 

@@ -71,6 +71,78 @@ def test_disk_offset_truncation_semantics():
         assert (int(np.float32(ox)), int(np.float32(oy))) == (ix, iy)
 
 
+# ---------------------------------------------------------------- reference header-only code
+# tests/golden/refheaders_kat.json: the reference's own Reservoir.h / Distribution.h / GBufferElement.h /
+# utils.h compiled with its vendored glm (oracle/kat/gen_refheaders.cpp), U streams replayed.
+def test_reservoir_add_sample_bit_exact_vs_reference():
+    """Reservoir::addSample / capConfidence / hasSample / LightSample::isValid (pg/Reservoir.h:6-59): the
+    oracle's res_update/res_take/res_cap consume the same draws, pick the same sample and accumulate
+    the bit-identical w_sum and confidence."""
+    L = O.lib()
+    for case in _kat("refheaders_kat.json")["reservoir"]:
+        w = np.array(case["w"], np.float32)
+        conf = np.array(case["conf"], np.int32)
+        u = np.array(case["u"], np.float32)
+        n = len(w)
+        wsum = np.zeros(1, np.float32)
+        out = np.zeros(6, np.int32)
+        taken = np.zeros(n, np.int32)
+        L.or_kat_reservoir(O._ptr(w), O._ptr(conf, O._i32p), n, O._ptr(u), len(u), case["cap"], O._ptr(wsum),
+                           O._ptr(out, O._i32p), O._ptr(taken, O._i32p))
+        assert wsum[0] == np.float32(case["w_sum"])
+        assert list(out) == [case["chosen"], case["draws"], case["confidence"], case["confidence_capped"],
+                             case["has_sample"], case["valid"]], case
+        assert list(np.nonzero(taken)[0]) == case["taken"]
+
+
+def test_light_sample_is_valid_vs_reference():
+    L = O.lib()
+    for *v, ok in _kat("refheaders_kat.json")["light_sample_valid"]:
+        a = np.array(v, np.float32)
+        assert L.or_kat_light_sample_valid(O._ptr(a[0:3]), O._ptr(a[3:6]), O._ptr(a[6:9])) == ok, v
+
+
+def test_cosine_distributions_bit_exact_vs_reference():
+    """CosineWeightedDistribution / CosineLobeDistribution sample + getPdf (pg/Distribution.h:7-68) with
+    the same (r1, r2) draws, incl. normals along the axes (Utils::orthogonal's branches), r1 = 0,
+    r2 -> 1 and lobe exponents 0..1000: directions and pdfs bit-identical."""
+    L = O.lib()
+    kat = _kat("refheaders_kat.json")
+    out = np.zeros(5, np.float32)
+    for row in kat["cosine_weighted"]:
+        r = np.array(row, np.float32)
+        L.or_kat_cosine(O._ptr(r[0:3]), r[3], r[4], O._ptr(r[9:12]), O._ptr(out))
+        assert np.array_equal(out[:3], r[5:8]) and out[3] == r[8] and out[4] == r[12], row
+    for row in kat["cosine_lobe"]:
+        r = np.array(row, np.float32)
+        L.or_kat_lobe(O._ptr(r[0:3]), r[3], r[4], r[5], O._ptr(r[10:13]), O._ptr(out))
+        assert np.array_equal(out[:3], r[6:9]) and out[3] == r[9] and out[4] == r[13], row
+    assert len(kat["cosine_weighted"]) >= 150 and len(kat["cosine_lobe"]) >= 100
+
+
+def test_utils_inline_helpers_vs_reference():
+    """Utils::powerHeuristic (= DirectMISIntegrator::powerHeuristic) and Utils::maxComponent (pg/utils.h:53-63)."""
+    L = O.lib()
+    kat = _kat("refheaders_kat.json")
+    for a, b, v in kat["power_heuristic"]:
+        assert np.float32(L.or_kat_power_heuristic(a, b)) == np.float32(v)
+    for *xyz, v in kat["max_component"]:
+        a = np.array(xyz, np.float32)
+        assert np.float32(L.or_kat_max_component(O._ptr(a))) == np.float32(v)
+
+
+def test_gbuffer_layout_vs_reference():
+    """GBuffer::setAt (pg/GBufferElement.h:59-70) stores pixel (x, y) at y*W+x of each SoA array -- the
+    row-major pixel index the oracle and the device G-buffer use; isValidForReSTIR <=> zero emission."""
+    g = _kat("refheaders_kat.json")["gbuffer"]
+    W = g["size"][0]
+    where = {i: j for i, j, *_ in g["linear_index"]}
+    for x, y, i, valid in g["set"]:
+        assert where[i] == y * W + x
+        assert valid == (0 if i == 2 else 1)
+    assert g["sizeof_element"] == 72          # SURVEY.md §8: 69 B of payload, padded to 72
+
+
 # ---------------------------------------------------------------- counter RNG
 def test_rng_deterministic_and_uniform():
     L = O.lib()
