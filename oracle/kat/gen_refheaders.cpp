@@ -2,7 +2,9 @@
 // (no stand-ins): pg/Reservoir.h (LightSample / Reservoir::addSample / hasSample / capConfidence,
 // :6-59), pg/Distribution.h (CosineWeightedDistribution / CosineLobeDistribution sample + getPdf,
 // :7-68), pg/GBufferElement.h (GBufferElement::isValidForReSTIR, GBuffer::setAt layout, :6-89) and
-// the inline helpers of pg/utils.h (Utils::powerHeuristic / maxComponent, :53-63), with the vendored
+// the inline helpers of pg/utils.h (Utils::powerHeuristic / maxComponent, :53-63), the MIS weights
+// ReSTIRIntegrator::m_area / m_brdf (pg/ReSTIRIntegrator.h:62-74) and CenterSampler
+// (pg/PixelSampler.h:12-17), with the vendored
 // glm 0.9.9 (and the vendored Embree 3 headers, declarations only: Ray.h names RTCRay).  Built from the files where they lie under /root/reference by oracle/kat/Makefile; the
 // only reference include that does not resolve on a case-sensitive file system, "Utils.h" in
 // Distribution.h, is a symlink to the reference's own utils.h (oracle/_build/refinc/Utils.h).
@@ -21,11 +23,22 @@
 #include <random>
 #include <vector>
 
+#include <memory>
+#include <string>
 #include <embree3/rtcore.h>   // vendored Embree 3.13.5 header: Ray.h (included by Reservoir.h) names RTCRay
+#include <FreeImage.h>        // vendored FreeImage header: Texture.h (via material.h) names BYTE
+#include <imgui.h>            // vendored ImGui header: PixelSampler.h (via camera.h) names ImGui
 #include "utils.h"
 #include "Reservoir.h"
 #include "Distribution.h"
 #include "GBufferElement.h"
+#include "PixelSampler.h"
+#include "ReSTIRIntegrator.h"
+
+// ReSTIRIntegrator's sample-count statics (defined in pg/ReSTIRIntegrator.cpp:13-35); each m_area /
+// m_brdf case below sets them
+int ReSTIRIntegrator::M_Area = 1;
+int ReSTIRIntegrator::M_Brdf = 1;
 
 static std::vector<float> g_stream;
 static size_t g_pos = 0;
@@ -40,6 +53,11 @@ glm::vec3 Utils::orthogonal(const glm::vec3& vec) {
     return glm::abs(vec.x) > glm::abs(vec.z) ? glm::vec3{vec.y, -vec.x, 0.0f} : glm::vec3{0.0f, vec.z, -vec.y};
 }
 
+// a float as JSON: non-finite values (an M_Area of 0 divides by zero) as the strings "inf", "-inf", "nan"
+static void pf(const char* sep, float v) {
+    if (std::isfinite(v)) std::printf("%s%.9g", sep, v);
+    else std::printf("%s\"%s\"", sep, std::isnan(v) ? "nan" : (v > 0 ? "inf" : "-inf"));
+}
 static void replay(const std::vector<float>& u) { g_stream = u; g_pos = 0; g_draws = 0; }
 static void pv(const char* sep, const glm::vec3& v) { std::printf("%s%.9g, %.9g, %.9g", sep, v.x, v.y, v.z); }
 
@@ -176,6 +194,33 @@ int main() {
         std::printf(", %.9g", Utils::maxComponent(v));
     }
     std::printf("]],\n");
+
+    // ---------------------------------------------------------------- ReSTIRIntegrator::m_area / m_brdf
+    std::printf(" \"mis_area_brdf\": [");
+    {
+        const int MA[] = {1, 32, 0, 4, 32, 1, 7};
+        const int MB[] = {1, 1, 1, 0, 2, 3, 5};
+        const float pv_[][2] = {{0.0f, 0.0f}, {1.0f, 0.0f}, {0.0f, 2.5f}, {0.37f, 1.9f}, {1e-30f, 3e-31f},
+                                {12.5f, 0.001f}, {1e20f, 1e19f}, {0.5f, 0.5f}};
+        int i = 0;
+        for (int m = 0; m < 7; ++m)
+            for (auto& q : pv_) {
+                ReSTIRIntegrator::M_Area = MA[m];
+                ReSTIRIntegrator::M_Brdf = MB[m];
+                const float a = ReSTIRIntegrator::m_area(q[0], q[1]);
+                const float b = ReSTIRIntegrator::m_brdf(q[1], q[0]);
+                std::printf("%s[%d, %d, %.9g, %.9g", i++ ? ", " : "", MA[m], MB[m], q[0], q[1]);
+                pf(", ", a);
+                pf(", ", b);
+                std::printf("]");
+            }
+    }
+    std::printf("],\n");
+    {
+        CenterSampler cs;
+        const glm::vec2 o = cs.takeSample();
+        std::printf(" \"center_sampler\": [%.9g, %.9g],\n", o.x, o.y);
+    }
 
     // ---------------------------------------------------------------- GBufferElement / GBuffer
     std::printf(" \"gbuffer\": {\"size\": [7, 5], \"set\": [");

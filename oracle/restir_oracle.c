@@ -1741,3 +1741,11 @@ void or_kat_lobe(const float* wr, float gamma, float r1, float r2, const float* 
 }
 float or_kat_power_heuristic(float a, float b) { return mis_power(a, b); }
 float or_kat_max_component(const float* v) { return maxc(V(v[0], v[1], v[2])); }
+/* ReSTIRIntegrator::m_area(pa, pb) / m_brdf(pb, pa) (pg/ReSTIRIntegrator.h:62-74) at M_Area = A, M_Brdf = B */
+void or_kat_mis(int A, int B, float pa, float pb, float* out2) {
+    or_params P;
+    memset(&P, 0, sizeof P);
+    P.m_area = A; P.m_brdf = B;
+    out2[0] = m_area(&P, pa, pb);
+    out2[1] = m_brdf(&P, pb, pa);
+}

@@ -91,6 +91,7 @@ def lib():
         L.or_kat_power_heuristic.argtypes = [ctypes.c_float, ctypes.c_float]
         L.or_kat_max_component.restype = ctypes.c_float
         L.or_kat_max_component.argtypes = [_f32p]
+        L.or_kat_mis.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float, _f32p]
         _lib = L
     return _lib
 

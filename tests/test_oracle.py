@@ -131,6 +131,19 @@ def test_utils_inline_helpers_vs_reference():
         assert np.float32(L.or_kat_max_component(O._ptr(a))) == np.float32(v)
 
 
+def test_mis_weights_bit_exact_vs_reference():
+    """ReSTIRIntegrator::m_area / m_brdf (pg/ReSTIRIntegrator.h:62-74, compiled from the reference header)
+    over M_Area/M_Brdf in {0..32} x pdf pairs incl. both zero, one zero, tiny and huge; CenterSampler
+    returns the pixel corner (0, 0) (pg/PixelSampler.h:12-17)."""
+    L = O.lib()
+    kat = _kat("refheaders_kat.json")
+    out = np.zeros(2, np.float32)
+    for a, b, pa, pb, wa, wb in kat["mis_area_brdf"]:
+        L.or_kat_mis(a, b, pa, pb, O._ptr(out))       # M_Area = 0 gives inf / nan: compared as such
+        assert np.array_equal(out, np.array([float(wa), float(wb)], np.float32), equal_nan=True), (a, b, pa, pb)
+    assert kat["center_sampler"] == [0, 0]
+
+
 def test_gbuffer_layout_vs_reference():
     """GBuffer::setAt (pg/GBufferElement.h:59-70) stores pixel (x, y) at y*W+x of each SoA array -- the
     row-major pixel index the oracle and the device G-buffer use; isValidForReSTIR <=> zero emission."""
