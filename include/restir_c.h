@@ -117,6 +117,8 @@ typedef struct {
     float total_ms;                /* totalFrameDuration (history copy is a pointer swap: 0) */
     uint64_t rays;                 /* closest-hit + occlusion rays traced this frame (device count) */
     uint64_t primary_rays;
+    uint64_t reproj_outside;       /* G-buffer elements the temporal pass rebuilt because a reprojection fell
+                                      beyond the tile's rows +- margin (0 for full frames; tiles only) */
 } rs_pass_times;
 
 /* ---- device lifecycle (rtcNewDevice / rtcReleaseDevice) ------------------------------------- */
@@ -314,7 +316,8 @@ int rs_dump_reservoirs(rs_context* ctx, float* host_out);
  *   rs_tile_spatial    : one spatial pass on the band (reads the halo rows)
  *   rs_tile_finish     : shade, history swap; returns the band's framebuffer device pointer
  * Per-pixel counter RNG keyed by the full-frame pixel index makes the result bit-identical to a
- * single-GPU frame when margin >= the temporal reprojection displacement. */
+ * single-GPU frame for any margin >= halo: a temporal reprojection beyond the tile's G-buffer rows
+ * rebuilds the element it needs from the frame's camera (counted in rs_pass_times.reproj_outside). */
 typedef struct {
     int32_t y0, y1;         /* band rows, 0 <= y0 < y1 <= height */
     int32_t margin;         /* G-buffer rows recomputed beyond the band (>= halo) */

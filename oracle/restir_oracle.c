@@ -653,6 +653,7 @@ typedef struct {
     int cache_im;             /* 1: cache calc_I_M per pixel (speed only; identical values) */
     float* im_cache[2];       /* 1/calc_I_M per pixel for Phong-dispatched surfaces */
     void* tile;               /* or_tile_state, allocated on first use */
+    uint64_t rebuilt;         /* tile mode: G elements the temporal pass rebuilt beyond the tile's rows */
 } or_ctx;
 
 or_ctx* or_ctx_create(int W, int H) {
@@ -903,35 +904,37 @@ static v3 primary_dir(const or_cam* c, int x, int y, int W, int H) {
     return nrmz(m3_mul(&c->inv_view, dc));
 }
 
-/* gBufferFillPass (pg/ReSTIRIntegrator.cpp:213-234) */
-static void pass_gbuffer(fctx* F, const or_cam* cam, or_gbe* G, float* im, int y0, int y1, uint64_t* rays) {
+/* gBufferFillPass (pg/ReSTIRIntegrator.cpp:213-234) for one pixel and the camera `cam` (Camera::GenerateRay,
+ * pg/camera.cpp:20-42, CenterSampler => pixel corner): the G element and its cached 1/I_M */
+static void gbuffer_elem(const fctx* F, const or_gcam* cam, int x, int y, or_gbe* e, float* imv, uint64_t* rc) {
     const or_params* P = F->P; const or_scene* s = F->s; int W = F->c->W, H = F->c->H;
+    v3 dc = V((float)x - (float)W / 2.0f, (float)H / 2.0f - (float)y, -cam->focal);
+    v3 d = nrmz(m3_mul(&cam->inv_view, dc));
+    hitinfo h = intersect(F, cam->pos, d, FLT_MIN + 0.01f, rc);
+    memset(e, 0, sizeof *e);
+    *imv = 0.0f;
+    if (h.hit) {
+        const or_mat* m = &s->mats[s->mat[h.prim]];
+        e->pos = h.point; e->nrm = h.normal;
+        e->depth = len(sub(h.point, cam->pos));
+        e->type = m->type; e->kd = m->kd; e->ks = m->ks; e->le = m->le; e->shin = m->shin;
+        apply_maps(s, h.prim, h.u, h.v, s->mat[h.prim], &e->kd, &e->ks, &e->shin, &e->nrm, 0);
+        if (e->type == MT_PHONG || e->type == MT_DIELECTRIC) {
+            v3 Vv = nrmz(sub(cam->pos, e->pos));
+            *imv = 1.0f / or_calc_I_M(dot(Vv, e->nrm), e->shin);
+        }
+    } else {
+        e->le = P->use_skybox ? sky_texel(s, d) : V(P->bg_color[0], P->bg_color[1], P->bg_color[2]);
+    }
+}
+static void pass_gbuffer(fctx* F, const or_cam* cam, or_gbe* G, float* im, int y0, int y1, uint64_t* rays) {
+    int W = F->c->W;
+    or_gcam gc; gc.pos = cam->eye; gc.view = cam->view; gc.inv_view = cam->inv_view; gc.focal = cam->focal;
     uint64_t rc = 0;
 #pragma omp parallel for schedule(dynamic, 1) reduction(+:rc)
-    for (int y = y0; y < y1; ++y) {
-        for (int x = 0; x < W; ++x) {
-            v3 d = primary_dir(cam, x, y, W, H);
-            hitinfo h = intersect(F, cam->eye, d, FLT_MIN + 0.01f, &rc);
-            or_gbe e; memset(&e, 0, sizeof e);
-            float imv = 0.0f;
-            if (h.hit) {
-                const or_mat* m = &s->mats[s->mat[h.prim]];
-                e.pos = h.point; e.nrm = h.normal;
-                e.depth = len(sub(h.point, cam->eye));
-                e.type = m->type; e.kd = m->kd; e.ks = m->ks; e.le = m->le; e.shin = m->shin;
-                apply_maps(s, h.prim, h.u, h.v, s->mat[h.prim], &e.kd, &e.ks, &e.shin, &e.nrm, 0);
-                if (e.type == MT_PHONG || e.type == MT_DIELECTRIC) {
-                    v3 Vv = nrmz(sub(cam->eye, e.pos));
-                    imv = 1.0f / or_calc_I_M(dot(Vv, e.nrm), e.shin);
-                }
-            } else {
-                e.le = P->use_skybox ? sky_texel(s, d) : V(P->bg_color[0], P->bg_color[1], P->bg_color[2]);
-            }
-            G[(size_t)y * W + x] = e;
-            im[(size_t)y * W + x] = imv;
-        }
-    }
-    (void)H;
+    for (int y = y0; y < y1; ++y)
+        for (int x = 0; x < W; ++x)
+            gbuffer_elem(F, &gc, x, y, &G[(size_t)y * W + x], &im[(size_t)y * W + x], &rc);
     *rays += rc;
 }
 
@@ -1080,8 +1083,8 @@ static int reproject(const or_gcam* gc, v3 ws, int W, int H, int* sx, int* sy) {
 /* temporalReusePass (pg/ReSTIRIntegrator.cpp:625-732) */
 static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* Rw, int y0, int y1, uint64_t* rays) {
     const or_params* P = F->P; int W = F->c->W, H = F->c->H;
-    uint64_t rc = 0;
-#pragma omp parallel for schedule(dynamic, 1) reduction(+:rc)
+    uint64_t rc = 0, rebuilt = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+:rc, rebuilt)
     for (int y = y0; y < y1; ++y)
         for (int x = 0; x < W; ++x) {
             size_t p = (size_t)y * W + x;
@@ -1091,10 +1094,17 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             const or_res* pr = &Rl[p];       /* previous reservoir read at the CURRENT pixel (:641) */
             int qx, qy;
             if (!reproject(F->gcp, cur->pos, W, H, &qx, &qy)) { Rw[p] = *cr; continue; }
-            /* tile mode: a reprojection outside the G-buffer margin counts as failed (full frame: never) */
-            if (qy < F->gy0 || qy >= F->gy1) { Rw[p] = *cr; continue; }
             size_t q = (size_t)qy * W + qx;
             const or_gbe* prev = &F->Gp[q];
+            float imq = F->imp[q];
+            /* tile mode: an element beyond the tile's G-buffer rows is rebuilt from the previous camera
+               (full frame: never) -- the product's k_temporal does the same */
+            or_gbe prev_alt;
+            if (qy < F->gy0 || qy >= F->gy1) {
+                gbuffer_elem(F, F->gcp, qx, qy, &prev_alt, &imq, &rc);
+                prev = &prev_alt;
+                rebuilt++;
+            }
             float cd = len(sub(cur->pos, ccam));
             float pd = len(sub(prev->pos, pcam));
             float dr = cd > pd ? pd / cd : cd / pd;
@@ -1102,8 +1112,13 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             const or_gbe* pac = &F->Gp[p];
             int fx, fy;
             if (!reproject(F->gc, pac->pos, W, H, &fx, &fy)) { Rw[p] = *cr; continue; }
-            if (fy < F->gy0 || fy >= F->gy1) { Rw[p] = *cr; continue; }
             const or_gbe* fw = &F->G[(size_t)fy * W + fx];
+            or_gbe fw_alt; float im_unused;
+            if (fy < F->gy0 || fy >= F->gy1) {
+                gbuffer_elem(F, F->gc, fx, fy, &fw_alt, &im_unused, &rc);
+                fw = &fw_alt;
+                rebuilt++;
+            }
             float cdp = len(sub(pac->pos, pcam));
             float pdp = len(sub(fw->pos, ccam));
             float drp = cdp > pdp ? pdp / cdp : cdp / pdp;
@@ -1111,7 +1126,7 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
 
             rng_t rng = rng_init(P->seed, F->frame, PASS_TEMPORAL, (uint32_t)p);
             or_res res = res_empty();
-            float imc = F->im[p], imq = F->imp[q];
+            float imc = F->im[p];
             sample_t cs = smp_of(cr), ps = smp_of(pr);
             float p_cur = eval_phat(F, cs, ccam, cur, imc, 1, &rc);
             float p_prev = eval_phat(F, cs, pcam, prev, imq, 1, &rc);
@@ -1134,6 +1149,7 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             Rw[p] = res;
         }
     *rays += rc;
+    F->c->rebuilt += rebuilt;
 }
 
 /* Sampling::sampleDiskUniform (pg/Sampling.cpp:78-87) + vec2 -> ivec2 truncation */
@@ -1749,3 +1765,4 @@ void or_kat_mis(int A, int B, float pa, float pb, float* out2) {
     out2[0] = m_area(&P, pa, pb);
     out2[1] = m_brdf(&P, pb, pa);
 }
+uint64_t or_ctx_rebuilt(const or_ctx* c) { return c->rebuilt; }

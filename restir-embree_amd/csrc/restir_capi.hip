@@ -97,6 +97,7 @@ struct rs_context {
     bool join_next = true;                 // the next frame waits for the context's stream
     GBuf G[kGRing] = {};
     GCam gcam[kGRing] = {};
+    float ginv[kGRing][9] = {};            // each slot's mat3(invViewMat) (a tile's temporal pass rebuilds G)
     int gcur = 0, gprev = 0;
     float4* R[kRRing] = {};
     int r_last = 2;
@@ -1163,6 +1164,8 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     // writes the slot after the current one; G[gcur] becomes the previous frame's
     int gnew = (c->gcur + 1) % kGRing;
     make_camera(cam, c->H, c->gcam[gnew], F.inv_view);
+    std::memcpy(c->ginv[gnew], F.inv_view, sizeof F.inv_view);
+    std::memcpy(F.inv_view_prev, c->ginv[c->gcur], sizeof F.inv_view_prev);
     F.cam = c->gcam[gnew];
     F.camp = c->gcam[c->gcur];
     // the frame's stream: lane seq mod (D+1) (run-ahead), else the context's stream
@@ -1383,6 +1386,7 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
         hipEventElapsedTime(&tot, c->ev[EV_BEGIN], c->ev[EV_SHADE]);
         t->gbuffer_initial_ms = a; t->visibility_ms = b; t->temporal_ms = d; t->spatial_ms = e; t->shade_ms = f;
         t->total_ms = tot; t->rays = c->h_cnt->rays; t->primary_rays = c->h_cnt->primary;
+        t->reproj_outside = c->h_cnt->reproj_outside;
         fold_slot(c, c->slot);
     }
     return RS_OK;
@@ -1399,7 +1403,7 @@ extern "C" int rs_get_timing_totals(rs_context* c, rs_pass_times* sum, uint32_t*
     sum->gbuffer_initial_ms = (float)c->tot_ms[0]; sum->visibility_ms = (float)c->tot_ms[1];
     sum->temporal_ms = (float)c->tot_ms[2]; sum->spatial_ms = (float)c->tot_ms[3];
     sum->shade_ms = (float)c->tot_ms[4]; sum->total_ms = (float)c->tot_ms[5];
-    sum->rays = tot.rays; sum->primary_rays = tot.primary;
+    sum->rays = tot.rays; sum->primary_rays = tot.primary; sum->reproj_outside = tot.reproj_outside;
     if (n_frames) *n_frames = (uint32_t)c->tot_frames;
     if (reset) {
         for (double& v : c->tot_ms) v = 0.0;

@@ -71,6 +71,7 @@ struct FrameConst {
     int y0, y1;           // band this context renders
     int gy0, gy1;         // G-buffer rows computed (band + margin, clamped)
     float inv_view[9];    // mat3(invViewMat), column-major (pg/camera.cpp:57)
+    float inv_view_prev[9];   // ... of the previous frame (a tile's temporal pass rebuilds G elements)
     GCam cam, camp;       // current / previous frame camera (pg/GBufferElement.h:136-139)
 };
 
@@ -150,6 +151,9 @@ __global__ void __launch_bounds__(kReduceThreads) k_reduce_counts(const uint2* p
     if (threadIdx.x == 0) {
         out->rays = r; out->primary = p;
         atomicAdd(&tot->rays, r); atomicAdd(&tot->primary, p);   // frames of several lanes may finish together
+        // the frame's temporal pass (same stream, earlier) has finished counting its tile-edge misses
+        const unsigned long long o = __hip_atomic_load(&out->reproj_outside, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (o) atomicAdd(&tot->reproj_outside, o);
         __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -241,15 +245,17 @@ __device__ __forceinline__ float m_brdf(const FrameConst& F, float pb, float pa)
     return pb / ((float)F.m_area * pa + (float)F.m_brdf * pb);
 }
 
-// gBufferFillPass (pg/ReSTIRIntegrator.cpp:213-234) + Camera::GenerateRay (pg/camera.cpp:20-42)
+// gBufferFillPass (pg/ReSTIRIntegrator.cpp:213-234) + Camera::GenerateRay (pg/camera.cpp:20-42) for the
+// camera `cam` (mat3(invViewMat) `m`): the current frame's, or the previous frame's when a tile rebuilds
+// a G element its rows do not hold (k_temporal)
 template <int T>
-__device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameConst& F, int x, int y, bool active) {
-    vec3 dc = mk((float)x - (float)F.W / 2.0f, (float)F.H / 2.0f - (float)y, -F.cam.focal);
-    const float* m = F.inv_view;
+__device__ __forceinline__ GElem gbuffer_fill_cam(const DevScene& S, const FrameConst& F, const GCam& cam,
+                                                  const float* m, int x, int y, bool active) {
+    vec3 dc = mk((float)x - (float)F.W / 2.0f, (float)F.H / 2.0f - (float)y, -cam.focal);
     vec3 dw = mk(m[0] * dc.x + m[3] * dc.y + m[6] * dc.z, m[1] * dc.x + m[4] * dc.y + m[7] * dc.z,
                  m[2] * dc.x + m[5] * dc.y + m[8] * dc.z);
     dw = normalize(dw);
-    SurfHit h = intersect<T>(S, active, F.cam.pos, dw, FLT_MIN + 0.01f);
+    SurfHit h = intersect<T>(S, active, cam.pos, dw, FLT_MIN + 0.01f);
     GElem g;
     g.pos = mk(0, 0, 0); g.nrm = g.pos; g.kd = g.pos; g.ks = g.pos; g.le = g.pos;
     g.shin = 0; g.depth = 0; g.type = 0; g.inv_im = 0;
@@ -257,10 +263,10 @@ __device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameCons
         MatRec mr = load_mat(S, h.mat);
         vec3 nrm = h.normal;
         if (S.texd) apply_maps(S, h, mr, nrm, false);                // textured scenes only (uniform)
-        g.pos = h.point; g.nrm = nrm; g.depth = length(h.point - F.cam.pos);
+        g.pos = h.point; g.nrm = nrm; g.depth = length(h.point - cam.pos);
         g.type = mr.type; g.kd = mr.kd; g.ks = mr.ks; g.le = mr.le; g.shin = mr.shin;
         if (g.type == MT_PHONG || g.type == MT_DIELECTRIC) {
-            vec3 V = normalize(F.cam.pos - g.pos);
+            vec3 V = normalize(cam.pos - g.pos);
 #ifdef RS_DIAG_NO_IM   // timing diagnostic only (scripts/initial_breakdown.py); breaks parity
             g.inv_im = 1.0f + 0.0f * dot(V, g.nrm);
 #else
@@ -271,6 +277,10 @@ __device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameCons
         g.le = F.use_sky ? sky_texel(S, dw) : F.bg;      // useSkybox ? sky : renderParams.bgColor (:231)
     }
     return g;
+}
+template <int T>
+__device__ __forceinline__ GElem gbuffer_fill(const DevScene& S, const FrameConst& F, int x, int y, bool active) {
+    return gbuffer_fill_cam<T>(S, F, F.cam, F.inv_view, x, y, active);
 }
 
 // TriangleCDF::getTriangle's index (pg/TriangleCDF.cpp:36-54): std::lower_bound(cdf2, ksi), narrowed
@@ -721,21 +731,33 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
     GElem cur = G.load(p);
     int qx = x, qy = y, fx = x, fy = y;
     bool ok = in && reproject(F.camp, cur.pos, F.W, F.H, qx, qy);
-    // rows outside the G-buffer margin of a tile are treated as a failed reprojection (counted)
-    if (ok && (qy < F.gy0 || qy >= F.gy1)) { ok = false; atomicAdd(C.outside, 1ull); }
-    const size_t q = ok ? (size_t)qy * F.W + qx : p;
+    // A tile holds the G-buffers of its rows +- margin only.  A reprojection beyond them (a miss
+    // pixel's position is (0,0,0), which projects anywhere) rebuilds the element it needs from the
+    // frame's camera -- gBufferFillPass is a function of (camera, pixel) -- so tiles stay bit-identical
+    // to the full frame.  Rare (a few pixels per frame): counted in Counters::reproj_outside.
+    const bool q_out = ok && (qy < F.gy0 || qy >= F.gy1);
+    const size_t q = ok && !q_out ? (size_t)qy * F.W + qx : p;
     GElem prev = Gp.load(q);
+    if (__ballot(q_out) != 0) {
+        const GElem alt = gbuffer_fill_cam<T>(S, F, F.camp, F.inv_view_prev, qx, qy, q_out);
+        if (q_out) { prev = alt; rays += 1u; atomicAdd(C.outside, 1ull); }
+    }
     if (ok) {
         float cd = length(cur.pos - F.cam.pos), pd = length(prev.pos - F.camp.pos);
         float dr = cd > pd ? pd / cd : cd / pd;
         ok = !(dr < 0.9f);
     }
+    vec3 pac = Gp.pos(p);
+    const bool fok = ok && reproject(F.cam, pac, F.W, F.H, fx, fy);
+    const bool f_out = fok && (fy < F.gy0 || fy >= F.gy1);
+    vec3 fw = G.pos(fok && !f_out ? (size_t)fy * F.W + fx : p);
+    if (__ballot(f_out) != 0) {
+        const GElem alt = gbuffer_fill_cam<T>(S, F, F.cam, F.inv_view, fx, fy, f_out);
+        if (f_out) { fw = alt.pos; rays += 1u; atomicAdd(C.outside, 1ull); }
+    }
     if (ok) {
-        vec3 pac = Gp.pos(p);
-        ok = reproject(F.cam, pac, F.W, F.H, fx, fy);
-        if (ok && (fy < F.gy0 || fy >= F.gy1)) { ok = false; atomicAdd(C.outside, 1ull); }
+        ok = fok;
         if (ok) {
-            vec3 fw = G.pos((size_t)fy * F.W + fx);
             float cdp = length(pac - F.camp.pos), pdp = length(fw - F.cam.pos);
             float drp = cdp > pdp ? pdp / cdp : cdp / pdp;
             ok = !(drp < 0.9f);

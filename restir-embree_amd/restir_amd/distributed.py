@@ -29,13 +29,14 @@ Band placement never changes the frame (tests), only which GPU computes which ro
 
 The per-pixel counter RNG is keyed by the full-frame pixel index, so the gathered frame is bit-identical
 to a single-GPU frame (tests/test_distributed.py, tests/test_gpu_tiles.py).  Temporal reprojection
-reads the previous G-buffer at reprojected pixels; those must lie within ``temporal_margin`` rows of
-the band (counted and treated as a failed reprojection otherwise -- SURVEY.md §8e deviation note).
+reads the previous (and, for its forward check, the current) G-buffer at reprojected pixels; a tile
+holds its rows +- max(halo, ``temporal_margin``) and rebuilds the rare element beyond them from the
+frame's camera (gBufferFillPass is a function of camera and pixel), so no margin beyond the spatial
+halo is needed for bit-identical frames.
 """
 from __future__ import annotations
 
 import ctypes
-import math
 
 import numpy as np
 
@@ -47,7 +48,10 @@ def band_rows(H: int, rank: int, world: int):
 def halo_rows(params) -> int:
     if not params.do_spatial or params.spatial_passes <= 0:
         return 0
-    return int(math.floor(math.sqrt(max(0.0, float(params.spatial_radius)))))
+    # float32 semantics, as the device forms the offset (trunc(sqrtf(U(0,R)) * cos)): for R just below a
+    # perfect square (24.999998f) sqrtf rounds to 5.0 where a float64 sqrt would give a 4-row halo
+    r = np.float32(max(0.0, float(params.spatial_radius)))
+    return int(np.floor(np.sqrt(r, dtype=np.float32)))
 
 
 class _CudaBuf:
@@ -174,7 +178,7 @@ LANES = 3   # run-ahead lanes of a context (kMaxAhead + 1 in restir_capi.hip)
 
 class TiledRenderer:
     def __init__(self, W: int, H: int, rank: int, world: int, device: int = 0, stream=None, backend=None,
-                 temporal_margin: int = 64, group=None, async_gather: bool = False):
+                 temporal_margin: int = 0, group=None, async_gather: bool = False):
         self.W, self.H, self.rank, self.world = W, H, rank, world
         self.bands = [band_rows(H, r, world) for r in range(world)]
         self.temporal_margin = temporal_margin

@@ -86,7 +86,8 @@ class CameraDesc(ctypes.Structure):
 class PassTimes(ctypes.Structure):
     _fields_ = [("gbuffer_initial_ms", ctypes.c_float), ("visibility_ms", ctypes.c_float),
                 ("temporal_ms", ctypes.c_float), ("spatial_ms", ctypes.c_float), ("shade_ms", ctypes.c_float),
-                ("total_ms", ctypes.c_float), ("rays", ctypes.c_uint64), ("primary_rays", ctypes.c_uint64)]
+                ("total_ms", ctypes.c_float), ("rays", ctypes.c_uint64), ("primary_rays", ctypes.c_uint64),
+                ("reproj_outside", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

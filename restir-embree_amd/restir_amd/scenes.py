@@ -246,8 +246,9 @@ def textured_cornell(n_lights: int = 8, seed: int = 5, sky: bool = True) -> Scen
     return sc
 
 
-def cornell_many_lights(n_lights: int = 1024, seed: int = 7, size: float = 0.03) -> Scene:
-    """C2: Cornell box with ``n_lights`` emissive quads (2*n_lights emissive triangles).
+def cornell_many_lights(n_lights: int = 1024, seed: int = 7, size: float = 0.02) -> Scene:
+    """C2: Cornell box with ``n_lights`` emissive quads of ``size`` x ``size`` m (2*n_lights emissive
+    triangles; SURVEY.md §8(d): 0.02 m quads).
 
     The reference has no point lights, so "1024 point lights" is encoded
     as 1024 small emissive quads: all but 16 placed uniformly on the ceiling (facing down), 16 on

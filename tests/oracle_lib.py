@@ -91,6 +91,8 @@ def lib():
         L.or_kat_power_heuristic.argtypes = [ctypes.c_float, ctypes.c_float]
         L.or_kat_max_component.restype = ctypes.c_float
         L.or_kat_max_component.argtypes = [_f32p]
+        L.or_ctx_rebuilt.restype = ctypes.c_uint64
+        L.or_ctx_rebuilt.argtypes = [ctypes.c_void_p]
         L.or_kat_mis.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float, _f32p]
         _lib = L
     return _lib

@@ -18,15 +18,15 @@ def _free_port():
     return p
 
 
-def _cfg():
+def _cfg(n_frames=3):
     from restir_amd import params as P, scenes
     sc = scenes.cornell_box(8)
     prm = P.default_params(m_area=4, do_spatial=1, spatial_neighbors=4, spatial_passes=2, do_temporal=1)
-    cams = [scenes.orbit_camera(sc.camera, f, 24, 0.25) for f in range(3)]
+    cams = [scenes.orbit_camera(sc.camera, f, 24, 0.25) for f in range(n_frames)]
     return sc, prm, cams
 
 
-def _worker(rank, world, port, W, H, out_path, rebalance=False):
+def _worker(rank, world, port, W, H, out_path, rebalance=False, margin=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "restir-embree_amd"), os.path.join(root, "tests")]
@@ -36,8 +36,9 @@ def _worker(rank, world, port, W, H, out_path, rebalance=False):
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     O.lib().or_set_num_threads(2)
-    sc, prm, cams = _cfg()
-    tr = TiledRenderer(W, H, rank, world, backend=O.OracleTileBackend(W, H), temporal_margin=H)
+    sc, prm, cams = _cfg(3 if margin is None else 8)
+    tr = TiledRenderer(W, H, rank, world, backend=O.OracleTileBackend(W, H),
+                       temporal_margin=H if margin is None else margin)
     s = tr.load_scene(sc)
     if rebalance:
         bands = tr.rebalance(lambda i: tr.render(s, cams[0], prm, i), n_frames=1, min_rows=6)
@@ -53,15 +54,17 @@ def _worker(rank, world, port, W, H, out_path, rebalance=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rebalance", [(2, False), (3, False), (3, True)])
-def test_tiled_frames_match_full_frame(world, rebalance, tmp_path):
-    """Equal bands and cost-balanced (unequal) bands both gather the full frame bit for bit."""
+@pytest.mark.parametrize("world,rebalance,margin", [(2, False, None), (3, False, None), (3, True, None), (3, False, 5)])
+def test_tiled_frames_match_full_frame(world, rebalance, margin, tmp_path):
+    """Equal bands and cost-balanced (unequal) bands both gather the full frame bit for bit -- also with a
+    G-buffer margin of only the spatial halo (5 rows), where the temporal pass's reprojections (moving
+    camera; miss pixels at (0,0,0) project into other bands) rebuild the elements beyond the tile."""
     import oracle_lib as O
     W, H = 40, 36
     out = str(tmp_path / "frames.npy")
-    mp.spawn(_worker, args=(world, _free_port(), W, H, out, rebalance), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), W, H, out, rebalance, margin), nprocs=world, join=True)
     got = np.load(out)
-    sc, prm, cams = _cfg()
+    sc, prm, cams = _cfg(3 if margin is None else 8)
     r = O.OracleRenderer(W, H)
     s = O.OracleScene(sc)
     for f, cam in enumerate(cams):
@@ -88,3 +91,43 @@ def test_halo_rows_and_bands():
     assert sum(b - a for a, b in (band_rows(1081, r, 8) for r in range(8))) == 1081
     assert halo_rows(P.metric_params()) == 5          # floor(sqrt(30))
     assert halo_rows(P.default_params()) == 0         # no spatial reuse -> nothing to exchange
+    # float32 semantics (the device's sqrtf): 24.999998f -> sqrtf rounds to 5.0, so 5 rows, not 4
+    assert halo_rows(P.metric_params(spatial_radius=24.999998)) == 5
+    assert halo_rows(P.metric_params(spatial_radius=24.9)) == 4
+
+
+def test_oracle_tiles_halo_margin_rebuild_bit_identical():
+    """Tile stages with a G-buffer margin of only the spatial halo under a moving camera (the miss pixels
+    around the box have position (0,0,0), which projects into other bands): the temporal pass rebuilds the
+    G elements beyond a tile's rows (counted: the path runs), so 4 in-process bands (halo copies between
+    the stages, as the RCCL exchange does) give the full frame bit for bit over 5 frames."""
+    import oracle_lib as O
+    from restir_amd import params as P, scenes
+    from restir_amd.distributed import band_rows, halo_rows
+    O.lib().or_set_num_threads(4)
+    sc = scenes.cornell_many_lights(64)
+    W, H, N = 96, 72, 4
+    prm = P.c3_params(m_area=4)
+    cams = [scenes.orbit_camera(sc.camera, f, 40, 0.6) for f in range(5)]
+    bes = [O.OracleTileBackend(W, H) for _ in range(N)]
+    hs = [be.load_scene(sc) for be in bes]
+    h = halo_rows(prm)
+    full, fs = O.OracleRenderer(W, H), O.OracleScene(sc)
+    for f, cam in enumerate(cams):
+        for r, be in enumerate(bes):
+            y0, y1 = band_rows(H, r, N)
+            be.begin(hs[r], cam, prm, f, y0, y1, h, h)
+        for be in bes:
+            be.temporal()
+        for p in range(prm.spatial_passes):
+            for r, be in enumerate(bes):
+                if r > 0:
+                    be.halo_tensor(0).copy_(bes[r - 1].halo_tensor(3))
+                if r < N - 1:
+                    be.halo_tensor(1).copy_(bes[r + 1].halo_tensor(2))
+            for be in bes:
+                be.spatial(p)
+        img = np.concatenate([be.finish().numpy().reshape(-1, W, 3) for be in bes], 0)
+        ref = full.render(fs, cam, prm, f)
+        assert np.array_equal(img, ref), f"frame {f}: {int(np.any(img != ref, -1).sum())} pixels differ"
+    assert sum(int(O.lib().or_ctx_rebuilt(be.r.h)) for be in bes) > 0

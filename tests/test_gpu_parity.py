@@ -232,8 +232,10 @@ def test_initial_split_bit_identical(which):
 def test_run_ahead_bit_identical(which):
     """Frame pipelining (initial pass of frame f+1 on the side stream, overlapping frame f's later
     passes) renders the same frames as strictly sequential frames, with temporal reuse, moving
-    geometry (rs_scene_update_positions between frames) and a fused-shade configuration; frames are
-    read back only at the end (from the frame ring) so the overlap really happens."""
+    geometry (rs_scene_update_positions between frames) and a fused-shade configuration.  The traversal
+    kind is pinned: AUTO's first six frames are tuning frames, which run alone on the context's stream;
+    pinned, every frame after the first runs on its lane beside the frames before it, and frames are
+    only cloned on the frames' stream (no host sync between frames), so the overlap really happens."""
     W, H = 96, 64
     upd = None
     cam = lambda f: scenes.orbit_camera(sc.camera, f, 48, 0.2)
@@ -253,6 +255,7 @@ def test_run_ahead_bit_identical(which):
     out = {}
     for ra in (0, 1, 2):
         g = Renderer(W, H, stream=st)
+        g.set_traversal("lane" if which == "c3" else "lockstep")
         g.set_run_ahead(ra)
         gs = g.load_scene(sc)
         frames = []

@@ -85,6 +85,7 @@ def _gpu_worker(rank, world, port, W, H, out_path, rebalance, async_gather=False
     prm = P.c3_params(m_area=8, spatial_passes=2)
     tr = TiledRenderer(W, H, rank, world, device=0, stream=torch.cuda.current_stream().cuda_stream,
                        temporal_margin=H, async_gather=async_gather)
+    tr.be.r.set_traversal("lockstep")      # no AUTO tuning frames (they run alone): frames use the lanes
     s = tr.load_scene(sc)
     if rebalance:   # bands from the GPU's own per-row wave times (unequal in general)
         bands = tr.rebalance(lambda i: tr.render(s, sc.camera, prm, i), n_frames=2, min_rows=6)
