@@ -1,27 +1,35 @@
 #!/usr/bin/env python
 """bench.py -- BASELINE.json metric: Mrays/s + frames/s at 1080p, 32 candidates, 4 spatial neighbours.
 
-Workload (configs[1], C2): Cornell box with 1024 emissive quads (2048 emissive triangles), 1920x1080,
-A=32 area + B=1 BRDF candidates, spatial reuse k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20.
-A "step" is one frame of the hot path (SimpleGuiDX11::produceRestir, pg/simpleguidx11.cpp:359-487):
-G-buffer + initial RIS, spatial reuse, shade.  Scene + buffers are resident in HBM before timing.
+Headline workload (configs[1], C2): Cornell box with 1024 emissive 0.02 m quads (2048 emissive
+triangles), 1920x1080, A=32 area + B=1 BRDF candidates, spatial reuse k=4 P=1 R=30 CONSTANT MIS,
+temporal off, cap 20.  A "step" is one frame of the hot path (SimpleGuiDX11::produceRestir,
+pg/simpleguidx11.cpp:359-487): G-buffer + initial RIS, spatial reuse, shade.  Scene + buffers are
+resident in HBM before timing; the framebuffer stays in HBM (zero-copy, rs_get_frame_device_ptr).
 
-N=1: one GPU renders the whole frame.  N>1 (torchrun): the frame is split into N row bands
-(strong scaling, one process per GPU); reservoir halo rows are exchanged over RCCL before each
-spatial pass and the band framebuffers are gathered to rank 0 (restir_amd/distributed.py).
+N=1 also measures, as extra keys of the same JSON line, the other single-GPU configs (C3 Sponza-like
+with temporal reuse, the full 240-frame C5 sequence, C2V = doVisibilityPass), each with its own
+ms_per_step, Mrays/s, rooflines and a bounded CPU baseline, and the drop-in C++ host path
+(include/restir.hpp through tools/restir_render, framebuffer copied to host memory every frame).
 
-Frames are pipelined by the library (run-ahead lanes, up to 3 frames in flight; RESTIR_RUNAHEAD=0
-renders strictly one frame after the other); every frame is still rendered completely.
+N>1 (torchrun): the frame is split into N row bands (strong scaling, one process per GPU); reservoir
+halo rows are exchanged over RCCL before each spatial pass and the band framebuffers are gathered to
+rank 0 (restir_amd/distributed.py).
 
-Output: one JSON line (rank 0) with value = whole-job frames/s, plus mrays_per_s, roofline of the
-dominant kernel (k_gbuffer_initial, algorithmic bytes, HIP-event timed on its stream), the whole-frame
-roofline at the job's frame rate, and cpu_baseline (the oracle restatement on this host's cores, N=1
-only).
+Frames are pipelined by the library (run-ahead lanes, up to 3 frames in flight); every frame is still
+rendered completely.  Rooflines (SURVEY.md §8(d) algorithmic bytes):
+  roofline         the whole frame: B_px (480 B at C2) x pixels / ms_per_step
+  kernel_roofline  the dominant kernel alone: its §8(d) bytes (186 B/px for G-buffer + initial) /
+                   its launch time measured with HIP events in a second window with one frame in
+                   flight (RESTIR_RUNAHEAD=0 semantics), flagged when that exceeds ms_per_step (the
+                   pipelined frame hides the kernel's ramp-up and tail behind its neighbours)
+  valu_issue       VALU wave-instructions per frame (rocprofv3 PMC, profiles/r02_pmc_<cfg>.json) /
+                   ms_per_step against 1024 SIMDs x 2.4 GHz / 2 cycles
 """
 import argparse
 import json
-import math
 import os
+import subprocess
 import sys
 import time
 
@@ -30,39 +38,55 @@ sys.path.insert(0, os.path.join(ROOT, "restir-embree_amd"))
 
 import numpy as np  # noqa: E402
 
+METRIC = "Mrays/s + frames/s at 1080p, 32 candidates, 4 spatial neighbours"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2   # wave64 VALU instr/ns: 1024 SIMDs, 2 cycles each, 2.4 GHz
 C5_FRAMES = 240
 TUNE_FRAMES = 6                # RS_TRAVERSAL_AUTO tuning frames (2 kinds x kTuneRuns, restir_capi.hip)
-VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2   # wave64 VALU instr/ns: 1024 SIMD-32s, 2 cycles each, 2.4 GHz
 WORKLOADS = {
     "C1": "Cornell box, 8 emissive quads, reference defaults (A=1 B=1, no reuse)",
-    "C2": "Cornell box + 1024 emissive quads, A=32 B=1, spatial k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20",
+    "C2": "Cornell box + 1024 emissive 0.02 m quads, A=32 B=1, spatial k=4 P=1 R=30 CONSTANT MIS, temporal off, cap 20",
     "C2V": "C2 with doVisibilityPass (initial candidates without shadow rays, one visibility ray per pixel)",
     "C3": "Sponza-like ~250k tris, 4096 emissive triangles (2048 lamp quads), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
     "C5": "C2 scene, 240-frame camera orbit (r=0.3) + moving lights (light CDF recomputed + BVH refit on the GPU every frame), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
 }
-# algorithmic bytes per pixel of the dominant kernel k_gbuffer_initial: G-buffer record write
-# (5 x float4 = 80 B) + reservoir write (3 x float4 = 48 B); scene/BVH reads are cache-resident
-# shared data, not per-pixel traffic.  DESIGN.md "Roofline".
-DOMINANT_BYTES_PER_PX = 80 + 48
+CONFIG_INDEX = {"C1": 0, "C2": 1, "C2V": 1, "C3": 2, "C5": 4}
 
 
-def frame_bytes_per_px(prm) -> int:
-    """Compulsory HBM bytes per pixel of one whole frame in this build's layout (each per-pixel record
-    read / written once per pass; neighbour and reprojected reads are the same records): initial
-    G + R write 128; visibility pass 68; temporal G cur + G prev + R cur + R prev read, R write 304; each spatial pass G + R
-    read, R write 176; framebuffer write 12 (fused into the last pass; a separate shade pass reads
-    G + R: +128).  SURVEY.md §8(d) prices the reference's unfused passes (480 B at C2)."""
-    b = 128
-    if prm.do_visibility_pass:                 # G position + reservoir read, W write
-        b += 16 + 48 + 4
-    if prm.do_temporal:
-        b += 304
-    if prm.do_spatial and prm.spatial_passes > 0:
-        b += 176 * prm.spatial_passes + 12
-    else:
-        b += 128 + 12
-    return b
+# SURVEY.md §8(d) algorithmic bytes per pixel-frame: G write 69, initial (G + R) 117, visibility 28,
+# temporal 282, spatial pass 165, shade 129 (G = 69 B, R = 48 B, F = 12 B; history = pointer swap)
+PASS_BYTES = {"gbuffer_initial_ms": 69 + 117, "visibility_ms": 28, "temporal_ms": 282, "spatial_ms": 165,
+              "shade_ms": 129}
+PASS_KERNEL = {"gbuffer_initial_ms": "k_gbuffer_initial", "visibility_ms": "k_visibility",
+               "temporal_ms": "k_temporal", "spatial_ms": "k_spatial", "shade_ms": "k_shade"}
+
+
+def survey_bytes_per_px(prm) -> int:
+    V = 1 if prm.do_visibility_pass else 0
+    T = 1 if prm.do_temporal else 0
+    P = prm.spatial_passes if prm.do_spatial else 0
+    return 69 + 117 + V * 28 + T * 282 + P * 165 + 129
+
+
+def workload(name):
+    from restir_amd import scenes
+    from restir_amd.params import metric_params, c3_params, default_params
+    camera = None                       # per-frame camera (C5 orbit); None = the scene's static camera
+    light_pos = None                    # per-frame emissive positions (C5 moving lights)
+    if name == "C1":
+        sc, prm = scenes.cornell_box(8), default_params()
+    elif name == "C2":
+        sc, prm = scenes.cornell_many_lights(1024), metric_params()
+    elif name == "C2V":   # doVisibilityPass variant (1 shadow ray instead of A per pixel)
+        sc, prm = scenes.cornell_many_lights(1024), metric_params(do_visibility_pass=1)
+    elif name == "C3":
+        sc, prm = scenes.sponza_like(), c3_params()
+        camera = lambda f: scenes.orbit_camera(sc.camera, f % C5_FRAMES, C5_FRAMES, 0.3)
+    else:   # C5: C2's scene, 240-frame camera orbit + moving lights, temporal reuse with M-cap 20
+        sc, prm = scenes.cornell_many_lights(1024), c3_params()
+        camera = lambda f: scenes.orbit_camera(sc.camera, f % C5_FRAMES, C5_FRAMES, 0.3)
+        light_pos = lambda f: scenes.moving_light_positions(sc, f % C5_FRAMES, C5_FRAMES)
+    return sc, prm, camera, light_pos
 
 
 def parse():
@@ -72,223 +96,332 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--scene", default="C2", choices=["C1", "C2", "C2V", "C3", "C5"])
+    ap.add_argument("--scene", default="C2", choices=list(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="N=1: skip the C3/C5/C2V and drop-in lines")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
 
 
-def cpu_baseline(sc, prm, W, H, threads):
-    """The oracle (CPU restatement, OpenMP) timed on this host: one full frame of the same workload."""
+# ---------------------------------------------------------------- CPU baseline (oracle = the checker)
+def cpu_baseline(name, W, H, threads, budget_s=12.0):
+    """The oracle (plain-C OpenMP restatement of the reference path, oracle/restir_oracle.c) timed on this
+    host, on a bounded sample of the same workload: whole frames for C1/C2/C2V (median, after a warm-up
+    frame); for C3/C5 (~10-40 s per 1080p frame on 16 cores) a centred band of rows rendered through the
+    oracle's tile stages (G-buffer + initial + temporal + spatial + shade of the band; the first frame
+    only builds the temporal history), scaled to the full frame by rows."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
-
     oracle_lib.build()
     L = oracle_lib.lib()
     n_threads = max(1, min(threads, os.cpu_count() or 1))
     L.or_set_num_threads(n_threads)
+    sc, prm, camera, light_pos = workload(name)
+    cam = camera or (lambda f: sc.camera)
     osc = oracle_lib.OracleScene(sc)
-    rr = oracle_lib.OracleRenderer(W, H)
-    rr.render(osc, sc.camera, prm, 0)          # warm-up frame (page-in, caches)
-    # median of up to 10 frames, bounded to ~10 s of CPU time (SURVEY.md §8d procedure, scaled down)
-    times, rays = [], []
+    times, rays, band_t, refr = [], [], [], []
     t_start = time.perf_counter()
-    for f in range(1, 11):
-        t0 = time.perf_counter()
-        rr.render(osc, sc.camera, prm, f)
-        times.append(time.perf_counter() - t0)
-        rays.append(rr.rays)
-        if time.perf_counter() - t_start > 10.0:
-            break
+    if name in ("C3", "C5"):
+        rows = max(8, H // (16 if name == "C3" else 8))
+        y0 = (H - rows) // 2
+        be = oracle_lib.OracleTileBackend(W, H)
+        halo = int(np.floor(np.sqrt(np.float32(prm.spatial_radius), dtype=np.float32)))
+        for f in range(6):
+            if light_pos is not None:
+                osc = oracle_lib.OracleScene(type(sc)(light_pos(f), sc.normals, sc.tri_material, sc.materials, sc.camera))
+            t0 = time.perf_counter()
+            be.begin(osc, cam(f), prm, f, y0, y0 + rows, halo, halo)
+            be.temporal()
+            for p in range(prm.spatial_passes):
+                be.spatial(p)
+            be.finish()
+            dt = time.perf_counter() - t0
+            if f > 0:
+                times.append(dt * H / rows)
+                rays.append(be.rays)
+                band_t.append(dt)
+                refr.append(be.reference_rays * H / rows)
+            if time.perf_counter() - t_start > budget_s and len(times) >= 1:
+                break
+        sample = (f"{len(times)} frames of a centred {rows}-row band of {W}x{H} (oracle tile stages; after 1 "
+                  f"history frame), scaled by {H}/{rows} rows")
+        mr = float(np.median([r / t for r, t in zip(rays, band_t)])) / 1e6
+    else:
+        rr = oracle_lib.OracleRenderer(W, H)
+        rr.render(osc, cam(0), prm, 0)          # warm-up frame (page-in, caches)
+        for f in range(1, 11):
+            t0 = time.perf_counter()
+            rr.render(osc, cam(f), prm, f)
+            times.append(time.perf_counter() - t0)
+            rays.append(rr.rays)
+            refr.append(rr.reference_rays)
+            if time.perf_counter() - t_start > budget_s:
+                break
+        sample = f"median of {len(times)} full {W}x{H} frames after 1 warm-up frame"
+        mr = float(np.median([r / t for r, t in zip(rays, times)])) / 1e6
     dt = float(np.median(times))
-    mr = float(np.median([r / t for r, t in zip(rays, times)])) / 1e6
-    return {"value": round(1.0 / dt, 5), "unit": "frames/s", "cores": n_threads, "kind": "port",
-            "sample": f"median of {len(times)} full {W}x{H} frames of the same workload after 1 warm-up frame "
-                      f"(oracle/restir_oracle.c, OpenMP, {n_threads} threads); s/frame={dt:.3f}; "
-                      f"Mrays/s={mr:.2f}"}
+    out = {"value": round(1.0 / dt, 5), "unit": "frames/s", "cores": n_threads, "kind": "port",
+           "sample": f"{sample}; oracle/restir_oracle.c (OpenMP, {n_threads} threads, scalar binary SAH BVH -- "
+                     f"not Embree's 4/8-wide SIMD BVH: the GPU/CPU ratio overstates the gap to an Embree-class CPU)",
+           "s_per_frame": round(dt, 4)}
+    if mr is not None:
+        out["mrays_per_s"] = round(mr, 2)
+    # rays the reference's code would trace for these frames (oracle-counted: every rtcIntersect1 and
+    # testOcclusion it reaches, incl. zero-contribution shadow rays and re-evaluated final p-hats)
+    out["reference_rays_per_frame"] = int(np.median(refr)) if refr else None
+    return out
+
+
+# ---------------------------------------------------------------- PMC figures committed under profiles/
+def pmc_for(name, W, H):
+    path = os.path.join(ROOT, "profiles", f"r02_pmc_{name}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return pmc if pmc.get("config") == f"{name}_{W}x{H}" else None
+
+
+# ---------------------------------------------------------------- one single-GPU config
+def run_single(name, W, H, steps, warmup, device, stream, cpu_threads, with_cpu, kernel_frames=5):
+    from restir_amd import Renderer
+    sc, prm, camera, light_pos = workload(name)
+    r = Renderer(W, H, device=device, stream=stream)
+    gs = r.load_scene(sc)
+    cam = camera or (lambda f: sc.camera)
+
+    def step(f):
+        if light_pos is not None:       # moving lights: new positions -> light CDF + BVH refit (timed)
+            gs.update_positions(light_pos(f))
+        r.produce_restir(gs, cam(f), prm, f, copy_out=False, timed=False)
+
+    import torch
+    # initialisation (like the scene load, outside warm-up and timing): RS_TRAVERSAL_AUTO times the two
+    # BVH walk kinds over a scene's first 6 frames, then the history is reset
+    for f in range(TUNE_FRAMES):
+        step(f)
+    r.reset_history()
+    for f in range(warmup):
+        step(f)
+    torch.cuda.synchronize()
+    r.timing_totals(reset=True)
+    t0 = time.perf_counter()
+    for f in range(steps):
+        step(warmup + f)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tot, n_timed = r.timing_totals(reset=True)
+    ms_per_step = dt / steps * 1e3
+    rays = int(tot.rays)
+    # kernel window: one frame in flight (run-ahead 0), HIP events around every pass on the frame's stream
+    r.set_run_ahead(0)
+    for f in range(2):
+        step(warmup + steps + f)
+    r.timing_totals(reset=True)
+    for f in range(kernel_frames):
+        step(warmup + steps + 2 + f)
+    ktot, kn = r.timing_totals(reset=True)
+    r.set_run_ahead(2)
+    iso = {k: float(getattr(ktot, k)) / max(1, kn) for k in PASS_BYTES}
+    iso_total = float(ktot.total_ms) / max(1, kn)
+    dom = max(iso, key=iso.get)
+    px = W * H
+    b_px = survey_bytes_per_px(prm)
+    frame_gbs = b_px * px / (ms_per_step * 1e-3) / 1e9
+    k_gbs = PASS_BYTES[dom] * px / (iso[dom] * 1e-3) / 1e9
+    _, last_kind, _ = r.traversal(gs)
+    pmc = pmc_for(name, W, H)
+    out = {
+        "value": round(steps / dt, 4), "unit": "frames/s", "ms_per_step": round(ms_per_step, 4), "steps": steps,
+        "warmup": warmup, "frames_timed_by_events": n_timed,
+        "config": {"workload": f"{name}: {WORKLOADS[name]}, {W}x{H}", "width": W, "height": H,
+                   "traversal": {0: "lockstep", 1: "lane"}.get(last_kind, str(last_kind)), "frames_in_flight": 3},
+        "mrays_per_s": round(rays / dt / 1e6, 2), "rays_per_frame": rays // max(1, steps),
+        "pass_ms_one_frame_in_flight": {k: round(v, 4) for k, v in iso.items()},
+        "frame_ms_one_frame_in_flight": round(iso_total, 4),
+        "roofline": {"bound": "hbm", "scope": "frame (all passes, frames in flight)", "bytes_per_px": b_px,
+                     "achieved": round(frame_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(frame_gbs / HBM_PEAK_GBS, 5),
+                     "traffic": pmc.get("frame_bytes") if pmc else None},
+        "kernel_roofline": {"bound": "hbm", "kernel": PASS_KERNEL[dom], "bytes_per_px": PASS_BYTES[dom],
+                            "kernel_ms": round(iso[dom], 4), "achieved": round(k_gbs, 2), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(k_gbs / HBM_PEAK_GBS, 5),
+                            "kernel_ms_le_ms_per_step": bool(iso[dom] <= ms_per_step),
+                            "traffic": (pmc.get("kernels", {}).get(PASS_KERNEL[dom], {}) or {}).get("hbm_bytes_corrected")
+                            if pmc else None,
+                            "timing": f"HIP events on the frame's stream, {kn} frames with one frame in flight"},
+    }
+    if pmc and pmc.get("frame_valu"):
+        v = float(pmc["frame_valu"])
+        out["valu_issue"] = {"scope": "frame", "valu_per_frame": v, "achieved": round(v / (ms_per_step * 1e-3) / 1e9, 2),
+                             "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
+                             "frac": round(v / (ms_per_step * 1e-3) / 1e9 / VALU_PEAK_GIPS, 4),
+                             "source": os.path.basename(pmc.get("_path", f"profiles/r02_pmc_{name}.json"))}
+    out["cpu_baseline"] = cpu_baseline(name, W, H, cpu_threads) if with_cpu else None
+    rr = (out["cpu_baseline"] or {}).get("reference_rays_per_frame")
+    if rr:
+        # comparable with the reference's Mrays/s: the rays ITS code would trace for the same frames
+        # (oracle-counted on the CPU-baseline sample; this build skips zero-contribution shadow rays and
+        # re-evaluated final p-hats, so it traces fewer -- rays_per_frame above)
+        out["reference_rays_per_frame"] = rr
+        out["reference_equivalent_mrays_per_s"] = round(rr * steps / dt / 1e6, 2)
+    if out["cpu_baseline"] and out["cpu_baseline"].get("value"):
+        out["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+    gs.close()
+    r.close()
+    return out
+
+
+def run_dropin(W, H, frames=120):
+    """The drop-in path a reference user runs: C++ host code over include/restir.hpp (member names of
+    SimpleGuiDX11) driving librestir_amd.so, the framebuffer landing in host memory every frame
+    (tools/restir_render --bench: produceRestir + frame_data on the host)."""
+    import tempfile
+    from restir_amd import scenes
+    exe = os.path.join(ROOT, "restir-embree_amd", "restir_render")
+    if not os.path.exists(exe):
+        return None
+    sc = scenes.cornell_many_lights(1024)
+    c = sc.camera
+    with tempfile.TemporaryDirectory() as d:
+        obj = os.path.join(d, "c2.obj")
+        scenes.write_obj(sc, obj)          # Raytracer::LoadScene(file) path: OBJ/MTL through the C ABI loader
+        cmd = [exe, "--bench", "--obj", obj, "--w", str(W), "--h", str(H), "--frames", str(frames),
+               "--area", "32", "--brdf", "1", "--spatial", "4", "--eye", *map(str, c.eye), "--at", *map(str, c.at),
+               "--fov", str(c.fov_y)]
+        try:
+            p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        except (OSError, subprocess.TimeoutExpired) as e:
+            return {"error": repr(e)}
+    for line in p.stdout.splitlines()[::-1]:
+        if line.startswith("{"):
+            try:
+                return json.loads(line)
+            except ValueError:
+                break
+    return {"error": (p.stderr or p.stdout)[-400:], "rc": p.returncode}
 
 
 def main():
     args = parse()
     import torch
-    from restir_amd import Renderer, scenes
-    from restir_amd.params import metric_params, c3_params, default_params
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    W, H = args.width, args.height
+    if world == 1:
+        torch.cuda.set_device(local)
+        # render on a dedicated torch stream shared with the library (torch's default stream is handle 0)
+        torch.cuda.set_stream(torch.cuda.Stream(device=local))
+        stream = torch.cuda.current_stream().cuda_stream
+        head = run_single(args.scene, W, H, args.steps, args.warmup, local, stream, args.cpu_threads,
+                          not args.no_cpu_baseline)
+        out = {"metric": METRIC, "value": head.pop("value"), "unit": "frames/s", "n_gpus": 1,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": head.pop("ms_per_step"),
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+               "data": f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX[args.scene]}])"}
+        head["config"]["parallelism"] = "1 GPU"
+        out.update(head)
+        if not args.no_extras and args.scene == "C2" and (W, H) == (1920, 1080):
+            extras = {}
+            for name, steps in (("C3", 20), ("C5", C5_FRAMES), ("C2V", args.steps)):
+                e = run_single(name, W, H, steps, args.warmup, local, stream, args.cpu_threads,
+                               not args.no_cpu_baseline)
+                e["data"] = f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX[name]}])"
+                extras[name] = e
+            out["configs"] = extras
+            torch.cuda.synchronize()
+            d = run_dropin(W, H)
+            if d is not None:
+                if "value" in d:
+                    d["frac_of_zero_copy"] = round(d["value"] / out["value"], 4)
+                out["dropin_host_framebuffer"] = d
+        print(json.dumps(out), flush=True)
+        return
+    run_multi(args, world, rank, local, W, H)
+
+
+def run_multi(args, world, rank, local, W, H):
+    import torch
+    import torch.distributed as dist
     # RESTIR_DIST_BACKEND=gloo rehearses the N>1 flow with more ranks than GPUs (ranks share devices,
     # halo/gather staged through host memory); the measured configuration is RCCL ("nccl"), one GPU per rank
     backend = os.environ.get("RESTIR_DIST_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    dist = None
     red_dev = "cpu" if backend == "gloo" else "cuda"
-    if world > 1:
-        import torch.distributed as dist
-        if backend == "gloo":
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    W, H = args.width, args.height
-    camera = None                       # per-frame camera (C5 orbit); None = the scene's static camera
-    light_pos = None                    # per-frame emissive positions (C5 moving lights)
-    if args.scene == "C1":
-        sc, prm = scenes.cornell_box(8), default_params()
-    elif args.scene == "C2":
-        sc, prm = scenes.cornell_many_lights(1024), metric_params()
-    elif args.scene == "C2V":   # SURVEY.md §8(d): doVisibilityPass variant (1 shadow ray instead of A per pixel)
-        sc, prm = scenes.cornell_many_lights(1024), metric_params(do_visibility_pass=1)
-    elif args.scene == "C3":
-        sc, prm = scenes.sponza_like(), c3_params()
-    else:   # C5: C2's scene, 240-frame camera orbit + moving lights, temporal reuse with M-cap 20
-        sc, prm = scenes.cornell_many_lights(1024), c3_params()
-        camera = lambda f: scenes.orbit_camera(sc.camera, f % C5_FRAMES, C5_FRAMES, 0.3)
-        light_pos = [scenes.moving_light_positions(sc, f, C5_FRAMES) for f in range(C5_FRAMES)]
-    # render on a dedicated torch stream shared with the library, so RCCL ops and the kernels of
-    # librestir_amd.so are ordered on one stream (torch's default stream has handle 0 = "none")
+    if backend == "gloo":
+        dist.init_process_group("gloo")
+    else:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    sc, prm, camera, light_pos = workload(args.scene)
+    cam = camera or (lambda f: sc.camera)
     torch.cuda.set_stream(torch.cuda.Stream(device=local))
     stream = torch.cuda.current_stream().cuda_stream
-
-    if world == 1:
-        r = Renderer(W, H, device=local, stream=stream)
-        gs = r.load_scene(sc)
-        render = lambda f: r.produce_restir(gs, camera(f) if camera else sc.camera, prm, f, copy_out=False,
-                                            timed=False)
-        eng = r
-    else:
-        from restir_amd.distributed import TiledRenderer
-        # async gather: frame f's band framebuffers travel to rank 0 while frame f+1 renders
-        tr = TiledRenderer(W, H, rank, world, device=local, stream=stream, async_gather=True)
-        gs = tr.load_scene(sc)
-        render = lambda f: tr.render(gs, camera(f) if camera else sc.camera, prm, f, gather=True, timed=False)
-        eng = tr
+    from restir_amd.distributed import TiledRenderer
+    # async gather: frame f's band framebuffers travel to rank 0 while frame f+1 renders
+    tr = TiledRenderer(W, H, rank, world, device=local, stream=stream, async_gather=True)
+    gs = tr.load_scene(sc)
 
     def step(f):
-        if light_pos is not None:       # moving lights: new positions -> light CDF + BVH rebuilt (timed)
-            gs.update_positions(light_pos[f % C5_FRAMES])
-        return render(f)
+        if light_pos is not None:
+            gs.update_positions(light_pos(f))
+        return tr.render(gs, cam(f), prm, f, gather=True, timed=False)
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    # initialisation (like the scene load, outside warm-up and timing): RS_TRAVERSAL_AUTO times the two
-    # BVH walk kinds over a scene's first 6 frames, then the history is reset
     for f in range(TUNE_FRAMES):
         step(f)
-    if world > 1:   # cost-balanced bands from 2 frames' per-row wave times (all ranks agree; resets history)
-        bands = tr.rebalance(step, n_frames=2)
-        if rank == 0:
-            print(f"bands: {bands}", file=sys.stderr)
-    eng.reset_history()
+    bands = tr.rebalance(step, n_frames=2)
+    if rank == 0:
+        print(f"bands: {bands}", file=sys.stderr)
+    tr.reset_history()
     for f in range(args.warmup):
         step(f)
-    barrier()
+    dist.barrier()
     torch.cuda.synchronize()
-    eng.timing_totals(reset=True)            # folds the warm-up frames away; no per-frame sync below
-    barrier()
+    tr.timing_totals(reset=True)
+    dist.barrier()
     t0 = time.perf_counter()
     for f in range(args.steps):
         step(args.warmup + f)
     torch.cuda.synchronize()
-    barrier()
+    dist.barrier()
     dt = time.perf_counter() - t0
-    tot, n_timed = eng.timing_totals()
-    if n_timed != args.steps:
-        print(f"warning: {n_timed} frames timed by events, expected {args.steps}", file=sys.stderr)
-    keys = ("gbuffer_initial_ms", "spatial_ms", "temporal_ms", "shade_ms", "total_ms")
-    acc = {k: float(getattr(tot, k)) for k in keys}
-    rays = int(tot.rays)
-    if dist is not None:
-        tt = torch.tensor([dt, float(rays)], dtype=torch.float64, device=red_dev)
-        dmax = tt.clone()
-        dist.all_reduce(dmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
-        dt, rays = float(dmax[0]), int(tt[1])
-        acc_t = torch.tensor([acc[k] for k in acc], dtype=torch.float64, device=tt.device)
-        dist.all_reduce(acc_t, op=dist.ReduceOp.MAX)
-        acc = {k: float(v) for k, v in zip(acc, acc_t.tolist())}
-    ms_per_step = dt / args.steps * 1e3
-    fps = args.steps / dt
-    mrays = rays / dt / 1e6
-    k_ms = acc["gbuffer_initial_ms"] / args.steps
-    px_band = W * math.ceil(H / world)
-    achieved = DOMINANT_BYTES_PER_PX * px_band / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
-    traffic = valu = frame_traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf) and world == 1:
-        try:
-            with open(tf) as f:
-                pmc = json.load(f)
-            if pmc.get("config") == f"{args.scene}_{W}x{H}":
-                traffic = pmc.get("k_gbuffer_initial_bytes_per_launch")
-                frame_traffic = pmc.get("frame_bytes")
-                valu = pmc.get("k_gbuffer_initial_valu_per_launch")
-        except Exception:
-            traffic = valu = frame_traffic = None
-    inflight = 1 + int(os.environ.get("RESTIR_RUNAHEAD", "2"))
-    trav_name = None
-    if world == 1:
-        _, last_kind, _ = r.traversal(gs)
-        trav_name = {0: "lockstep", 1: "lane"}.get(last_kind)
-    else:
-        _, last_kind, _ = tr.be.r.traversal(gs)
-        trav_name = {0: "lockstep", 1: "lane"}.get(last_kind) + " (rank 0)"
+    tot, _ = tr.timing_totals()
+    tt = torch.tensor([dt, float(tot.rays), float(tot.reproj_outside)], dtype=torch.float64, device=red_dev)
+    dmax = tt[:1].clone()
+    dist.all_reduce(dmax, op=dist.ReduceOp.MAX)
+    sums = tt[1:].clone()
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+    dt, rays, outside = float(dmax[0]), int(sums[0]), int(sums[1])
+    _, last_kind, _ = tr.be.r.traversal(gs)
     if rank == 0:
-        out = {
-            "metric": "Mrays/s + frames/s at 1080p, 32 candidates, 4 spatial neighbours",
-            "value": round(fps, 4),
-            "unit": "frames/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": f"synthetic (procedural scene, BASELINE.json configs[{ {'C1': 0, 'C2': 1, 'C2V': 1, 'C3': 2, 'C5': 4}[args.scene]}])",
-            "config": {"workload": f"{args.scene}: {WORKLOADS[args.scene]}, {W}x{H}",
-                       "width": W, "height": H, "parallelism": f"row-bands x{world}" if world > 1 else "1 GPU",
-                       "traversal": trav_name, "frames_in_flight": inflight},
-            "mrays_per_s": round(mrays, 2),
-            "rays_per_frame": rays // max(1, args.steps),
-            "pass_ms": {k: round(v / args.steps, 4) for k, v in acc.items()},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "kernel": "k_gbuffer_initial", "bytes_per_px": DOMINANT_BYTES_PER_PX,
-                         "kernel_ms": round(k_ms, 4)},
-            # the kernel's real limiter is instruction issue / latency, not HBM: VALU wave-instructions
-            # per launch (PMC SQ_INSTS_VALU, profiles/pmc_traffic.json) over the live kernel time, against
-            # 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU op (MI355X_MICROARCH.md)
-            # the whole frame (all passes) at the job's frame rate -- with frames in flight on the
-            # library's lanes the kernels overlap, so per-kernel launch durations (above) include the
-            # time they share the GPU with other frames' kernels; this is the pipeline's figure
-            "frame_roofline": {"bound": "hbm", "bytes_per_px": frame_bytes_per_px(prm), "unit": "GB/s",
-                               "achieved": round(frame_bytes_per_px(prm) * W * H / (ms_per_step * 1e-3) / 1e9, 2),
-                               "peak": HBM_PEAK_GBS, "traffic": frame_traffic,
-                               "frac": round(frame_bytes_per_px(prm) * W * H / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)},
-            "valu_issue": None if not valu or k_ms <= 0 else {
-                "achieved": round(valu / (k_ms * 1e-3) / 1e9, 2), "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
-                "frac": round(valu / (k_ms * 1e-3) / 1e9 / VALU_PEAK_GIPS, 4), "valu_per_launch": valu},
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            try:
-                out["cpu_baseline"] = cpu_baseline(sc, prm, W, H, args.cpu_threads)
-            except Exception as e:  # the baseline is reported, never required for the GPU number
-                out["cpu_baseline"] = {"value": None, "error": repr(e)}
-        else:
-            out["cpu_baseline"] = None
+        ms = dt / args.steps * 1e3
+        b_px = survey_bytes_per_px(prm)
+        gbs = b_px * W * H / (ms * 1e-3) / 1e9
+        out = {"metric": METRIC, "value": round(args.steps / dt, 4), "unit": "frames/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+               "data": f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX[args.scene]}])",
+               "config": {"workload": f"{args.scene}: {WORKLOADS[args.scene]}, {W}x{H}", "width": W, "height": H,
+                          "parallelism": f"row-bands x{world}", "bands": bands,
+                          "traversal": {0: "lockstep", 1: "lane"}.get(last_kind, str(last_kind)) + " (rank 0)",
+                          "frames_in_flight": 3},
+               "mrays_per_s": round(rays / dt / 1e6, 2), "rays_per_frame": rays // max(1, args.steps),
+               "reproj_rebuilt_per_frame": outside / max(1, args.steps),
+               "roofline": {"bound": "hbm", "scope": "frame (all passes, all ranks)", "bytes_per_px": b_px,
+                            "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                            "frac": round(gbs / (HBM_PEAK_GBS * world), 5), "traffic": None},
+               "cpu_baseline": None}
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -55,11 +55,20 @@ class Renderer {
 public:
     Renderer(int width, int height, int hip_device = 0, void* hip_stream = nullptr) : width_(width), height_(height) {
         check(rs_context_create(hip_device, width, height, hip_stream, &ctx_), nullptr);
-        frame_.assign((size_t)width * height * 3, 0.0f);
+        const size_t bytes = (size_t)width * height * 3 * sizeof(float);
+        for (auto& b : ring_) {                 // page-locked frame_data ring (asynchronous readback)
+            void* p = nullptr;
+            check(rs_host_alloc(ctx_, bytes, &p), ctx_);
+            b = static_cast<float*>(p);
+            std::memset(b, 0, bytes);
+        }
+        shown_ = ring_[0];
     }
     ~Renderer() {
+        if (ctx_) rs_synchronize(ctx_);
         if (scene_) rs_scene_destroy(scene_);
         if (ctx_) rs_context_destroy(ctx_);
+        for (auto b : ring_) rs_host_free(b);
     }
     Renderer(const Renderer&) = delete;
     Renderer& operator=(const Renderer&) = delete;
@@ -80,22 +89,43 @@ public:
 
     // SimpleGuiDX11::produceRestir(t): one frame with the current camera_ and params; frame_data()
     // then holds the linear-HDR framebuffer, the duration members the per-pass device times.
+    //   pipelineDepth = 0 (reference semantics): frame_data() is this frame (the call waits for it).
+    //   pipelineDepth = d (1..2): the frame's readback into host memory runs while the next frames
+    //     render, and frame_data() is the frame d frames back (frameDataIndex() says which; finish()
+    //     brings it up to date) -- the producer loop's accumulate/tonemap then lags d frames.  d = 2 keeps
+    //     as many frames in flight as the library's run-ahead lanes (3).
+    //   timePasses = false: no per-frame pass timing (the duration members are not updated; that saves
+    //     the host sync rs_render_frame needs to read the device times back).
     void produceRestir(float t = 0.0f) {
         (void)t;
         if (!scene_) throw Error(RS_E_INVALID, "produceRestir: no scene loaded");
         rs_pass_times pt{};
-        check(rs_render_frame(ctx_, scene_, &camera_, &params, frameCtr, frame_.data(), &pt), ctx_);
-        gBUfferFillDuration = pt.gbuffer_initial_ms;   // G-buffer fill and initial RIS run fused
-        initialCandidatesGenDuration = 0.0f;
-        visibilityPassDuration = pt.visibility_ms;
-        temporalReusePassDuration = pt.temporal_ms;
-        spatialReusePassDuration = pt.spatial_ms;
-        shadingPassDuration = pt.shade_ms;
-        bufferCopyDuration = 0.0f;                      // history is a pointer swap
-        totalFrameDuration = pt.total_ms;
-        raysTraced = pt.rays;
+        check(rs_render_frame(ctx_, scene_, &camera_, &params, frameCtr, nullptr, timePasses ? &pt : nullptr), ctx_);
+        Pending p{0, ring_[cur_], (long long)frameCtr};
+        check(rs_frame_readback(ctx_, p.buf, &p.ticket), ctx_);
+        pending_[n_pending_++] = p;
+        cur_ = (cur_ + 1) % kRing;
+        const int depth = pipelineDepth < 0 ? 0 : (pipelineDepth > kRing - 1 ? kRing - 1 : pipelineDepth);
+        while (n_pending_ > depth) publish();
+        if (timePasses) {
+            gBUfferFillDuration = pt.gbuffer_initial_ms;   // G-buffer fill and initial RIS run fused
+            initialCandidatesGenDuration = 0.0f;
+            visibilityPassDuration = pt.visibility_ms;
+            temporalReusePassDuration = pt.temporal_ms;
+            spatialReusePassDuration = pt.spatial_ms;
+            shadingPassDuration = pt.shade_ms;
+            bufferCopyDuration = 0.0f;                      // history is a pointer swap
+            totalFrameDuration = pt.total_ms;
+            raysTraced = pt.rays;
+        }
         ++frameCtr;
     }
+    // pipelined mode: wait for the outstanding readbacks; frame_data() is then the last frame produced
+    void finish() {
+        while (n_pending_ > 0) publish();
+    }
+    // frameCtr of the frame frame_data() holds (-1 before the first one has landed)
+    long long frameDataIndex() const { return shown_frame_; }
     void resetHistory() { check(rs_reset_history(ctx_), ctx_); }
 
     // The producer loop's post block after produceRestir (pg/simpleguidx11.cpp:246-333, OIDN excluded):
@@ -112,7 +142,7 @@ public:
     }
     const float* display_device_data() const { return display_device_; }   // device W*H*4 float RGBA
 
-    const float* frame_data() const { return frame_.data(); }    // W*H*3, row-major, y=0 top
+    const float* frame_data() const { return shown_; }           // W*H*3, row-major, y=0 top
     int width() const { return width_; }
     int height() const { return height_; }
     rs_context* handle() { return ctx_; }
@@ -120,6 +150,8 @@ public:
     Camera camera_;
     Params params;
     uint32_t frameCtr = 0;
+    int pipelineDepth = 0;
+    bool timePasses = true;
     float gBUfferFillDuration = 0, initialCandidatesGenDuration = 0, visibilityPassDuration = 0,
           temporalReusePassDuration = 0, spatialReusePassDuration = 0, shadingPassDuration = 0,
           bufferCopyDuration = 0, totalFrameDuration = 0;
@@ -132,6 +164,20 @@ public:
     double accumulatorMean = 0.0, accumulatorVariance = 0.0;
 
 private:
+    struct Pending { uint64_t ticket; float* buf; long long frame; };
+    static constexpr int kRing = 3;
+    void publish() {                            // the oldest outstanding readback becomes frame_data()
+        check(rs_frame_wait(ctx_, pending_[0].ticket), ctx_);
+        shown_ = pending_[0].buf; shown_frame_ = pending_[0].frame;
+        for (int i = 1; i < n_pending_; ++i) pending_[i - 1] = pending_[i];
+        --n_pending_;
+    }
+    float* ring_[kRing] = {};
+    float* shown_ = nullptr;
+    Pending pending_[kRing] = {};
+    int n_pending_ = 0;
+    long long shown_frame_ = -1;
+    int cur_ = 0;
     const float* display_device_ = nullptr;
     void replace_scene(rs_scene* s) {
         if (scene_) rs_scene_destroy(scene_);
@@ -140,7 +186,6 @@ private:
     int width_, height_;
     rs_context* ctx_ = nullptr;
     rs_scene* scene_ = nullptr;
-    std::vector<float> frame_;
 };
 
 }  // namespace restir

@@ -204,6 +204,18 @@ int rs_get_timing_totals(rs_context* ctx, rs_pass_times* sum, uint32_t* n_frames
 /* Device pointer to the framebuffer (frame_data): W*H*3 floats, valid until the next render (with a
  * frame ring of 2: until the render after next). */
 int rs_get_frame_device_ptr(rs_context* ctx, const float** dptr);
+/* Asynchronous framebuffer readback (the reference's frame_data, pg/simpleguidx11.h:152, is host memory
+ * the passes write in place).  rs_frame_readback enqueues a copy of the last rendered frame's W*H*3
+ * floats into host_dst on the context's stream, ordered after that frame, and returns a ticket
+ * without waiting; rs_frame_wait blocks until that copy has landed.  The next frame that would overwrite
+ * the framebuffer being read (the same run-ahead lane) waits for the copy on the device, so the copy
+ * overlaps the following frames' rendering.  host_dst should be page-locked (rs_host_alloc) for the
+ * copy to be asynchronous. */
+int rs_frame_readback(rs_context* ctx, float* host_dst, uint64_t* ticket);
+int rs_frame_wait(rs_context* ctx, uint64_t ticket);
+/* Page-locked host memory for rs_frame_readback (hipHostMalloc on the context's device). */
+int rs_host_alloc(rs_context* ctx, size_t bytes, void** out);
+void rs_host_free(void* p);
 /* Forget the previous frame (frameCtr = 0): the next frame skips temporal reuse. */
 int rs_reset_history(rs_context* ctx);
 /* Wait for all work queued on the context's stream. */

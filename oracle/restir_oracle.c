@@ -654,6 +654,7 @@ typedef struct {
     float* im_cache[2];       /* 1/calc_I_M per pixel for Phong-dispatched surfaces */
     void* tile;               /* or_tile_state, allocated on first use */
     uint64_t rebuilt;         /* tile mode: G elements the temporal pass rebuilt beyond the tile's rows */
+    uint64_t ref_rays;        /* the last frame's reference-equivalent ray count (fold_ref) */
 } or_ctx;
 
 or_ctx* or_ctx_create(int W, int H) {
@@ -715,6 +716,21 @@ static inline int res_add(or_res* r, sample_t s, float w, int conf, rng_t* rng) 
 /* Reservoir::capConfidence (pg/Reservoir.h:54-56) */
 static inline void res_cap(or_res* r, int cap) { r->conf = r->conf < cap ? r->conf : cap; }
 
+/* ------------------------------------------------------------------ reference-equivalent ray count
+ * Rays the REFERENCE would trace for the same frame: every rtcIntersect1 (primary + BRDF rays) and every
+ * testOcclusion its code reaches -- each visibility-tested evaluateF with a valid sample at a
+ * non-emissive pixel (pg/ReSTIRIntegrator.cpp:185-206; also when L_i*f_r*G is zero, a ray this
+ * restatement and the product skip), the final p-hats it re-evaluates (initial :289, temporal
+ * :706/:721/:727, spatial :481) and every pixel of visibilityPass (:302-312).  Per thread (no atomics
+ * in the timed CPU baseline), folded once per frame. */
+static _Thread_local uint64_t tl_ref;
+static uint64_t fold_ref(void) {
+    uint64_t t = 0;
+#pragma omp parallel reduction(+:t)
+    { t += tl_ref; tl_ref = 0; }
+    return t;
+}
+
 /* ------------------------------------------------------------------ per-frame context */
 typedef struct {
     const or_scene* s; or_ctx* c; const or_params* P; uint32_t frame;
@@ -739,6 +755,7 @@ static hitinfo intersect(const fctx* F, v3 o, v3 d, float tnear, uint64_t* rays)
     hitinfo hi; hi.hit = 0; hi.prim = 0xffffffffu; hi.t = FLT_MAX; hi.point = V(0, 0, 0); hi.normal = V(0, 0, 0);
     hi.u = 0.0f; hi.v = 0.0f;
     (*rays)++;
+    tl_ref++;
     or_hit h = closest_hit(F->s, o, d, tnear, FLT_MAX);
     if (!h.hit) return hi;
     const or_scene* s = F->s; uint32_t t = h.prim;
@@ -789,6 +806,7 @@ static v3 eval_brdf(const or_gbe* g, v3 cam, v3 wi, float im_cached, int use_cac
  * when L_i*f_r*G is exactly zero in every channel: the product is then 0 whatever V is. */
 static v3 evaluate_f(const fctx* F, sample_t smp, v3 cam, const or_gbe* g, float im, int test_vis, uint64_t* rays) {
     if (!smp_valid(smp) || g->le.x > 0 || g->le.y > 0 || g->le.z > 0) return V(0, 0, 0);
+    tl_ref += test_vis ? 1u : 0u;
     v3 ld = sub(smp.p, g->pos);
     float r2 = dot(ld, ld);
     ld = nrmz(ld);
@@ -1043,6 +1061,7 @@ static void pass_initial(fctx* F, or_res* Rw, int y0, int y1, uint64_t* rays) {
                 }
             }
             float ph = sample_valid(&r) ? best_phat : 0.0f;
+            tl_ref += (tv && sample_valid(&r)) ? 1u : 0u;        /* :289 re-evaluated with visibility */
             r.W = ph > 0.0f ? 1.0f / ph * r.wsum : 0.0f;
             res_cap(&r, P->confidence_cap);
             Rw[p] = r;
@@ -1058,6 +1077,7 @@ static void pass_visibility(fctx* F, or_res* Rw, int y0, int y1, uint64_t* rays)
     for (int y = y0; y < y1; ++y)
         for (int x = 0; x < W; ++x) {
             size_t p = (size_t)y * W + x;
+            tl_ref++;                    /* the reference traces it for every pixel */
             /* invalid samples only ever carry W == 0 already: skip their (meaningless) ray */
             if (!sample_valid(&Rw[p])) continue;
             if (occluded(F, F->G[p].pos, Rw[p].p, &rc)) Rw[p].W = 0;
@@ -1133,6 +1153,7 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             float m_cur = p_cur * (float)cr->conf / (p_cur * (float)cr->conf + p_prev * (float)pr->conf);
             if (!(m_cur > 0)) m_cur = 0.0f;
             float ph_cur = p_cur;  /* :706 re-evaluates the identical p-hat */
+            tl_ref += (smp_valid(cs) && !nonzero_pos(cur->le)) ? 1u : 0u;
             float w_cur = m_cur * ph_cur * cr->W;
             int took_cur = res_add(&res, cs, w_cur, cr->conf, &rng);
             p_cur = eval_phat(F, ps, ccam, cur, imc, 1, &rc);
@@ -1140,11 +1161,13 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             float m_prev = p_prev * (float)pr->conf / (p_cur * (float)cr->conf + p_prev * (float)pr->conf);
             if (!(m_prev > 0)) m_prev = 0.0f;
             float ph_prev = p_cur;  /* :721 re-evaluates the identical p-hat */
+            tl_ref += (smp_valid(ps) && !nonzero_pos(cur->le)) ? 1u : 0u;
             float w_prev = m_prev * ph_prev * pr->W;
             int took_prev = res_add(&res, ps, w_prev, pr->conf, &rng);
             res_cap(&res, P->confidence_cap);
             /* final p-hat (:727) of the surviving sample at the current pixel */
             float fph = took_prev ? ph_prev : (took_cur ? ph_cur : 0.0f);
+            tl_ref += (sample_valid(&res) && !nonzero_pos(cur->le)) ? 1u : 0u;
             res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
             Rw[p] = res;
         }
@@ -1245,12 +1268,15 @@ static void pass_spatial(fctx* F, const or_res* Rr, or_res* Rw, int pass_idx, in
             }
             /* final p-hat (:481): p-hat of the surviving sample at this pixel = sel_phat */
             float fph = sample_valid(&res) ? sel_phat : 0.0f;
+            tl_ref += sample_valid(&res) ? 1u : 0u;
             if (P->spatial_mis == MIS_CONSTANT || P->spatial_mis == MIS_BALANCE || P->spatial_mis == MIS_PAIRWISE) {
                 res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
             } else if (P->spatial_mis == MIS_DEBIAS_Z) {
                 int Z = 0; float corr = 1.0f;
-                for (int i = 0; i < cnt; ++i)
+                for (int i = 0; i < cnt; ++i) {
+                    tl_ref++;
                     if (!occluded(F, F->G[nb[i]].pos, res.p, &rc)) Z += 1;
+                }
                 if (Z > 0 && M > 0) corr = (1.0f / (float)Z) / rcpM;
                 res.W = fph > 0.0f ? corr * res.wsum / fph : 0.0f;
             } else if (P->spatial_mis == MIS_DEBIAS_CONTRIB) {
@@ -1325,6 +1351,7 @@ int or_tile_begin(or_ctx* c, const or_scene* s, const float* cam7, const or_para
     if (y0 < 0 || y1 > H || y0 >= y1 || margin < 0 || halo < 0 || halo > margin) return -1;
     or_tile_state* T = tile_of(c);
     if (!T) return -1;
+    (void)fold_ref();            /* drop counts of earlier non-frame calls (trace hooks, MIS frames) */
     T->P = *P; T->y0 = y0; T->y1 = y1; T->halo = halo; T->rays = 0;
     T->cam = make_cam(cam7, W, H);
     /* G-buffer ping-pong instead of gBufferLastFrame.setDataFrom (:480) */
@@ -1397,6 +1424,7 @@ int or_tile_finish(or_ctx* c, float* out_rgb, uint64_t* rays_out) {
     if (!T || !T->active) return -1;
     or_tile_temporal(c);
     pass_shade(&T->F, c->r[T->rcur], out_rgb, T->y0, T->y1, &T->rays);
+    c->ref_rays = fold_ref();
     c->r_last = T->rcur;
     c->frames++;
     T->active = 0;
@@ -1766,3 +1794,4 @@ void or_kat_mis(int A, int B, float pa, float pb, float* out2) {
     out2[1] = m_brdf(&P, pb, pa);
 }
 uint64_t or_ctx_rebuilt(const or_ctx* c) { return c->rebuilt; }
+uint64_t or_ctx_ref_rays(const or_ctx* c) { return c->ref_rays; }

@@ -162,6 +162,14 @@ struct rs_context {
     uint32_t acc_frames = 0;
     uint64_t post_px = 0;                  // pixels the last rs_post_frame's statistics cover
     rs_camera cam_last = {};               // camera of the last frame (rs_export_png's sidecar)
+    // asynchronous framebuffer readback (rs_frame_readback): ticket ring, and per lane the readback its
+    // framebuffer is under (that lane's next frame waits for it before writing)
+    bool readback_kernel = true;           // copy kernel into page-locked memory (env RESTIR_READBACK=sdma: DMA)
+    static constexpr int kRb = 8;
+    hipEvent_t rb_ev[kRb] = {};
+    bool rb_busy[kRb] = {};
+    uint64_t rb_seq = 0;
+    hipEvent_t fb_read[kLanes] = {};
 };
 
 // --------------------------------------------------------------------------- helpers
@@ -317,6 +325,8 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->split_mode = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->split_mode = RS_SPLIT_OFF;
     }
+    if (const char* t = std::getenv("RESTIR_READBACK"))        // kernel (default) | sdma
+        c->readback_kernel = std::strcmp(t, "sdma") != 0;
     if (const char* t = std::getenv("RESTIR_RUNAHEAD"))        // run-ahead depth 0..kMaxAhead
         c->ahead = std::max(0, std::min(kMaxAhead, std::atoi(t)));
     {
@@ -402,6 +412,7 @@ extern "C" void rs_context_destroy(rs_context* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (auto st : c->lane) if (st) hipStreamSynchronize(st);
+    for (auto e : c->rb_ev) if (e) hipEventDestroy(e);
     for (auto& g : c->G) {
         float4* f[5] = {g.g0, g.g1, g.g2, g.g3, g.g4};
         for (auto* p : f) if (p) hipFree(p);
@@ -1183,6 +1194,10 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     }
     const bool on_ctx = D == 0 || c->join_next || c->tuning;   // a traversal-tuning frame runs alone
     c->fs = on_ctx ? c->stream : c->lane[c->li];
+    if (c->fb_read[c->li]) {                    // the lane's framebuffer is still being read back
+        HIPCHK(c, hipStreamWaitEvent(c->fs, c->fb_read[c->li], 0));
+        c->fb_read[c->li] = nullptr;
+    }
     c->fb = c->fbs[c->li];
     c->d_cnt = c->cnts[c->li]; c->d_red = c->reds[c->li];
     // reservoir ring: `last` = the previous frame's final buffer (reservoirsLastFrame, a pointer swap,
@@ -1457,6 +1472,8 @@ extern "C" int rs_render_direct_mis(rs_context* c, const rs_scene* s, const rs_c
     c->fs = c->stream; c->li = 0;                 // the context's stream (after every frame enqueued so far)
     c->d_cnt = c->cnts[0]; c->d_red = c->reds[0];
     sync_all(c);                                  // lane 0's slots may still be in use
+    c->fb = c->fbs[0];
+    if (c->fb_read[0]) { HIPCHK(c, hipEventSynchronize(c->fb_read[0])); c->fb_read[0] = nullptr; }
     if (!use_parts(c, 0, grid_waves(g))) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
     c->join_next = true;
     HIPCHK(c, hipMemsetAsync(c->d_cnt, 0, sizeof(Counters), c->stream));
@@ -1491,6 +1508,69 @@ extern "C" int rs_get_frame_device_ptr(rs_context* c, const float** dptr) {
     if (!c || !dptr) return fail(c, RS_E_INVALID, "rs_get_frame_device_ptr: null argument");
     *dptr = c->fb;
     return RS_OK;
+}
+
+// Readback of the framebuffer into page-locked host memory by a copy kernel on the copy stream: the
+// SDMA engine moved 24.9 MB in ~1.8 ms (~14 GB/s, longer than a C2 frame); CU stores to host memory
+// over the host link are faster; 256 workgroups of 256 threads share the CUs with the frames in flight
+// for the copy's duration.
+typedef float rb_v4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) k_readback(const rb_v4* __restrict__ src, rb_v4* dst, size_t n4) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store(src[i], dst + i);
+}
+
+extern "C" int rs_frame_readback(rs_context* c, float* dst, uint64_t* ticket) {
+    if (!c || !dst || !ticket) return fail(c, RS_E_INVALID, "rs_frame_readback: null argument");
+    if (c->active) return fail(c, RS_E_INVALID, "rs_frame_readback: a tile frame is in flight");
+    HIPCHK(c, enter(c));
+    if (!c->rb_ev[0])
+        for (int i = 0; i < rs_context::kRb; ++i) HIPCHK(c, hipEventCreateWithFlags(&c->rb_ev[i], hipEventDisableTiming));
+    const uint64_t t = ++c->rb_seq;
+    const int k = (int)(t % rs_context::kRb);
+    if (c->rb_busy[k]) HIPCHK(c, hipEventSynchronize(c->rb_ev[k]));   // the slot's ticket kRb ago
+    const size_t bytes = (size_t)c->W * c->H * 3 * sizeof(float);
+    // page-locked destination (rs_host_alloc / hipHostMalloc) and 16-B aligned: copy kernel (RESTIR_READBACK=
+    // sdma forces the DMA engine); pageable memory: hipMemcpyAsync (staged by the runtime).  Both on the
+    // context's stream, which is ordered after every frame enqueued so far (rs_tile_finish) and runs nothing
+    // else while frames run on their lanes: a fifth stream would share one of the process's 4 hardware
+    // queues with a lane and serialise the copy with that lane's next frame.
+    hipPointerAttribute_t at{};
+    void* ddst = nullptr;
+    const bool kernel_ok = c->readback_kernel && bytes % 16 == 0 && ((uintptr_t)dst & 15) == 0 &&
+                           hipPointerGetAttributes(&at, dst) == hipSuccess && at.type == hipMemoryTypeHost &&
+                           hipHostGetDevicePointer(&ddst, dst, 0) == hipSuccess && ddst != nullptr;
+    (void)hipGetLastError();                   // a pageable pointer leaves an error in the per-thread slot
+    if (kernel_ok) {
+        k_readback<<<256, 256, 0, c->stream>>>((const rb_v4*)c->fb, (rb_v4*)ddst, bytes / 16);
+        HIPCHK(c, hipGetLastError());
+    } else {
+        HIPCHK(c, hipMemcpyAsync(dst, c->fb, bytes, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipEventRecord(c->rb_ev[k], c->stream));
+    c->rb_busy[k] = true;
+    c->fb_read[c->li] = c->rb_ev[k];
+    *ticket = t;
+    return RS_OK;
+}
+
+extern "C" int rs_frame_wait(rs_context* c, uint64_t t) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_frame_wait: null context");
+    if (t == 0 || t > c->rb_seq) return fail(c, RS_E_INVALID, "rs_frame_wait: unknown ticket");
+    if (c->rb_seq - t >= (uint64_t)rs_context::kRb) return RS_OK;    // its slot was reused: waited for then
+    HIPCHK(c, enter(c));
+    HIPCHK(c, hipEventSynchronize(c->rb_ev[t % rs_context::kRb]));
+    return RS_OK;
+}
+
+extern "C" int rs_host_alloc(rs_context* c, size_t bytes, void** out) {
+    if (!c || !out || bytes == 0) return fail(c, RS_E_INVALID, "rs_host_alloc: bad argument");
+    HIPCHK(c, enter(c));
+    HIPCHK(c, hipHostMalloc(out, bytes, hipHostMallocDefault));
+    return RS_OK;
+}
+extern "C" void rs_host_free(void* p) {
+    if (p) hipHostFree(p);
 }
 
 extern "C" int rs_reset_history(rs_context* c) {

@@ -32,7 +32,8 @@ EXPORTED_SYMBOLS = [
     "rs_post_reset", "rs_scene_rebuild", "rs_render_direct_mis", "rs_scene_create_textured", "rs_scene_set_sky",
     "rs_scene_load_sky", "rs_image_decode", "rs_context_set_initial_split", "rs_context_get_initial_split",
     "rs_context_set_frame_ring", "rs_context_set_run_ahead", "rs_tile_stream", "rs_export_png",
-    "rs_image_encode_png", "rs_context_track_row_costs", "rs_get_row_costs",
+    "rs_image_encode_png", "rs_context_track_row_costs", "rs_get_row_costs", "rs_frame_readback", "rs_frame_wait",
+    "rs_host_alloc", "rs_host_free",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -189,6 +190,11 @@ def load_library(path: str = LIB_PATH):
                                   ctypes.POINTER(i32), vp, ctypes.c_size_t]
     L.rs_render_direct_mis.argtypes = [vp, vp, ctypes.POINTER(CameraDesc), ctypes.POINTER(FrameParams), u32, u32, fp,
                                        ctypes.POINTER(PassTimes)]
+    L.rs_frame_readback.argtypes = [vp, fp, ctypes.POINTER(ctypes.c_uint64)]
+    L.rs_frame_wait.argtypes = [vp, ctypes.c_uint64]
+    L.rs_host_alloc.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
+    L.rs_host_free.argtypes = [vp]
+    L.rs_host_free.restype = None
     _lib = L
     return L
 

@@ -428,3 +428,37 @@ def moving_light_positions(scene: Scene, frame: int, n_frames: int = 240, amplit
         t = quads[:, j]
         pos[t] = (pos[t].reshape(-1, 3, 3) + off[:, None, :]).reshape(-1, 9).astype(np.float32)
     return pos
+
+
+def write_obj(scene: Scene, obj_path: str) -> None:
+    """Write ``scene`` as OBJ + MTL (``<obj>.mtl`` beside it) for rs_scene_load_obj / Raytracer::LoadScene.
+    Kd / Ks are written sRGB-compressed so the loader's expansion (pg/ModelLoader.cpp:80-97) recovers the
+    linear values; Ke, Ns and the material class (Pc) as they are; per-vertex normals; triangles in the
+    scene's order (one usemtl run per material change)."""
+    import os
+
+    def comp(v):
+        v = float(np.float32(v))
+        return 0.0 if v <= 0 else (v * 12.92 if v <= 0.0031308 else 1.055 * v ** (1 / 2.4) - 0.055)
+
+    mtl = os.path.splitext(obj_path)[0] + ".mtl"
+    with open(mtl, "w") as f:
+        for i, m in enumerate(scene.materials):
+            f.write(f"newmtl m{i}\nPc {m.type}\nKd {' '.join(f'{comp(c):.9g}' for c in m.kd)}\n"
+                    f"Ks {' '.join(f'{comp(c):.9g}' for c in m.ks)}\nKe {' '.join(f'{c:.9g}' for c in m.le)}\n"
+                    f"Ns {m.shininess:.9g}\n")
+    P = np.asarray(scene.positions, np.float32).reshape(-1, 3)
+    N = np.asarray(scene.normals, np.float32).reshape(-1, 3)
+    with open(obj_path, "w") as f:
+        f.write(f"mtllib {os.path.basename(mtl)}\n")
+        f.write("".join(f"v {x:.9g} {y:.9g} {z:.9g}\n" for x, y, z in P))
+        f.write("".join(f"vn {x:.9g} {y:.9g} {z:.9g}\n" for x, y, z in N))
+        cur = -1
+        lines = []
+        for t in range(scene.n_tris):
+            if scene.tri_material[t] != cur:
+                cur = int(scene.tri_material[t])
+                lines.append(f"usemtl m{cur}\n")
+            b = 3 * t + 1
+            lines.append(f"f {b}//{b} {b + 1}//{b + 1} {b + 2}//{b + 2}\n")
+        f.write("".join(lines))

