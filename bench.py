@@ -315,7 +315,9 @@ def main():
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     W, H = args.width, args.height
-    if world == 1:
+    # RESTIR_FORCE_MULTI=1 runs the N>1 code path with one rank (a rehearsal of the multi-GPU flow on a
+    # one-GPU box: RCCL refuses two ranks on one device)
+    if world == 1 and not os.environ.get("RESTIR_FORCE_MULTI"):
         torch.cuda.set_device(local)
         # render on a dedicated torch stream shared with the library (torch's default stream is handle 0)
         torch.cuda.set_stream(torch.cuda.Stream(device=local))
@@ -348,6 +350,87 @@ def main():
 
 
 def run_multi(args, world, rank, local, W, H):
+    """N>1: the native multi-GPU path behind the C ABI (rs_mgpu_*: RCCL point-to-point halo exchange and
+    gather on each frame's stream, csrc/rs_mgpu.hip) with torch.distributed over gloo as the control
+    plane only (the RCCL id broadcast, barriers, max-over-ranks timing).  RESTIR_MGPU=python (or the
+    RESTIR_DIST_BACKEND=gloo rehearsal with ranks sharing a GPU) runs the Python orchestration
+    (restir_amd/distributed.py) instead."""
+    if os.environ.get("RESTIR_MGPU", "cabi") == "python" or os.environ.get("RESTIR_DIST_BACKEND") == "gloo":
+        return run_multi_python(args, world, rank, local, W, H)
+    import torch
+    import torch.distributed as dist
+    from restir_amd import Renderer
+    from restir_amd.mgpu import MultiGpuFrame
+    dist.init_process_group("gloo")
+    sc, prm, camera, light_pos = workload(args.scene)
+    cam = camera or (lambda f: sc.camera)
+    torch.cuda.set_device(local)
+    r = Renderer(W, H, device=local)
+    gs = r.load_scene(sc)
+    uid = [MultiGpuFrame.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    m = MultiGpuFrame(r, rank=rank, world=world, unique_id=uid[0])
+
+    def step(f):
+        if light_pos is not None:
+            gs.update_positions(light_pos(f))
+        m.render([gs], cam(f), prm, f, gather=True)
+
+    for f in range(TUNE_FRAMES):
+        step(f)
+    bands = m.rebalance([gs], cam(0), prm, 0, 2, 8)
+    if rank == 0:
+        print(f"bands: {bands}", file=sys.stderr)
+    for f in range(args.warmup):
+        step(f)
+    r.synchronize()
+    torch.cuda.synchronize()
+    dist.barrier()
+    r.timing_totals(reset=True)
+    t0 = time.perf_counter()
+    for f in range(args.steps):
+        step(args.warmup + f)
+    r.synchronize()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    tot, _ = r.timing_totals()
+    red = torch.tensor([dt, float(tot.rays), float(tot.reproj_outside)], dtype=torch.float64)
+    dmax = red[:1].clone()
+    dist.all_reduce(dmax, op=dist.ReduceOp.MAX)
+    sums = red[1:].clone()
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+    dt, rays, outside = float(dmax[0]), int(sums[0]), int(sums[1])
+    _, last_kind, _ = r.traversal(gs)
+    if rank == 0:
+        print(json.dumps(multi_line(args, world, W, H, prm, dt, rays, outside, bands, last_kind,
+                                    "rs_mgpu (C ABI): RCCL point-to-point halo + gather")), flush=True)
+    dist.barrier()
+    m.close()
+    dist.destroy_process_group()
+
+
+def multi_line(args, world, W, H, prm, dt, rays, outside, bands, last_kind, path):
+    ms = dt / args.steps * 1e3
+    b_px = survey_bytes_per_px(prm)
+    gbs = b_px * W * H / (ms * 1e-3) / 1e9
+    return {"metric": METRIC, "value": round(args.steps / dt, 4), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX[args.scene]}])",
+            "config": {"workload": f"{args.scene}: {WORKLOADS[args.scene]}, {W}x{H}", "width": W, "height": H,
+                       "parallelism": f"row-bands x{world}", "bands": bands, "multi_gpu_path": path,
+                       "traversal": {0: "lockstep", 1: "lane"}.get(last_kind, str(last_kind)) + " (rank 0)",
+                       "frames_in_flight": 3},
+            "mrays_per_s": round(rays / dt / 1e6, 2), "rays_per_frame": rays // max(1, args.steps),
+            "reproj_rebuilt_per_frame": outside / max(1, args.steps),
+            "roofline": {"bound": "hbm", "scope": "frame (all passes, all ranks)", "bytes_per_px": b_px,
+                         "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                         "frac": round(gbs / (HBM_PEAK_GBS * world), 5), "traffic": None},
+            "cpu_baseline": None}
+
+
+def run_multi_python(args, world, rank, local, W, H):
     import torch
     import torch.distributed as dist
     # RESTIR_DIST_BACKEND=gloo rehearses the N>1 flow with more ranks than GPUs (ranks share devices,
@@ -402,24 +485,8 @@ def run_multi(args, world, rank, local, W, H):
     dt, rays, outside = float(dmax[0]), int(sums[0]), int(sums[1])
     _, last_kind, _ = tr.be.r.traversal(gs)
     if rank == 0:
-        ms = dt / args.steps * 1e3
-        b_px = survey_bytes_per_px(prm)
-        gbs = b_px * W * H / (ms * 1e-3) / 1e9
-        out = {"metric": METRIC, "value": round(args.steps / dt, 4), "unit": "frames/s", "n_gpus": world,
-               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-               "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-               "data": f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX[args.scene]}])",
-               "config": {"workload": f"{args.scene}: {WORKLOADS[args.scene]}, {W}x{H}", "width": W, "height": H,
-                          "parallelism": f"row-bands x{world}", "bands": bands,
-                          "traversal": {0: "lockstep", 1: "lane"}.get(last_kind, str(last_kind)) + " (rank 0)",
-                          "frames_in_flight": 3},
-               "mrays_per_s": round(rays / dt / 1e6, 2), "rays_per_frame": rays // max(1, args.steps),
-               "reproj_rebuilt_per_frame": outside / max(1, args.steps),
-               "roofline": {"bound": "hbm", "scope": "frame (all passes, all ranks)", "bytes_per_px": b_px,
-                            "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
-                            "frac": round(gbs / (HBM_PEAK_GBS * world), 5), "traffic": None},
-               "cpu_baseline": None}
-        print(json.dumps(out), flush=True)
+        print(json.dumps(multi_line(args, world, W, H, prm, dt, rays, outside, bands, last_kind,
+                                    "restir_amd.distributed (Python): torch.distributed halo + gather")), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

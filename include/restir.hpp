@@ -146,6 +146,7 @@ public:
     int width() const { return width_; }
     int height() const { return height_; }
     rs_context* handle() { return ctx_; }
+    rs_scene* scene_handle() { return scene_; }
 
     Camera camera_;
     Params params;
@@ -186,6 +187,64 @@ private:
     int width_, height_;
     rs_context* ctx_ = nullptr;
     rs_scene* scene_ = nullptr;
+};
+
+// The N-GPU frame (rs_mgpu_*) with the same member surface: N row bands, one Renderer
+// (context) per rank, all driven from this thread (rs_mgpu_create_local: halo exchange and gather by
+// device copies; rank i on HIP device i % device_count).  frame_data() is rank 0's gathered frame.  A
+// multi-process deployment uses rs_mgpu_create with an RCCL id instead.
+class MultiGpuRenderer {
+public:
+    MultiGpuRenderer(int width, int height, int ranks, int device_count = 1) : width_(width), height_(height) {
+        if (ranks < 1 || device_count < 1) throw Error(RS_E_INVALID, "MultiGpuRenderer: ranks and device_count must be >= 1");
+        for (int i = 0; i < ranks; ++i) ranks_.emplace_back(new Renderer(width, height, i % device_count));
+        frame_.assign((size_t)width * height * 3, 0.0f);
+    }
+    ~MultiGpuRenderer() {
+        if (m_) rs_mgpu_destroy(m_);
+        for (auto* r : ranks_) delete r;
+    }
+    MultiGpuRenderer(const MultiGpuRenderer&) = delete;
+    MultiGpuRenderer& operator=(const MultiGpuRenderer&) = delete;
+
+    int ranks() const { return (int)ranks_.size(); }
+    Renderer& rank(int i) { return *ranks_[i]; }       // load the scene into every rank (LoadScene)
+    // one frame as N bands, gathered into frame_data() (synchronous)
+    void produceRestir(float t = 0.0f) {
+        (void)t;
+        if (!m_) {
+            std::vector<rs_context*> ctxs;
+            for (auto* r : ranks_) ctxs.push_back(r->handle());
+            check(rs_mgpu_create_local(ctxs.data(), (int)ctxs.size(), &m_), ranks_[0]->handle());
+        }
+        std::vector<const rs_scene*> scenes;
+        for (auto* r : ranks_) {
+            if (!r->scene_handle()) throw Error(RS_E_INVALID, "MultiGpuRenderer: load the scene into every rank");
+            scenes.push_back(r->scene_handle());
+        }
+        check(rs_mgpu_render_frame(m_, scenes.data(), &camera_, &params, frameCtr, 1, frame_.data(), nullptr),
+              ranks_[0]->handle());
+        ++frameCtr;
+    }
+    // cost-balanced bands from n_frames of per-row wave times (resets the history)
+    void rebalance(int n_frames = 2, int min_rows = 8) {
+        produceRestir();                              // creates the group
+        std::vector<const rs_scene*> scenes;
+        for (auto* r : ranks_) scenes.push_back(r->scene_handle());
+        check(rs_mgpu_rebalance(m_, scenes.data(), &camera_, &params, frameCtr, n_frames, min_rows), ranks_[0]->handle());
+        frameCtr = 0;
+    }
+    const float* frame_data() const { return frame_.data(); }
+
+    Camera camera_;
+    Params params;
+    uint32_t frameCtr = 0;
+
+private:
+    int width_, height_;
+    std::vector<Renderer*> ranks_;
+    rs_mgpu* m_ = nullptr;
+    std::vector<float> frame_;
 };
 
 }  // namespace restir

@@ -349,6 +349,48 @@ int rs_tile_temporal(rs_context* ctx);
 int rs_tile_spatial(rs_context* ctx, int pass_index);
 int rs_tile_finish(rs_context* ctx, const float** band_rgb_dptr, rs_pass_times* times);
 
+/* ---- multi-GPU frames behind the ABI (SURVEY.md §8b rs_mgpu_render_frame, §8e) ------------------
+ * The caller of the reference (SimpleGuiDX11::Producer, pg/simpleguidx11.cpp:240-241) renders one frame
+ * per produceRestir; here a frame of `world` row bands is rendered by one rs_mgpu_render_frame call per
+ * rank (process), each rank on its own GPU context: G-buffer + initial RIS of its rows, temporal, then
+ * before every spatial pass a point-to-point halo exchange of floor(sqrt(R)) reservoir rows with each
+ * neighbour (RCCL ncclSend/ncclRecv group on the frame's stream; one communicator per run-ahead lane so
+ * frames in flight communicate independently), shade, and a gather of the band framebuffers into rank
+ * 0's context framebuffer (rs_get_frame_device_ptr / rs_frame_readback on rank 0 then see the full
+ * frame).  The gathered frame is bit-identical to a single-GPU frame.
+ *   rank 0: rs_mgpu_unique_id(id); distribute id to every rank (MPI, a file, torch.distributed, ...)
+ *   every rank: rs_context_create(device) -> rs_scene_* (same scene) -> rs_mgpu_create(ctx, rank, world, id)
+ *               per frame: rs_mgpu_render_frame(m, &scene, camera, params, frame, gather=1, host_or_NULL, NULL)
+ * rs_mgpu_create_local drives `world` contexts of ONE process (a rank per context; transfers are device
+ * copies) -- several GPUs from one thread, or ranks sharing a GPU (tests).  `scenes` holds one scene per
+ * local rank (each loaded on that rank's context).  Calls are collective: every rank calls them in the
+ * same order. */
+typedef struct rs_mgpu rs_mgpu;
+#define RS_MGPU_ID_BYTES 128
+int rs_mgpu_unique_id(uint8_t id[RS_MGPU_ID_BYTES]);
+int rs_mgpu_create(rs_context* ctx, int rank, int world, const uint8_t id[RS_MGPU_ID_BYTES], rs_mgpu** out);
+int rs_mgpu_create_local(rs_context* const* ctxs, int world, rs_mgpu** out);
+void rs_mgpu_destroy(rs_mgpu* m);
+/* row bands: bounds[0] = 0 < bounds[1] < ... < bounds[world] = height (equal bands at creation) */
+int rs_mgpu_set_bands(rs_mgpu* m, const int32_t* bounds);
+int rs_mgpu_get_bands(const rs_mgpu* m, int32_t* bounds);
+/* Cost-balanced bands: renders n_frames (no gather) while the pass kernels record per-row wave time
+ * (rs_context_track_row_costs), all-reduces the rows' costs, moves the boundaries to equal cost (every
+ * band >= max(min_rows, halo) rows; same split on every rank), resets the history. */
+int rs_mgpu_rebalance(rs_mgpu* m, const rs_scene* const* scenes, const rs_camera* camera,
+                      const rs_frame_params* params, uint32_t first_frame, int n_frames, int min_rows);
+/* One frame.  gather != 0: bands -> rank 0's framebuffer; frame_rgb_host (rank 0, optional) receives it
+ * (synchronous).  times (optional, synchronous): the first local rank's pass times. */
+int rs_mgpu_render_frame(rs_mgpu* m, const rs_scene* const* scenes, const rs_camera* camera,
+                         const rs_frame_params* params, uint32_t frame_index, int gather, float* frame_rgb_host,
+                         rs_pass_times* times);
+/* the first local rank's framebuffer (on rank 0 after a gather: the full frame) */
+int rs_mgpu_frame_device_ptr(rs_mgpu* m, const float** dptr);
+int rs_mgpu_reset_history(rs_mgpu* m);
+/* host values summed (op 0) or maxed (op 1) over all ranks in place (RCCL all-reduce; synchronous) --
+ * for the caller's timing / statistics, not on the frame's data path */
+int rs_mgpu_allreduce(rs_mgpu* m, double* values, int n, int op);
+
 /* ---- test hook: raw BVH queries (rtcIntersect1 / rtcOccluded1 semantics) ----------------------
  * n rays, host arrays o[3n], d[3n], tnear[n], tfar[n].  any_hit=0: closest hit -> t_out[n] (-1 on miss),
  * prim_out[n] (original triangle index, -1 on miss); any_hit=1: prim_out[n] = 1 if occluded else 0.

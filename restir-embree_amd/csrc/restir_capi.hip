@@ -10,6 +10,7 @@
 #include "rs_refit.h"
 #include "../../include/restir_c.h"
 #include "rs_image.h"
+#include "rs_internal.h"
 
 #include <cmath>
 #include <cstdio>
@@ -164,12 +165,13 @@ struct rs_context {
     rs_camera cam_last = {};               // camera of the last frame (rs_export_png's sidecar)
     // asynchronous framebuffer readback (rs_frame_readback): ticket ring, and per lane the readback its
     // framebuffer is under (that lane's next frame waits for it before writing)
-    bool readback_kernel = true;           // copy kernel into page-locked memory (env RESTIR_READBACK=sdma: DMA)
+    bool readback_kernel = false;          // DMA engine (default) or a copy kernel (env RESTIR_READBACK=kernel)
     static constexpr int kRb = 8;
     hipEvent_t rb_ev[kRb] = {};
     bool rb_busy[kRb] = {};
     uint64_t rb_seq = 0;
     hipEvent_t fb_read[kLanes] = {};
+    hipEvent_t join_ev = nullptr;          // rs::ctx_join
 };
 
 // --------------------------------------------------------------------------- helpers
@@ -325,8 +327,8 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->split_mode = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->split_mode = RS_SPLIT_OFF;
     }
-    if (const char* t = std::getenv("RESTIR_READBACK"))        // kernel (default) | sdma
-        c->readback_kernel = std::strcmp(t, "sdma") != 0;
+    if (const char* t = std::getenv("RESTIR_READBACK"))        // sdma (default) | kernel
+        c->readback_kernel = std::strcmp(t, "kernel") == 0;
     if (const char* t = std::getenv("RESTIR_RUNAHEAD"))        // run-ahead depth 0..kMaxAhead
         c->ahead = std::max(0, std::min(kMaxAhead, std::atoi(t)));
     {
@@ -413,6 +415,7 @@ extern "C" void rs_context_destroy(rs_context* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     for (auto st : c->lane) if (st) hipStreamSynchronize(st);
     for (auto e : c->rb_ev) if (e) hipEventDestroy(e);
+    if (c->join_ev) hipEventDestroy(c->join_ev);
     for (auto& g : c->G) {
         float4* f[5] = {g.g0, g.g1, g.g2, g.g3, g.g4};
         for (auto* p : f) if (p) hipFree(p);
@@ -1510,10 +1513,11 @@ extern "C" int rs_get_frame_device_ptr(rs_context* c, const float** dptr) {
     return RS_OK;
 }
 
-// Readback of the framebuffer into page-locked host memory by a copy kernel on the copy stream: the
-// SDMA engine moved 24.9 MB in ~1.8 ms (~14 GB/s, longer than a C2 frame); CU stores to host memory
-// over the host link are faster; 256 workgroups of 256 threads share the CUs with the frames in flight
-// for the copy's duration.
+// Readback of the framebuffer into page-locked host memory.  Alone, a copy kernel's stores over the host
+// link move a 1080p frame (24.9 MB) in 0.46 ms (54 GB/s) against the DMA engine's 0.84 ms (30 GB/s)
+// (scripts/host_link_bw.hip); beside the frames in flight the kernel competes with them for CUs and the
+// DMA engine wins: C2 1080p drop-in 652 vs 533 frames/s at pipeline depth 2 (scripts/dropin_ab.sh).
+// So the DMA engine is the default, the kernel an option (RESTIR_READBACK=kernel).
 typedef float rb_v4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256) k_readback(const rb_v4* __restrict__ src, rb_v4* dst, size_t n4) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
@@ -1530,8 +1534,8 @@ extern "C" int rs_frame_readback(rs_context* c, float* dst, uint64_t* ticket) {
     const int k = (int)(t % rs_context::kRb);
     if (c->rb_busy[k]) HIPCHK(c, hipEventSynchronize(c->rb_ev[k]));   // the slot's ticket kRb ago
     const size_t bytes = (size_t)c->W * c->H * 3 * sizeof(float);
-    // page-locked destination (rs_host_alloc / hipHostMalloc) and 16-B aligned: copy kernel (RESTIR_READBACK=
-    // sdma forces the DMA engine); pageable memory: hipMemcpyAsync (staged by the runtime).  Both on the
+    // DMA engine (hipMemcpyAsync; pageable memory is staged by the runtime), or with RESTIR_READBACK=kernel
+    // and a page-locked, 16-B aligned destination a copy kernel.  Both on the
     // context's stream, which is ordered after every frame enqueued so far (rs_tile_finish) and runs nothing
     // else while frames run on their lanes: a fifth stream would share one of the process's 4 hardware
     // queues with a lane and serialise the copy with that lane's next frame.
@@ -1815,3 +1819,20 @@ extern "C" int rs_debug_trace(rs_context* c, const rs_scene* s, uint32_t n, cons
     if (e != hipSuccess || e2 != hipSuccess) return fail(c, RS_E_HIP, "rs_debug_trace: kernel failed");
     return RS_OK;
 }
+
+// ---------------------------------------------------------------- internal helpers (rs_internal.h)
+namespace rs {
+hipStream_t ctx_stream(rs_context* c) { return c->stream; }
+int ctx_device(const rs_context* c) { return c->device; }
+int ctx_width(const rs_context* c) { return c->W; }
+int ctx_height(const rs_context* c) { return c->H; }
+int ctx_fail(rs_context* c, int code, const std::string& msg) { return fail(c, code, msg); }
+int ctx_join(rs_context* c, hipStream_t st) {
+    HIPCHK(c, enter(c));
+    if (st == c->stream) return RS_OK;
+    if (!c->join_ev) HIPCHK(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->join_ev, st));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->join_ev, 0));   // captured now: the event may be re-recorded
+    return RS_OK;
+}
+}  // namespace rs

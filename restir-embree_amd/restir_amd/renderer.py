@@ -33,7 +33,9 @@ EXPORTED_SYMBOLS = [
     "rs_scene_load_sky", "rs_image_decode", "rs_context_set_initial_split", "rs_context_get_initial_split",
     "rs_context_set_frame_ring", "rs_context_set_run_ahead", "rs_tile_stream", "rs_export_png",
     "rs_image_encode_png", "rs_context_track_row_costs", "rs_get_row_costs", "rs_frame_readback", "rs_frame_wait",
-    "rs_host_alloc", "rs_host_free",
+    "rs_host_alloc", "rs_host_free", "rs_mgpu_unique_id", "rs_mgpu_create", "rs_mgpu_create_local",
+    "rs_mgpu_destroy", "rs_mgpu_set_bands", "rs_mgpu_get_bands", "rs_mgpu_rebalance", "rs_mgpu_render_frame",
+    "rs_mgpu_frame_device_ptr", "rs_mgpu_reset_history", "rs_mgpu_allreduce",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -195,6 +197,22 @@ def load_library(path: str = LIB_PATH):
     L.rs_host_alloc.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
     L.rs_host_free.argtypes = [vp]
     L.rs_host_free.restype = None
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    L.rs_mgpu_unique_id.argtypes = [u8p]
+    L.rs_mgpu_create.argtypes = [vp, i32, i32, u8p, ctypes.POINTER(vp)]
+    L.rs_mgpu_create_local.argtypes = [ctypes.POINTER(vp), i32, ctypes.POINTER(vp)]
+    L.rs_mgpu_destroy.argtypes = [vp]
+    L.rs_mgpu_destroy.restype = None
+    L.rs_mgpu_set_bands.argtypes = [vp, i32p]
+    L.rs_mgpu_get_bands.argtypes = [vp, i32p]
+    L.rs_mgpu_rebalance.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(CameraDesc), ctypes.POINTER(FrameParams),
+                                    u32, i32, i32]
+    L.rs_mgpu_render_frame.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(CameraDesc), ctypes.POINTER(FrameParams),
+                                       u32, i32, fp, ctypes.POINTER(PassTimes)]
+    L.rs_mgpu_frame_device_ptr.argtypes = [vp, ctypes.POINTER(vp)]
+    L.rs_mgpu_reset_history.argtypes = [vp]
+    L.rs_mgpu_allreduce.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i32, i32]
     _lib = L
     return L
 

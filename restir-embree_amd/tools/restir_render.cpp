@@ -5,14 +5,19 @@
 //
 //   restir_render [--obj file.obj] [--w 1920 --h 1080] [--frames 10] [--area 32] [--brdf 1]
 //                 [--spatial k] [--temporal] [--out frame.pfm] [--eye x y z --at x y z --fov deg]
-//                 [--bench]
+//                 [--bench] [--ranks N [--compare]]
 // --bench: the drop-in throughput -- frames/s of produceRestir with frame_data landing in host memory
 // every frame, pipelined (pipelineDepth 2 and 1: readbacks overlapping the next frames, timePasses off)
 // and with the reference's synchronous semantics; one JSON line.
+// --ranks N: the frames as N row bands, one context per rank (HIP device rank % device count) driven from
+// this thread through rs_mgpu_create_local / rs_mgpu_render_frame (halo exchange + gather by device
+// copies); --compare also renders them on one context and reports whether every frame is bit-identical.
 #include "../../include/restir.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <memory>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -24,10 +29,19 @@ static void quad(std::vector<float>& P, std::vector<float>& N, const float a[3],
     for (auto* v : t) { P.insert(P.end(), v, v + 3); N.insert(N.end(), n, n + 3); }
 }
 
+static void write_pfm(const std::string& path, int W, int H, const float* rgb) {
+    FILE* fp = std::fopen(path.c_str(), "wb");
+    if (!fp) throw restir::Error(RS_E_IO, "cannot write " + path);
+    std::fprintf(fp, "PF\n%d %d\n-1.0\n", W, H);
+    for (int y = H - 1; y >= 0; --y) std::fwrite(rgb + (size_t)y * W * 3, 4, (size_t)W * 3, fp);
+    std::fclose(fp);
+}
+
 int main(int argc, char** argv) {
     std::string obj, out;
     int W = 512, H = 512, frames = 5;
-    bool bench = false, cam_set = false;
+    bool bench = false, cam_set = false, compare = false;
+    int ranks = 0;
     float eye[3] = {0, 0, 0}, at[3] = {0, 0, 0}, fov = 40.0f;
     restir::Renderer* rp = nullptr;
     restir::Params prm;
@@ -44,38 +58,72 @@ int main(int argc, char** argv) {
         else if (a == "--temporal") prm.do_temporal = 1;
         else if (a == "--out") out = next();
         else if (a == "--bench") bench = true;
+        else if (a == "--ranks") ranks = std::atoi(next());
+        else if (a == "--compare") compare = true;
         else if (a == "--eye") { for (float& v : eye) v = (float)std::atof(next()); cam_set = true; }
         else if (a == "--at") { for (float& v : at) v = (float)std::atof(next()); cam_set = true; }
         else if (a == "--fov") fov = (float)std::atof(next());
     }
-    try {
-        restir::Renderer r(W, H);
-        rp = &r;
-        r.params = prm;
+    // Raytracer::LoadScene: the OBJ file, or the C1 Cornell box built in memory
+    auto load = [&](restir::Renderer& r) {
         if (!obj.empty()) {
             r.LoadScene(obj);
             r.camera_ = restir::Camera(1.878f, -7.724f, 1.602f, 0, 0, 0, 55.0f);   // tutorial_3 camera
-        } else {
-            // C1: Cornell box [-1,1]^2 x [0,2], one ceiling light
-            std::vector<float> P, N, LP, LN;
-            const float f0[3] = {-1, -1, 0}, f1[3] = {1, -1, 0}, f2[3] = {1, 1, 0}, f3[3] = {-1, 1, 0};
-            const float c0[3] = {-1, -1, 2}, c1[3] = {-1, 1, 2}, c2[3] = {1, 1, 2}, c3[3] = {1, -1, 2};
-            const float up[3] = {0, 0, 1}, dn[3] = {0, 0, -1}, bk[3] = {0, -1, 0};
-            quad(P, N, f0, f1, f2, f3, up);
-            quad(P, N, c0, c1, c2, c3, dn);
-            const float b0[3] = {-1, 1, 0}, b1[3] = {1, 1, 0}, b2[3] = {1, 1, 2}, b3[3] = {-1, 1, 2};
-            quad(P, N, b0, b1, b2, b3, bk);
-            const float l0[3] = {-0.25f, -0.25f, 1.98f}, l1[3] = {-0.25f, 0.25f, 1.98f}, l2[3] = {0.25f, 0.25f, 1.98f},
-                        l3[3] = {0.25f, -0.25f, 1.98f};
-            quad(LP, LN, l0, l1, l2, l3, dn);
-            std::vector<rs_mesh_desc> meshes = {{(uint32_t)(P.size() / 9), P.data(), N.data(), 0},
-                                                {(uint32_t)(LP.size() / 9), LP.data(), LN.data(), 1}};
-            rs_material_desc white{}, light{};
-            white.diffuse[0] = white.diffuse[1] = white.diffuse[2] = 0.73f; white.type = 1; white.shininess = 1;
-            light.emission[0] = 17; light.emission[1] = 12; light.emission[2] = 4; light.type = 1;
-            r.LoadScene(meshes, {white, light});
-            r.camera_ = restir::Camera(0.0f, -3.9f, 1.0f, 0.0f, 0.0f, 1.0f, 40.0f);
+            return;
         }
+        // C1: Cornell box [-1,1]^2 x [0,2], one ceiling light
+        std::vector<float> P, N, LP, LN;
+        const float f0[3] = {-1, -1, 0}, f1[3] = {1, -1, 0}, f2[3] = {1, 1, 0}, f3[3] = {-1, 1, 0};
+        const float c0[3] = {-1, -1, 2}, c1[3] = {-1, 1, 2}, c2[3] = {1, 1, 2}, c3[3] = {1, -1, 2};
+        const float up[3] = {0, 0, 1}, dn[3] = {0, 0, -1}, bk[3] = {0, -1, 0};
+        quad(P, N, f0, f1, f2, f3, up);
+        quad(P, N, c0, c1, c2, c3, dn);
+        const float b0[3] = {-1, 1, 0}, b1[3] = {1, 1, 0}, b2[3] = {1, 1, 2}, b3[3] = {-1, 1, 2};
+        quad(P, N, b0, b1, b2, b3, bk);
+        const float l0[3] = {-0.25f, -0.25f, 1.98f}, l1[3] = {-0.25f, 0.25f, 1.98f}, l2[3] = {0.25f, 0.25f, 1.98f},
+                    l3[3] = {0.25f, -0.25f, 1.98f};
+        quad(LP, LN, l0, l1, l2, l3, dn);
+        std::vector<rs_mesh_desc> meshes = {{(uint32_t)(P.size() / 9), P.data(), N.data(), 0},
+                                            {(uint32_t)(LP.size() / 9), LP.data(), LN.data(), 1}};
+        rs_material_desc white{}, light{};
+        white.diffuse[0] = white.diffuse[1] = white.diffuse[2] = 0.73f; white.type = 1; white.shininess = 1;
+        light.emission[0] = 17; light.emission[1] = 12; light.emission[2] = 4; light.type = 1;
+        r.LoadScene(meshes, {white, light});
+        r.camera_ = restir::Camera(0.0f, -3.9f, 1.0f, 0.0f, 0.0f, 1.0f, 40.0f);
+    };
+    try {
+        if (ranks > 0) {
+            int ndev = 1;
+            if (const char* e = std::getenv("RESTIR_DEVICES")) ndev = std::max(1, std::atoi(e));
+            restir::MultiGpuRenderer mg(W, H, ranks, ndev);
+            for (int i = 0; i < ranks; ++i) load(mg.rank(i));
+            mg.camera_ = mg.rank(0).camera_;
+            if (cam_set) mg.camera_ = restir::Camera(eye[0], eye[1], eye[2], at[0], at[1], at[2], fov);
+            mg.params = prm;
+            std::unique_ptr<restir::Renderer> one;
+            if (compare) {
+                one.reset(new restir::Renderer(W, H));
+                load(*one);
+                one->camera_ = mg.camera_;
+                one->params = prm;
+            }
+            bool same = true;
+            for (int f = 0; f < frames; ++f) {
+                mg.produceRestir();
+                if (one) {
+                    one->produceRestir();
+                    same = same && std::memcmp(one->frame_data(), mg.frame_data(), (size_t)W * H * 12) == 0;
+                }
+            }
+            std::printf("{\"ranks\": %d, \"frames\": %d, \"compared\": %s, \"bit_identical\": %s}\n", ranks, frames,
+                        compare ? "true" : "false", compare ? (same ? "true" : "false") : "null");
+            if (!out.empty()) write_pfm(out, W, H, mg.frame_data());
+            return compare && !same ? 2 : 0;
+        }
+        restir::Renderer r(W, H);
+        rp = &r;
+        r.params = prm;
+        load(r);
         if (cam_set) r.camera_ = restir::Camera(eye[0], eye[1], eye[2], at[0], at[1], at[2], fov);
         if (bench) {
             using clk = std::chrono::steady_clock;
@@ -112,13 +160,7 @@ int main(int argc, char** argv) {
                         r.accumulatorMean, r.accumulatorVariance, r.accFrameCtr);
         }
         r.finish();
-        if (!out.empty()) {
-            FILE* fp = std::fopen(out.c_str(), "wb");
-            if (!fp) throw restir::Error(RS_E_IO, "cannot write " + out);
-            std::fprintf(fp, "PF\n%d %d\n-1.0\n", W, H);
-            for (int y = H - 1; y >= 0; --y) std::fwrite(r.frame_data() + (size_t)y * W * 3, 4, (size_t)W * 3, fp);
-            std::fclose(fp);
-        }
+        if (!out.empty()) write_pfm(out, W, H, r.frame_data());
     } catch (const restir::Error& e) {
         std::fprintf(stderr, "error %d: %s\n", e.code, e.what());
         return 1;

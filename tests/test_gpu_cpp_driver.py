@@ -62,3 +62,14 @@ def test_frame_readback_matches_synchronous_copy():
     for f in range(6):
         assert L.rs_frame_wait(b.h, tickets[f]) == 0
         assert np.array_equal(bufs[f], want[f]), f
+
+
+def test_cpp_driver_multi_gpu_ranks_bit_identical():
+    """A C++ host renders tiled frames through restir::MultiGpuRenderer (rs_mgpu_create_local +
+    rs_mgpu_render_frame): 3 row bands with temporal + spatial reuse, bit-identical to one context."""
+    import json
+    p = subprocess.run([TOOL, "--w", "80", "--h", "60", "--frames", "4", "--area", "4", "--spatial", "4", "--temporal",
+                        "--ranks", "3", "--compare"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d == {"ranks": 3, "frames": 4, "compared": True, "bit_identical": True}

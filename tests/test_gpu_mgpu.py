@@ -1,0 +1,96 @@
+"""GPU tests of the multi-GPU path behind the C ABI (rs_mgpu_*, csrc/rs_mgpu.hip): the C++ orchestration
+renders row-band sharded frames that are bit-identical to a single context's frames.
+
+On the one-GPU test box the ranks are contexts of one process (rs_mgpu_create_local: halo exchange and
+gather as device copies -- RCCL refuses two ranks on one device); RCCL mode is exercised with world 1
+(communicator setup, the frame path without peers).  The N-GPU RCCL runs are bench.py's."""
+import numpy as np
+import pytest
+
+from restir_amd import params as P
+from restir_amd import scenes
+from restir_amd.mgpu import MultiGpuFrame
+from restir_amd.renderer import Renderer
+
+pytestmark = pytest.mark.gpu
+
+
+def _full_frames(sc, W, H, prm, cams, light_pos=None):
+    g = Renderer(W, H)
+    gs = g.load_scene(sc)
+    out = []
+    for f, c in enumerate(cams):
+        if light_pos is not None:
+            gs.update_positions(light_pos(f))
+        out.append(g.produce_restir(gs, c, prm, f).copy())
+    return out
+
+
+@pytest.mark.parametrize("world,which", [(2, "c2"), (4, "c3"), (3, "c5")])
+def test_local_mgpu_bit_identical(world, which):
+    W, H = 96, 64
+    light_pos = None
+    if which == "c2":
+        sc, prm = scenes.cornell_many_lights(256), P.metric_params(m_area=8)
+    elif which == "c3":
+        sc, prm = scenes.sponza_like(target_tris=30_000, n_lamps=128), P.c3_params(m_area=6, spatial_passes=2)
+    else:
+        sc, prm = scenes.cornell_many_lights(256), P.c3_params(m_area=6)
+        light_pos = lambda f: scenes.moving_light_positions(sc, f, 48)
+    cams = [scenes.orbit_camera(sc.camera, f, 48, 0.3) for f in range(5)]
+    ref = _full_frames(sc, W, H, prm, cams, light_pos)
+    rs = [Renderer(W, H) for _ in range(world)]
+    for r in rs:
+        r.set_traversal("lockstep")               # frames on the run-ahead lanes (no AUTO tuning frames)
+    ss = [r.load_scene(sc) for r in rs]
+    m = MultiGpuFrame(rs)
+    assert m.bands()[0][0] == 0 and m.bands()[-1][1] == H
+    for f, c in enumerate(cams):
+        if light_pos is not None:
+            for s in ss:
+                s.update_positions(light_pos(f))
+        img = m.render(ss, c, prm, f, copy_out=True)
+        assert np.array_equal(img, ref[f]), f"{which} world {world} frame {f}: {int(np.any(img != ref[f], -1).sum())} px"
+    m.close()
+
+
+def test_local_mgpu_rebalance_and_frames_in_flight():
+    """rs_mgpu_rebalance (row costs all-reduced, balanced split, history reset) gives unequal bands; frames
+    then rendered back to back without host sync (gather into rank 0's lane framebuffers, cloned on the
+    stream) equal the single-context frames."""
+    import torch
+    from restir_amd.distributed import _CudaBuf
+    W, H, world = 96, 72, 3
+    sc, prm = scenes.cornell_many_lights(256), P.c3_params(m_area=6)
+    cams = [scenes.orbit_camera(sc.camera, f, 48, 0.3) for f in range(6)]
+    torch.cuda.set_stream(torch.cuda.Stream())
+    st = torch.cuda.current_stream().cuda_stream
+    rs = [Renderer(W, H, stream=st) for _ in range(world)]
+    for r in rs:
+        r.set_traversal("lockstep")
+    ss = [r.load_scene(sc) for r in rs]
+    m = MultiGpuFrame(rs)
+    bands = m.rebalance(ss, cams[0], prm, 0, 2, 6)
+    assert bands != [(0, 24), (24, 48), (48, 72)] and all(b - a >= 6 for a, b in bands), bands
+    clones = []
+    for f, c in enumerate(cams):
+        m.render(ss, c, prm, f)
+        clones.append(torch.as_tensor(_CudaBuf(m.frame_device_ptr(), W * H * 12, "<f4", 4), device="cuda").clone())
+    ref = _full_frames(sc, W, H, prm, cams)
+    for f in range(len(cams)):
+        assert np.array_equal(clones[f].cpu().numpy().reshape(H, W, 3), ref[f]), f
+    m.close()
+
+
+def test_rccl_world1_and_allreduce():
+    """RCCL mode with one rank: unique id, communicators (one per lane), frames, all-reduce of host values."""
+    W, H = 64, 48
+    sc, prm = scenes.cornell_many_lights(128), P.metric_params(m_area=4)
+    r = Renderer(W, H)
+    s = r.load_scene(sc)
+    m = MultiGpuFrame(r, rank=0, world=1, unique_id=MultiGpuFrame.unique_id())
+    img = m.render([s], sc.camera, prm, 0, copy_out=True, timed=True)
+    ref = _full_frames(sc, W, H, prm, [sc.camera])[0]
+    assert np.array_equal(img, ref) and m.last_times.rays > 0
+    assert np.allclose(m.allreduce([1.5, 2.0], "max"), [1.5, 2.0])
+    m.close()
