@@ -5,6 +5,7 @@
 // (pg/Scene.cpp:8-16, pg/ModelLoader.cpp:218-321, pg/TriangleCDF.cpp:8-34), computes the camera
 // (pg/camera.cpp:12-84) and sequences the passes of produceRestir (pg/simpleguidx11.cpp:359-487).
 #include "rs_passes.h"
+#include "rs_queue.h"
 #include "rs_mis.h"
 #include "rs_post.h"
 #include "rs_refit.h"
@@ -172,6 +173,14 @@ struct rs_context {
     uint64_t rb_seq = 0;
     hipEvent_t fb_read[kLanes] = {};
     hipEvent_t join_ev = nullptr;          // rs::ctx_join
+    // queued initial pass (rs_queue.h): mode (RS_SPLIT_* values: AUTO = incoherent scenes), the last
+    // frame's choice, per-lane queue storage (sized for the largest launch so far)
+    int queue_mode = RS_SPLIT_OFF;
+    bool queue = false;
+    QBuf qb[kLanes] = {};
+    size_t q_slots[kLanes] = {}, q_px[kLanes] = {}, q_waves[kLanes] = {};
+    int q_A[kLanes] = {}, q_B[kLanes] = {};
+    int cus = 256;
 };
 
 // --------------------------------------------------------------------------- helpers
@@ -327,6 +336,10 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->split_mode = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->split_mode = RS_SPLIT_OFF;
     }
+    if (const char* t = std::getenv("RESTIR_QUEUE")) {         // auto (default) | on | off
+        if (!std::strcmp(t, "on")) c->queue_mode = RS_SPLIT_ON;
+        else if (!std::strcmp(t, "off")) c->queue_mode = RS_SPLIT_OFF;
+    }
     if (const char* t = std::getenv("RESTIR_READBACK"))        // sdma (default) | kernel
         c->readback_kernel = std::strcmp(t, "kernel") == 0;
     if (const char* t = std::getenv("RESTIR_RUNAHEAD"))        // run-ahead depth 0..kMaxAhead
@@ -335,6 +348,7 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0) cus = 256;
         c->wave_slots = cus * 4 * RS_INITIAL_WAVES;
+        c->cus = cus;
     }
     *out = c;
     return RS_OK;
@@ -415,6 +429,10 @@ extern "C" void rs_context_destroy(rs_context* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     for (auto st : c->lane) if (st) hipStreamSynchronize(st);
     for (auto e : c->rb_ev) if (e) hipEventDestroy(e);
+    for (auto& q : c->qb) {
+        void* ptrs[] = {q.ray, q.rid, q.cnt, q.cw, q.occ, q.brdf, q.bw};
+        for (void* p : ptrs) if (p) hipFree(p);
+    }
     if (c->join_ev) hipEventDestroy(c->join_ev);
     for (auto& g : c->G) {
         float4* f[5] = {g.g0, g.g1, g.g2, g.g3, g.g4};
@@ -1140,9 +1158,48 @@ static bool want_split(const rs_context* c, const rs_frame_params* P, int gy0, i
     const size_t rounds = c->ahead > 0 ? 1 : 3;
     return c->trav == TRAV_LOCKSTEP && grid_waves(grid_rows(c->W, gy0, gy1)) < rounds * c->wave_slots;
 }
+// the queued initial pass (rs_queue.h) for incoherent scenes: AUTO = the frame walks per lane (the
+// traversal kind AUTO picked for C3-like scenes; lockstep walks of coherent rays gain nothing from lane
+// refill and would pay the queue's memory traffic)
+static bool want_queue(const rs_context* c, const rs_frame_params* P, int gy0, int gy1) {
+    if (c->split || P->m_area <= 0 || P->m_area > 255 || (size_t)(gy1 - gy0) * c->W >= (1u << 24)) return false;
+    if (c->queue_mode == RS_SPLIT_ON) return true;
+    if (c->queue_mode == RS_SPLIT_OFF) return false;
+    return c->trav == TRAV_LANE;
+}
+static dim3 grid_q_trace(const rs_context* c, size_t n_seg) {
+    const size_t wgs = std::min((n_seg + 3) / 4, (size_t)c->cus * RS_Q_TRACE_WAVES);
+    return dim3((unsigned)std::max<size_t>(1, wgs));
+}
+// queue storage of lane k for a launch of n_waves generate waves over px local pixels
+static int ensure_queue(rs_context* c, int k, size_t n_waves, size_t px, int A, int B) {
+    QBuf& q = c->qb[k];
+    const size_t slots = n_waves * 64 * (size_t)A;
+    if (slots > c->q_slots[k] || px > c->q_px[k] || n_waves > c->q_waves[k] || A > c->q_A[k] || B > c->q_B[k]) {
+        sync_all(c);
+        void* ptrs[] = {q.ray, q.rid, q.cnt, q.cw, q.occ, q.brdf, q.bw};
+        for (void* p : ptrs) if (p) hipFree(p);
+        q = QBuf{};
+        c->q_slots[k] = c->q_px[k] = c->q_waves[k] = 0; c->q_A[k] = c->q_B[k] = 0;
+        const size_t pa = px * (size_t)std::max(1, A), pb = px * (size_t)std::max(1, B);
+        HIPCHK(c, hipMalloc(&q.ray, slots * sizeof(float4)));
+        HIPCHK(c, hipMalloc(&q.rid, slots * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&q.cnt, n_waves * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&q.cw, pa * sizeof(float2)));
+        HIPCHK(c, hipMalloc(&q.occ, pa));
+        HIPCHK(c, hipMalloc(&q.brdf, pb * 3 * sizeof(float4)));
+        HIPCHK(c, hipMalloc(&q.bw, pb * sizeof(float)));
+        c->q_slots[k] = slots; c->q_px[k] = px; c->q_waves[k] = n_waves; c->q_A[k] = A; c->q_B[k] = B;
+    }
+    q.P = (uint32_t)px;
+    q.A = A;
+    return RS_OK;
+}
 static bool reserve_count_slots(rs_context* c, int k, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
     size_t need = (c->split ? grid_waves(grid_split(c->W, gy0, gy1), kSplit) : grid_waves(grid_rows(c->W, gy0, gy1))) +
                   grid_waves(grid_rows(c->W, y0, y1)) * (4 + (size_t)std::max(0, P->spatial_passes));
+    if (c->queue)
+        need += grid_waves(grid_q_trace(c, grid_waves(grid_rows(c->W, gy0, gy1)))) + grid_waves(grid_rows(c->W, y0, y1));
     return use_parts(c, k, need);
 }
 
@@ -1228,6 +1285,11 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     c->temporal_ran = c->spatial_ran = c->ev_temporal = false;
     const DevScene S = s->dev();
     c->split = want_split(c, P, F.gy0, F.gy1);
+    c->queue = want_queue(c, P, F.gy0, F.gy1);
+    if (c->queue) {
+        const size_t nw = grid_waves(grid_rows(c->W, F.gy0, F.gy1));
+        if (int rc = ensure_queue(c, c->li, nw, (size_t)(F.gy1 - F.gy0) * c->W, P->m_area, P->m_brdf)) return rc;
+    }
     if (!reserve_count_slots(c, c->li, P, F.gy0, F.gy1, F.y0, F.y1)) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
     if (c->fs != c->stream && c->lane_wait[c->li]) {   // this lane's previous frame ran on the context's stream
         HIPCHK(c, hipStreamWaitEvent(c->fs, c->lane_wait[c->li], 0));
@@ -1250,6 +1312,16 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
         const dim3 gs = grid_split(c->W, F.gy0, F.gy1);
         LAUNCH_TRAV_BS(c, k_gbuffer_initial_split, gs, 64 * kSplit, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
                     c->shade_fused ? 1 : 0, count_slot(c, gs, kSplit));
+    } else if (c->queue) {
+        const QBuf& Q = c->qb[c->li];
+        LAUNCH_TRAV(c, k_q_generate, gg, S, F, c->G[gnew], Q, count_slot(c, gg));
+        HIPCHK(c, hipGetLastError());
+        const size_t n_seg = grid_waves(gg);
+        const dim3 gt = grid_q_trace(c, n_seg);
+        k_q_trace<<<gt, 256, 0, c->fs>>>(S, F, c->G[gnew], Q, (uint32_t)n_seg, count_slot(c, gt));
+        HIPCHK(c, hipGetLastError());
+        k_q_resolve<<<gb, 256, 0, c->fs>>>(S, F, c->G[gnew], Q, ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
+                                           count_slot(c, gb));
     } else {
         LAUNCH_TRAV(c, k_gbuffer_initial, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                     count_slot(c, gg));

@@ -300,7 +300,10 @@ fail:
 // preorder skip-pointer layout as above.  Deterministic: ties go to the smaller index, node ids come
 // from prefix sums, no atomics decide structure.
 // ============================================================================================
-constexpr int kRadius = 16;
+#ifndef RS_PLOC_RADIUS
+#define RS_PLOC_RADIUS 16
+#endif
+constexpr int kRadius = RS_PLOC_RADIUS;
 constexpr int kPlocBlock = 256;
 #ifndef RS_LEAF_MAX
 #define RS_LEAF_MAX 8

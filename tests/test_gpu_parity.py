@@ -567,3 +567,41 @@ def test_obj_loader_matches_array_scene():
     g2 = Renderer(48, 48)
     b = g2.produce_restir(g2.load_scene(sc), sc.camera, P.default_params(), 0)
     _assert_close(a, b, "obj loader")
+
+
+@pytest.mark.parametrize("which", ["c3", "c2", "brdf2", "odd"])
+def test_queued_initial_pass_bit_identical(which):
+    """The queued initial pass (rs_queue.h: candidates -> compacted ray queue -> persistent refilling
+    any-hit walks -> the addSample stream) renders frames bit-identical to the one-thread-per-pixel pass,
+    for both traversal kinds of the G-buffer/BRDF rays, with temporal + spatial reuse, B=2 BRDF
+    candidates, odd candidate counts and a ragged image; AUTO uses it for per-lane scenes only."""
+    import os
+    W, H = 72, 40
+    cam = lambda f: scenes.orbit_camera(sc.camera, f, 240, 0.3)
+    if which == "c3":
+        sc, prm = scenes.sponza_like(target_tris=30_000, n_lamps=128), P.c3_params(m_area=9)
+    elif which == "c2":
+        sc, prm = scenes.cornell_many_lights(256), P.metric_params(m_area=7)
+    elif which == "brdf2":
+        sc, prm = scenes.cornell_box(8), P.default_params(m_area=5, m_brdf=2, do_temporal=1, do_spatial=1)
+    else:
+        sc, prm, W, H = scenes.cornell_box(8), P.default_params(m_area=3, m_brdf=0, do_spatial=1), 45, 27
+    out = {}
+    old = os.environ.get("RESTIR_QUEUE")
+    try:
+        for q in ("off", "on"):
+            os.environ["RESTIR_QUEUE"] = q
+            for trav in ("lockstep", "lane"):
+                g = Renderer(W, H)
+                g.set_traversal(trav)
+                gs = g.load_scene(sc)
+                out[q, trav] = [g.produce_restir(gs, cam(f), prm, f).copy() for f in range(3)]
+    finally:
+        if old is None:
+            os.environ.pop("RESTIR_QUEUE", None)
+        else:
+            os.environ["RESTIR_QUEUE"] = old
+    ref = out["off", "lockstep"]
+    for k, v in out.items():
+        for f in range(3):
+            assert np.array_equal(ref[f], v[f]), f"{which} {k} frame {f}"
