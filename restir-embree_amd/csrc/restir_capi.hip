@@ -28,6 +28,10 @@ int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int*
                    std::vector<int>& lvl_off, std::string& err);
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
               const std::vector<int>& lvl_off, hipStream_t st, int* tail, std::string& err);
+int bvh_crec_build(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, float4** d_crec, int** d_rec_node,
+                   int** d_node2rec, uint32_t* n_rec, std::string& err);
+int bvh_crec_emit(const float4* d_nodes, const int* d_rec_node, const int* d_node2rec, uint32_t n_rec, float4* d_crec,
+                  hipStream_t st);
 }
 
 using namespace rs;
@@ -50,6 +54,10 @@ struct rs_scene {
     int* d_emis_tri = nullptr;
     int *d_refit_order = nullptr, *d_refit_lvl = nullptr;
     std::vector<int> refit_lvl;
+    // child-box records of the interior nodes (rs_scene.h), re-emitted after every refit
+    float4* d_crec = nullptr;
+    int *d_crec_node = nullptr, *d_node2rec = nullptr;
+    uint32_t n_crec = 0;
     float* h_stage[2] = {nullptr, nullptr};
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     int stage_i = 0;
@@ -70,6 +78,7 @@ struct rs_scene {
         S.nodes = d_nodes; S.tris = d_tris; S.tri_nrm = d_tri_nrm; S.mats = d_mats; S.emis = d_emis; S.cdf = d_cdf; S.cdf_guide = d_cdf_guide;
         S.n_nodes = n_nodes; S.n_tris = n_tris; S.n_emis = n_emis; S.n_mats = n_mats;
         S.tri_uv = d_uv; S.tri_tan = d_tan; S.tex = d_tex; S.texd = d_texd; S.sky = sky;
+        S.crec = d_crec; S.n_crec = n_crec;
         return S;
     }
 };
@@ -705,10 +714,11 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     c->join_next = true;
     if (hipStreamSynchronize(st) != hipSuccess) { err = "stream sync failed"; return -1; }   // frames in flight
     void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide, s->d_emis_tri,
-                   s->d_refit_order, s->d_refit_lvl};
+                   s->d_refit_order, s->d_refit_lvl, s->d_crec, s->d_crec_node, s->d_node2rec};
     for (void* p : old) if (p) hipFree(p);
     s->d_pos = nullptr; s->d_nodes = nullptr; s->d_tris = nullptr; s->d_emis = nullptr; s->d_cdf = nullptr;
     s->d_cdf_guide = nullptr; s->d_emis_tri = nullptr; s->d_refit_order = nullptr; s->d_refit_lvl = nullptr;
+    s->d_crec = nullptr; s->d_crec_node = nullptr; s->d_node2rec = nullptr; s->n_crec = 0;
     s->n_nodes = 0; s->refit_lvl.clear();
     s->n_emis = ne;
     if (n) {
@@ -736,6 +746,10 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     else { err = "BVH build failed: " + berr; rc = -1; }
     hipEventDestroy(e0); hipEventDestroy(e1);
     if (rc == 0 && bvh_refit_plan(s->d_nodes, s->n_nodes, st, &s->d_refit_order, &s->d_refit_lvl, s->refit_lvl, berr) != 0) {
+        err = berr; rc = -1;
+    }
+    if (rc == 0 && bvh_crec_build(s->d_nodes, s->n_nodes, st, &s->d_crec, &s->d_crec_node, &s->d_node2rec, &s->n_crec,
+                                  berr) != 0) {
         err = berr; rc = -1;
     }
     return rc;
@@ -884,6 +898,8 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
     k_scene_update<<<2, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, s->d_emis,
                                               s->d_cdf, s->d_cdf_guide, R);
     HIPCHK(c, hipGetLastError());
+    if (bvh_crec_emit(s->d_nodes, s->d_crec_node, s->d_node2rec, s->n_crec, s->d_crec, st) != 0)
+        return fail(c, RS_E_HIP, "rs_scene_update_positions: child-record emit failed");
     return RS_OK;
 }
 
@@ -1016,7 +1032,7 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     if (s->ctx) sync_all(s->ctx);
     void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
                     s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage, s->d_tex, s->d_texd, s->d_uv,
-                    s->d_tan};
+                    s->d_tan, s->d_crec, s->d_crec_node, s->d_node2rec};
     for (void* p : ptrs) if (p) hipFree(p);
     for (int k = 0; k < 2; ++k) {
         if (s->h_stage[k]) hipHostFree(s->h_stage[k]);

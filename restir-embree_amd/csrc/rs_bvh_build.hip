@@ -621,6 +621,67 @@ int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_
     return 0;
 }
 
+// ---------------------------------------------------------------- child-box records (rs_scene.h)
+// record r of interior node i = rec_node[r]: its children L = i + 1 and R = skip(L), each as the child's
+// box + link (record index of an interior child, ~leaf word of a leaf child), and skip(i)
+__global__ void k_crec_emit(const float4* __restrict__ nodes, const int* __restrict__ rec_node,
+                            const int* __restrict__ node2rec, uint32_t n_rec, float4* crec) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rec) return;
+    const int i = rec_node[r], L = i + 1;
+    const float4 aL = nodes[2 * L], bL = nodes[2 * L + 1];
+    const int R = __float_as_int(aL.w);
+    const float4 aR = nodes[2 * R], bR = nodes[2 * R + 1];
+    const int wL = __float_as_int(bL.w), wR = __float_as_int(bR.w);
+    const int lL = wL >= 0 ? ~wL : node2rec[L], lR = wR >= 0 ? ~wR : node2rec[R];
+    crec[4 * r + 0] = make_float4(aL.x, aL.y, aL.z, __int_as_float(lL));
+    crec[4 * r + 1] = make_float4(bL.x, bL.y, bL.z, __int_as_float(lR));
+    crec[4 * r + 2] = make_float4(aR.x, aR.y, aR.z, nodes[2 * i].w);
+    crec[4 * r + 3] = make_float4(bR.x, bR.y, bR.z, 0.0f);
+}
+
+// Record numbering (host, once per topology): interior nodes in preorder.  Checks that the tree is
+// binary (skip(R) == skip(i)); otherwise, or for a single-leaf tree, no records (*n_rec = 0).
+int bvh_crec_build(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, float4** d_crec, int** d_rec_node,
+                   int** d_node2rec, uint32_t* n_rec, std::string& err) {
+    *d_crec = nullptr; *d_rec_node = nullptr; *d_node2rec = nullptr; *n_rec = 0;
+    if (n_nodes < 3) return 0;
+    std::vector<float4> h(2 * (size_t)n_nodes);
+    if (hipMemcpyAsync(h.data(), d_nodes, h.size() * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) { err = "child records: node download failed"; return -1; }
+    auto skip = [&](uint32_t i) { int v; std::memcpy(&v, &h[2 * i].w, 4); return v; };
+    auto leaf = [&](uint32_t i) { int v; std::memcpy(&v, &h[2 * i + 1].w, 4); return v; };
+    std::vector<int> rec_node, node2rec(n_nodes, -1);
+    for (uint32_t i = 0; i < n_nodes; ++i) {
+        if (leaf(i) >= 0) continue;
+        const int L = (int)i + 1;
+        if (L >= (int)n_nodes) return 0;
+        const int R = skip((uint32_t)L);
+        if (R <= L || R >= (int)n_nodes || skip((uint32_t)R) != skip(i)) return 0;   // not binary: no records
+        node2rec[i] = (int)rec_node.size();
+        rec_node.push_back((int)i);
+    }
+    const uint32_t nr = (uint32_t)rec_node.size();
+    if (hipMalloc(d_crec, (size_t)nr * 4 * sizeof(float4)) != hipSuccess ||
+        hipMalloc(d_rec_node, nr * sizeof(int)) != hipSuccess ||
+        hipMalloc(d_node2rec, (size_t)n_nodes * sizeof(int)) != hipSuccess) { err = "child records: hipMalloc failed"; return -1; }
+    if (hipMemcpyAsync(*d_rec_node, rec_node.data(), nr * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(*d_node2rec, node2rec.data(), (size_t)n_nodes * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
+        err = "child records: upload failed"; return -1;
+    }
+    k_crec_emit<<<(nr + 255) / 256, 256, 0, st>>>(d_nodes, *d_rec_node, *d_node2rec, nr, *d_crec);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) { err = "child records: emit failed"; return -1; }
+    *n_rec = nr;
+    return 0;
+}
+// stream-ordered re-emission after a refit (same topology)
+int bvh_crec_emit(const float4* d_nodes, const int* d_rec_node, const int* d_node2rec, uint32_t n_rec, float4* d_crec,
+                  hipStream_t st) {
+    if (!n_rec) return 0;
+    k_crec_emit<<<(n_rec + 255) / 256, 256, 0, st>>>(d_nodes, d_rec_node, d_node2rec, n_rec, d_crec);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // builder selection: PLOC by default; RESTIR_BVH=lbvh selects the Karras LBVH (kept for comparison)
 int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes, float4** d_tris,
               std::string& err) {

@@ -158,12 +158,42 @@ __global__ void __launch_bounds__(kReduceThreads) k_reduce_counts(const uint2* p
     }
 }
 
+// Workgroup -> screen tile.  The dispatcher hands workgroup b (row-major over the grid) to XCD b % 8,
+// each XCD with its own 4 MB L2.  RS_TILE_ORDER:
+//   0  tile = b (row-major): every XCD samples the whole frame -- its L2 holds the BVH of every view ray
+//   1  XCD k renders vertical stripe k of the frame (row-major inside the stripe): neighbouring tiles,
+//      whose rays touch the same BVH nodes, share an L2; stripes keep the XCDs' costs balanced where
+//      cost varies by row (ceiling vs floor)
+//   2  as 1, each stripe bottom-up
+//   3  row-major, bottom-up (the expensive floor rows of the Cornell box first, cheap ceiling rows last)
+// Every pixel's work is independent of the order: results are identical for every order.
+#ifndef RS_TILE_ORDER
+#define RS_TILE_ORDER 0
+#endif
+__device__ __forceinline__ void tile_of(int& bx, int& by) {
+    const uint32_t gx = gridDim.x, gy = gridDim.y, n = gx * gy, b = blockIdx.y * gx + blockIdx.x;
+    if (RS_TILE_ORDER == 0 || n < 8) { bx = blockIdx.x; by = blockIdx.y; return; }
+    if (RS_TILE_ORDER == 3) { bx = blockIdx.x; by = gy - 1 - blockIdx.y; return; }
+    // dispatch slot s of XCD k -> position t in the stripe order (XCD k takes the k-th 1/8 of it)
+    const uint32_t k = b & 7u, s = b >> 3, q = n >> 3, r = n & 7u;
+    const uint32_t t = k < r ? k * (q + 1) + s : r * (q + 1) + (k - r) * q + s;
+    // stripe order: stripes of w tile columns (the last one narrower), row-major inside a stripe
+    const uint32_t w = (gx + 7) >> 3, sz = w * gy, i = t / sz, l = t - i * sz;
+    const uint32_t wi = gx - i * w < w ? gx - i * w : w;
+    uint32_t ry = l / wi;
+    if (RS_TILE_ORDER == 2) ry = gy - 1 - ry;
+    bx = (int)(i * w + (l - (l / wi) * wi));
+    by = (int)ry;
+}
+
 // 8x8 tile per wave, 16x16 per workgroup, rows [ya, yb).  Returns whether the pixel exists; x/y are
 // clamped into the image so out-of-range lanes can run the (convergent) code on a valid pixel.
 __device__ __forceinline__ bool pixel_of(int ya, int yb, int W, int& x, int& y) {
     int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    y = ya + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    int bx, by;
+    tile_of(bx, by);
+    x = bx * 16 + (wave & 1) * 8 + (lane & 7);
+    y = ya + by * 16 + (wave >> 1) * 8 + (lane >> 3);
     bool in = x < W && y < yb;
     x = x < W ? x : W - 1;
     y = y < yb ? y : yb - 1;
@@ -593,7 +623,9 @@ __global__ void __launch_bounds__(64 * kSplit, RS_WAVES(T, RS_INITIAL_WAVES, RS_
     if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
     __shared__ SplitLds L;
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-    int x = blockIdx.x * 8 + (lane & 7), y = F.gy0 + blockIdx.y * 8 + (lane >> 3);
+    int bx, by;
+    tile_of(bx, by);
+    int x = bx * 8 + (lane & 7), y = F.gy0 + by * 8 + (lane >> 3);
     const bool in = x < F.W && y < F.gy1;
     x = x < F.W ? x : F.W - 1;
     y = y < F.gy1 ? y : F.gy1 - 1;

@@ -36,6 +36,9 @@ struct DevScene {
     const uint8_t* tex;       // texel bytes of every texture
     const int4* texd;         // 2 per texture: (byte offset, width, height, pitch), (pixel bytes, format, 0, 0)
     int sky;                  // texture index of the equirect sky, -1 none
+    // child-box records of the interior nodes (TRAV_LANE walks, see "child-box walks" below), 4 per record
+    const float4* crec;
+    uint32_t n_crec;          // 0: none (single-leaf tree) -> the skip-pointer walks
 };
 constexpr int kCdfGuide = 1024;
 
@@ -141,10 +144,11 @@ __device__ __forceinline__ void closest_visit(const DevScene& S, float4 a, float
 // Branch-lean per-lane walks: uniform loop condition, select-based cursor updates, the leaf's
 // triangles in a wave-uniform loop up to the largest leaf among the lanes -- no per-lane exec-mask
 // regions (C3: +21 % over the branchy loop).
-__device__ __forceinline__ bool occluded_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-    vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+// walk from node `i` (0xffffffff: no walk) to the end of the preorder
+__device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i, vec3 o, vec3 d, vec3 inv, float tnear,
+                                                   float tfar) {
     const uint32_t n = S.n_nodes;
-    uint32_t i = active ? 0u : 0xffffffffu, occ = 0u;
+    uint32_t occ = 0u;
     while (__ballot(i < n) != 0) {
         const bool live = i < n;
         const uint32_t ii = live ? i : 0u;
@@ -166,11 +170,13 @@ __device__ __forceinline__ bool occluded_lane(const DevScene& S, bool active, ve
     }
     return occ != 0u;
 }
-__device__ __forceinline__ Hit closest_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-    vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
+__device__ __forceinline__ bool occluded_lane_skip(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    return occluded_lane_from(S, active ? 0u : 0xffffffffu, o, d, inv, tnear, tfar);
+}
+__device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i, vec3 o, vec3 d, vec3 inv, float tnear,
+                                                  Hit& h) {
     const uint32_t n = S.n_nodes;
-    uint32_t i = active ? 0u : 0xffffffffu;
     while (__ballot(i < n) != 0) {
         const bool live = i < n;
         const uint32_t ii = live ? i : 0u;
@@ -194,7 +200,165 @@ __device__ __forceinline__ Hit closest_lane(const DevScene& S, bool active, vec3
         }
         i = !live ? i : ((hit & (leaf < 0)) ? i + 1 : skip);
     }
+}
+__device__ __forceinline__ Hit closest_lane_skip(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
+    closest_lane_from(S, active ? 0u : 0xffffffffu, o, d, inv, tnear, h);
     return h;
+}
+
+// ---------------------------------------------------------------- child-box walks (TRAV_LANE)
+// The skip-pointer walk fetches a node to test that node's own box, so every child of every entered
+// node costs one dependent load -- about twice the entered nodes.  A child-box record holds BOTH
+// children's boxes of an interior node (64 B = 4 x float4):
+//   c0 = (L.lo, Llink)   c1 = (L.hi, Rlink)   c2 = (R.lo, skip)   c3 = (R.hi, 0)
+//   link >= 0: the child's record index (interior child); link < 0: ~leaf word of a leaf child, whose
+//   triangles are tested straight from the parent's visit (leaf nodes are never fetched)
+//   skip: the node following this subtree in the preorder (skip-pointer index)
+// so a walk loads one record per ENTERED interior node.  Right children whose box was hit wait on a
+// short per-lane stack in registers (RS_CSTACK entries, shifted: no scratch); when it overflows the
+// oldest entry is dropped and, once the stack runs empty, the walk finishes as a skip-pointer walk: an
+// any-hit walk (always left first, so every dropped entry is a right child of an ancestor) from the
+// current record's skip, after which the preorder holds every dropped subtree; a closest-hit walk
+// (nearer child first) from the root, culled by the closest hit found so far.  Same boxes, same
+// conservative box test and the same triangle tests (any-hit: existence; closest: the tie rule), so
+// results are bit-identical to the skip-pointer walks; closest-hit walks also enter the nearer child
+// first.  Records are emitted from the nodes at build time and after every refit (rs_bvh_build.hip).
+#ifndef RS_CSTACK
+#define RS_CSTACK 6
+#endif
+#ifndef RS_CREC
+#define RS_CREC 1
+#endif
+struct CStack {
+    uint32_t s[RS_CSTACK];
+    int sp;
+    bool dropped;
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int k = 0; k < RS_CSTACK; ++k) s[k] = 0u;
+        sp = 0; dropped = false;
+    }
+    __device__ __forceinline__ void push(bool c, uint32_t v) {
+        dropped = dropped | (c & (sp == RS_CSTACK));
+#pragma unroll
+        for (int k = RS_CSTACK - 1; k > 0; --k) s[k] = c ? s[k - 1] : s[k];
+        s[0] = c ? v : s[0];
+        sp = c ? (sp < RS_CSTACK ? sp + 1 : sp) : sp;
+    }
+    __device__ __forceinline__ void pop(bool c) {
+#pragma unroll
+        for (int k = 0; k < RS_CSTACK - 1; ++k) s[k] = c ? s[k + 1] : s[k];
+        sp = c ? sp - 1 : sp;
+    }
+};
+// slab test returning the entry distance (closest-hit child order)
+__device__ __forceinline__ bool box_test_t(float4 a, float4 b, vec3 o, vec3 inv, float tnear, float tfar, float& tin) {
+    float tx0 = (a.x - o.x) * inv.x, tx1 = (b.x - o.x) * inv.x;
+    float ty0 = (a.y - o.y) * inv.y, ty1 = (b.y - o.y) * inv.y;
+    float tz0 = (a.z - o.z) * inv.z, tz1 = (b.z - o.z) * inv.z;
+    float t0 = fmaxf(fmaxf(fmaxf(tnear, fminf(tx0, tx1)), fminf(ty0, ty1)), fminf(tz0, tz1));
+    float t1 = fminf(fminf(fminf(tfar, fmaxf(tx0, tx1)), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    tin = t0;
+    return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
+}
+
+__device__ __forceinline__ bool occluded_crec(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    constexpr uint32_t kDone = 0xffffffffu;
+    uint32_t cur = active ? 0u : kDone, resume = kDone, occ = 0u;
+    CStack st;
+    st.init();
+    while (__ballot(cur != kDone) != 0) {
+        const bool live = cur != kDone;
+        const uint32_t r = live ? cur : 0u;
+        const float4 c0 = S.crec[4 * r], c1 = S.crec[4 * r + 1], c2 = S.crec[4 * r + 2], c3 = S.crec[4 * r + 3];
+        const int lL = __float_as_int(c0.w), lR = __float_as_int(c1.w);
+        const bool hL = live & box_test(c0, c1, o, inv, tnear, tfar);
+        const bool hR = live & box_test(c2, c3, o, inv, tnear, tfar);
+        const int wL = ~lL, wR = ~lR;
+        const int nL = (hL & (lL < 0)) ? (wL & 7) + 1 : 0, nR = (hR & (lR < 0)) ? (wR & 7) + 1 : 0;
+        for (int j = 0; j < 16; ++j) {
+            const bool want = (j < nL + nR) & (occ == 0u);
+            if (__ballot(want) == 0) break;
+            const int t = j < nL ? (wL >> 3) + j : (wR >> 3) + (j - nL);
+            const float4* T = S.tris + 3 * (want ? t : 0);
+            float tt, u, v;
+            const bool h = tri_test_nb(T[0], T[1], T[2], o, d, tnear, tfar, tt, u, v);
+            occ = (want & h) ? 1u : occ;
+        }
+        const bool iL = hL & (lL >= 0), iR = hR & (lR >= 0);
+        const bool go = live & (occ == 0u);
+        const bool none = !iL & !iR;
+        const bool pop = go & none & (st.sp > 0);
+        const uint32_t top = st.s[0];
+        st.pop(pop);
+        st.push(go & iL & iR, (uint32_t)lR);
+        resume = (go & none & !pop & st.dropped) ? __float_as_uint(c2.w) : resume;
+        const uint32_t nxt = iL ? (uint32_t)lL : (iR ? (uint32_t)lR : (pop ? top : kDone));
+        cur = !live ? cur : (go ? nxt : kDone);
+    }
+    if (__ballot(resume != kDone) != 0)            // a stack overflowed: finish as a skip-pointer walk
+        occ |= occluded_lane_from(S, occ ? kDone : resume, o, d, inv, tnear, tfar) ? 1u : 0u;
+    return occ != 0u;
+}
+
+__device__ __forceinline__ Hit closest_crec(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    constexpr uint32_t kDone = 0xffffffffu;
+    Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
+    uint32_t cur = active ? 0u : kDone, resume = kDone;
+    CStack st;
+    st.init();
+    while (__ballot(cur != kDone) != 0) {
+        const bool live = cur != kDone;
+        const uint32_t r = live ? cur : 0u;
+        const float4 c0 = S.crec[4 * r], c1 = S.crec[4 * r + 1], c2 = S.crec[4 * r + 2], c3 = S.crec[4 * r + 3];
+        const int lL = __float_as_int(c0.w), lR = __float_as_int(c1.w);
+        float tL, tR;
+        const bool hL = live & box_test_t(c0, c1, o, inv, tnear, h.t, tL);
+        const bool hR = live & box_test_t(c2, c3, o, inv, tnear, h.t, tR);
+        const int wL = ~lL, wR = ~lR;
+        const int nL = (hL & (lL < 0)) ? (wL & 7) + 1 : 0, nR = (hR & (lR < 0)) ? (wR & 7) + 1 : 0;
+        for (int j = 0; j < 16; ++j) {
+            const bool want = j < nL + nR;
+            if (__ballot(want) == 0) break;
+            const int t = j < nL ? (wL >> 3) + j : (wR >> 3) + (j - nL);
+            const float4* T = S.tris + 3 * (want ? t : 0);
+            const float4 T0 = T[0];
+            float tt, u, v;
+            const bool hh = want & tri_test_nb(T0, T[1], T[2], o, d, tnear, h.t, tt, u, v);
+            const int prim = __float_as_int(T0.w);
+            const bool better = hh & (h.prim < 0 || tt < h.t || (tt == h.t && prim < h.prim));
+            h.t = better ? tt : h.t; h.u = better ? u : h.u; h.v = better ? v : h.v;
+            h.prim = better ? prim : h.prim;
+        }
+        const bool iL = hL & (lL >= 0), iR = hR & (lR >= 0);
+        const bool none = !iL & !iR;
+        const bool pop = live & none & (st.sp > 0);
+        const uint32_t top = st.s[0];
+        st.pop(pop);
+        const bool rfirst = tR < tL;                  // both entered: the nearer first, the other waits
+        st.push(live & iL & iR, rfirst ? (uint32_t)lL : (uint32_t)lR);
+        // an overflowed closest-hit walk restarts the skip-pointer walk at the root (nearer-first order
+        // may have dropped a LEFT child, which precedes the current record in the preorder)
+        resume = (live & none & !pop & st.dropped) ? 0u : resume;
+        const uint32_t nxt = (iL & iR) ? (rfirst ? (uint32_t)lR : (uint32_t)lL)
+                                       : (iL ? (uint32_t)lL : (iR ? (uint32_t)lR : (pop ? top : kDone)));
+        cur = !live ? cur : nxt;
+    }
+    if (__ballot(resume != kDone) != 0) closest_lane_from(S, resume, o, d, inv, tnear, h);
+    return h;
+}
+
+__device__ __forceinline__ bool occluded_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    if (RS_CREC && S.n_crec) return occluded_crec(S, active, o, d, tnear, tfar);
+    return occluded_lane_skip(S, active, o, d, tnear, tfar);
+}
+__device__ __forceinline__ Hit closest_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    if (RS_CREC && S.n_crec) return closest_crec(S, active, o, d, tnear, tfar);
+    return closest_lane_skip(S, active, o, d, tnear, tfar);
 }
 
 // ---------------------------------------------------------------- wave-coherent walks (TRAV_LOCKSTEP)
