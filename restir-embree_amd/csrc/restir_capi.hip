@@ -28,10 +28,10 @@ int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int*
                    std::vector<int>& lvl_off, std::string& err);
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
               const std::vector<int>& lvl_off, hipStream_t st, int* tail, std::string& err);
-int bvh_crec_build(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, float4** d_crec, int** d_rec_node,
-                   int** d_node2rec, uint32_t* n_rec, std::string& err);
+int bvh_crec_build(const float4* d_nodes, uint32_t n_nodes, uint32_t n_tris, hipStream_t st, float4** d_crec,
+                   uint32_t** d_cskip, int** d_rec_node, int** d_node2rec, uint32_t* n_rec, std::string& err);
 int bvh_crec_emit(const float4* d_nodes, const int* d_rec_node, const int* d_node2rec, uint32_t n_rec, float4* d_crec,
-                  hipStream_t st);
+                  uint32_t* d_cskip, hipStream_t st);
 }
 
 using namespace rs;
@@ -56,6 +56,7 @@ struct rs_scene {
     std::vector<int> refit_lvl;
     // child-box records of the interior nodes (rs_scene.h), re-emitted after every refit
     float4* d_crec = nullptr;
+    uint32_t* d_cskip = nullptr;
     int *d_crec_node = nullptr, *d_node2rec = nullptr;
     uint32_t n_crec = 0;
     float* h_stage[2] = {nullptr, nullptr};
@@ -78,7 +79,7 @@ struct rs_scene {
         S.nodes = d_nodes; S.tris = d_tris; S.tri_nrm = d_tri_nrm; S.mats = d_mats; S.emis = d_emis; S.cdf = d_cdf; S.cdf_guide = d_cdf_guide;
         S.n_nodes = n_nodes; S.n_tris = n_tris; S.n_emis = n_emis; S.n_mats = n_mats;
         S.tri_uv = d_uv; S.tri_tan = d_tan; S.tex = d_tex; S.texd = d_texd; S.sky = sky;
-        S.crec = d_crec; S.n_crec = n_crec;
+        S.crec = d_crec; S.cskip = d_cskip; S.n_crec = n_crec;
         return S;
     }
 };
@@ -160,6 +161,13 @@ struct rs_context {
     bool tuning = false;
     hipEvent_t tune_ev[16] = {};           // tuning frame: events around each spatial kernel (halo exchanges excluded)
     int tune_n = 0;
+    // tile-row dispatch order (rs_passes.h tile_of): per-row wave time of full-frame tuning frames, one
+    // buffer per traversal kind; the chosen kind's costs order the 16-px tile rows, costliest first
+    float* d_tune_cost[2] = {nullptr, nullptr};
+    int* d_order = nullptr;
+    int n_order = 0;
+    bool order_on = true;                  // RESTIR_TILE_ORDER=off: row-major dispatch
+    bool tune_rows = false;                // this tuning frame records per-row cost
     // candidate-split initial pass (rs_passes.h k_gbuffer_initial_split): requested mode, last frame's
     int split_mode = RS_SPLIT_AUTO;
     bool split = false;
@@ -349,6 +357,8 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->queue_mode = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->queue_mode = RS_SPLIT_OFF;
     }
+    if (const char* t = std::getenv("RESTIR_TILE_ORDER"))      // cost (default) | off (row-major)
+        c->order_on = std::strcmp(t, "off") != 0;
     if (const char* t = std::getenv("RESTIR_READBACK"))        // sdma (default) | kernel
         c->readback_kernel = std::strcmp(t, "kernel") == 0;
     if (const char* t = std::getenv("RESTIR_RUNAHEAD"))        // run-ahead depth 0..kMaxAhead
@@ -461,6 +471,8 @@ extern "C" void rs_context_destroy(rs_context* c) {
         for (auto& e : slot) if (e) hipEventDestroy(e);
     for (auto& e : c->ev_gt) if (e) hipEventDestroy(e);
     for (auto& e : c->tune_ev) if (e) hipEventDestroy(e);
+    for (float* p : c->d_tune_cost) if (p) hipFree(p);
+    if (c->d_order) hipFree(c->d_order);
     for (auto st : c->lane) if (st) hipStreamDestroy(st);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -714,11 +726,11 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     c->join_next = true;
     if (hipStreamSynchronize(st) != hipSuccess) { err = "stream sync failed"; return -1; }   // frames in flight
     void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide, s->d_emis_tri,
-                   s->d_refit_order, s->d_refit_lvl, s->d_crec, s->d_crec_node, s->d_node2rec};
+                   s->d_refit_order, s->d_refit_lvl, s->d_crec, s->d_cskip, s->d_crec_node, s->d_node2rec};
     for (void* p : old) if (p) hipFree(p);
     s->d_pos = nullptr; s->d_nodes = nullptr; s->d_tris = nullptr; s->d_emis = nullptr; s->d_cdf = nullptr;
     s->d_cdf_guide = nullptr; s->d_emis_tri = nullptr; s->d_refit_order = nullptr; s->d_refit_lvl = nullptr;
-    s->d_crec = nullptr; s->d_crec_node = nullptr; s->d_node2rec = nullptr; s->n_crec = 0;
+    s->d_crec = nullptr; s->d_cskip = nullptr; s->d_crec_node = nullptr; s->d_node2rec = nullptr; s->n_crec = 0;
     s->n_nodes = 0; s->refit_lvl.clear();
     s->n_emis = ne;
     if (n) {
@@ -748,8 +760,8 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     if (rc == 0 && bvh_refit_plan(s->d_nodes, s->n_nodes, st, &s->d_refit_order, &s->d_refit_lvl, s->refit_lvl, berr) != 0) {
         err = berr; rc = -1;
     }
-    if (rc == 0 && bvh_crec_build(s->d_nodes, s->n_nodes, st, &s->d_crec, &s->d_crec_node, &s->d_node2rec, &s->n_crec,
-                                  berr) != 0) {
+    if (rc == 0 && bvh_crec_build(s->d_nodes, s->n_nodes, n, st, &s->d_crec, &s->d_cskip, &s->d_crec_node,
+                                  &s->d_node2rec, &s->n_crec, berr) != 0) {
         err = berr; rc = -1;
     }
     return rc;
@@ -898,7 +910,7 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
     k_scene_update<<<2, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, s->d_emis,
                                               s->d_cdf, s->d_cdf_guide, R);
     HIPCHK(c, hipGetLastError());
-    if (bvh_crec_emit(s->d_nodes, s->d_crec_node, s->d_node2rec, s->n_crec, s->d_crec, st) != 0)
+    if (bvh_crec_emit(s->d_nodes, s->d_crec_node, s->d_node2rec, s->n_crec, s->d_crec, s->d_cskip, st) != 0)
         return fail(c, RS_E_HIP, "rs_scene_update_positions: child-record emit failed");
     return RS_OK;
 }
@@ -1032,7 +1044,7 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     if (s->ctx) sync_all(s->ctx);
     void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
                     s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage, s->d_tex, s->d_texd, s->d_uv,
-                    s->d_tan, s->d_crec, s->d_crec_node, s->d_node2rec};
+                    s->d_tan, s->d_crec, s->d_cskip, s->d_crec_node, s->d_node2rec};
     for (void* p : ptrs) if (p) hipFree(p);
     for (int k = 0; k < 2; ++k) {
         if (s->h_stage[k]) hipHostFree(s->h_stage[k]);
@@ -1098,6 +1110,31 @@ static void pick_traversal(rs_context* c, const rs_scene* s) {
         if (!e && hipEventCreate(&e) != hipSuccess) { e = nullptr; return; }   // untimed: stays un-tuned
     c->tune_n = 0;
     c->tuning = true;
+    // full-frame tuning frames also record per-row cost for the tile-row dispatch order
+    c->tune_rows = false;
+    if (c->order_on && !c->track_rows && c->tile.y0 == 0 && c->tile.y1 == c->H) {
+        float*& p = c->d_tune_cost[c->trav];
+        if (!p && hipMalloc(&p, (size_t)c->H * sizeof(float)) == hipSuccess)
+            (void)hipMemsetAsync(p, 0, (size_t)c->H * sizeof(float), c->stream);
+        c->tune_rows = p != nullptr;
+    }
+}
+// The tuning frames' per-row wave time of the chosen kind -> tile-row dispatch order, costliest first
+// (ties: top row first).  Full frames only; the frames are already synchronised here.
+static void order_tile_rows(rs_context* c, int kind) {
+    c->tune_rows = false;
+    if (!c->d_tune_cost[kind]) return;
+    std::vector<float> rc((size_t)c->H);
+    if (hipMemcpy(rc.data(), c->d_tune_cost[kind], rc.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) return;
+    const int n = (c->H + 15) / 16;
+    std::vector<double> cost(n, 0.0);
+    for (int y = 0; y < c->H; ++y) cost[y / 16] += rc[y];
+    std::vector<int> order(n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+    if (!c->d_order && hipMalloc(&c->d_order, (size_t)n * sizeof(int)) != hipSuccess) { c->d_order = nullptr; return; }
+    if (hipMemcpy(c->d_order, order.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) return;
+    c->n_order = n;
 }
 static void record_traversal_time(rs_context* c) {
     if (!c->tuning) return;
@@ -1118,8 +1155,10 @@ static void record_traversal_time(rs_context* c) {
     }
     const rs_scene* s = c->scene;
     if (++s->trav_runs[c->trav] > 1) s->trav_ms[c->trav] += ms;
-    if (s->trav_runs[TRAV_LOCKSTEP] >= kTuneRuns && s->trav_runs[TRAV_LANE] >= kTuneRuns)
+    if (s->trav_runs[TRAV_LOCKSTEP] >= kTuneRuns && s->trav_runs[TRAV_LANE] >= kTuneRuns) {
         s->trav_choice = s->trav_ms[TRAV_LANE] < s->trav_ms[TRAV_LOCKSTEP] ? TRAV_LANE : TRAV_LOCKSTEP;
+        order_tile_rows(c, s->trav_choice);
+    }
 }
 static size_t grid_waves(dim3 g, int waves_per_block = 4) { return (size_t)g.x * g.y * waves_per_block; }
 
@@ -1153,8 +1192,8 @@ static CountSlot count_slot(rs_context* c, dim3 grid, int waves_per_block = 4) {
             c->part_used = 0;                   // out of memory: recount from slot 0 (totals undercount)
         }
     }
-    CountSlot s{c->d_part + c->part_used, &c->d_cnt->reproj_outside, c->track_rows ? c->d_rowcost : nullptr,
-                c->F.y0, c->F.y1};
+    float* rows = c->track_rows ? c->d_rowcost : (c->tune_rows ? c->d_tune_cost[c->trav] : nullptr);
+    CountSlot s{c->d_part + c->part_used, &c->d_cnt->reproj_outside, rows, c->F.y0, c->F.y1};
     c->part_used += n;
     return s;
 }
@@ -1246,6 +1285,7 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     F.seed = P->seed; F.frame = frame_index;
     F.W = c->W; F.H = c->H;
     F.y0 = tile->y0; F.y1 = tile->y1;
+    F.row_order = c->n_order ? c->d_order : nullptr; F.n_order = c->n_order;
     F.gy0 = std::max(0, tile->y0 - tile->margin); F.gy1 = std::min(c->H, tile->y1 + tile->margin);
     // G-buffer ring (replaces gBufferLastFrame.setDataFrom, pg/simpleguidx11.cpp:480): this frame
     // writes the slot after the current one; G[gcur] becomes the previous frame's

@@ -126,7 +126,7 @@ __device__ __forceinline__ vec3 mis_light_part(const DevScene& S, const FrameCon
 template <int T>
 __global__ void __launch_bounds__(256) k_direct_mis(DevScene S, FrameConst F, int spp, float* fb, CountSlot C) {
     int x, y;
-    const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const bool in = pixel_of(F, F.y0, F.y1, x, y);
     const uint64_t t0 = wave_clock();
     const uint32_t pix = (uint32_t)y * (uint32_t)F.W + (uint32_t)x;
     uint32_t rays = in ? 1u : 0u;

@@ -73,6 +73,8 @@ struct FrameConst {
     float inv_view[9];    // mat3(invViewMat), column-major (pg/camera.cpp:57)
     float inv_view_prev[9];   // ... of the previous frame (a tile's temporal pass rebuilds G elements)
     GCam cam, camp;       // current / previous frame camera (pg/GBufferElement.h:136-139)
+    const int* row_order; // full-frame launches: grid row -> 16-px tile row, costliest first (or null)
+    int n_order;          // entries of row_order (== the grid's rows when it applies)
 };
 
 struct Counters { unsigned long long rays, primary, reproj_outside; };   // per-frame totals
@@ -158,40 +160,32 @@ __global__ void __launch_bounds__(kReduceThreads) k_reduce_counts(const uint2* p
     }
 }
 
-// Workgroup -> screen tile.  The dispatcher hands workgroup b (row-major over the grid) to XCD b % 8,
-// each XCD with its own 4 MB L2.  RS_TILE_ORDER:
-//   0  tile = b (row-major): every XCD samples the whole frame -- its L2 holds the BVH of every view ray
-//   1  XCD k renders vertical stripe k of the frame (row-major inside the stripe): neighbouring tiles,
-//      whose rays touch the same BVH nodes, share an L2; stripes keep the XCDs' costs balanced where
-//      cost varies by row (ceiling vs floor)
-//   2  as 1, each stripe bottom-up
-//   3  row-major, bottom-up (the expensive floor rows of the Cornell box first, cheap ceiling rows last)
-// Every pixel's work is independent of the order: results are identical for every order.
-#ifndef RS_TILE_ORDER
-#define RS_TILE_ORDER 0
+// Workgroup -> screen tile.  Workgroups are dispatched in grid order, so a full-frame launch takes its
+// 16-px tile rows in the context's cost order (costliest first: the longest-running workgroups start
+// early and the cheap ones fill the launch's tail -- C2's floor rows cost ~2x its ceiling rows), measured
+// during the traversal tuning frames (restir_capi.hip record_traversal_time).  Every pixel's work is
+// independent of the order: results are identical for any order.  (Giving each XCD a vertical stripe
+// of the frame instead, so neighbouring tiles share an L2, measured 1.85x slower on C2 and 3 % on C3.)
+__device__ __forceinline__ int order_row(const int* order, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const int __attribute__((address_space(4)))* cint_ptr;   // uniform index: scalar load
+    return ((cint_ptr)(order + i))[0];
+#else
+    return order[i];
 #endif
-__device__ __forceinline__ void tile_of(int& bx, int& by) {
-    const uint32_t gx = gridDim.x, gy = gridDim.y, n = gx * gy, b = blockIdx.y * gx + blockIdx.x;
-    if (RS_TILE_ORDER == 0 || n < 8) { bx = blockIdx.x; by = blockIdx.y; return; }
-    if (RS_TILE_ORDER == 3) { bx = blockIdx.x; by = gy - 1 - blockIdx.y; return; }
-    // dispatch slot s of XCD k -> position t in the stripe order (XCD k takes the k-th 1/8 of it)
-    const uint32_t k = b & 7u, s = b >> 3, q = n >> 3, r = n & 7u;
-    const uint32_t t = k < r ? k * (q + 1) + s : r * (q + 1) + (k - r) * q + s;
-    // stripe order: stripes of w tile columns (the last one narrower), row-major inside a stripe
-    const uint32_t w = (gx + 7) >> 3, sz = w * gy, i = t / sz, l = t - i * sz;
-    const uint32_t wi = gx - i * w < w ? gx - i * w : w;
-    uint32_t ry = l / wi;
-    if (RS_TILE_ORDER == 2) ry = gy - 1 - ry;
-    bx = (int)(i * w + (l - (l / wi) * wi));
-    by = (int)ry;
+}
+__device__ __forceinline__ void tile_of(const FrameConst& F, int ya, int yb, int& bx, int& by) {
+    bx = blockIdx.x; by = blockIdx.y;
+    if (F.row_order && ya == 0 && yb == F.H && (uint32_t)F.n_order == gridDim.y) by = order_row(F.row_order, blockIdx.y);
 }
 
 // 8x8 tile per wave, 16x16 per workgroup, rows [ya, yb).  Returns whether the pixel exists; x/y are
 // clamped into the image so out-of-range lanes can run the (convergent) code on a valid pixel.
-__device__ __forceinline__ bool pixel_of(int ya, int yb, int W, int& x, int& y) {
+__device__ __forceinline__ bool pixel_of(const FrameConst& F, int ya, int yb, int& x, int& y) {
+    const int W = F.W;
     int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int bx, by;
-    tile_of(bx, by);
+    tile_of(F, ya, yb, bx, by);
     x = bx * 16 + (wave & 1) * 8 + (lane & 7);
     y = ya + by * 16 + (wave >> 1) * 8 + (lane >> 3);
     bool in = x < W && y < yb;
@@ -569,7 +563,7 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
     if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
     int x, y;
     uint32_t rays = 0;
-    const bool in = pixel_of(F.gy0, F.gy1, F.W, x, y);
+    const bool in = pixel_of(F, F.gy0, F.gy1, x, y);
     const size_t p = (size_t)y * F.W + x;
     __shared__ float4 frame_lds[5 * 256];
     const FrameSlot fs{frame_lds, (int)threadIdx.x, 256};
@@ -623,9 +617,7 @@ __global__ void __launch_bounds__(64 * kSplit, RS_WAVES(T, RS_INITIAL_WAVES, RS_
     if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
     __shared__ SplitLds L;
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-    int bx, by;
-    tile_of(bx, by);
-    int x = bx * 8 + (lane & 7), y = F.gy0 + by * 8 + (lane >> 3);
+    int x = blockIdx.x * 8 + (lane & 7), y = F.gy0 + blockIdx.y * 8 + (lane >> 3);
     const bool in = x < F.W && y < F.gy1;
     x = x < F.W ? x : F.W - 1;
     y = y < F.gy1 ? y : F.gy1 - 1;
@@ -724,7 +716,7 @@ __global__ void __launch_bounds__(256) k_visibility(DevScene S, FrameConst F, GB
     const uint64_t t0 = wave_clock();
     int x, y;
     uint32_t rays = 0;
-    const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const bool in = pixel_of(F, F.y0, F.y1, x, y);
     const size_t p = (size_t)y * F.W + x;
     Res r = R.load(p);
     const bool need = in && smp_valid(smp_of(r));
@@ -757,7 +749,7 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
     const uint64_t t0 = wave_clock();
     int x, y;
     uint32_t rays = 0;
-    const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const bool in = pixel_of(F, F.y0, F.y1, x, y);
     const size_t p = (size_t)y * F.W + x;
     Res cr = Rr.load(p);
     GElem cur = G.load(p);
@@ -865,7 +857,7 @@ k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, 
     const uint64_t t0 = wave_clock();
     int x, y;
     uint32_t rays = 0;
-    const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const bool in = pixel_of(F, F.y0, F.y1, x, y);
     const size_t p = (size_t)y * F.W + x;
     const vec3 cam = F.cam.pos;
     GElem th = G.load(p);
@@ -1044,7 +1036,7 @@ __global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G,
     const uint64_t t0 = wave_clock();
     int x, y;
     uint32_t rays = 0;
-    const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const bool in = pixel_of(F, F.y0, F.y1, x, y);
     const size_t p = (size_t)y * F.W + x;
     Res r = Rr.load(p);
     GElem g = G.load(p);

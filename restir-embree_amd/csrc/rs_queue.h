@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(256, RS_Q_GEN_WAVES) k_q_generate(DevScene S, 
     if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
     int x, y;
     uint32_t rays = 0;
-    const bool in = pixel_of(F.gy0, F.gy1, F.W, x, y);
+    const bool in = pixel_of(F, F.gy0, F.gy1, x, y);
     const size_t p = (size_t)y * F.W + x;
     const uint32_t lp = (uint32_t)(p - (size_t)F.gy0 * F.W);
     __shared__ float4 frame_lds[5 * 256];
@@ -187,7 +187,7 @@ __global__ void __launch_bounds__(256) k_q_resolve(DevScene S, FrameConst F, GBu
                                                    int fuse_shade, CountSlot C) {
     const uint64_t t0 = wave_clock();
     int x, y;
-    const bool in = pixel_of(F.y0, F.y1, F.W, x, y);
+    const bool in = pixel_of(F, F.y0, F.y1, x, y);
     const size_t p = (size_t)y * F.W + x;
     const uint32_t lp = (uint32_t)(p - (size_t)F.gy0 * F.W);
     const GElem g = G.load(p);

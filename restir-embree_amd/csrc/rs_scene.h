@@ -36,8 +36,9 @@ struct DevScene {
     const uint8_t* tex;       // texel bytes of every texture
     const int4* texd;         // 2 per texture: (byte offset, width, height, pitch), (pixel bytes, format, 0, 0)
     int sky;                  // texture index of the equirect sky, -1 none
-    // child-box records of the interior nodes (TRAV_LANE walks, see "child-box walks" below), 4 per record
+    // child-box records of the interior nodes (TRAV_LANE walks, see "child-box walks" below)
     const float4* crec;
+    const uint32_t* cskip;    // per record: the node after its subtree (skip pointer), overflow fallback
     uint32_t n_crec;          // 0: none (single-leaf tree) -> the skip-pointer walks
 };
 constexpr int kCdfGuide = 1024;
@@ -211,26 +212,40 @@ __device__ __forceinline__ Hit closest_lane_skip(const DevScene& S, bool active,
 // ---------------------------------------------------------------- child-box walks (TRAV_LANE)
 // The skip-pointer walk fetches a node to test that node's own box, so every child of every entered
 // node costs one dependent load -- about twice the entered nodes.  A child-box record holds BOTH
-// children's boxes of an interior node (64 B = 4 x float4):
-//   c0 = (L.lo, Llink)   c1 = (L.hi, Rlink)   c2 = (R.lo, skip)   c3 = (R.hi, 0)
-//   link >= 0: the child's record index (interior child); link < 0: ~leaf word of a leaf child, whose
-//   triangles are tested straight from the parent's visit (leaf nodes are never fetched)
-//   skip: the node following this subtree in the preorder (skip-pointer index)
-// so a walk loads one record per ENTERED interior node.  Right children whose box was hit wait on a
-// short per-lane stack in registers (RS_CSTACK entries, shifted: no scratch); when it overflows the
-// oldest entry is dropped and, once the stack runs empty, the walk finishes as a skip-pointer walk: an
-// any-hit walk (always left first, so every dropped entry is a right child of an ancestor) from the
-// current record's skip, after which the preorder holds every dropped subtree; a closest-hit walk
-// (nearer child first) from the root, culled by the closest hit found so far.  Same boxes, same
-// conservative box test and the same triangle tests (any-hit: existence; closest: the tie rule), so
-// results are bit-identical to the skip-pointer walks; closest-hit walks also enter the nearer child
-// first.  Records are emitted from the nodes at build time and after every refit (rs_bvh_build.hip).
+// children's boxes of an interior node, so a walk loads one record per ENTERED interior node; a leaf
+// child's triangles are tested straight from its parent's visit (leaf nodes are never fetched).
+//
+// The per-lane walks of C3 keep the vector-memory pipeline busy (TA/TD ~90 % busy on k_gbuffer_initial;
+// loading every record twice costs +57 % time); a 32-B record (two 16-B loads instead of four) quantises
+// the children's boxes to 8 bits:
+//   RS_CREC == 2, 2 x uint4:
+//     w0..w2  origin O (float; the record's box lo)       w3.b0  biased exponent e of the scale s = 2^(e-127)
+//     w3.b1-3 L.lo q    w4.b0-2 L.hi q    w4.b3,w5.b0-1 R.lo q    w5.b2-3,w6.b0 R.hi q
+//     w6.b1-3 + w7.b0-3: two 28-bit links (bit 27: leaf; leaf: first tri << 3 | count - 1, else record)
+//   coordinate = O + q * s, emitted rounded OUTWARD (rs_bvh_build.hip k_crec_emit checks every one with
+//   this same expression), e == 0: a box that could not be quantised -- always entered
+//   RS_CREC == 1: 64 B exact records, 4 x float4: (L.lo, Llink) (L.hi, Rlink) (R.lo, skip) (R.hi, 0),
+//   link >= 0 a record, < 0 ~leaf word
+// Right children whose box was hit wait on a short per-lane stack in registers (RS_CSTACK entries,
+// shifted: no scratch); when it overflows the oldest entry is dropped and, once the stack runs empty,
+// the walk finishes as a skip-pointer walk: an any-hit walk (always left first, so every dropped entry
+// is a right child of an ancestor) from the current record's skip (S.cskip), after which the preorder
+// holds every dropped subtree; a closest-hit walk (nearer child first) from the root, culled by the
+// closest hit found so far.  Every box the walk tests contains the exact box, the box test is the same
+// conservative slab test and the triangle tests are the same (any-hit: existence; closest: the tie
+// rule), so results are bit-identical to the skip-pointer walks.  Records are emitted from the nodes at
+// build time and after every refit (rs_bvh_build.hip).
 #ifndef RS_CSTACK
 #define RS_CSTACK 6
 #endif
+// Default 0 (skip-pointer walks): measured on C3 (k_gbuffer_initial, lane walks, 1080p): skip pointers
+// 23.6 ms, 64-B records 23.8-25.1 ms, 32-B quantised records 31.3 ms -- the record walk halves the
+// dependent loads and the L1 misses but not the lane-loads, and the dequantisation VALU sits on the
+// walk's critical path.  Kept as a build option (-DRS_CREC=1/2), tested bit-identical.
 #ifndef RS_CREC
-#define RS_CREC 1
+#define RS_CREC 0
 #endif
+constexpr int kCrecWords = RS_CREC == 2 ? 2 : 4;     // float4 per record
 struct CStack {
     uint32_t s[RS_CSTACK];
     int sp;
@@ -263,6 +278,66 @@ __device__ __forceinline__ bool box_test_t(float4 a, float4 b, vec3 o, vec3 inv,
     tin = t0;
     return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
 }
+// quantised coordinate -> float; the emitter rounds q outward against exactly this expression
+__device__ __forceinline__ float crec_deq(float o, uint32_t q, float s) { return o + (float)q * s; }
+
+// One record visit: both children's box tests against [tnear, tfar], decoded links.
+struct CVisit {
+    bool hL, hR;           // box hit
+    float tL, tR;          // entry distances (closest-hit order)
+    bool leafL, leafR;
+    uint32_t aL, aR;       // interior: record index; leaf: first triangle
+    int cL, cR;            // leaf triangle counts
+};
+template <bool Ordered>   // Ordered: entry distances for the closest-hit child order
+__device__ __forceinline__ CVisit crec_visit(const DevScene& S, bool live, uint32_t r, vec3 o, vec3 inv, float tnear,
+                                             float tfar) {
+    CVisit v;
+    v.tL = v.tR = 0.0f;
+#if RS_CREC == 2
+    const uint4* R4 = (const uint4*)S.crec + 2 * (size_t)r;
+    const uint4 a = R4[0], b = R4[1];
+    const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
+    const uint32_t eb = a.w & 0xffu;
+    const float s = __uint_as_float(eb << 23);
+    const float4 Llo = make_float4(crec_deq(ox, (a.w >> 8) & 0xffu, s), crec_deq(oy, (a.w >> 16) & 0xffu, s),
+                                   crec_deq(oz, a.w >> 24, s), 0.0f);
+    const float4 Lhi = make_float4(crec_deq(ox, b.x & 0xffu, s), crec_deq(oy, (b.x >> 8) & 0xffu, s),
+                                   crec_deq(oz, (b.x >> 16) & 0xffu, s), 0.0f);
+    const float4 Rlo = make_float4(crec_deq(ox, b.x >> 24, s), crec_deq(oy, b.y & 0xffu, s),
+                                   crec_deq(oz, (b.y >> 8) & 0xffu, s), 0.0f);
+    const float4 Rhi = make_float4(crec_deq(ox, (b.y >> 16) & 0xffu, s), crec_deq(oy, b.y >> 24, s),
+                                   crec_deq(oz, b.z & 0xffu, s), 0.0f);
+    const bool any = eb == 0u;                       // unquantisable record: enter both children
+    if (Ordered) {
+        v.hL = live & (any | box_test_t(Llo, Lhi, o, inv, tnear, tfar, v.tL));
+        v.hR = live & (any | box_test_t(Rlo, Rhi, o, inv, tnear, tfar, v.tR));
+        v.tL = any ? tnear : v.tL; v.tR = any ? tnear : v.tR;
+    } else {
+        v.hL = live & (any | box_test(Llo, Lhi, o, inv, tnear, tfar));
+        v.hR = live & (any | box_test(Rlo, Rhi, o, inv, tnear, tfar));
+    }
+    const uint32_t lL = (b.z >> 8) | ((b.w & 0xfu) << 24), lR = b.w >> 4;
+    v.leafL = (lL >> 27) & 1u; v.leafR = (lR >> 27) & 1u;
+    v.aL = v.leafL ? (lL >> 3) & 0xffffffu : lL; v.aR = v.leafR ? (lR >> 3) & 0xffffffu : lR;
+    v.cL = (int)(lL & 7u) + 1; v.cR = (int)(lR & 7u) + 1;
+#else
+    const float4* R4 = S.crec + 4 * (size_t)r;
+    const float4 c0 = R4[0], c1 = R4[1], c2 = R4[2], c3 = R4[3];
+    if (Ordered) {
+        v.hL = live & box_test_t(c0, c1, o, inv, tnear, tfar, v.tL);
+        v.hR = live & box_test_t(c2, c3, o, inv, tnear, tfar, v.tR);
+    } else {
+        v.hL = live & box_test(c0, c1, o, inv, tnear, tfar);
+        v.hR = live & box_test(c2, c3, o, inv, tnear, tfar);
+    }
+    const int lL = __float_as_int(c0.w), lR = __float_as_int(c1.w);
+    v.leafL = lL < 0; v.leafR = lR < 0;
+    v.aL = v.leafL ? (uint32_t)(~lL) >> 3 : (uint32_t)lL; v.aR = v.leafR ? (uint32_t)(~lR) >> 3 : (uint32_t)lR;
+    v.cL = (~lL & 7) + 1; v.cR = (~lR & 7) + 1;
+#endif
+    return v;
+}
 
 __device__ __forceinline__ bool occluded_crec(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -273,30 +348,26 @@ __device__ __forceinline__ bool occluded_crec(const DevScene& S, bool active, ve
     while (__ballot(cur != kDone) != 0) {
         const bool live = cur != kDone;
         const uint32_t r = live ? cur : 0u;
-        const float4 c0 = S.crec[4 * r], c1 = S.crec[4 * r + 1], c2 = S.crec[4 * r + 2], c3 = S.crec[4 * r + 3];
-        const int lL = __float_as_int(c0.w), lR = __float_as_int(c1.w);
-        const bool hL = live & box_test(c0, c1, o, inv, tnear, tfar);
-        const bool hR = live & box_test(c2, c3, o, inv, tnear, tfar);
-        const int wL = ~lL, wR = ~lR;
-        const int nL = (hL & (lL < 0)) ? (wL & 7) + 1 : 0, nR = (hR & (lR < 0)) ? (wR & 7) + 1 : 0;
+        const CVisit v = crec_visit<false>(S, live, r, o, inv, tnear, tfar);
+        const int nL = (v.hL & v.leafL) ? v.cL : 0, nR = (v.hR & v.leafR) ? v.cR : 0;
         for (int j = 0; j < 16; ++j) {
             const bool want = (j < nL + nR) & (occ == 0u);
             if (__ballot(want) == 0) break;
-            const int t = j < nL ? (wL >> 3) + j : (wR >> 3) + (j - nL);
-            const float4* T = S.tris + 3 * (want ? t : 0);
-            float tt, u, v;
-            const bool h = tri_test_nb(T[0], T[1], T[2], o, d, tnear, tfar, tt, u, v);
+            const uint32_t t = j < nL ? v.aL + j : v.aR + (j - nL);
+            const float4* T = S.tris + 3 * (want ? t : 0u);
+            float tt, u, w;
+            const bool h = tri_test_nb(T[0], T[1], T[2], o, d, tnear, tfar, tt, u, w);
             occ = (want & h) ? 1u : occ;
         }
-        const bool iL = hL & (lL >= 0), iR = hR & (lR >= 0);
+        const bool iL = v.hL & !v.leafL, iR = v.hR & !v.leafR;
         const bool go = live & (occ == 0u);
         const bool none = !iL & !iR;
         const bool pop = go & none & (st.sp > 0);
         const uint32_t top = st.s[0];
         st.pop(pop);
-        st.push(go & iL & iR, (uint32_t)lR);
-        resume = (go & none & !pop & st.dropped) ? __float_as_uint(c2.w) : resume;
-        const uint32_t nxt = iL ? (uint32_t)lL : (iR ? (uint32_t)lR : (pop ? top : kDone));
+        st.push(go & iL & iR, v.aR);
+        if (go & none & !pop & st.dropped) resume = S.cskip[r];      // rare: the stack overflowed
+        const uint32_t nxt = iL ? v.aL : (iR ? v.aR : (pop ? top : kDone));
         cur = !live ? cur : (go ? nxt : kDone);
     }
     if (__ballot(resume != kDone) != 0)            // a stack overflowed: finish as a skip-pointer walk
@@ -314,38 +385,32 @@ __device__ __forceinline__ Hit closest_crec(const DevScene& S, bool active, vec3
     while (__ballot(cur != kDone) != 0) {
         const bool live = cur != kDone;
         const uint32_t r = live ? cur : 0u;
-        const float4 c0 = S.crec[4 * r], c1 = S.crec[4 * r + 1], c2 = S.crec[4 * r + 2], c3 = S.crec[4 * r + 3];
-        const int lL = __float_as_int(c0.w), lR = __float_as_int(c1.w);
-        float tL, tR;
-        const bool hL = live & box_test_t(c0, c1, o, inv, tnear, h.t, tL);
-        const bool hR = live & box_test_t(c2, c3, o, inv, tnear, h.t, tR);
-        const int wL = ~lL, wR = ~lR;
-        const int nL = (hL & (lL < 0)) ? (wL & 7) + 1 : 0, nR = (hR & (lR < 0)) ? (wR & 7) + 1 : 0;
+        const CVisit v = crec_visit<true>(S, live, r, o, inv, tnear, h.t);
+        const int nL = (v.hL & v.leafL) ? v.cL : 0, nR = (v.hR & v.leafR) ? v.cR : 0;
         for (int j = 0; j < 16; ++j) {
             const bool want = j < nL + nR;
             if (__ballot(want) == 0) break;
-            const int t = j < nL ? (wL >> 3) + j : (wR >> 3) + (j - nL);
-            const float4* T = S.tris + 3 * (want ? t : 0);
+            const uint32_t t = j < nL ? v.aL + j : v.aR + (j - nL);
+            const float4* T = S.tris + 3 * (want ? t : 0u);
             const float4 T0 = T[0];
-            float tt, u, v;
-            const bool hh = want & tri_test_nb(T0, T[1], T[2], o, d, tnear, h.t, tt, u, v);
+            float tt, u, w;
+            const bool hh = want & tri_test_nb(T0, T[1], T[2], o, d, tnear, h.t, tt, u, w);
             const int prim = __float_as_int(T0.w);
             const bool better = hh & (h.prim < 0 || tt < h.t || (tt == h.t && prim < h.prim));
-            h.t = better ? tt : h.t; h.u = better ? u : h.u; h.v = better ? v : h.v;
+            h.t = better ? tt : h.t; h.u = better ? u : h.u; h.v = better ? w : h.v;
             h.prim = better ? prim : h.prim;
         }
-        const bool iL = hL & (lL >= 0), iR = hR & (lR >= 0);
+        const bool iL = v.hL & !v.leafL, iR = v.hR & !v.leafR;
         const bool none = !iL & !iR;
         const bool pop = live & none & (st.sp > 0);
         const uint32_t top = st.s[0];
         st.pop(pop);
-        const bool rfirst = tR < tL;                  // both entered: the nearer first, the other waits
-        st.push(live & iL & iR, rfirst ? (uint32_t)lL : (uint32_t)lR);
+        const bool rfirst = v.tR < v.tL;              // both entered: the nearer first, the other waits
+        st.push(live & iL & iR, rfirst ? v.aL : v.aR);
         // an overflowed closest-hit walk restarts the skip-pointer walk at the root (nearer-first order
         // may have dropped a LEFT child, which precedes the current record in the preorder)
         resume = (live & none & !pop & st.dropped) ? 0u : resume;
-        const uint32_t nxt = (iL & iR) ? (rfirst ? (uint32_t)lR : (uint32_t)lL)
-                                       : (iL ? (uint32_t)lL : (iR ? (uint32_t)lR : (pop ? top : kDone)));
+        const uint32_t nxt = (iL & iR) ? (rfirst ? v.aR : v.aL) : (iL ? v.aL : (iR ? v.aR : (pop ? top : kDone)));
         cur = !live ? cur : nxt;
     }
     if (__ballot(resume != kDone) != 0) closest_lane_from(S, resume, o, d, inv, tnear, h);

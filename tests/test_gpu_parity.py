@@ -166,14 +166,15 @@ def test_phong_scene_c3_small():
 @pytest.mark.parametrize("which", ["c2", "c3"])
 def test_traversal_kinds_bit_identical(which):
     """LOCKSTEP, LANE and AUTO (which alternates the kinds over its first six frames) render
-    bit-identical frames, matching the oracle; AUTO has settled on a kind after six frames."""
+    bit-identical frames, matching the oracle; AUTO has settled on a kind after six frames, and its
+    later frames dispatch the tile rows in the measured cost order (ragged last tile row included)."""
     if which == "c2":
         sc, prm, W, H = scenes.cornell_many_lights(1024), P.metric_params(), 64, 48
         cam = lambda f: sc.camera
     else:
         sc, prm, W, H = scenes.sponza_like(target_tris=30_000, n_lamps=128), P.c3_params(m_area=8), 64, 40
         cam = lambda f: scenes.orbit_camera(sc.camera, f, 240, 0.3)
-    n_frames = 7
+    n_frames = 9
     frames = {}
     for mode in ("lockstep", "lane", "auto"):
         g = Renderer(W, H)
