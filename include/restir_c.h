@@ -163,10 +163,13 @@ void rs_scene_destroy(rs_scene* scene);
 /* Animated geometry (C5 moving lights; the reference cannot move geometry -- the Embree analogue is
  * rtcUpdateGeometryBuffer + rtcCommitGeometry + rtcCommitScene): replaces all n_tris*9 vertex
  * positions (and, if normals != NULL, the vertex normals) in the scene's triangle order, recomputes
- * the emissive-triangle CDF on the device and refits the BVH in place (same topology; every query
- * answers bit-identically to a freshly built tree).  Materials and triangle count are unchanged.
- * Asynchronous: stream-ordered after the frames already enqueued on the context's stream, no host
- * synchronisation (the caller's arrays are copied before return); no tile frame may be open. */
+ * the emissive-triangle CDF on the device and refits the BVH (same topology; every query answers
+ * bit-identically to a freshly built tree).  Materials and triangle count are unchanged.
+ * Asynchronous, no host synchronisation (the caller's arrays are copied before return); no tile frame
+ * may be open.  Frames already enqueued render the old geometry, later frames the new: with frames in
+ * flight (run-ahead > 0) and normals == NULL the refit and tables are written to a second copy of the
+ * scene's device data, ordered only after the frames that read that copy, and swapped in (the
+ * pipeline keeps running); otherwise the update is written in place after every enqueued frame. */
 int rs_scene_update_positions(rs_scene* scene, const float* positions, const float* normals);
 /* Full rebuild of the CDF and a new PLOC tree from the scene's current positions -- restores tree
  * quality after large motions, where a refit tree's boxes grow.  Synchronous. */
