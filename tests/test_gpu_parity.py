@@ -229,7 +229,7 @@ def test_initial_split_bit_identical(which):
     _assert_close(out["lane", "on"][0], o.render(os_, cam(0), prm, 0), f"{which} split vs oracle")
 
 
-@pytest.mark.parametrize("which", ["c2", "c3", "c5", "fused"])
+@pytest.mark.parametrize("which", ["c2", "c3", "c5", "c5mix", "fused"])
 def test_run_ahead_bit_identical(which):
     """Frame pipelining (initial pass of frame f+1 on the side stream, overlapping frame f's later
     passes) renders the same frames as strictly sequential frames, with temporal reuse, moving
@@ -246,7 +246,13 @@ def test_run_ahead_bit_identical(which):
         sc, prm = scenes.sponza_like(target_tris=30_000, n_lamps=128), P.c3_params(m_area=6)
     elif which == "c5":
         sc, prm = scenes.cornell_many_lights(256), P.c3_params(m_area=6)
-        upd = lambda f: scenes.moving_light_positions(sc, f, 48)
+        upd = lambda f: (scenes.moving_light_positions(sc, f, 48), None)
+    elif which == "c5mix":
+        # pipelined updates (the second scene copy), frames without an update, and in-place updates
+        # with normals (which drain the pipeline) in one sequence
+        sc, prm = scenes.cornell_many_lights(256), P.c3_params(m_area=6)
+        upd = lambda f: (None if f % 4 == 2 else scenes.moving_light_positions(sc, f, 48),
+                         sc.normals if f % 4 == 3 else None)
     else:
         sc, prm = scenes.cornell_box(8), P.default_params(m_area=4)
     import torch
@@ -254,22 +260,25 @@ def test_run_ahead_bit_identical(which):
     torch.cuda.set_stream(torch.cuda.Stream())       # the clones below are ordered on the frames' stream
     st = torch.cuda.current_stream().cuda_stream
     out = {}
+    n_frames = 10 if which == "c5mix" else 6
     for ra in (0, 1, 2):
         g = Renderer(W, H, stream=st)
         g.set_traversal("lane" if which == "c3" else "lockstep")
         g.set_run_ahead(ra)
         gs = g.load_scene(sc)
         frames = []
-        for f in range(6):
+        for f in range(n_frames):
             if upd:
-                gs.update_positions(upd(f))
+                pos, nrm = upd(f)
+                if pos is not None:
+                    gs.update_positions(pos, nrm)
             g.produce_restir(gs, cam(f), prm, f, copy_out=False, timed=False)
             frames.append(torch.as_tensor(_CudaBuf(g.frame_device_ptr(), W * H * 12, "<f4", 4), device="cuda").clone())
         out[ra] = [t.cpu().numpy().reshape(H, W, 3) for t in frames]
-    for f in range(6):
+    for f in range(n_frames):
         for ra in (1, 2):
             assert np.array_equal(out[0][f], out[ra][f]), f"{which} depth {ra} frame {f}"
-    if which != "c5":
+    if which not in ("c5", "c5mix"):
         o, os_ = O.OracleRenderer(W, H), O.OracleScene(sc)
         for f in range(2):
             _assert_close(out[2][f], o.render(os_, cam(f), prm, f), f"{which} run-ahead frame {f}")
