@@ -1002,6 +1002,7 @@ extern "C" int rs_scene_rebuild(rs_scene* s) {
     HIPCHK(c, enter(c));
     std::vector<float> pos(9 * (size_t)s->n_tris);
     if (!pos.empty()) {
+        if (s->update_recorded) HIPCHK(c, hipStreamWaitEvent(c->stream, s->update_ev, 0));   // a pipelined update
         HIPCHK(c, hipMemcpyAsync(pos.data(), s->d_pos, pos.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
@@ -2022,6 +2023,7 @@ extern "C" int rs_debug_trace(rs_context* c, const rs_scene* s, uint32_t n, cons
     hipMemcpyAsync(dd + 3 * (size_t)n, d, 3 * (size_t)n * 4, hipMemcpyHostToDevice, c->stream);
     hipMemcpyAsync(dd + 6 * (size_t)n, tnear, (size_t)n * 4, hipMemcpyHostToDevice, c->stream);
     hipMemcpyAsync(dd + 7 * (size_t)n, tfar, (size_t)n * 4, hipMemcpyHostToDevice, c->stream);
+    if (s->update_recorded) HIPCHK(c, hipStreamWaitEvent(c->stream, s->update_ev, 0));   // a pipelined update
     k_debug_trace<<<(n + 255) / 256, 256, 0, c->stream>>>(s->dev(), n, dd, dd + 3 * (size_t)n, dd + 6 * (size_t)n,
                                                           dd + 7 * (size_t)n, any_hit, dd + 8 * (size_t)n, dp);
     hipError_t e = hipGetLastError();
