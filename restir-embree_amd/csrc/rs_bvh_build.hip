@@ -646,10 +646,42 @@ __device__ __forceinline__ uint32_t crec_link(const float4* nodes, const int* no
     return w >= 0 ? (1u << 27) | (uint32_t)w : (uint32_t)node2rec[c];   // leaf word = first << 3 | count - 1
 }
 #endif
+#if RS_CREC == 3
+// binary16 bits of x rounded toward -inf (up = false) or +inf (up = true): the RNE conversion, then one
+// ulp outward when it rounded inward (overflow goes to +-inf, which stays conservative)
+__device__ __forceinline__ uint32_t f2h_out(float x, bool up) {
+    const _Float16 h = (_Float16)x;
+    const float back = (float)h;
+    uint32_t u = __builtin_bit_cast(unsigned short, h);
+    if (x == x && (up ? back < x : back > x)) {
+        const bool neg = (u & 0x8000u) != 0u;
+        if (up) u = neg ? (u == 0x8000u ? 0x0001u : u - 1u) : u + 1u;
+        else    u = neg ? u + 1u : (u == 0u ? 0x8001u : u - 1u);
+    }
+    return u;
+}
+#endif
 __global__ void k_crec_emit(const float4* __restrict__ nodes, const int* __restrict__ rec_node,
                             const int* __restrict__ node2rec, uint32_t n_rec, float4* crec, uint32_t* cskip) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_rec) return;
+#if RS_CREC == 3
+    {   // half node r (records = nodes); a non-finite coordinate widens to the infinite box
+        const float4 a = nodes[2 * r], b = nodes[2 * r + 1];
+        const int lw = __float_as_int(b.w);
+        auto lo = [](float v) { return v == v ? f2h_out(v, false) : 0xfc00u; };
+        auto hi = [](float v) { return v == v ? f2h_out(v, true) : 0x7c00u; };
+        uint4 q;
+        q.x = lo(a.x) | (lo(a.y) << 16);
+        q.y = lo(a.z) | (hi(b.x) << 16);
+        q.z = hi(b.y) | (hi(b.z) << 16);
+        q.w = lw >= 0 ? (0x80000000u | (uint32_t)lw) : __float_as_uint(a.w);
+        ((uint4*)crec)[r] = q;
+        cskip[r] = __float_as_uint(a.w);
+        return;
+    }
+#endif
+#if RS_CREC != 3
     const int i = rec_node[r], L = i + 1;
     const float4 aL = nodes[2 * L], bL = nodes[2 * L + 1];
     const int R = __float_as_int(aL.w);
@@ -700,6 +732,7 @@ __global__ void k_crec_emit(const float4* __restrict__ nodes, const int* __restr
     crec[4 * r + 2] = make_float4(aR.x, aR.y, aR.z, nodes[2 * i].w);
     crec[4 * r + 3] = make_float4(bR.x, bR.y, bR.z, 0.0f);
 #endif
+#endif
 }
 
 // Record numbering (host, once per topology): interior nodes in preorder.  Checks that the tree is
@@ -708,7 +741,25 @@ __global__ void k_crec_emit(const float4* __restrict__ nodes, const int* __restr
 int bvh_crec_build(const float4* d_nodes, uint32_t n_nodes, uint32_t n_tris, hipStream_t st, float4** d_crec,
                    uint32_t** d_cskip, int** d_rec_node, int** d_node2rec, uint32_t* n_rec, std::string& err) {
     *d_crec = nullptr; *d_cskip = nullptr; *d_rec_node = nullptr; *d_node2rec = nullptr; *n_rec = 0;
-    if (!RS_CREC || n_nodes < 3 || n_tris >= (1u << 24)) return 0;   // walks use the skip pointers
+    if (!RS_CREC) return 0;                                          // walks use the float nodes
+    if (RS_CREC == 3) {   // half nodes: one record per node, identity numbering (leaf words < 2^31)
+        if (n_nodes == 0 || n_tris >= (1u << 27)) return 0;
+        std::vector<int> id(n_nodes);
+        for (uint32_t i = 0; i < n_nodes; ++i) id[i] = (int)i;
+        if (hipMalloc(d_crec, (size_t)n_nodes * kCrecWords * sizeof(float4)) != hipSuccess ||
+            hipMalloc(d_cskip, n_nodes * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(d_rec_node, n_nodes * sizeof(int)) != hipSuccess ||
+            hipMalloc(d_node2rec, (size_t)n_nodes * sizeof(int)) != hipSuccess) { err = "half nodes: hipMalloc failed"; return -1; }
+        if (hipMemcpyAsync(*d_rec_node, id.data(), n_nodes * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(*d_node2rec, id.data(), n_nodes * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
+            err = "half nodes: upload failed"; return -1;
+        }
+        k_crec_emit<<<(n_nodes + 255) / 256, 256, 0, st>>>(d_nodes, *d_rec_node, *d_node2rec, n_nodes, *d_crec, *d_cskip);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) { err = "half nodes: emit failed"; return -1; }
+        *n_rec = n_nodes;
+        return 0;
+    }
+    if (n_nodes < 3 || n_tris >= (1u << 24)) return 0;   // walks use the skip pointers
     std::vector<float4> h(2 * (size_t)n_nodes);
     if (hipMemcpyAsync(h.data(), d_nodes, h.size() * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess) { err = "child records: node download failed"; return -1; }

@@ -142,6 +142,33 @@ __device__ __forceinline__ void closest_visit(const DevScene& S, float4 a, float
 }
 
 // ---------------------------------------------------------------- per-lane walks (TRAV_LANE)
+// node format of the per-lane walks: 0 skip-pointer float nodes, 1/2 child-box records, 3 half nodes
+#ifndef RS_CREC
+#define RS_CREC 0
+#endif
+// Node fetch of the per-lane skip-pointer walks.  RS_CREC == 3: one 16-B record per node (half the
+// lane-loads of the 32-B float node, which bound these walks -- §3.8 of DESIGN.md): the box as six
+// binary16 values rounded OUTWARD (rs_bvh_build.hip k_crec_emit), so it contains the exact box and the
+// walk visits a superset of the exact walk's nodes with the same triangle tests -- bit-identical hits;
+// w: interior -> skip pointer, leaf -> 1 << 31 | first << 3 | count - 1 (a leaf's skip is i + 1 in the
+// preorder).
+__device__ __forceinline__ float h2f(uint32_t bits) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(bits & 0xffffu));
+}
+__device__ __forceinline__ void lane_node(const DevScene& S, uint32_t i, float4& a, float4& b, uint32_t& skip, int& leaf) {
+    if (RS_CREC == 3 && S.n_crec) {
+        const uint4 q = ((const uint4*)S.crec)[i];
+        a = make_float4(h2f(q.x), h2f(q.x >> 16), h2f(q.y), 0.0f);
+        b = make_float4(h2f(q.y >> 16), h2f(q.z), h2f(q.z >> 16), 0.0f);
+        const bool lf = (int)q.w < 0;
+        skip = lf ? i + 1u : q.w;
+        leaf = lf ? (int)(q.w & 0x7fffffffu) : -1;
+    } else {
+        a = S.nodes[2 * i]; b = S.nodes[2 * i + 1];
+        skip = (uint32_t)__float_as_int(a.w);
+        leaf = __float_as_int(b.w);
+    }
+}
 // Branch-lean per-lane walks: uniform loop condition, select-based cursor updates, the leaf's
 // triangles in a wave-uniform loop up to the largest leaf among the lanes -- no per-lane exec-mask
 // regions (C3: +21 % over the branchy loop).
@@ -153,9 +180,10 @@ __device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i
     while (__ballot(i < n) != 0) {
         const bool live = i < n;
         const uint32_t ii = live ? i : 0u;
-        const float4 a = S.nodes[2 * ii], b = S.nodes[2 * ii + 1];
-        const uint32_t skip = (uint32_t)__float_as_int(a.w);
-        const int leaf = __float_as_int(b.w);
+        float4 a, b;
+        uint32_t skip;
+        int leaf;
+        lane_node(S, ii, a, b, skip, leaf);
         const bool hit = live & box_test(a, b, o, inv, tnear, tfar);
         const bool in_leaf = hit & (leaf >= 0);
         const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
@@ -181,9 +209,10 @@ __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i,
     while (__ballot(i < n) != 0) {
         const bool live = i < n;
         const uint32_t ii = live ? i : 0u;
-        const float4 a = S.nodes[2 * ii], b = S.nodes[2 * ii + 1];
-        const uint32_t skip = (uint32_t)__float_as_int(a.w);
-        const int leaf = __float_as_int(b.w);
+        float4 a, b;
+        uint32_t skip;
+        int leaf;
+        lane_node(S, ii, a, b, skip, leaf);
         const bool hit = live & box_test(a, b, o, inv, tnear, h.t);
         const bool in_leaf = hit & (leaf >= 0);
         const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
@@ -242,10 +271,8 @@ __device__ __forceinline__ Hit closest_lane_skip(const DevScene& S, bool active,
 // 23.6 ms, 64-B records 23.8-25.1 ms, 32-B quantised records 31.3 ms -- the record walk halves the
 // dependent loads and the L1 misses but not the lane-loads, and the dequantisation VALU sits on the
 // walk's critical path.  Kept as a build option (-DRS_CREC=1/2), tested bit-identical.
-#ifndef RS_CREC
-#define RS_CREC 0
-#endif
-constexpr int kCrecWords = RS_CREC == 2 ? 2 : 4;     // float4 per record
+constexpr int kCrecWords = RS_CREC == 2 ? 2 : (RS_CREC == 3 ? 1 : 4);     // float4 per record
+#define RS_CREC_REC (RS_CREC == 1 || RS_CREC == 2)   // child-box record walks (3: half-precision nodes)
 struct CStack {
     uint32_t s[RS_CSTACK];
     int sp;
@@ -418,11 +445,11 @@ __device__ __forceinline__ Hit closest_crec(const DevScene& S, bool active, vec3
 }
 
 __device__ __forceinline__ bool occluded_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-    if (RS_CREC && S.n_crec) return occluded_crec(S, active, o, d, tnear, tfar);
+    if (RS_CREC_REC && S.n_crec) return occluded_crec(S, active, o, d, tnear, tfar);
     return occluded_lane_skip(S, active, o, d, tnear, tfar);
 }
 __device__ __forceinline__ Hit closest_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-    if (RS_CREC && S.n_crec) return closest_crec(S, active, o, d, tnear, tfar);
+    if (RS_CREC_REC && S.n_crec) return closest_crec(S, active, o, d, tnear, tfar);
     return closest_lane_skip(S, active, o, d, tnear, tfar);
 }
 
