@@ -1976,10 +1976,13 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
         Hit h; h.t = tf[i]; h.u = h.v = 0; h.prim = -1;
         while (cur < S.n_nodes && !occ) {
             const uint32_t k = cur;
-            const float4 a = S.nodes[2 * k], b = S.nodes[2 * k + 1];
+            float4 a, b;                       // the per-lane walks' node format (RS_CREC == 3: half nodes)
+            uint32_t skp;
+            int leaf;
+            lane_node(S, k, a, b, skp, leaf);
+            a.w = __uint_as_float(skp); b.w = __int_as_float(leaf);
             const float tmax = any == 5 ? tf[i] : h.t;
             ++visits;
-            const int leaf = __float_as_int(b.w);
             if (any == 4 && leaf >= 0 && box_test(a, b, O, inv, tn[i], tmax)) tris += (leaf & 7) + 1;
             if (any == 5) {
                 cur = (uint32_t)__float_as_int(a.w);

@@ -743,7 +743,8 @@ int bvh_crec_build(const float4* d_nodes, uint32_t n_nodes, uint32_t n_tris, hip
     *d_crec = nullptr; *d_cskip = nullptr; *d_rec_node = nullptr; *d_node2rec = nullptr; *n_rec = 0;
     if (!RS_CREC) return 0;                                          // walks use the float nodes
     if (RS_CREC == 3) {   // half nodes: one record per node, identity numbering (leaf words < 2^31)
-        if (n_nodes == 0 || n_tris >= (1u << 27)) return 0;
+        if (n_nodes == 0) return 0;
+        if (n_tris >= (1u << 27)) { err = "half nodes: more than 2^27 triangles"; return -1; }
         std::vector<int> id(n_nodes);
         for (uint32_t i = 0; i < n_nodes; ++i) id[i] = (int)i;
         if (hipMalloc(d_crec, (size_t)n_nodes * kCrecWords * sizeof(float4)) != hipSuccess ||

@@ -156,7 +156,7 @@ __device__ __forceinline__ float h2f(uint32_t bits) {
     return (float)__builtin_bit_cast(_Float16, (unsigned short)(bits & 0xffffu));
 }
 __device__ __forceinline__ void lane_node(const DevScene& S, uint32_t i, float4& a, float4& b, uint32_t& skip, int& leaf) {
-    if (RS_CREC == 3 && S.n_crec) {
+    if (RS_CREC == 3) {   // built for every non-empty tree (bvh_crec_build fails otherwise)
         const uint4 q = ((const uint4*)S.crec)[i];
         a = make_float4(h2f(q.x), h2f(q.x >> 16), h2f(q.y), 0.0f);
         b = make_float4(h2f(q.y >> 16), h2f(q.z), h2f(q.z >> 16), 0.0f);
@@ -168,6 +168,23 @@ __device__ __forceinline__ void lane_node(const DevScene& S, uint32_t i, float4&
         skip = (uint32_t)__float_as_int(a.w);
         leaf = __float_as_int(b.w);
     }
+}
+// RS_CREC == 3: a leaf whose half box was hit is re-tested against its exact float box before its
+// triangles are (the outward-rounded boxes of leaves next to a ray's origin surface would otherwise add
+// ~1.3 triangle tests per shadow ray on C3, which cost more than the halved node loads save)
+__device__ __forceinline__ bool leaf_exact(const DevScene& S, bool in_leaf, uint32_t i, vec3 o, vec3 inv, float tnear,
+                                           float tfar) {
+#if RS_CREC == 3 && !defined(RS_HALF_LOOSE_LEAVES)
+    if (__ballot(in_leaf) == 0) return false;
+    bool r = false;
+    if (in_leaf) {                        // only the lanes on a hit leaf load its exact box
+        const float4 a = S.nodes[2 * i], b = S.nodes[2 * i + 1];
+        r = box_test(a, b, o, inv, tnear, tfar);
+    }
+    return r;
+#else
+    return in_leaf;
+#endif
 }
 // Branch-lean per-lane walks: uniform loop condition, select-based cursor updates, the leaf's
 // triangles in a wave-uniform loop up to the largest leaf among the lanes -- no per-lane exec-mask
@@ -185,7 +202,7 @@ __device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i
         int leaf;
         lane_node(S, ii, a, b, skip, leaf);
         const bool hit = live & box_test(a, b, o, inv, tnear, tfar);
-        const bool in_leaf = hit & (leaf >= 0);
+        const bool in_leaf = leaf_exact(S, hit & (leaf >= 0), ii, o, inv, tnear, tfar);
         const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
         for (int j = 0; j < 8; ++j) {
             const bool want = (j < cnt) & (occ == 0u);
@@ -214,7 +231,7 @@ __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i,
         int leaf;
         lane_node(S, ii, a, b, skip, leaf);
         const bool hit = live & box_test(a, b, o, inv, tnear, h.t);
-        const bool in_leaf = hit & (leaf >= 0);
+        const bool in_leaf = leaf_exact(S, hit & (leaf >= 0), ii, o, inv, tnear, h.t);
         const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
         for (int j = 0; j < 8; ++j) {
             const bool want = j < cnt;
@@ -236,6 +253,68 @@ __device__ __forceinline__ Hit closest_lane_skip(const DevScene& S, bool active,
     Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
     closest_lane_from(S, active ? 0u : 0xffffffffu, o, d, inv, tnear, h);
     return h;
+}
+
+// K any-hit rays of one lane sharing an origin (a pixel's area-candidate pair), one per-lane walk over
+// the union of their skip-pointer paths: each step fetches the lane's smallest cursor once and tests
+// every ray whose cursor is on it, so the paths' common prefix (the top of the tree) is fetched once
+// instead of K times.  Each ray's cursor sequence is its own walk's -- the same box and triangle tests,
+// bit-identical results.  RS_LANE_UNION=0: the K walks one after the other.
+#ifndef RS_LANE_UNION
+#define RS_LANE_UNION 0
+#endif
+template <int K>
+__device__ __forceinline__ void occluded_lane_union(const DevScene& S, const bool* active, vec3 o, const vec3* d,
+                                                    float tnear, const float* tfar, bool* occ) {
+    constexpr uint32_t kDone = 0xffffffffu;
+    vec3 inv[K];
+    uint32_t cur[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        inv[k] = mk(1.0f / d[k].x, 1.0f / d[k].y, 1.0f / d[k].z);
+        cur[k] = active[k] ? 0u : kDone;
+    }
+    const uint32_t n = S.n_nodes;
+    uint32_t occb = 0u;
+    uint32_t m = cur[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) m = cur[k] < m ? cur[k] : m;
+    while (__ballot(m < n) != 0) {
+        const bool live = m < n;
+        const uint32_t ii = live ? m : 0u;
+        float4 a, b;
+        uint32_t skip;
+        int leaf;
+        lane_node(S, ii, a, b, skip, leaf);
+        uint32_t hbb = 0u;
+#pragma unroll
+        for (int k = 0; k < K; ++k) hbb |= (live & (cur[k] == m) && box_test(a, b, o, inv[k], tnear, tfar[k])) ? (1u << k) : 0u;
+        const int first = leaf >> 3, cnt = (leaf >= 0) & (hbb != 0u) ? (leaf & 7) + 1 : 0;
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t want = j < cnt ? hbb & ~occb : 0u;
+            if (__ballot(want != 0u) == 0) break;
+            const float4* T = S.tris + 3 * (want ? first + j : 0);
+            const float4 T0 = T[0], T1 = T[1], T2 = T[2];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (__ballot((want >> k) & 1u) != 0) {
+                    float t, u, v;
+                    const bool h = tri_test_nb(T0, T1, T2, o, d[k], tnear, tfar[k], t, u, v);
+                    occb |= (((want >> k) & 1u) && h) ? (1u << k) : 0u;
+                }
+            }
+        }
+        uint32_t nm = kDone;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t nx = ((occb >> k) & 1u) ? kDone : ((((hbb >> k) & 1u) && leaf < 0) ? m + 1u : skip);
+            cur[k] = (live & (cur[k] == m)) ? nx : cur[k];
+            nm = cur[k] < nm ? cur[k] : nm;
+        }
+        m = nm;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) occ[k] = (occb >> k) & 1u;
 }
 
 // ---------------------------------------------------------------- child-box walks (TRAV_LANE)
@@ -645,6 +724,8 @@ __device__ __forceinline__ void trace_any_multi(const DevScene& S, const bool* a
                                                 float tnear, const float* tfar, bool* occ) {
     if (T == TRAV_LOCKSTEP) {
         occluded_wave_multi<K>(S, active, o, d, tnear, tfar, occ);
+    } else if (RS_LANE_UNION && !(RS_CREC_REC && S.n_crec)) {
+        occluded_lane_union<K>(S, active, o, d, tnear, tfar, occ);
     } else {   // one walk after the other (measured faster than interleaving the K walks, and than one
                // loop running a lane's walks back to back: that spilled the hot loop, 2.5x slower on C3)
 #pragma unroll
