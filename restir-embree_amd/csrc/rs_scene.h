@@ -186,6 +186,20 @@ __device__ __forceinline__ bool leaf_exact(const DevScene& S, bool in_leaf, uint
     return in_leaf;
 #endif
 }
+// RS_LANE_LOOKAHEAD=1: the walk carries node i + 1 beside node i.  The next node is i + 1 after every
+// entered interior node and after every leaf (a leaf's skip is i + 1 in the preorder), so those steps
+// start without waiting on a dependent load; the load of the new i + 1 (and, after a miss, of the skip
+// target) is issued at the end of each step.  Same nodes visited in the same order: bit-identical.
+#ifndef RS_LANE_LOOKAHEAD
+#define RS_LANE_LOOKAHEAD 0
+#endif
+#define RS_LA (RS_LANE_LOOKAHEAD && RS_CREC == 0)
+__device__ __forceinline__ void la_advance(const DevScene& S, bool next_is_ahead, uint32_t nx, uint32_t n, float4& ca,
+                                           float4& cb, float4& na, float4& nb) {
+    if (next_is_ahead) { ca = na; cb = nb; }
+    else if (nx < n) { ca = S.nodes[2 * nx]; cb = S.nodes[2 * nx + 1]; }
+    if (nx < n - 1u) { na = S.nodes[2 * nx + 2]; nb = S.nodes[2 * nx + 3]; }
+}
 // Branch-lean per-lane walks: uniform loop condition, select-based cursor updates, the leaf's
 // triangles in a wave-uniform loop up to the largest leaf among the lanes -- no per-lane exec-mask
 // regions (C3: +21 % over the branchy loop).
@@ -194,13 +208,23 @@ __device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i
                                                    float tfar) {
     const uint32_t n = S.n_nodes;
     uint32_t occ = 0u;
+#if RS_LA
+    float4 ca = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cb = ca, na = ca, nb = ca;
+    la_advance(S, false, i, n, ca, cb, na, nb);
+#endif
     while (__ballot(i < n) != 0) {
         const bool live = i < n;
         const uint32_t ii = live ? i : 0u;
+#if RS_LA
+        const float4 a = ca, b = cb;
+        const uint32_t skip = (uint32_t)__float_as_int(a.w);
+        const int leaf = __float_as_int(b.w);
+#else
         float4 a, b;
         uint32_t skip;
         int leaf;
         lane_node(S, ii, a, b, skip, leaf);
+#endif
         const bool hit = live & box_test(a, b, o, inv, tnear, tfar);
         const bool in_leaf = leaf_exact(S, hit & (leaf >= 0), ii, o, inv, tnear, tfar);
         const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
@@ -212,7 +236,11 @@ __device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i
             const bool h = tri_test_nb(T[0], T[1], T[2], o, d, tnear, tfar, t, u, v);
             occ = (want & h) ? 1u : occ;
         }
-        i = !live ? i : (occ ? 0xffffffffu : ((hit & (leaf < 0)) ? i + 1 : skip));
+        const uint32_t nx = !live ? i : (occ ? 0xffffffffu : ((hit & (leaf < 0)) ? i + 1 : skip));
+#if RS_LA
+        la_advance(S, live & (nx == i + 1u), nx, n, ca, cb, na, nb);
+#endif
+        i = nx;
     }
     return occ != 0u;
 }
@@ -223,13 +251,23 @@ __device__ __forceinline__ bool occluded_lane_skip(const DevScene& S, bool activ
 __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i, vec3 o, vec3 d, vec3 inv, float tnear,
                                                   Hit& h) {
     const uint32_t n = S.n_nodes;
+#if RS_LA
+    float4 ca = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cb = ca, na = ca, nb = ca;
+    la_advance(S, false, i, n, ca, cb, na, nb);
+#endif
     while (__ballot(i < n) != 0) {
         const bool live = i < n;
         const uint32_t ii = live ? i : 0u;
+#if RS_LA
+        const float4 a = ca, b = cb;
+        const uint32_t skip = (uint32_t)__float_as_int(a.w);
+        const int leaf = __float_as_int(b.w);
+#else
         float4 a, b;
         uint32_t skip;
         int leaf;
         lane_node(S, ii, a, b, skip, leaf);
+#endif
         const bool hit = live & box_test(a, b, o, inv, tnear, h.t);
         const bool in_leaf = leaf_exact(S, hit & (leaf >= 0), ii, o, inv, tnear, h.t);
         const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
@@ -245,7 +283,11 @@ __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i,
             h.t = better ? t : h.t; h.u = better ? u : h.u; h.v = better ? v : h.v;
             h.prim = better ? prim : h.prim;
         }
-        i = !live ? i : ((hit & (leaf < 0)) ? i + 1 : skip);
+        const uint32_t nx = !live ? i : ((hit & (leaf < 0)) ? i + 1 : skip);
+#if RS_LA
+        la_advance(S, live & (nx == i + 1u), nx, n, ca, cb, na, nb);
+#endif
+        i = nx;
     }
 }
 __device__ __forceinline__ Hit closest_lane_skip(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
