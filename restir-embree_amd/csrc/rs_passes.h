@@ -47,7 +47,8 @@
 #define RS_TEMPORAL_WAVES_LANE RS_TEMPORAL_WAVES
 #endif
 #define RS_WAVES(T, lockstep, lane) ((T) == TRAV_LANE ? (lane) : (lockstep))
-// area candidates whose shadow rays share one lockstep traversal (occluded_wave_multi)
+// area candidates whose shadow rays share one lockstep traversal (occluded_wave_multi); 4 measured on
+// C2 1080p: 694-698 frames/s at a 4-wave budget (700-704 with 2), 560 at 5 waves (register spills)
 #ifndef RS_RIS_BATCH
 #define RS_RIS_BATCH 2
 #endif
