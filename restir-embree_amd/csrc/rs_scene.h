@@ -244,8 +244,52 @@ __device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i
     }
     return occ != 0u;
 }
+// RS_LANE_DEFER=k: deferred leaves for the any-hit per-lane walk (Aila & Laine's while-while idea): a lane
+// whose walk reaches a hit leaf parks there, the others keep stepping through interior nodes, and the
+// wave tests the parked lanes' triangles together once >= k lanes are parked (or no lane can step) --
+// the wave-wide triangle loop runs for many lanes at once instead of at almost every step.  Every ray
+// still makes its own tests in its own order: bit-identical.
+#ifndef RS_LANE_DEFER
+#define RS_LANE_DEFER 0
+#endif
+__device__ __forceinline__ bool occluded_lane_defer(const DevScene& S, uint32_t i, vec3 o, vec3 d, vec3 inv, float tnear,
+                                                    float tfar) {
+    const uint32_t n = S.n_nodes;
+    uint32_t occ = 0u, parked = 0u, pskip = 0u;
+    int pleaf = 0;
+    while (__ballot(i < n) != 0) {
+        const bool step = (i < n) & (parked == 0u);
+        const uint32_t ii = step ? i : 0u;
+        const float4 a = S.nodes[2 * ii], b = S.nodes[2 * ii + 1];
+        const uint32_t skip = (uint32_t)__float_as_int(a.w);
+        const int leaf = __float_as_int(b.w);
+        const bool hit = step & box_test(a, b, o, inv, tnear, tfar);
+        const bool to_leaf = hit & (leaf >= 0);
+        i = (step & !to_leaf) ? (hit ? i + 1 : skip) : i;
+        parked = to_leaf ? 1u : parked;
+        pleaf = to_leaf ? leaf : pleaf;
+        pskip = to_leaf ? skip : pskip;
+        const uint64_t pk = __ballot(parked != 0u);
+        if (__popcll(pk) >= RS_LANE_DEFER || (pk != 0 && __ballot((i < n) & (parked == 0u)) == 0)) {   // wave-uniform
+            const int first = pleaf >> 3, cnt = parked ? (pleaf & 7) + 1 : 0;
+            for (int j = 0; j < 8; ++j) {
+                const bool want = (j < cnt) & (occ == 0u);
+                if (__ballot(want) == 0) break;
+                const float4* T = S.tris + 3 * (want ? first + j : 0);
+                float t, u, v;
+                const bool h = tri_test_nb(T[0], T[1], T[2], o, d, tnear, tfar, t, u, v);
+                occ = (want & h) ? 1u : occ;
+            }
+            i = parked ? (occ ? 0xffffffffu : pskip) : i;
+            parked = 0u;
+        }
+    }
+    return occ != 0u;
+}
 __device__ __forceinline__ bool occluded_lane_skip(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    if (RS_LANE_DEFER > 0 && RS_CREC == 0)
+        return occluded_lane_defer(S, active ? 0u : 0xffffffffu, o, d, inv, tnear, tfar);
     return occluded_lane_from(S, active ? 0u : 0xffffffffu, o, d, inv, tnear, tfar);
 }
 __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i, vec3 o, vec3 d, vec3 inv, float tnear,
