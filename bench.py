@@ -387,6 +387,7 @@ def run_multi(args, world, rank, local, W, H):
     torch.cuda.synchronize()
     dist.barrier()
     r.timing_totals(reset=True)
+    m.stats(reset=True)
     t0 = time.perf_counter()
     for f in range(args.steps):
         step(args.warmup + f)
@@ -394,17 +395,31 @@ def run_multi(args, world, rank, local, W, H):
     torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
-    tot, _ = r.timing_totals()
+    tot, n_timed = r.timing_totals()
+    xs = m.stats()
     red = torch.tensor([dt, float(tot.rays), float(tot.reproj_outside)], dtype=torch.float64)
     dmax = red[:1].clone()
     dist.all_reduce(dmax, op=dist.ReduceOp.MAX)
     sums = red[1:].clone()
     dist.all_reduce(sums, op=dist.ReduceOp.SUM)
     dt, rays, outside = float(dmax[0]), int(sums[0]), int(sums[1])
+    # per rank: band kernel time per frame (pass events), halo bytes and exchange / gather time per frame
+    nf = max(1, xs["frames"])
+    mine = [float(tot.total_ms) / max(1, n_timed), xs["halo_bytes_sent"] / nf, xs["halo_bytes_recv"] / nf,
+            xs["halo_ms"] / nf, xs["gather_ms"] / nf, xs["gather_bytes"] / nf]
+    per_rank = [None] * world
+    dist.all_gather_object(per_rank, mine)
     _, last_kind, _ = r.traversal(gs)
     if rank == 0:
-        print(json.dumps(multi_line(args, world, W, H, prm, dt, rays, outside, bands, last_kind,
-                                    "rs_mgpu (C ABI): RCCL point-to-point halo + gather")), flush=True)
+        line = multi_line(args, world, W, H, prm, dt, rays, outside, bands, last_kind,
+                          "rs_mgpu (C ABI): RCCL point-to-point halo + gather")
+        line["per_rank"] = [{"rank": q, "band_rows": bands[q][1] - bands[q][0], "band_ms": round(v[0], 4),
+                             "halo_bytes_sent": int(v[1]), "halo_bytes_recv": int(v[2]), "halo_ms": round(v[3], 4),
+                             "gather_ms": round(v[4], 4), "gather_bytes_recv": int(v[5])}
+                            for q, v in enumerate(per_rank)]
+        line["per_rank_note"] = ("per frame; band_ms = the rank's pass kernels (HIP events, frames overlap); halo_ms / "
+                                 "gather_ms = HIP-event span of the RCCL group on the frame's stream incl. waiting for peers")
+        print(json.dumps(line), flush=True)
     dist.barrier()
     m.close()
     dist.destroy_process_group()

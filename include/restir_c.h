@@ -393,6 +393,16 @@ int rs_mgpu_reset_history(rs_mgpu* m);
 /* host values summed (op 0) or maxed (op 1) over all ranks in place (RCCL all-reduce; synchronous) --
  * for the caller's timing / statistics, not on the frame's data path */
 int rs_mgpu_allreduce(rs_mgpu* m, double* values, int n, int op);
+/* Transfer statistics of this process's ranks since creation / the last reset (synchronous: waits for
+ * every frame enqueued).  Times are HIP-event spans on the frame's stream of the first local rank: a
+ * halo exchange (each spatial pass, first 4 timed) and the gather, including any wait for the peer. */
+typedef struct rs_mgpu_stats {
+    uint64_t frames;
+    uint64_t halo_bytes_sent, halo_bytes_recv;   /* reservoir halo rows, all local ranks */
+    uint64_t gather_bytes;                       /* framebuffer rows received by rank 0 */
+    double halo_ms, gather_ms;
+} rs_mgpu_stats;
+int rs_mgpu_get_stats(rs_mgpu* m, rs_mgpu_stats* out, int reset);
 
 /* ---- test hook: raw BVH queries (rtcIntersect1 / rtcOccluded1 semantics) ----------------------
  * n rays, host arrays o[3n], d[3n], tnear[n], tfar[n].  any_hit=0: closest hit -> t_out[n] (-1 on miss),

@@ -28,10 +28,6 @@ int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int*
                    std::vector<int>& lvl_off, std::string& err);
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
               const std::vector<int>& lvl_off, hipStream_t st, int* tail, std::string& err);
-int bvh_crec_build(const float4* d_nodes, uint32_t n_nodes, uint32_t n_tris, hipStream_t st, float4** d_crec,
-                   uint32_t** d_cskip, int** d_rec_node, int** d_node2rec, uint32_t* n_rec, std::string& err);
-int bvh_crec_emit(const float4* d_nodes, const int* d_rec_node, const int* d_node2rec, uint32_t n_rec, float4* d_crec,
-                  uint32_t* d_cskip, hipStream_t st);
 }
 
 using namespace rs;
@@ -54,11 +50,6 @@ struct rs_scene {
     int* d_emis_tri = nullptr;
     int *d_refit_order = nullptr, *d_refit_lvl = nullptr;
     std::vector<int> refit_lvl;
-    // child-box records of the interior nodes (rs_scene.h), re-emitted after every refit
-    float4* d_crec = nullptr;
-    uint32_t* d_cskip = nullptr;
-    int *d_crec_node = nullptr, *d_node2rec = nullptr;
-    uint32_t n_crec = 0;
     float* h_stage[2] = {nullptr, nullptr};
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     int stage_i = 0;
@@ -88,7 +79,6 @@ struct rs_scene {
         S.nodes = d_nodes; S.tris = d_tris; S.tri_nrm = d_tri_nrm; S.mats = d_mats; S.emis = d_emis; S.cdf = d_cdf; S.cdf_guide = d_cdf_guide;
         S.n_nodes = n_nodes; S.n_tris = n_tris; S.n_emis = n_emis; S.n_mats = n_mats;
         S.tri_uv = d_uv; S.tri_tan = d_tan; S.tex = d_tex; S.texd = d_texd; S.sky = sky;
-        S.crec = d_crec; S.cskip = d_cskip; S.n_crec = n_crec;
         return S;
     }
 };
@@ -368,9 +358,10 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->split_mode = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->split_mode = RS_SPLIT_OFF;
     }
-    if (const char* t = std::getenv("RESTIR_QUEUE")) {         // auto (default) | on | off
+    if (const char* t = std::getenv("RESTIR_QUEUE")) {         // off (default: measured slower) | on | auto
         if (!std::strcmp(t, "on")) c->queue_mode = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->queue_mode = RS_SPLIT_OFF;
+        else if (!std::strcmp(t, "auto")) c->queue_mode = RS_SPLIT_AUTO;
     }
     if (const char* t = std::getenv("RESTIR_TILE_ORDER"))      // cost (default) | off (row-major)
         c->order_on = std::strcmp(t, "off") != 0;
@@ -748,11 +739,10 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
         s->update_recorded = false;
     }
     void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide, s->d_emis_tri,
-                   s->d_refit_order, s->d_refit_lvl, s->d_crec, s->d_cskip, s->d_crec_node, s->d_node2rec};
+                   s->d_refit_order, s->d_refit_lvl};
     for (void* p : old) if (p) hipFree(p);
     s->d_pos = nullptr; s->d_nodes = nullptr; s->d_tris = nullptr; s->d_emis = nullptr; s->d_cdf = nullptr;
     s->d_cdf_guide = nullptr; s->d_emis_tri = nullptr; s->d_refit_order = nullptr; s->d_refit_lvl = nullptr;
-    s->d_crec = nullptr; s->d_cskip = nullptr; s->d_crec_node = nullptr; s->d_node2rec = nullptr; s->n_crec = 0;
     s->n_nodes = 0; s->refit_lvl.clear();
     s->n_emis = ne;
     if (n) {
@@ -780,10 +770,6 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     else { err = "BVH build failed: " + berr; rc = -1; }
     hipEventDestroy(e0); hipEventDestroy(e1);
     if (rc == 0 && bvh_refit_plan(s->d_nodes, s->n_nodes, st, &s->d_refit_order, &s->d_refit_lvl, s->refit_lvl, berr) != 0) {
-        err = berr; rc = -1;
-    }
-    if (rc == 0 && bvh_crec_build(s->d_nodes, s->n_nodes, n, st, &s->d_crec, &s->d_cskip, &s->d_crec_node,
-                                  &s->d_node2rec, &s->n_crec, berr) != 0) {
         err = berr; rc = -1;
     }
     return rc;
@@ -921,9 +907,9 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
     HIPCHK(c, enter(c));
     const size_t nf = 9 * (size_t)s->n_tris;
     if (nf == 0) return RS_OK;
-    // frames in flight and positions only (no normals, no child-box records): pipelined into the other
+    // frames in flight and positions only (no normals): pipelined into the other
     // scene copy; otherwise in place after every enqueued frame (the next frame joins the context stream)
-    const bool pipelined = c->ahead > 0 && !normals && s->n_crec == 0;
+    const bool pipelined = c->ahead > 0 && !normals;
     const int L = c->ahead > 0 ? (int)(c->seq % (uint64_t)(c->ahead + 1)) : 0;
     hipStream_t st = pipelined ? c->lane[L] : c->stream;
     const int k = s->stage_i;
@@ -981,8 +967,6 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
     RefitArgs R{nodes, tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, tail[0], tail[1]};
     k_scene_update<<<2, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, em, cdf, guide, R);
     HIPCHK(c, hipGetLastError());
-    if (bvh_crec_emit(s->d_nodes, s->d_crec_node, s->d_node2rec, s->n_crec, s->d_crec, s->d_cskip, st) != 0)
-        return fail(c, RS_E_HIP, "rs_scene_update_positions: child-record emit failed");
     HIPCHK(c, hipEventRecord(s->update_ev, st));
     s->update_recorded = true;
     if (pipelined) {                             // later frames read the new copy
@@ -1123,7 +1107,7 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     if (s->ctx) sync_all(s->ctx);
     void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
                     s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage, s->d_tex, s->d_texd, s->d_uv,
-                    s->d_tan, s->d_crec, s->d_cskip, s->d_crec_node, s->d_node2rec, s->a_nodes, s->a_tris, s->a_emis,
+                    s->d_tan, s->a_nodes, s->a_tris, s->a_emis,
                     s->a_cdf, s->a_cdf_guide};
     for (void* p : ptrs) if (p) hipFree(p);
     for (int k = 0; k < 2; ++k) {
@@ -1976,11 +1960,8 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
         Hit h; h.t = tf[i]; h.u = h.v = 0; h.prim = -1;
         while (cur < S.n_nodes && !occ) {
             const uint32_t k = cur;
-            float4 a, b;                       // the per-lane walks' node format (RS_CREC == 3: half nodes)
-            uint32_t skp;
-            int leaf;
-            lane_node(S, k, a, b, skp, leaf);
-            a.w = __uint_as_float(skp); b.w = __int_as_float(leaf);
+            const float4 a = S.nodes[2 * k], b = S.nodes[2 * k + 1];
+            const int leaf = __float_as_int(b.w);
             const float tmax = any == 5 ? tf[i] : h.t;
             ++visits;
             if (any == 4 && leaf >= 0 && box_test(a, b, O, inv, tn[i], tmax)) tris += (leaf & 7) + 1;

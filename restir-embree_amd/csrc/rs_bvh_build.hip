@@ -25,7 +25,6 @@
 #include <cstring>
 #include <algorithm>
 #include "rs_refit.h"
-#include "rs_scene.h"     // child-box record format (RS_CREC, crec_deq)
 
 namespace rs {
 
@@ -620,183 +619,6 @@ int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_
     }
     if (hipGetLastError() != hipSuccess) { err = "refit launch failed"; return -1; }
     return 0;
-}
-
-// ---------------------------------------------------------------- child-box records (rs_scene.h)
-// record r of interior node i = rec_node[r]: its children L = i + 1 and R = skip(L) (boxes + links) and
-// skip(i) (cskip, the overflow fallback of the walks)
-#if RS_CREC == 2
-// outward 8-bit quantisation against the walk's own dequantisation expression (crec_deq)
-__device__ __forceinline__ uint32_t crec_q_lo(float o, float s, float lo) {
-    float f = floorf((lo - o) / s);
-    f = f < 0.0f ? 0.0f : (f > 255.0f ? 255.0f : f);
-    uint32_t q = (uint32_t)f;
-    while (q > 0u && crec_deq(o, q, s) > lo) --q;
-    return q;                                       // q == 0: o <= lo (o is the minimum of the children)
-}
-__device__ __forceinline__ bool crec_q_hi(float o, float s, float hi, uint32_t& q) {
-    float f = ceilf((hi - o) / s);
-    f = f < 0.0f ? 0.0f : (f > 255.0f ? 255.0f : f);
-    q = (uint32_t)f;
-    while (q < 255u && crec_deq(o, q, s) < hi) ++q;
-    return crec_deq(o, q, s) >= hi;
-}
-__device__ __forceinline__ uint32_t crec_link(const float4* nodes, const int* node2rec, int c) {
-    const int w = __float_as_int(nodes[2 * c + 1].w);
-    return w >= 0 ? (1u << 27) | (uint32_t)w : (uint32_t)node2rec[c];   // leaf word = first << 3 | count - 1
-}
-#endif
-#if RS_CREC == 3
-// binary16 bits of x rounded toward -inf (up = false) or +inf (up = true): the RNE conversion, then one
-// ulp outward when it rounded inward (overflow goes to +-inf, which stays conservative)
-__device__ __forceinline__ uint32_t f2h_out(float x, bool up) {
-    const _Float16 h = (_Float16)x;
-    const float back = (float)h;
-    uint32_t u = __builtin_bit_cast(unsigned short, h);
-    if (x == x && (up ? back < x : back > x)) {
-        const bool neg = (u & 0x8000u) != 0u;
-        if (up) u = neg ? (u == 0x8000u ? 0x0001u : u - 1u) : u + 1u;
-        else    u = neg ? u + 1u : (u == 0u ? 0x8001u : u - 1u);
-    }
-    return u;
-}
-#endif
-__global__ void k_crec_emit(const float4* __restrict__ nodes, const int* __restrict__ rec_node,
-                            const int* __restrict__ node2rec, uint32_t n_rec, float4* crec, uint32_t* cskip) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_rec) return;
-#if RS_CREC == 3
-    {   // half node r (records = nodes); a non-finite coordinate widens to the infinite box
-        const float4 a = nodes[2 * r], b = nodes[2 * r + 1];
-        const int lw = __float_as_int(b.w);
-        auto lo = [](float v) { return v == v ? f2h_out(v, false) : 0xfc00u; };
-        auto hi = [](float v) { return v == v ? f2h_out(v, true) : 0x7c00u; };
-        uint4 q;
-        q.x = lo(a.x) | (lo(a.y) << 16);
-        q.y = lo(a.z) | (hi(b.x) << 16);
-        q.z = hi(b.y) | (hi(b.z) << 16);
-        q.w = lw >= 0 ? (0x80000000u | (uint32_t)lw) : __float_as_uint(a.w);
-        ((uint4*)crec)[r] = q;
-        cskip[r] = __float_as_uint(a.w);
-        return;
-    }
-#endif
-#if RS_CREC != 3
-    const int i = rec_node[r], L = i + 1;
-    const float4 aL = nodes[2 * L], bL = nodes[2 * L + 1];
-    const int R = __float_as_int(aL.w);
-    const float4 aR = nodes[2 * R], bR = nodes[2 * R + 1];
-    cskip[r] = __float_as_uint(nodes[2 * i].w);
-#if RS_CREC == 2
-    const float lo[2][3] = {{aL.x, aL.y, aL.z}, {aR.x, aR.y, aR.z}}, hi[2][3] = {{bL.x, bL.y, bL.z}, {bR.x, bR.y, bR.z}};
-    float o[3], ext = 0.0f;
-    bool finite = true;
-    for (int a = 0; a < 3; ++a) {
-        o[a] = fminf(lo[0][a], lo[1][a]);
-        const float top = fmaxf(hi[0][a], hi[1][a]);
-        finite = finite && isfinite(o[a]) && isfinite(top) && isfinite(lo[0][a]) && isfinite(lo[1][a]) &&
-                 isfinite(hi[0][a]) && isfinite(hi[1][a]);
-        ext = fmaxf(ext, top - o[a]);
-    }
-    uint32_t q[2][2][3] = {};                        // [child][lo/hi][axis]
-    uint32_t eb = 0u;                                // 0: not quantised, the walk enters both children
-    if (finite && isfinite(ext)) {
-        int k = -126;
-        if (ext > 0.0f) { frexpf(ext / 255.0f, &k); }   // ext / 255 < 2^k
-        for (int e = (k < -126 ? -126 : k); e <= 127 && !eb; ++e) {
-            const float s = __uint_as_float((uint32_t)(e + 127) << 23);
-            bool ok = true;
-            for (int c = 0; c < 2; ++c)
-                for (int a = 0; a < 3; ++a) {
-                    q[c][0][a] = crec_q_lo(o[a], s, lo[c][a]);
-                    ok = ok && crec_q_hi(o[a], s, hi[c][a], q[c][1][a]);
-                }
-            if (ok) eb = (uint32_t)(e + 127);
-        }
-    }
-    const uint32_t lL = crec_link(nodes, node2rec, L), lR = crec_link(nodes, node2rec, R);
-    uint4 w0, w1;
-    w0.x = __float_as_uint(o[0]); w0.y = __float_as_uint(o[1]); w0.z = __float_as_uint(o[2]);
-    w0.w = eb | (q[0][0][0] << 8) | (q[0][0][1] << 16) | (q[0][0][2] << 24);
-    w1.x = q[0][1][0] | (q[0][1][1] << 8) | (q[0][1][2] << 16) | (q[1][0][0] << 24);
-    w1.y = q[1][0][1] | (q[1][0][2] << 8) | (q[1][1][0] << 16) | (q[1][1][1] << 24);
-    w1.z = q[1][1][2] | ((lL & 0xffffffu) << 8);
-    w1.w = (lL >> 24) | (lR << 4);
-    uint4* out = (uint4*)crec + 2 * (size_t)r;
-    out[0] = w0; out[1] = w1;
-#else
-    const int wL = __float_as_int(bL.w), wR = __float_as_int(bR.w);
-    const int lL = wL >= 0 ? ~wL : node2rec[L], lR = wR >= 0 ? ~wR : node2rec[R];
-    crec[4 * r + 0] = make_float4(aL.x, aL.y, aL.z, __int_as_float(lL));
-    crec[4 * r + 1] = make_float4(bL.x, bL.y, bL.z, __int_as_float(lR));
-    crec[4 * r + 2] = make_float4(aR.x, aR.y, aR.z, nodes[2 * i].w);
-    crec[4 * r + 3] = make_float4(bR.x, bR.y, bR.z, 0.0f);
-#endif
-#endif
-}
-
-// Record numbering (host, once per topology): interior nodes in preorder.  Checks that the tree is
-// binary (skip(R) == skip(i)) and fits the link fields; otherwise, or for a single-leaf tree, no records
-// (*n_rec = 0: the walks use the skip pointers).
-int bvh_crec_build(const float4* d_nodes, uint32_t n_nodes, uint32_t n_tris, hipStream_t st, float4** d_crec,
-                   uint32_t** d_cskip, int** d_rec_node, int** d_node2rec, uint32_t* n_rec, std::string& err) {
-    *d_crec = nullptr; *d_cskip = nullptr; *d_rec_node = nullptr; *d_node2rec = nullptr; *n_rec = 0;
-    if (!RS_CREC) return 0;                                          // walks use the float nodes
-    if (RS_CREC == 3) {   // half nodes: one record per node, identity numbering (leaf words < 2^31)
-        if (n_nodes == 0) return 0;
-        if (n_tris >= (1u << 27)) { err = "half nodes: more than 2^27 triangles"; return -1; }
-        std::vector<int> id(n_nodes);
-        for (uint32_t i = 0; i < n_nodes; ++i) id[i] = (int)i;
-        if (hipMalloc(d_crec, (size_t)n_nodes * kCrecWords * sizeof(float4)) != hipSuccess ||
-            hipMalloc(d_cskip, n_nodes * sizeof(uint32_t)) != hipSuccess ||
-            hipMalloc(d_rec_node, n_nodes * sizeof(int)) != hipSuccess ||
-            hipMalloc(d_node2rec, (size_t)n_nodes * sizeof(int)) != hipSuccess) { err = "half nodes: hipMalloc failed"; return -1; }
-        if (hipMemcpyAsync(*d_rec_node, id.data(), n_nodes * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
-            hipMemcpyAsync(*d_node2rec, id.data(), n_nodes * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
-            err = "half nodes: upload failed"; return -1;
-        }
-        k_crec_emit<<<(n_nodes + 255) / 256, 256, 0, st>>>(d_nodes, *d_rec_node, *d_node2rec, n_nodes, *d_crec, *d_cskip);
-        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) { err = "half nodes: emit failed"; return -1; }
-        *n_rec = n_nodes;
-        return 0;
-    }
-    if (n_nodes < 3 || n_tris >= (1u << 24)) return 0;   // walks use the skip pointers
-    std::vector<float4> h(2 * (size_t)n_nodes);
-    if (hipMemcpyAsync(h.data(), d_nodes, h.size() * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) { err = "child records: node download failed"; return -1; }
-    auto skip = [&](uint32_t i) { int v; std::memcpy(&v, &h[2 * i].w, 4); return v; };
-    auto leaf = [&](uint32_t i) { int v; std::memcpy(&v, &h[2 * i + 1].w, 4); return v; };
-    std::vector<int> rec_node, node2rec(n_nodes, -1);
-    for (uint32_t i = 0; i < n_nodes; ++i) {
-        if (leaf(i) >= 0) continue;
-        const int L = (int)i + 1;
-        if (L >= (int)n_nodes) return 0;
-        const int R = skip((uint32_t)L);
-        if (R <= L || R >= (int)n_nodes || skip((uint32_t)R) != skip(i)) return 0;   // not binary: no records
-        node2rec[i] = (int)rec_node.size();
-        rec_node.push_back((int)i);
-    }
-    const uint32_t nr = (uint32_t)rec_node.size();
-    if (nr >= (1u << 27)) return 0;
-    if (hipMalloc(d_crec, (size_t)nr * kCrecWords * sizeof(float4)) != hipSuccess ||
-        hipMalloc(d_cskip, nr * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(d_rec_node, nr * sizeof(int)) != hipSuccess ||
-        hipMalloc(d_node2rec, (size_t)n_nodes * sizeof(int)) != hipSuccess) { err = "child records: hipMalloc failed"; return -1; }
-    if (hipMemcpyAsync(*d_rec_node, rec_node.data(), nr * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(*d_node2rec, node2rec.data(), (size_t)n_nodes * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
-        err = "child records: upload failed"; return -1;
-    }
-    k_crec_emit<<<(nr + 255) / 256, 256, 0, st>>>(d_nodes, *d_rec_node, *d_node2rec, nr, *d_crec, *d_cskip);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) { err = "child records: emit failed"; return -1; }
-    *n_rec = nr;
-    return 0;
-}
-// stream-ordered re-emission after a refit (same topology)
-int bvh_crec_emit(const float4* d_nodes, const int* d_rec_node, const int* d_node2rec, uint32_t n_rec, float4* d_crec,
-                  uint32_t* d_cskip, hipStream_t st) {
-    if (!n_rec) return 0;
-    k_crec_emit<<<(n_rec + 255) / 256, 256, 0, st>>>(d_nodes, d_rec_node, d_node2rec, n_rec, d_crec, d_cskip);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // builder selection: PLOC by default; RESTIR_BVH=lbvh selects the Karras LBVH (kept for comparison)

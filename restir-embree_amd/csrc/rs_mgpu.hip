@@ -54,8 +54,13 @@ struct GpuRank {
     int finish() { return rs_tile_finish(ctx, &band, times); }
     void* halo(int which, size_t* bytes) {
         void* p = nullptr;
+        *bytes = 0;
         if (rs_tile_halo_ptr(ctx, which, &p, bytes) != RS_OK) return nullptr;
         return p;
+    }
+    // the full-frame framebuffer the band was rendered into (rows at their place)
+    char* frame_base() {
+        return band ? (char*)const_cast<float*>(band) - (size_t)y0 * ctx_width(ctx) * 3 * sizeof(float) : nullptr;
     }
 };
 
@@ -91,83 +96,132 @@ struct rs_mgpu {
         return ctx_fail(ranks.empty() ? nullptr : ranks[0].ctx, code, "rs_mgpu: " + m);
     }
 
-    // ---- halo exchange (the Comm interface of rs::mgpu::render_frame)
-    int exchange_halo(std::vector<GpuRank*>& rk, int pass) {
-        (void)pass;
-        if (world == 1) return 0;
-        if (!local) {
-            GpuRank& g = *rk[0];
-            const int r = rank_ids[0];
-            size_t bs = 0, br = 0;
-            NCCLCHK(this, ncclGroupStart());
-            for (int side = 0; side < 2; ++side) {
-                const int peer = side == 0 ? r - 1 : r + 1;
-                if (peer < 0 || peer >= world) continue;
-                void* snd = g.halo(side == 0 ? 2 : 3, &bs);
-                void* rcv = g.halo(side == 0 ? 0 : 1, &br);
-                if (!snd || !rcv) continue;
-                ncclSend(snd, bs, ncclUint8, peer, comm[g.lane], g.st);
-                ncclRecv(rcv, br, ncclUint8, peer, comm[g.lane], g.st);
-            }
-            NCCLCHK(this, ncclGroupEnd());
-            return 0;
-        }
-        // local: every rank's stream waits for its neighbours' last stage, copies their edge rows into its
-        // halo rows; then the neighbours wait for those copies (their next pass writes the buffer read)
-        const int n = (int)rk.size();
-        for (int i = 0; i < n; ++i) HIPCHK_M(this, hipEventRecord(ev_a[i], rk[i]->st));
-        for (int i = 0; i < n; ++i) {
-            for (int side = 0; side < 2; ++side) {
-                const int j = side == 0 ? i - 1 : i + 1;
-                if (j < 0 || j >= n) continue;
-                size_t bs = 0, br = 0;
-                void* snd = rk[j]->halo(side == 0 ? 3 : 2, &bs);
-                void* rcv = rk[i]->halo(side == 0 ? 0 : 1, &br);
-                if (!snd || !rcv || bs != br) continue;
-                HIPCHK_M(this, hipStreamWaitEvent(rk[i]->st, ev_a[j], 0));
-                HIPCHK_M(this, hipMemcpyAsync(rcv, snd, br, hipMemcpyDeviceToDevice, rk[i]->st));
-            }
-        }
-        for (int i = 0; i < n; ++i) HIPCHK_M(this, hipEventRecord(ev_b[i], rk[i]->st));
-        for (int i = 0; i < n; ++i)
-            for (int j : {i - 1, i + 1})
-                if (j >= 0 && j < n) HIPCHK_M(this, hipStreamWaitEvent(rk[i]->st, ev_b[j], 0));
+    // ---- transfer statistics (rs_mgpu_get_stats): per frame, HIP events around each halo exchange and
+    // the gather on rank 0's (local: local rank 0's) frame stream, folded when the ring slot is reused
+    static constexpr int kStatRing = 8, kTimedPasses = 4;
+    hipEvent_t sev[kStatRing][2 * kTimedPasses + 2] = {};
+    int s_nx[kStatRing] = {};                   // exchanges recorded in the slot
+    bool s_gather[kStatRing] = {}, s_pending[kStatRing] = {};
+    int s_slot = 0;
+    size_t halo_bytes = 0;                      // per halo slot of the frame in progress
+    rs_mgpu_stats stats{};
+    void fold(int k) {
+        if (!s_pending[k]) return;
+        s_pending[k] = false;
+        float ms = 0.0f;
+        for (int x = 0; x < s_nx[k]; ++x)
+            if (hipEventSynchronize(sev[k][2 * x + 1]) == hipSuccess && hipEventElapsedTime(&ms, sev[k][2 * x], sev[k][2 * x + 1]) == hipSuccess)
+                stats.halo_ms += ms;
+        if (s_gather[k] && hipEventSynchronize(sev[k][2 * kTimedPasses + 1]) == hipSuccess &&
+            hipEventElapsedTime(&ms, sev[k][2 * kTimedPasses], sev[k][2 * kTimedPasses + 1]) == hipSuccess)
+            stats.gather_ms += ms;
+    }
+    int begin_frame_stats() {
+        s_slot = (s_slot + 1) % kStatRing;
+        fold(s_slot);
+        if (!sev[s_slot][0])
+            for (auto& e : sev[s_slot]) HIPCHK_M(this, hipEventCreate(&e));
+        s_nx[s_slot] = 0; s_gather[s_slot] = false; s_pending[s_slot] = true;
+        stats.frames++;
         return 0;
     }
 
-    // ---- gather: band framebuffers -> rank 0's context framebuffer (full frame, rows at their place)
-    int gather(std::vector<GpuRank*>& rk) {
+    // RCCL point-to-point link of one frame: its lane's communicator, its stream; every call checked
+    struct NcclLink {
+        rs_mgpu* m; ncclComm_t comm; hipStream_t st;
+        int group_start() { NCCLCHK(m, ncclGroupStart()); return 0; }
+        int group_end() { NCCLCHK(m, ncclGroupEnd()); return 0; }
+        int send(const void* p, size_t b, int peer) { NCCLCHK(m, ncclSend(p, b, ncclUint8, peer, comm, st)); return 0; }
+        int recv(void* p, size_t b, int peer) { NCCLCHK(m, ncclRecv(p, b, ncclUint8, peer, comm, st)); return 0; }
+    };
+
+    // local mode: every rank's plan paired with its neighbours' (rs::mgpu::pair_local); each recv is a copy
+    // on the receiver's stream after the sender's last stage, and the sender's next stage waits for it
+    int local_exchange(std::vector<GpuRank*>& rk, const std::vector<std::vector<mgpu::Xfer>>& plans) {
+        const int n = (int)rk.size();
+        for (int i = 0; i < n; ++i) HIPCHK_M(this, hipEventRecord(ev_a[i], rk[i]->st));
+        std::vector<std::vector<char>> readers(n, std::vector<char>(n, 0));   // readers[j][i]: i copied from j
+        int rc = mgpu::pair_local(plans, rank_ids, [&](int i, const mgpu::Xfer& x, int j, const mgpu::Xfer& y) -> int {
+            void *dst = nullptr, *src = nullptr;
+            if (x.slot == mgpu::kFrameRows) {
+                dst = rk[i]->frame_base() + x.offset;
+                src = rk[j]->frame_base() + y.offset;
+            } else {
+                size_t bd = 0, bs = 0;
+                dst = rk[i]->halo(x.slot, &bd);
+                src = rk[j]->halo(y.slot, &bs);
+                if (bd != x.bytes || bs != y.bytes) return -2;
+            }
+            if (!dst || !src) return -2;
+            HIPCHK_M(this, hipStreamWaitEvent(rk[i]->st, ev_a[j], 0));
+            HIPCHK_M(this, hipMemcpyAsync(dst, src, x.bytes, hipMemcpyDeviceToDevice, rk[i]->st));
+            readers[j][i] = 1;
+            return 0;
+        });
+        if (rc == -1) return error(RS_E_INVALID, "local exchange: a transfer plan has no matching sender");
+        if (rc == -2) return error(RS_E_INVALID, "local exchange: a halo or framebuffer is missing or has the wrong size");
+        if (rc) return rc;
+        for (int i = 0; i < n; ++i) HIPCHK_M(this, hipEventRecord(ev_b[i], rk[i]->st));
+        for (int j = 0; j < n; ++j)                  // senders: their next stage writes the buffers read
+            for (int i = 0; i < n; ++i)
+                if (readers[j][i]) HIPCHK_M(this, hipStreamWaitEvent(rk[j]->st, ev_b[i], 0));
+        return 0;
+    }
+
+    // ---- halo exchange (the Comm interface of rs::mgpu::render_frame)
+    int exchange_halo(std::vector<GpuRank*>& rk, int pass) {
         if (world == 1) return 0;
-        const size_t row = (size_t)W * 3;
+        const bool timed = pass < kTimedPasses;
+        if (timed) HIPCHK_M(this, hipEventRecord(sev[s_slot][2 * pass], rk[0]->st));
+        std::vector<std::vector<mgpu::Xfer>> plans;
+        for (size_t i = 0; i < rk.size(); ++i) {
+            plans.push_back(mgpu::halo_plan(rank_ids[i], world, halo_bytes));
+            stats.halo_bytes_sent += mgpu::plan_bytes(plans.back(), true);
+            stats.halo_bytes_recv += mgpu::plan_bytes(plans.back(), false);
+        }
         if (!local) {
             GpuRank& g = *rk[0];
-            const int r = rank_ids[0];
-            NCCLCHK(this, ncclGroupStart());
-            if (r == 0) {
-                float* full = const_cast<float*>(g.band) - (size_t)g.y0 * row;
-                for (int q = 1; q < world; ++q)
-                    ncclRecv(full + (size_t)bounds[q] * row, (size_t)(bounds[q + 1] - bounds[q]) * row, ncclFloat32, q,
-                             comm[g.lane], g.st);
-            } else {
-                ncclSend(g.band, (size_t)(g.y1 - g.y0) * row, ncclFloat32, 0, comm[g.lane], g.st);
-            }
-            NCCLCHK(this, ncclGroupEnd());
-            if (r == 0) return ctx_join(g.ctx, g.st);
-            return 0;
+            NcclLink link{this, comm[g.lane], g.st};
+            const int rc = mgpu::issue_plan(g, plans[0], link);
+            if (rc == -2) return error(RS_E_INVALID, "halo exchange: the tile has no halo rows the plan needs");
+            if (rc) return rc;
+        } else if (int rc = local_exchange(rk, plans)) {
+            return rc;
         }
-        const int n = (int)rk.size();
-        GpuRank& g0 = *rk[0];
-        float* full = const_cast<float*>(g0.band) - (size_t)g0.y0 * row;
-        for (int i = 1; i < n; ++i) {
-            HIPCHK_M(this, hipEventRecord(ev_a[i], rk[i]->st));
-            HIPCHK_M(this, hipStreamWaitEvent(g0.st, ev_a[i], 0));
-            HIPCHK_M(this, hipMemcpyAsync(full + (size_t)rk[i]->y0 * row, rk[i]->band,
-                                          (size_t)(rk[i]->y1 - rk[i]->y0) * row * sizeof(float),
-                                          hipMemcpyDeviceToDevice, g0.st));
+        if (timed) {
+            HIPCHK_M(this, hipEventRecord(sev[s_slot][2 * pass + 1], rk[0]->st));
+            s_nx[s_slot] = pass + 1;
         }
-        HIPCHK_M(this, hipEventRecord(ev_b[0], g0.st));
-        for (int i = 1; i < n; ++i) HIPCHK_M(this, hipStreamWaitEvent(rk[i]->st, ev_b[0], 0));   // band reuse
-        return ctx_join(g0.ctx, g0.st);
+        return 0;
+    }
+
+    // ---- gather: band framebuffers -> rank 0's context framebuffer (full frame, rows at their place).
+    // Every rank's context stream then waits for the gather (ctx_join): later work there -- the next
+    // frame on the context stream, rs_synchronize, an all-reduce on comm[0] -- is ordered after the
+    // transfer that reads (senders) or writes (rank 0) this lane's framebuffer.
+    int gather(std::vector<GpuRank*>& rk) {
+        if (world == 1) return 0;
+        HIPCHK_M(this, hipEventRecord(sev[s_slot][2 * kTimedPasses], rk[0]->st));
+        const size_t row = (size_t)W * 3 * sizeof(float);
+        std::vector<std::vector<mgpu::Xfer>> plans;
+        for (size_t i = 0; i < rk.size(); ++i) {
+            plans.push_back(mgpu::gather_plan(rank_ids[i], bounds, row));
+            stats.gather_bytes += mgpu::plan_bytes(plans.back(), false);
+        }
+        if (!local) {
+            GpuRank& g = *rk[0];
+            NcclLink link{this, comm[g.lane], g.st};
+            const int rc = mgpu::issue_plan(g, plans[0], link);
+            if (rc == -2) return error(RS_E_INVALID, "gather: no framebuffer");
+            if (rc) return rc;
+        } else if (int rc = local_exchange(rk, plans)) {
+            return rc;
+        }
+        HIPCHK_M(this, hipEventRecord(sev[s_slot][2 * kTimedPasses + 1], rk[0]->st));
+        s_gather[s_slot] = true;
+        for (auto* g : rk)
+            if (int rc = ctx_join(g->ctx, g->st)) return rc;
+        return 0;
     }
 
     // sum (op 0) or max (op 1) of n doubles over all ranks, in place (host values)
@@ -263,8 +317,10 @@ extern "C" int rs_mgpu_create_local(rs_context* const* ctxs, int world, rs_mgpu*
 
 extern "C" void rs_mgpu_destroy(rs_mgpu* m) {
     if (!m) return;
-    for (auto& g : m->ranks) if (g.ctx) rs_synchronize(g.ctx);
+    for (auto& g : m->ranks) if (g.ctx) rs_synchronize(g.ctx);   // every frame's transfers joined it
     for (auto& c : m->comm) if (c) ncclCommDestroy(c);
+    for (auto& slot : m->sev)
+        for (auto e : slot) if (e) hipEventDestroy(e);
     for (auto e : m->ev_a) if (e) hipEventDestroy(e);
     for (auto e : m->ev_b) if (e) hipEventDestroy(e);
     if (m->d_red) hipFree(m->d_red);
@@ -303,6 +359,9 @@ extern "C" int rs_mgpu_render_frame(rs_mgpu* m, const rs_scene* const* scenes, c
         g.times = i == 0 ? times : nullptr;
         m->rank_ptrs.push_back(&g);
     }
+    m->halo_bytes = (size_t)halo * m->W * 3 * sizeof(float) * 4;    // h rows x W x 48-B reservoirs
+    if (m->world > 1)
+        if (int rc = m->begin_frame_stats()) return rc;
     // G-buffer margin = the halo: a temporal reprojection beyond a tile's rows rebuilds its element
     if (int rc = mgpu::render_frame(m->rank_ptrs, *m, m->bounds, m->rank_ids, P->do_spatial ? P->spatial_passes : 0,
                                     halo, halo, gather != 0))
@@ -324,6 +383,16 @@ extern "C" int rs_mgpu_reset_history(rs_mgpu* m) {
     if (!m) return RS_E_INVALID;
     for (auto& g : m->ranks)
         if (int rc = rs_reset_history(g.ctx)) return rc;
+    return RS_OK;
+}
+
+extern "C" int rs_mgpu_get_stats(rs_mgpu* m, rs_mgpu_stats* out, int reset) {
+    if (!m || !out) return RS_E_INVALID;
+    for (auto& g : m->ranks)
+        if (int rc = rs_synchronize(g.ctx)) return rc;
+    for (int k = 0; k < rs_mgpu::kStatRing; ++k) m->fold(k);
+    *out = m->stats;
+    if (reset) m->stats = rs_mgpu_stats{};
     return RS_OK;
 }
 

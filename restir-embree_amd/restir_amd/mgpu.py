@@ -20,6 +20,15 @@ from .renderer import CameraDesc, PassTimes, RestirError, camera_desc, load_libr
 ID_BYTES = 128
 
 
+class MgpuStats(ctypes.Structure):
+    """rs_mgpu_stats (include/restir_c.h)"""
+    _fields_ = [("frames", ctypes.c_uint64), ("halo_bytes_sent", ctypes.c_uint64), ("halo_bytes_recv", ctypes.c_uint64),
+                ("gather_bytes", ctypes.c_uint64), ("halo_ms", ctypes.c_double), ("gather_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 def _addr(h):
     return h.value if isinstance(h, ctypes.c_void_p) else int(h)
 
@@ -104,6 +113,13 @@ class MultiGpuFrame:
         self._check(self.lib.rs_mgpu_allreduce(self.h, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), v.size,
                                                0 if op == "sum" else 1))
         return v
+
+    def stats(self, reset: bool = False) -> dict:
+        """Transfer statistics since creation / the last reset (synchronous): halo and gather bytes, and
+        the HIP-event time of the exchanges on the first local rank's frame streams."""
+        st = MgpuStats()
+        self._check(self.lib.rs_mgpu_get_stats(self.h, ctypes.byref(st), 1 if reset else 0))
+        return st.as_dict()
 
     def close(self):
         if self.h:

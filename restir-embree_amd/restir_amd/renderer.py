@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = [
     "rs_image_encode_png", "rs_context_track_row_costs", "rs_get_row_costs", "rs_frame_readback", "rs_frame_wait",
     "rs_host_alloc", "rs_host_free", "rs_mgpu_unique_id", "rs_mgpu_create", "rs_mgpu_create_local",
     "rs_mgpu_destroy", "rs_mgpu_set_bands", "rs_mgpu_get_bands", "rs_mgpu_rebalance", "rs_mgpu_render_frame",
-    "rs_mgpu_frame_device_ptr", "rs_mgpu_reset_history", "rs_mgpu_allreduce",
+    "rs_mgpu_frame_device_ptr", "rs_mgpu_reset_history", "rs_mgpu_allreduce", "rs_mgpu_get_stats",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -213,6 +213,7 @@ def load_library(path: str = LIB_PATH):
     L.rs_mgpu_frame_device_ptr.argtypes = [vp, ctypes.POINTER(vp)]
     L.rs_mgpu_reset_history.argtypes = [vp]
     L.rs_mgpu_allreduce.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i32, i32]
+    L.rs_mgpu_get_stats.argtypes = [vp, vp, i32]
     _lib = L
     return L
 

@@ -94,3 +94,26 @@ def test_rccl_world1_and_allreduce():
     assert np.array_equal(img, ref) and m.last_times.rays > 0
     assert np.allclose(m.allreduce([1.5, 2.0], "max"), [1.5, 2.0])
     m.close()
+
+
+def test_local_mgpu_transfer_stats():
+    """rs_mgpu_get_stats: the halo and gather bytes of the transfer plans (rs_mgpu_core.h) per frame, and
+    event-timed exchange spans."""
+    W, H, world, frames = 96, 64, 3, 4
+    sc, prm = scenes.cornell_many_lights(128), P.metric_params(m_area=4)
+    rs = [Renderer(W, H) for _ in range(world)]
+    for r in rs:
+        r.set_traversal("lockstep")
+    ss = [r.load_scene(sc) for r in rs]
+    m = MultiGpuFrame(rs)
+    for f in range(frames):
+        m.render(ss, sc.camera, prm, f)
+    st = m.stats(reset=True)
+    h = 5                                          # floor(sqrt(30))
+    b = m.bands()
+    assert st["frames"] == frames
+    assert st["halo_bytes_sent"] == st["halo_bytes_recv"] == frames * 2 * (world - 1) * h * W * 48
+    assert st["gather_bytes"] == frames * (H - b[0][1]) * W * 12
+    assert st["halo_ms"] > 0 and st["gather_ms"] > 0
+    assert m.stats()["frames"] == 0
+    m.close()

@@ -35,6 +35,8 @@ def _harness():
     L.harness_balanced.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_int32)]
     L.harness_halo.argtypes = [ctypes.c_float]
+    L.harness_plan_check.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
     return L
 
 
@@ -107,3 +109,33 @@ def test_native_band_balancing_matches_python():
             assert [(int(out[i]), int(out[i + 1])) for i in range(world)] == py, (H, world, mr)
     for r in (30.0, 24.999998, 24.9, 25.0, 0.5, 0.0):
         assert L.harness_halo(r) == halo_rows(P.metric_params(spatial_radius=r))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("bands", ["equal", "rebalanced"])
+def test_rccl_transfer_plans_pair_up(world, bands):
+    """The RCCL branch's pairing (rs_mgpu_core.h halo_plan / gather_plan through issue_plan, the code
+    rs_mgpu.hip posts to ncclSend/ncclRecv) recorded per rank on a fake link: every send has exactly one recv
+    of equal bytes from the same peer on the same lane communicator, at 1080p and 4K with equal and
+    cost-rebalanced bands, for each of the 3 run-ahead lanes."""
+    from restir_amd.distributed import balanced_bands
+    L = _harness()
+    rng = np.random.default_rng(world)
+    for W, H in ((1920, 1080), (3840, 2160)):
+        if bands == "equal":
+            b = [r * H // world for r in range(world + 1)]
+        else:
+            cost = rng.uniform(0.2, 3.0, H) * np.linspace(0.3, 2.5, H)
+            b = [0] + [e for _, e in balanced_bands(cost, world, 8)]
+        bounds = np.ascontiguousarray(b, np.int32)
+        for lane in range(3):
+            msg = ctypes.create_string_buffer(256)
+            n = L.harness_plan_check(world, bounds.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), W, H, 5, lane, msg, 256)
+            assert n > 0, (n, msg.value.decode())
+            # 4 halo ops per interior boundary (send + recv each way) + 2 gather ops per non-root rank
+            assert n == 4 * (world - 1) + 2 * (world - 1)
+
+
+def test_rccl_plan_checker_rejects_broken_plans():
+    L = _harness()
+    assert L.harness_plan_check_negative() == 0
