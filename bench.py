@@ -99,8 +99,56 @@ def parse():
     ap.add_argument("--scene", default="C2", choices=list(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N=1: skip the C3/C5/C2V and drop-in lines")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="oracle threads for the CPU baseline; 0 = every core available to this process")
     return ap.parse_args()
+
+
+def host_cpu():
+    """The host the CPU baseline runs on: CPU model (lscpu's 'Model name' = /proc/cpuinfo 'model name'),
+    nproc, the cores this process may run on (sched_getaffinity), the cgroup CPU quota and OMP_NUM_THREADS
+    (the pool's per-GPU CPU share)."""
+    info = {"model": None, "nproc": os.cpu_count(), "affinity_cores": None, "cgroup_cpu_max": None,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.lower().startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        info["affinity_cores"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            info["cgroup_cpu_max"] = f.read().strip()
+    except OSError:
+        pass
+    return info
+
+
+def baseline_threads(requested):
+    """Every core available to the process, within the CPU share the pool grants (a cgroup quota or
+    OMP_NUM_THREADS: the GPU box sets OMP_NUM_THREADS to the per-GPU share and asks worker pools to
+    stay within it)."""
+    if requested and requested > 0:
+        return requested
+    hc = host_cpu()
+    n = hc["affinity_cores"] or hc["nproc"] or 1
+    q = hc["cgroup_cpu_max"]
+    if q and q.split()[0] != "max":
+        try:
+            quota, period = (int(v) for v in q.split()[:2])
+            n = min(n, max(1, quota // period))
+        except ValueError:
+            pass
+    omp = hc["omp_num_threads"]
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 # ---------------------------------------------------------------- CPU baseline (oracle = the checker)
@@ -114,7 +162,7 @@ def cpu_baseline(name, W, H, threads, budget_s=12.0):
     import oracle_lib
     oracle_lib.build()
     L = oracle_lib.lib()
-    n_threads = max(1, min(threads, os.cpu_count() or 1))
+    n_threads = baseline_threads(threads)
     L.or_set_num_threads(n_threads)
     sc, prm, camera, light_pos = workload(name)
     cam = camera or (lambda f: sc.camera)
@@ -145,6 +193,8 @@ def cpu_baseline(name, W, H, threads, budget_s=12.0):
                 break
         sample = (f"{len(times)} frames of a centred {rows}-row band of {W}x{H} (oracle tile stages; after 1 "
                   f"history frame), scaled by {H}/{rows} rows")
+        band = {"rows": rows, "y0": y0, "frames_timed": len(times),
+                "full_frame_equivalents_timed": round(len(times) * rows / H, 4)}
         mr = float(np.median([r / t for r, t in zip(rays, band_t)])) / 1e6
     else:
         rr = oracle_lib.OracleRenderer(W, H)
@@ -158,12 +208,14 @@ def cpu_baseline(name, W, H, threads, budget_s=12.0):
             if time.perf_counter() - t_start > budget_s:
                 break
         sample = f"median of {len(times)} full {W}x{H} frames after 1 warm-up frame"
+        band = {"rows": H, "y0": 0, "frames_timed": len(times), "full_frame_equivalents_timed": len(times)}
         mr = float(np.median([r / t for r, t in zip(rays, times)])) / 1e6
     dt = float(np.median(times))
     out = {"value": round(1.0 / dt, 5), "unit": "frames/s", "cores": n_threads, "kind": "port",
            "sample": f"{sample}; oracle/restir_oracle.c (OpenMP, {n_threads} threads, scalar binary SAH BVH -- "
                      f"not Embree's 4/8-wide SIMD BVH: the GPU/CPU ratio overstates the gap to an Embree-class CPU)",
-           "s_per_frame": round(dt, 4)}
+           "s_per_frame": round(dt, 4), "band": band, "host": host_cpu(),
+           "timing_scope": "all passes of produceRestir (pg/simpleguidx11.cpp:361-486 totalFrameDuration), no post-frame"}
     if mr is not None:
         out["mrays_per_s"] = round(mr, 2)
     # rays the reference's code would trace for these frames (oracle-counted: every rtcIntersect1 and

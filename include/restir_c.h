@@ -104,7 +104,13 @@ typedef struct {
     float tfar_offset;
     float normal_offset;
     uint32_t seed;                 /* counter-RNG seed (replaces Utils' mt19937{123}, pg/utils.cpp:175) */
-    int32_t reserved;
+    int32_t debug_reprojection;    /* debugReprojection (pg/ReSTIRIntegrator.cpp:30, :647-689): the temporal pass
+                                      paints rejected reprojections into the G-buffer emission -- (100,100,0)
+                                      no backward reprojection, (0,100,0) depth ratio, (100,0,100) no forward
+                                      reprojection at the pixel, (0,0,100) at the forward-reprojected pixel of
+                                      a failed forward depth check.  Applied after the pass (the reference's
+                                      parallel loop races on them); full frames only (RS_E_UNSUPPORTED on a
+                                      partial tile) */
 } rs_frame_params;
 
 /* Per-pass device time in ms (the reference's std::chrono pass timers, pg/simpleguidx11.h:120-127). */

@@ -638,7 +638,7 @@ typedef struct {
     int32_t do_spatial, do_temporal, do_visibility_pass, reject_dissimilar, spatial_mis;
     int32_t use_skybox; float bg_color[3];
     float tnear_offset, tfar_offset, normal_offset;
-    uint32_t seed; int32_t reserved;
+    uint32_t seed; int32_t debug_reprojection;
 } or_params;  /* snapshot of pg/ReSTIRIntegrator.cpp:13-35 statics + pg/RenderParams.h:5-17 */
 
 typedef struct { v3 pos, nrm, kd, ks, le; float shin, depth; int type; } or_gbe; /* pg/GBufferElement.h:6-17 */
@@ -1100,10 +1100,16 @@ static int reproject(const or_gcam* gc, v3 ws, int W, int H, int* sx, int* sy) {
     return 1;
 }
 
-/* temporalReusePass (pg/ReSTIRIntegrator.cpp:625-732) */
+/* temporalReusePass (pg/ReSTIRIntegrator.cpp:625-732).  debugReprojection (:30, :647-689): the rejection
+ * colours go into the current G-buffer's emission AFTER the pass (the reference's OpenMP loop writes them
+ * while other pixels read -- a race; here no pixel of the pass sees them), a pixel's own colour winning
+ * over a forward-check mark (0,0,100) from another pixel. */
 static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* Rw, int y0, int y1, uint64_t* rays) {
     const or_params* P = F->P; int W = F->c->W, H = F->c->H;
     uint64_t rc = 0, rebuilt = 0;
+    const size_t npx = (size_t)W * H;
+    uint8_t* dbg = P->debug_reprojection ? (uint8_t*)calloc(2 * npx, 1) : NULL;
+#define DBG_OWN(code) do { if (dbg) dbg[p] = (code); } while (0)
 #pragma omp parallel for schedule(dynamic, 1) reduction(+:rc, rebuilt)
     for (int y = y0; y < y1; ++y)
         for (int x = 0; x < W; ++x) {
@@ -1113,7 +1119,7 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             const or_res* cr = &Rr[p];
             const or_res* pr = &Rl[p];       /* previous reservoir read at the CURRENT pixel (:641) */
             int qx, qy;
-            if (!reproject(F->gcp, cur->pos, W, H, &qx, &qy)) { Rw[p] = *cr; continue; }
+            if (!reproject(F->gcp, cur->pos, W, H, &qx, &qy)) { Rw[p] = *cr; DBG_OWN(1); continue; }
             size_t q = (size_t)qy * W + qx;
             const or_gbe* prev = &F->Gp[q];
             float imq = F->imp[q];
@@ -1128,10 +1134,10 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             float cd = len(sub(cur->pos, ccam));
             float pd = len(sub(prev->pos, pcam));
             float dr = cd > pd ? pd / cd : cd / pd;
-            if (dr < 0.9f) { Rw[p] = *cr; continue; }
+            if (dr < 0.9f) { Rw[p] = *cr; DBG_OWN(2); continue; }
             const or_gbe* pac = &F->Gp[p];
             int fx, fy;
-            if (!reproject(F->gc, pac->pos, W, H, &fx, &fy)) { Rw[p] = *cr; continue; }
+            if (!reproject(F->gc, pac->pos, W, H, &fx, &fy)) { Rw[p] = *cr; DBG_OWN(3); continue; }
             const or_gbe* fw = &F->G[(size_t)fy * W + fx];
             or_gbe fw_alt; float im_unused;
             if (fy < F->gy0 || fy >= F->gy1) {
@@ -1142,7 +1148,11 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             float cdp = len(sub(pac->pos, pcam));
             float pdp = len(sub(fw->pos, ccam));
             float drp = cdp > pdp ? pdp / cdp : cdp / pdp;
-            if (drp < 0.9f) { Rw[p] = *cr; continue; }
+            if (drp < 0.9f) {
+                Rw[p] = *cr;
+                if (dbg) dbg[npx + (size_t)fy * W + fx] = 1;   /* the same value from any pixel */
+                continue;
+            }
 
             rng_t rng = rng_init(P->seed, F->frame, PASS_TEMPORAL, (uint32_t)p);
             or_res res = res_empty();
@@ -1171,6 +1181,16 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
             res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
             Rw[p] = res;
         }
+#undef DBG_OWN
+    if (dbg) {
+        or_gbe* G = (or_gbe*)F->G;    /* the context's current G-buffer */
+        for (size_t q = 0; q < npx; ++q) {
+            const uint8_t own = dbg[q], fwd = dbg[npx + q];
+            if (!own && !fwd) continue;
+            G[q].le = own == 1 ? V(100, 100, 0) : own == 2 ? V(0, 100, 0) : own == 3 ? V(100, 0, 100) : V(0, 0, 100);
+        }
+        free(dbg);
+    }
     *rays += rc;
     F->c->rebuilt += rebuilt;
 }

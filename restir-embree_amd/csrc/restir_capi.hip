@@ -23,7 +23,7 @@
 
 namespace rs {
 int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes, float4** d_tris,
-              std::string& err);
+              WideBvh* wide, std::string& err);
 int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int** d_order, int** d_lvl_off,
                    std::vector<int>& lvl_off, std::string& err);
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
@@ -50,6 +50,10 @@ struct rs_scene {
     int* d_emis_tri = nullptr;
     int *d_refit_order = nullptr, *d_refit_lvl = nullptr;
     std::vector<int> refit_lvl;
+    // 8-wide tree of the per-lane walks (rs_scene.h); dropped (walks fall back to the skip pointers) once
+    // the positions move -- it is not refit
+    WideBvh wide;
+    bool wide_on = false;
     float* h_stage[2] = {nullptr, nullptr};
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     int stage_i = 0;
@@ -79,6 +83,7 @@ struct rs_scene {
         S.nodes = d_nodes; S.tris = d_tris; S.tri_nrm = d_tri_nrm; S.mats = d_mats; S.emis = d_emis; S.cdf = d_cdf; S.cdf_guide = d_cdf_guide;
         S.n_nodes = n_nodes; S.n_tris = n_tris; S.n_emis = n_emis; S.n_mats = n_mats;
         S.tri_uv = d_uv; S.tri_tan = d_tan; S.tex = d_tex; S.texd = d_texd; S.sky = sky;
+        S.wnodes = wide_on ? wide.nodes : nullptr; S.wtris = wide.tris; S.n_wnodes = wide_on ? wide.n_nodes : 0u;
         return S;
     }
 };
@@ -197,6 +202,7 @@ struct rs_context {
     hipEvent_t join_ev = nullptr;          // rs::ctx_join
     // queued initial pass (rs_queue.h): mode (RS_SPLIT_* values: AUTO = incoherent scenes), the last
     // frame's choice, per-lane queue storage (sized for the largest launch so far)
+    uint8_t* d_dbg = nullptr;              // debugReprojection marks (FrameConst::dbg), on first use
     int queue_mode = RS_SPLIT_OFF;
     bool queue = false;
     QBuf qb[kLanes] = {};
@@ -739,7 +745,8 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
         s->update_recorded = false;
     }
     void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide, s->d_emis_tri,
-                   s->d_refit_order, s->d_refit_lvl};
+                   s->d_refit_order, s->d_refit_lvl, s->wide.nodes, s->wide.tris};
+    s->wide = WideBvh{}; s->wide_on = false;
     for (void* p : old) if (p) hipFree(p);
     s->d_pos = nullptr; s->d_nodes = nullptr; s->d_tris = nullptr; s->d_emis = nullptr; s->d_cdf = nullptr;
     s->d_cdf_guide = nullptr; s->d_emis_tri = nullptr; s->d_refit_order = nullptr; s->d_refit_lvl = nullptr;
@@ -764,7 +771,8 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     hipEventCreate(&e0); hipEventCreate(&e1);
     hipEventRecord(e0, st);
     std::string berr;
-    int rc = build_bvh(s->d_pos, n, st, &s->d_nodes, &s->n_nodes, &s->d_tris, berr);
+    int rc = build_bvh(s->d_pos, n, st, &s->d_nodes, &s->n_nodes, &s->d_tris, &s->wide, berr);
+    s->wide_on = rc == 0 && s->wide.n_nodes > 0;   // deeper than the walk's stack: overflow falls back (rs_scene.h)
     hipEventRecord(e1, st);
     if (rc == 0 && hipStreamSynchronize(st) == hipSuccess) hipEventElapsedTime(&s->build_ms, e0, e1);
     else { err = "BVH build failed: " + berr; rc = -1; }
@@ -960,6 +968,7 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
         k_set_normals<<<(s->n_tris + 255) / 256, 256, 0, st>>>(s->d_nrm_stage, s->n_tris, s->d_tri_nrm);
     }
     HIPCHK(c, hipEventRecord(s->stage_ev[k], st));
+    s->wide_on = false;                          // later frames walk the refit binary tree (S.n_wnodes = 0)
     std::string err;
     int tail[2];
     if (bvh_refit(nodes, tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, s->refit_lvl, st, tail, err) != 0)
@@ -1107,7 +1116,7 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     if (s->ctx) sync_all(s->ctx);
     void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
                     s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage, s->d_tex, s->d_texd, s->d_uv,
-                    s->d_tan, s->a_nodes, s->a_tris, s->a_emis,
+                    s->d_tan, s->wide.nodes, s->wide.tris, s->a_nodes, s->a_tris, s->a_emis,
                     s->a_cdf, s->a_cdf_guide};
     for (void* p : ptrs) if (p) hipFree(p);
     for (int k = 0; k < 2; ++k) {
@@ -1336,6 +1345,8 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     if (P->do_spatial && (P->spatial_neighbors < 0 || P->spatial_neighbors > 64))
         return fail(c, RS_E_INVALID, "rs_frame_params: spatial_neighbors must be in [0, 64]");
     if (P->spatial_mis < 0 || P->spatial_mis > 4) return fail(c, RS_E_INVALID, "rs_frame_params: bad spatial_mis");
+    if (P->debug_reprojection && (tile->y0 != 0 || tile->y1 != c->H))
+        return fail(c, RS_E_UNSUPPORTED, "debug_reprojection: full frames only (its marks land on any pixel)");
     if (tile->y0 < 0 || tile->y1 > c->H || tile->y0 >= tile->y1 || tile->margin < 0 || tile->halo < 0 ||
         tile->halo > tile->margin)
         return fail(c, RS_E_INVALID, "rs_tile_begin: bad tile (need 0<=y0<y1<=H, 0<=halo<=margin)");
@@ -1353,6 +1364,9 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     F.W = c->W; F.H = c->H;
     F.y0 = tile->y0; F.y1 = tile->y1;
     F.row_order = c->n_order ? c->d_order : nullptr; F.n_order = c->n_order;
+    F.debug_reproj = P->debug_reprojection ? 1 : 0;
+    if (F.debug_reproj && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 2 * (size_t)c->W * c->H));
+    F.dbg = c->d_dbg;
     F.gy0 = std::max(0, tile->y0 - tile->margin); F.gy1 = std::min(c->H, tile->y1 + tile->margin);
     // G-buffer ring (replaces gBufferLastFrame.setDataFrom, pg/simpleguidx11.cpp:480): this frame
     // writes the slot after the current one; G[gcur] becomes the previous frame's
@@ -1498,9 +1512,15 @@ extern "C" int rs_tile_temporal(rs_context* c) {
         const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
         // the previous frame's final reservoirs and G-buffer (another lane may still be finishing it)
         if (c->prev_done && c->fs != c->stream) HIPCHK(c, hipStreamWaitEvent(c->fs, c->prev_done, 0));
+        const size_t npx = (size_t)c->W * c->H;
+        if (c->F.debug_reproj) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 2 * npx, c->fs));
         LAUNCH_TRAV(c, k_temporal, gb, S, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]},
                     ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
+        if (c->F.debug_reproj) {
+            k_debug_reproj<<<(unsigned)((npx + 255) / 256), 256, 0, c->fs>>>(c->G[c->gcur], c->d_dbg, (uint32_t)npx);
+            HIPCHK(c, hipGetLastError());
+        }
         c->rcur = c->rb;
         c->temporal_ran = true;
     }
@@ -1953,7 +1973,23 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
     const bool act = i0 < n;
     const uint32_t i = act ? i0 : n - 1;
     vec3 O = mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), D = mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    if (any == 4 || any == 5) {   // BVH statistics of the per-lane walk: visits << 16 | triangle tests
+    if (any >= 8 && any <= 10) {  // timing probes of the 8-wide walk: 8 closest walk with the ray's tfar,
+        const vec3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);   // 9 any-hit without triangle tests,
+        Hit h; h.t = tf[i]; h.u = h.v = 0.0f; h.prim = -1;        // 10 any-hit with statistics off
+        uint32_t occ = 0u, lost = 0u;
+        if (any == 8) wide_walk<false>(S, act, O, D, inv, tn[i], tf[i], h, occ, lost);
+        else if (any == 9) wide_walk<true, false, true>(S, act, O, D, inv, tn[i], tf[i], h, occ, lost);
+        else wide_walk<true>(S, act, O, D, inv, tn[i], tf[i], h, occ, lost);
+        if (act) { prim_out[i] = any == 8 ? h.prim : (int32_t)occ; t_out[i] = (float)lost; }
+    } else if (any == 6 || any == 7) {   // 8-wide walk statistics: node fetches << 16 | triangle tests; t = stack overflow
+        if (S.n_wnodes == 0u) { if (act) { prim_out[i] = -1; t_out[i] = -1.0f; } return; }
+        const vec3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+        Hit h; h.t = tf[i]; h.u = h.v = 0.0f; h.prim = -1;
+        uint32_t occ = 0u, lost = 0u, st = 0u;
+        if (any == 7) wide_walk<true, true>(S, act, O, D, inv, tn[i], tf[i], h, occ, lost, &st);
+        else wide_walk<false, true>(S, act, O, D, inv, tn[i], tf[i], h, occ, lost, &st);
+        if (act) { prim_out[i] = (int32_t)st; t_out[i] = (float)lost; }
+    } else if (any == 4 || any == 5) {   // BVH statistics of the per-lane walk: visits << 16 | triangle tests
         vec3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
         uint32_t cur = act ? 0u : 0xffffffffu, visits = 0, tris = 0;
         bool occ = false;

@@ -25,6 +25,7 @@
 #include <cstring>
 #include <algorithm>
 #include "rs_refit.h"
+#include "rs_wide.h"
 
 namespace rs {
 
@@ -452,6 +453,48 @@ __global__ void k_ploc_emit(const float4* nlo, const float4* nhi, const int* par
     out[2 * idx + 1] = make_float4(b.x, b.y, b.z, __int_as_float(info));
 }
 
+
+// wide-leaf triangles (v0, prim) (e1) (e2) in tri_prims order, like k_leaf_tris
+__global__ void k_wide_tris(const float* __restrict__ pos, const int* __restrict__ prims, uint32_t n, float4* tris) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int prim = prims[k];
+    const float* p = pos + 9 * (size_t)prim;
+    const float v0x = p[0], v0y = p[1], v0z = p[2];
+    tris[3 * k] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
+    tris[3 * k + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
+    tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
+}
+
+// downloads the PLOC tree, collapses it on the host, uploads the wide nodes and gathers their triangles
+static int build_wide(const float* d_pos, const float4* nlo_d, const float4* nhi_d, int n, int root, hipStream_t st,
+                      WideBvh* w, std::string& err) {
+    const size_t total = 2 * (size_t)n - 1;
+    std::vector<float4> nlo(total), nhi(total);
+    if (hipMemcpyAsync(nlo.data(), nlo_d, total * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(nhi.data(), nhi_d, total * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) { err = "wide BVH: download failed"; return -1; }
+    std::vector<uint32_t> nodes;
+    std::vector<int> prims;
+    int depth = 0;
+    if (build_wide_host((const float*)nlo.data(), (const float*)nhi.data(), n, root, nodes, prims, depth, err) != 0) return -1;
+    int* d_prims = nullptr;
+    if (hipMalloc(&w->nodes, nodes.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&w->tris, prims.size() * 3 * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&d_prims, prims.size() * sizeof(int)) != hipSuccess) { err = "wide BVH: hipMalloc failed"; hipFree(d_prims); return -1; }
+    if (hipMemcpyAsync(w->nodes, nodes.data(), nodes.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_prims, prims.data(), prims.size() * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
+        err = "wide BVH: upload failed"; hipFree(d_prims); return -1;
+    }
+    k_wide_tris<<<((uint32_t)prims.size() + 255) / 256, 256, 0, st>>>(d_pos, d_prims, (uint32_t)prims.size(), w->tris);
+    const bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+    hipFree(d_prims);
+    if (!ok) { err = "wide BVH: triangle gather failed"; return -1; }
+    w->n_nodes = (uint32_t)(nodes.size() / 20);
+    w->depth = depth;
+    return 0;
+}
+
 #define PLOC_CHECK(x)                                                                  \
     do {                                                                               \
         hipError_t e_ = (x);                                                           \
@@ -459,7 +502,7 @@ __global__ void k_ploc_emit(const float4* nlo, const float4* nhi, const int* par
     } while (0)
 
 int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes,
-                   float4** d_tris, std::string& err) {
+                   float4** d_tris, WideBvh* wide, std::string& err) {
     *d_nodes = nullptr; *d_tris = nullptr; *n_nodes = 0;
     if (n == 0) return 0;
     if (n >= (1u << 27)) { err = "too many triangles for the leaf index"; return -1; }
@@ -556,6 +599,7 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
     k_ploc_emit<<<(total + B - 1) / B, B, 0, st>>>(nlo, nhi, parent, cnt, kept, collapsed, (int)n, d_pos, nodes, tris);
     PLOC_CHECK(hipGetLastError());
     PLOC_CHECK(hipStreamSynchronize(st));
+    if (wide && build_wide(d_pos, nlo, nhi, (int)n, root, st, wide, err) != 0) goto fail;
     *d_nodes = nodes; *d_tris = tris; *n_nodes = (uint32_t)kept_root;
     nodes = nullptr; tris = nullptr;
 fail: {
@@ -622,11 +666,14 @@ int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_
 }
 
 // builder selection: PLOC by default; RESTIR_BVH=lbvh selects the Karras LBVH (kept for comparison)
+// (RESTIR_WIDE=off: no wide tree, the per-lane walks use the skip pointers)
 int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes, float4** d_tris,
-              std::string& err) {
+              WideBvh* wide, std::string& err) {
     const char* e = getenv("RESTIR_BVH");
+    const char* w = getenv("RESTIR_WIDE");
+    if (w && std::string(w) == "off") wide = nullptr;
     if (e && std::string(e) == "lbvh") return build_bvh_lbvh(d_pos, n, st, d_nodes, n_nodes, d_tris, err);
-    return build_bvh_ploc(d_pos, n, st, d_nodes, n_nodes, d_tris, err);
+    return build_bvh_ploc(d_pos, n, st, d_nodes, n_nodes, d_tris, wide, err);
 }
 
 }  // namespace rs

@@ -76,6 +76,8 @@ struct FrameConst {
     GCam cam, camp;       // current / previous frame camera (pg/GBufferElement.h:136-139)
     const int* row_order; // full-frame launches: grid row -> 16-px tile row, costliest first (or null)
     int n_order;          // entries of row_order (== the grid's rows when it applies)
+    int debug_reproj;     // debugReprojection: k_temporal records, k_debug_reproj paints (full frames)
+    uint8_t* dbg;         // 2 x W*H bytes: [p] the pixel's own rejection (1..3), [W*H + p] forward-check hit
 };
 
 struct Counters { unsigned long long rays, primary, reproj_outside; };   // per-frame totals
@@ -756,6 +758,8 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
     GElem cur = G.load(p);
     int qx = x, qy = y, fx = x, fy = y;
     bool ok = in && reproject(F.camp, cur.pos, F.W, F.H, qx, qy);
+    uint32_t dcode = (in && !ok) ? 1u : 0u;          // debugReprojection (pg/ReSTIRIntegrator.cpp:647-689)
+    bool dfwd = false;
     // A tile holds the G-buffers of its rows +- margin only.  A reprojection beyond them (a miss
     // pixel's position is (0,0,0), which projects anywhere) rebuilds the element it needs from the
     // frame's camera -- gBufferFillPass is a function of (camera, pixel) -- so tiles stay bit-identical
@@ -771,9 +775,11 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
         float cd = length(cur.pos - F.cam.pos), pd = length(prev.pos - F.camp.pos);
         float dr = cd > pd ? pd / cd : cd / pd;
         ok = !(dr < 0.9f);
+        dcode = ok ? dcode : 2u;
     }
     vec3 pac = Gp.pos(p);
     const bool fok = ok && reproject(F.cam, pac, F.W, F.H, fx, fy);
+    dcode = (ok && !fok) ? 3u : dcode;
     const bool f_out = fok && (fy < F.gy0 || fy >= F.gy1);
     vec3 fw = G.pos(fok && !f_out ? (size_t)fy * F.W + fx : p);
     if (__ballot(f_out) != 0) {
@@ -786,7 +792,13 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
             float cdp = length(pac - F.camp.pos), pdp = length(fw - F.cam.pos);
             float drp = cdp > pdp ? pdp / cdp : cdp / pdp;
             ok = !(drp < 0.9f);
+            dfwd = !ok;
         }
+    }
+    if (F.debug_reproj) {                             // recorded; painted by k_debug_reproj after the pass
+        const size_t n = (size_t)F.W * F.H;
+        if (dcode) F.dbg[p] = (uint8_t)dcode;
+        if (dfwd) F.dbg[n + (size_t)fy * F.W + fx] = 1u;
     }
     Res out = cr;
     if (__ballot(ok) != 0) {
@@ -815,6 +827,17 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
     }
     if (in) Rw.store(p, out);
     count_rays(C, rays, 0, t0, y);
+}
+
+// debugReprojection's colours (pg/ReSTIRIntegrator.cpp:648,663,675,689) into the current G-buffer emission,
+// after the temporal pass: a pixel's own rejection wins over a forward-check mark from another pixel
+__global__ void k_debug_reproj(GBuf G, const uint8_t* __restrict__ dbg, uint32_t n) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t own = dbg[p], fwd = dbg[n + p];
+    if (!own && !fwd) return;
+    const vec3 c = own == 1u ? mk(100, 100, 0) : (own == 2u ? mk(0, 100, 0) : (own == 3u ? mk(100, 0, 100) : mk(0, 0, 100)));
+    G.g4[p] = f4(c, G.g4[p].w);
 }
 
 // Sampling::sampleDiskUniform (pg/Sampling.cpp:78-87) -> glm::vec<2,int> (truncation), clamped to

@@ -20,6 +20,15 @@
 
 namespace rs {
 
+// 8-wide tree of the per-lane walks (built by rs_bvh_build.hip build_wide, walked by rs_scene.h; layout
+// there).  Device allocations owned by the scene.
+struct WideBvh {
+    uint4* nodes = nullptr;      // 5 per node
+    float4* tris = nullptr;      // 3 per wide-leaf triangle
+    uint32_t n_nodes = 0;
+    int depth = 0;               // deepest level (root = 0)
+};
+
 constexpr int kRefitBlock = 1024;
 constexpr int kRefitSmall = 4 * kRefitBlock;     // levels up to this many nodes go to the 1-block batch
 

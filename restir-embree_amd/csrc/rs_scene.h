@@ -36,6 +36,10 @@ struct DevScene {
     const uint8_t* tex;       // texel bytes of every texture
     const int4* texd;         // 2 per texture: (byte offset, width, height, pitch), (pixel bytes, format, 0, 0)
     int sky;                  // texture index of the equirect sky, -1 none
+    // 8-wide tree of the per-lane walks (rs_bvh_build.hip build_wide); n_wnodes = 0: skip-pointer walks
+    const uint4* wnodes;      // 5 per node
+    const float4* wtris;      // 3 per wide-leaf triangle: (v0, prim) (e1) (e2)
+    uint32_t n_wnodes;
 };
 constexpr int kCdfGuide = 1024;
 
@@ -169,10 +173,7 @@ __device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i
     }
     return occ != 0u;
 }
-__device__ __forceinline__ bool occluded_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-    const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    return occluded_lane_from(S, active ? 0u : 0xffffffffu, o, d, inv, tnear, tfar);
-}
+
 __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i, vec3 o, vec3 d, vec3 inv, float tnear,
                                                   Hit& h) {
     const uint32_t n = S.n_nodes;
@@ -200,10 +201,168 @@ __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i,
         i = !live ? i : ((hit & (leaf < 0)) ? i + 1 : skip);
     }
 }
+
+
+
+// ---------------------------------------------------------------- 8-wide per-lane walks (TRAV_LANE)
+// The skip-pointer walk fetches every child of every entered node to test that child's box: ~75 dependent
+// 32-B node loads per C3 shadow ray, and the per-lane walks are bound by those lane-loads and the VALU of
+// one box test per step.  The 8-wide tree (rs_bvh_build.hip build_wide: 80-B nodes
+// holding the quantised boxes of up to 8 children) tests all children of a node per fetch: ~14 node
+// fetches per shadow ray (5 x 16-B loads each), i.e. about half the lane-loads, a fifth of the
+// dependent-load chain, and 8 box tests per fetch that share the node's per-axis setup.
+// Traversal: a group = (first interior child node, mask of its hit slots still to visit); a step pops one
+// slot from the current group (pushing the rest on a short per-lane register stack), fetches that node,
+// tests its 8 child boxes, tests its hit leaf triangles (one triangle per leaf slot, a wave-uniform loop
+// like the skip walk's) and makes the hit interior children the next group; an empty group pops the
+// stack.  The box test is conservative: the quantised planes contain the exact child box (built outward)
+// and the interval is widened by the float error of t = q * (s / d) + (o - org) / d (relative 4 ulp as in
+// box_test, and per axis 2^-22 |(o - org) / d| for the rounding of that term, folded into the offsets) --
+// a superset of the exact test, so with the same triangle tests and tie rule the results are those of every
+// other walk.  (One bound for all axes was tried first: an axis the ray is nearly parallel to has a huge
+// |(o - org) / d|, and that bound opened every box of the tree for such rays -- 100x slower walks.)
+// A stack overflow (a tree deeper than kWideStack levels) drops the oldest group and finishes with the
+// skip-pointer walk from the root (any-hit: if not yet occluded; closest: culled by the hit so far).
+#ifndef RS_WIDE_STACK
+#define RS_WIDE_STACK 8
+#endif
+constexpr int kWideStack = RS_WIDE_STACK;
+struct WideStack {
+    uint32_t s[kWideStack];   // s[0] = top: base << 8 | mask
+    int n;
+    uint32_t lost;
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int k = 0; k < kWideStack; ++k) s[k] = 0u;
+        n = 0; lost = 0u;
+    }
+    __device__ __forceinline__ void push(bool c, uint32_t v) {
+        lost |= (c & (n == kWideStack)) ? 1u : 0u;
+#pragma unroll
+        for (int k = kWideStack - 1; k > 0; --k) s[k] = c ? s[k - 1] : s[k];
+        s[0] = c ? v : s[0];
+        n = c ? (n < kWideStack ? n + 1 : n) : n;
+    }
+    __device__ __forceinline__ uint32_t pop(bool c) {
+        const uint32_t top = s[0];
+#pragma unroll
+        for (int k = 0; k < kWideStack - 1; ++k) s[k] = c ? s[k + 1] : s[k];
+        n = c ? n - 1 : n;
+        return top;
+    }
+};
+__device__ __forceinline__ float ubyte_f(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xffu); }
+// the 8 child boxes of node (w0..w4) against the ray; bit c = slot c hit (valid slots only)
+__device__ __forceinline__ uint32_t wide_hits(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, vec3 o, vec3 inv,
+                                              float tnear, float tfar) {
+    const uint32_t eb = w0.w;
+    const vec3 s = mk(__uint_as_float((eb & 0xffu) << 23), __uint_as_float(((eb >> 8) & 0xffu) << 23),
+                      __uint_as_float(((eb >> 16) & 0xffu) << 23));
+    const vec3 a = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);                 // exact (power-of-two scale)
+    const vec3 b = mk((__uint_as_float(w0.x) - o.x) * inv.x, (__uint_as_float(w0.y) - o.y) * inv.y,
+                      (__uint_as_float(w0.z) - o.z) * inv.z);
+    // per axis the near (far) t lowered (raised) by 2^-22 |b|: the rounding of b and of b -+ that bound
+    // (an axis the ray is almost parallel to has a huge |b| and widens only itself)
+    const float ex = 2.384185791015625e-07f * fabsf(b.x), ey = 2.384185791015625e-07f * fabsf(b.y),
+                ez = 2.384185791015625e-07f * fabsf(b.z);
+    const vec3 bn = mk(b.x - ex, b.y - ey, b.z - ez), bf = mk(b.x + ex, b.y + ey, b.z + ez);
+    // near / far planes per axis by the direction's sign (lo bytes near for a positive direction)
+    const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
+    const uint32_t nx0 = px ? w1.z : w3.x, nx1 = px ? w1.w : w3.y, fx0 = px ? w3.x : w1.z, fx1 = px ? w3.y : w1.w;
+    const uint32_t ny0 = py ? w2.x : w3.z, ny1 = py ? w2.y : w3.w, fy0 = py ? w3.z : w2.x, fy1 = py ? w3.w : w2.y;
+    const uint32_t nz0 = pz ? w2.z : w4.x, nz1 = pz ? w2.w : w4.y, fz0 = pz ? w4.x : w2.z, fz1 = pz ? w4.y : w2.w;
+    const float lo_k = 1.0f - 4.0f * FLT_EPSILON, hi_k = 1.0f + 4.0f * FLT_EPSILON;
+    uint32_t hits = 0u;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int k = c & 3;
+        const uint32_t qnx = c < 4 ? nx0 : nx1, qny = c < 4 ? ny0 : ny1, qnz = c < 4 ? nz0 : nz1;
+        const uint32_t qfx = c < 4 ? fx0 : fx1, qfy = c < 4 ? fy0 : fy1, qfz = c < 4 ? fz0 : fz1;
+        const float tnx = fmaf(ubyte_f(qnx, k), a.x, bn.x), tny = fmaf(ubyte_f(qny, k), a.y, bn.y);
+        const float tnz = fmaf(ubyte_f(qnz, k), a.z, bn.z);
+        const float tfx = fmaf(ubyte_f(qfx, k), a.x, bf.x), tfy = fmaf(ubyte_f(qfy, k), a.y, bf.y);
+        const float tfz = fmaf(ubyte_f(qfz, k), a.z, bf.z);
+        const float t0 = fmaxf(fmaxf(fmaxf(tnear, tnx), tny), tnz);
+        const float t1 = fminf(fminf(fminf(tfar, tfx), tfy), tfz);
+        hits |= (t0 * lo_k <= t1 * hi_k) ? (1u << c) : 0u;
+    }
+    const uint32_t nv = w0.w >> 28;
+    return hits & ((1u << nv) - 1u);
+}
+// Stats (rs_debug_trace only): *stats = node fetches << 16 | triangle tests of this lane's walk
+template <bool Any, bool Stats = false, bool NoTri = false>
+__device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o, vec3 d, vec3 inv, float tnear,
+                                          float tfar, Hit& h, uint32_t& occ, uint32_t& lost, uint32_t* stats = nullptr) {
+    uint32_t gb = 0u, gm = active ? 1u : 0u;       // root group: node 0, slot 0
+    WideStack st;
+    st.init();
+    uint32_t n_fetch = 0u, n_tri = 0u;
+    while (__ballot(gm != 0u) != 0) {
+        if (Stats) n_fetch += gm != 0u ? 1u : 0u;
+        const bool live = gm != 0u;
+        const uint32_t slot = (uint32_t)__builtin_ctz(gm | 0x100u);
+        const uint32_t node = live ? gb + slot : 0u;
+        const uint32_t rest = gm & (gm - 1u);
+        st.push(live & (rest != 0u), (gb << 8) | rest);
+        const uint4* P = S.wnodes + 5 * (size_t)node;
+        const uint4 w0 = P[0], w1 = P[1], w2 = P[2], w3 = P[3], w4 = P[4];
+        const float tf = Any ? tfar : h.t;
+        uint32_t hits = live ? wide_hits(w0, w1, w2, w3, w4, o, inv, tnear, tf) : 0u;
+        const uint32_t ni = (w0.w >> 24) & 0xfu;
+        uint32_t tm = NoTri ? 0u : hits >> ni;      // leaf slots ni.. -> triangles tri_base + (slot - ni)
+        const uint32_t tb = w1.y;
+        while (__ballot(tm != 0u && (!Any || occ == 0u)) != 0) {
+            const bool want = tm != 0u && (!Any || occ == 0u);
+            if (Stats) n_tri += want ? 1u : 0u;
+            const uint32_t j = (uint32_t)__builtin_ctz(tm | 0x100u);
+            tm &= tm - 1u;
+            const float4* T = S.wtris + 3 * (size_t)(want ? tb + j : 0u);
+            const float4 T0 = T[0];
+            float t, u, v;
+            const bool hh = want & tri_test_nb(T0, T[1], T[2], o, d, tnear, Any ? tfar : h.t, t, u, v);
+            if (Any) {
+                occ = hh ? 1u : occ;
+            } else {
+                const int prim = __float_as_int(T0.w);
+                const bool better = hh & (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim));
+                h.t = better ? t : h.t; h.u = better ? u : h.u; h.v = better ? v : h.v;
+                h.prim = better ? prim : h.prim;
+            }
+        }
+        const uint32_t ngm = (Any && occ) ? 0u : (hits & ((1u << ni) - 1u));
+        const bool pop = live & (ngm == 0u) & (st.n > 0) & !(Any && occ);
+        const uint32_t top = st.pop(pop);
+        gb = !live ? gb : (ngm ? w1.x : (pop ? top >> 8 : 0u));
+        gm = !live ? 0u : (ngm ? ngm : (pop ? top & 0xffu : 0u));
+        if (Any && occ) st.n = 0;
+    }
+    lost = st.lost;
+    if (Stats) *stats = (n_fetch << 16) | (n_tri & 0xffffu);
+}
+
+__device__ __forceinline__ bool occluded_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
+    const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    if (S.n_wnodes == 0u) return occluded_lane_from(S, active ? 0u : 0xffffffffu, o, d, inv, tnear, tfar);
+    uint32_t occ = 0u, lost = 0u;
+    Hit h;
+    wide_walk<true>(S, active, o, d, inv, tnear, tfar, h, occ, lost);
+#ifdef RS_WIDE_NO_FALLBACK
+    lost = 0u;
+#endif
+    if (__ballot(lost != 0u && occ == 0u) != 0)      // a dropped group: the skip-pointer walk decides
+        occ = occluded_lane_from(S, (lost != 0u && occ == 0u) ? 0u : 0xffffffffu, o, d, inv, tnear, tfar) ? 1u : occ;
+    return occ != 0u;
+}
 __device__ __forceinline__ Hit closest_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
-    closest_lane_from(S, active ? 0u : 0xffffffffu, o, d, inv, tnear, h);
+    if (S.n_wnodes == 0u) {
+        closest_lane_from(S, active ? 0u : 0xffffffffu, o, d, inv, tnear, h);
+        return h;
+    }
+    uint32_t occ = 0u, lost = 0u;
+    wide_walk<false>(S, active, o, d, inv, tnear, tfar, h, occ, lost);
+    if (__ballot(lost != 0u) != 0) closest_lane_from(S, lost != 0u ? 0u : 0xffffffffu, o, d, inv, tnear, h);
     return h;
 }
 

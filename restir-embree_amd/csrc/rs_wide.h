@@ -1,0 +1,136 @@
+// rs_wide.h -- host-side collapse of the PLOC tree into the 8-wide tree of the per-lane walks (plain C++:
+// rs_bvh_build.hip calls it after a build; tests/cpp/wide_harness.cpp checks its invariants on the CPU).
+#pragma once
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace rs {
+// ============================================================================================
+// 8-wide tree for the per-lane walks (rs_scene.h "8-wide per-lane walks").  Collapsed on the host from
+// the PLOC tree (its merge links), once per build: every wide node is a PLOC internal node whose up to 8
+// children come from opening, largest surface area first, the internal children of the node until there
+// are 8 (Wald et al. 2008 / Ylitie et al. 2017's greedy collapse).  Leaves hold ONE triangle.  Layout
+// (breadth-first, so a node's interior children are consecutive nodes and its leaf triangles consecutive
+// wide-leaf triangles): interior children occupy slots 0..ni-1, leaf children slots ni..nv-1.
+// Node = 5 x uint4 (80 B):
+//   w0 = origin o.xyz (float), ex | ey << 8 | ez << 16 | ni << 24 | nv << 28
+//   w1 = child_base, tri_base, qlo.x[0..3], qlo.x[4..7]      (q: one byte per slot)
+//   w2 = qlo.y[0..3], qlo.y[4..7], qlo.z[0..3], qlo.z[4..7]
+//   w3 = qhi.x[0..3], qhi.x[4..7], qhi.y[0..3], qhi.y[4..7]
+//   w4 = qhi.z[0..3], qhi.z[4..7], 0, 0
+// A child's box is o + q * s per axis, s = 2^(e - 127); o is a multiple of s, so every plane o + q*s is an
+// exact float, and the planes are rounded OUTWARD (lo down, hi up) from the exact child box: the walk's
+// box test is a superset of the exact one (results cannot change, rs_scene.h).
+// ============================================================================================
+namespace wide {
+struct WBox { float lo[3], hi[3]; };
+inline int h_f2i(float f) { int i; std::memcpy(&i, &f, 4); return i; }
+inline uint32_t h_f2u(float f) { uint32_t i; std::memcpy(&i, &f, 4); return i; }
+inline double exp2i(int e) { return std::ldexp(1.0, e); }
+// quantisation frame of one axis: s = 2^e >= extent / 255 and >= the float spacing at the box, o = a float
+// multiple of s <= lo with o + 255 s >= hi; every child box [clo, chi] quantises OUTWARD to bytes ql, qh with
+// o + ql s <= clo and o + qh s >= chi, all checked in double, where o, s and q are exact (the first k that
+// satisfies every check is taken)
+inline bool wide_axis(float lo, float hi, const float* clo, const float* chi, int nv, int& e, float& o, uint8_t* ql,
+                      uint8_t* qh) {
+    const double ext = (double)hi - (double)lo;
+    int k = -126;
+    if (ext > 0) { int x; std::frexp(ext / 255.0, &x); k = std::max(-126, x); }   // ext / 255 < 2^x
+    const float big = std::max(std::fabs(lo), std::fabs(hi));
+    if (big > 0) { int x; std::frexp((double)big, &x); k = std::max(k, x - 24); }  // ulp(big) <= 2^(x-24)
+    for (; k <= 127; ++k) {
+        const double sd = exp2i(k);
+        const float of = (float)(std::floor((double)lo / sd) * sd);
+        const double od = (double)of;
+        if (od > (double)lo || od + 255.0 * sd < (double)hi || std::floor(od / sd) * sd != od) continue;
+        bool ok = true;
+        for (int i = 0; i < nv && ok; ++i) {
+            // estimate in double (the difference chi - od may round), then step to the exact outward byte:
+            // od + q * sd is a multiple of sd no larger than the box, exact in double, so the tests are exact
+            double a = std::floor(((double)clo[i] - od) / sd), b = std::ceil(((double)chi[i] - od) / sd);
+            a = std::max(0.0, std::min(255.0, a)); b = std::max(0.0, std::min(255.0, b));
+            while (a > 0.0 && od + a * sd > (double)clo[i]) a -= 1.0;
+            while (b < 255.0 && od + b * sd < (double)chi[i]) b += 1.0;
+            ok = od + a * sd <= (double)clo[i] && od + b * sd >= (double)chi[i];
+            ql[i] = (uint8_t)a; qh[i] = (uint8_t)b;
+        }
+        if (ok) { e = k; o = of; return true; }
+    }
+    return false;
+}
+}  // namespace wide
+using namespace wide;
+
+// nlo / nhi: the PLOC nodes as 4 floats each (ids < n: primitives, hi.w = triangle index bits; ids >= n:
+// internal, lo.w / hi.w = left / right child id bits); out: 20 words per wide node
+inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, std::vector<uint32_t>& out,
+                           std::vector<int>& tri_prims, int& depth, std::string& err) {
+    out.clear(); tri_prims.clear(); depth = 0;
+    if (n <= 0) return 0;
+    auto is_prim = [&](int c) { return c < n; };
+    auto box = [&](int c) { WBox b; const float* a = nlo + 4 * (size_t)c; const float* z = nhi + 4 * (size_t)c;
+        for (int k = 0; k < 3; ++k) { b.lo[k] = a[k]; b.hi[k] = z[k]; } return b; };
+    auto area = [&](int c) { const float* a = nlo + 4 * (size_t)c; const float* z = nhi + 4 * (size_t)c;
+        const float ex = z[0] - a[0], ey = z[1] - a[1], ez = z[2] - a[2]; return ex * ey + ey * ez + ez * ex; };
+    std::vector<int> queue = {root}, level = {0};          // wide node i = PLOC node queue[i]
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const int c = queue[qi];
+        std::vector<int> kids;
+        if (is_prim(c)) kids = {c};
+        else kids = {h_f2i(nlo[4 * (size_t)c + 3]), h_f2i(nhi[4 * (size_t)c + 3])};
+        while (kids.size() < 8) {
+            int best = -1; float ba = -1.0f;
+            for (int i = 0; i < (int)kids.size(); ++i)
+                if (!is_prim(kids[i]) && area(kids[i]) > ba) { ba = area(kids[i]); best = i; }
+            if (best < 0) break;
+            const int x = kids[best];
+            kids.erase(kids.begin() + best);
+            kids.push_back(h_f2i(nlo[4 * (size_t)x + 3]));
+            kids.push_back(h_f2i(nhi[4 * (size_t)x + 3]));
+        }
+        std::stable_partition(kids.begin(), kids.end(), [&](int k) { return !is_prim(k); });
+        int ni = 0;
+        while (ni < (int)kids.size() && !is_prim(kids[ni])) ++ni;
+        const int nv = (int)kids.size();
+        const uint32_t child_base = (uint32_t)queue.size(), tri_base = (uint32_t)tri_prims.size();
+        for (int i = 0; i < ni; ++i) { queue.push_back(kids[i]); level.push_back(level[qi] + 1); depth = std::max(depth, level[qi] + 1); }
+        for (int i = ni; i < nv; ++i) tri_prims.push_back(h_f2i(nhi[4 * (size_t)kids[i] + 3]));
+        // quantisation frame from the union of the children (= the PLOC node's box)
+        WBox u = box(kids[0]);
+        for (int i = 1; i < nv; ++i) {
+            const WBox b = box(kids[i]);
+            for (int a = 0; a < 3; ++a) { u.lo[a] = std::min(u.lo[a], b.lo[a]); u.hi[a] = std::max(u.hi[a], b.hi[a]); }
+        }
+        int e[3]; float o[3];
+        uint8_t qlo[3][8] = {}, qhi[3][8] = {};
+        for (int a = 0; a < 3; ++a) {
+            if (!std::isfinite(u.lo[a]) || !std::isfinite(u.hi[a])) { err = "wide BVH: non-finite box"; return -1; }
+            float clo[8], chi[8];
+            for (int i = 0; i < nv; ++i) { const WBox b = box(kids[i]); clo[i] = b.lo[a]; chi[i] = b.hi[a]; }
+            if (!wide_axis(u.lo[a], u.hi[a], clo, chi, nv, e[a], o[a], qlo[a], qhi[a])) {
+                err = "wide BVH: no conservative quantisation"; return -1;
+            }
+        }
+        auto pack = [](const uint8_t* q, int first) {
+            return (uint32_t)q[first] | ((uint32_t)q[first + 1] << 8) | ((uint32_t)q[first + 2] << 16) | ((uint32_t)q[first + 3] << 24);
+        };
+        const uint32_t w[20] = {
+            h_f2u(o[0]), h_f2u(o[1]), h_f2u(o[2]),
+            (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16) | ((uint32_t)ni << 24) |
+                ((uint32_t)nv << 28),
+            child_base, tri_base, pack(qlo[0], 0), pack(qlo[0], 4),
+            pack(qlo[1], 0), pack(qlo[1], 4), pack(qlo[2], 0), pack(qlo[2], 4),
+            pack(qhi[0], 0), pack(qhi[0], 4), pack(qhi[1], 0), pack(qhi[1], 4),
+            pack(qhi[2], 0), pack(qhi[2], 4), 0u, 0u};
+        out.insert(out.end(), w, w + 20);
+        if (queue.size() >= (1u << 24)) { err = "wide BVH: too many nodes"; return -1; }
+    }
+    return 0;
+}
+
+
+}  // namespace rs

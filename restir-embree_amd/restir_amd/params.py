@@ -37,7 +37,7 @@ class FrameParams(ctypes.Structure):
         ("tfar_offset", ctypes.c_float),          # RenderParams::tfarOffset
         ("normal_offset", ctypes.c_float),        # RenderParams::normalOffset
         ("seed", ctypes.c_uint32),                # counter-RNG base seed (reference: mt19937{123})
-        ("reserved", ctypes.c_int32),
+        ("debug_reprojection", ctypes.c_int32),   # debugReprojection (:30, :647-689)
     ]
 
 
@@ -52,7 +52,7 @@ def default_params(**kw) -> FrameParams:
     p.bg_color[0] = p.bg_color[1] = p.bg_color[2] = 0.5
     p.tnear_offset, p.tfar_offset, p.normal_offset = 0.01, 0.001, 0.001
     p.seed = 123
-    p.reserved = 0
+    p.debug_reprojection = 0
     for k, v in kw.items():
         if k == "bg_color":
             for i in range(3):

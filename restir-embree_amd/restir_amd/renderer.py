@@ -531,9 +531,14 @@ class Renderer:
         return self.frame_data if copy_out else None
 
     def debug_trace(self, scene: Scene, o, d, tnear, tfar, any_hit: bool, lockstep: bool = True,
-                    stats: bool = False):
-        """Raw BVH queries.  stats=True: per-lane walk statistics instead -- returns
-        (visits, triangle_tests) int arrays per ray."""
+                    stats: bool = False, wide_stats: bool = False):
+        """Raw BVH queries.  stats=True: per-lane skip-pointer walk statistics instead -- returns
+        (visits, triangle_tests) int arrays per ray; wide_stats=True: the 8-wide walk's (node fetches,
+        triangle tests, stack overflow flags)."""
+        if wide_stats:
+            t, prim = self._debug_trace(scene, o, d, tnear, tfar, 7 if any_hit else 6)
+            p = prim.view(np.uint32)
+            return (p >> 16).astype(np.int64), (p & 0xFFFF).astype(np.int64), t
         if stats:
             t, prim = self._debug_trace(scene, o, d, tnear, tfar, 5 if any_hit else 4)
             p = prim.view(np.uint32)

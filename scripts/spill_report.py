@@ -14,7 +14,11 @@ PKG = os.path.join(ROOT, "restir-embree_amd")
 def flags():
     mk = open(os.path.join(PKG, "Makefile")).read()
     f = re.search(r"HIPFLAGS \?=(.*?)\n(?!\s)", mk, re.S).group(1).replace("\\\n", " ").replace("$(ARCH)", "gfx950")
-    return [x for x in f.split() if not x.startswith("-W")]
+    out = [x for x in f.split() if not x.startswith("-W")]
+    for extra in os.environ.get("EXTRA_FLAGS", "").split():   # e.g. EXTRA_FLAGS=-DRS_INITIAL_WAVES_LANE=6
+        name = extra.split("=")[0]
+        out = [x for x in out if x.split("=")[0] != name] + [extra]
+    return out
 
 
 def main():
@@ -38,6 +42,7 @@ def main():
         ops = [k for k, l in enumerate(body) if "scratch_load" in l or "scratch_store" in l]
         inner = sorted(min(hi - lo for lo, hi in loops if lo <= k <= hi) for k in ops
                        if any(lo <= k <= hi for lo, hi in loops))
+        vg = re.search(r"\.vgpr_count:\s+(\d+)", s[end:end + 200000])
         print(f"{name[:64]}: {len(ops)} scratch ops, {len(inner)} in loops (innermost loop lengths {inner[:16]})")
 
 

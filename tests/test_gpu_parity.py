@@ -615,3 +615,31 @@ def test_queued_initial_pass_bit_identical(which):
     for k, v in out.items():
         for f in range(3):
             assert np.array_equal(ref[f], v[f]), f"{which} {k} frame {f}"
+
+
+def test_debug_reprojection_matches_oracle():
+    """debugReprojection (pg/ReSTIRIntegrator.cpp:30, :647-689) on a moving camera with temporal + spatial
+    reuse: the rejection colours land in the G-buffer emission bit-exactly where the oracle puts them (all
+    four kinds occur), and the frames -- shaded from the painted G-buffer -- agree within tolerance.  A
+    partial tile refuses the flag (its marks can land on any pixel)."""
+    sc = scenes.sponza_like(target_tris=20_000, n_lamps=64)
+    prm, prm0 = P.c3_params(m_area=6, debug_reprojection=1), P.c3_params(m_area=6)
+    W, H = 96, 64
+    cams = [scenes.orbit_camera(sc.camera, 3 * f, 48, 0.6) for f in range(4)]
+    g, o, g0 = Renderer(W, H), O.OracleRenderer(W, H), Renderer(W, H)
+    gs, os_, gs0 = g.load_scene(sc), O.OracleScene(sc), g0.load_scene(sc)
+    colours = {(100.0, 100.0, 0.0), (0.0, 100.0, 0.0), (100.0, 0.0, 100.0), (0.0, 0.0, 100.0)}
+    seen = set()
+    for f, c in enumerate(cams):
+        a = g.produce_restir(gs, c, prm, f).copy()
+        b = o.render(os_, c, prm, f)
+        le_g, le_o = g.gbuffer()[..., 12:15], o.gbuffer()[..., 12:15]
+        assert np.array_equal(le_g, le_o), f"frame {f}: {int(np.any(le_g != le_o, -1).sum())} G emissions differ"
+        seen |= {tuple(map(float, v)) for v in le_g.reshape(-1, 3)} & colours
+        _assert_close(a, b, f"debug_reprojection frame {f}")
+        a0 = g0.produce_restir(gs0, c, prm0, f).copy()
+        if f > 0:
+            assert not np.array_equal(a, a0)          # the flag changes the picture
+    assert seen == colours, seen
+    with pytest.raises(RestirError):
+        g.tile_begin(gs, cams[0], prm, 0, 0, H // 2, 8, 5)
