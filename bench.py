@@ -226,15 +226,20 @@ def cpu_baseline(name, W, H, threads, budget_s=12.0):
 
 # ---------------------------------------------------------------- PMC figures committed under profiles/
 def pmc_for(name, W, H):
-    path = os.path.join(ROOT, "profiles", f"r02_pmc_{name}.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        with open(path) as f:
-            pmc = json.load(f)
-    except (OSError, ValueError):
-        return None
-    return pmc if pmc.get("config") == f"{name}_{W}x{H}" else None
+    """The newest committed PMC summary of this config (profiles/r03_pmc_<cfg>.json, else r02)."""
+    for rnd in ("r03", "r02"):
+        path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{name}.json")
+        if not os.path.exists(path):
+            continue
+        try:
+            with open(path) as f:
+                pmc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if pmc.get("config") == f"{name}_{W}x{H}":
+            pmc["_path"] = f"profiles/{rnd}_pmc_{name}.json"
+            return pmc
+    return None
 
 
 # ---------------------------------------------------------------- one single-GPU config
@@ -311,7 +316,7 @@ def run_single(name, W, H, steps, warmup, device, stream, cpu_threads, with_cpu,
         out["valu_issue"] = {"scope": "frame", "valu_per_frame": v, "achieved": round(v / (ms_per_step * 1e-3) / 1e9, 2),
                              "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
                              "frac": round(v / (ms_per_step * 1e-3) / 1e9 / VALU_PEAK_GIPS, 4),
-                             "source": os.path.basename(pmc.get("_path", f"profiles/r02_pmc_{name}.json"))}
+                             "source": pmc.get("_path")}
     out["cpu_baseline"] = cpu_baseline(name, W, H, cpu_threads) if with_cpu else None
     rr = (out["cpu_baseline"] or {}).get("reference_rays_per_frame")
     if rr:

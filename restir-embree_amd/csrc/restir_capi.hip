@@ -64,6 +64,12 @@ struct rs_scene {
     float* a_cdf = nullptr;
     int* a_cdf_guide = nullptr;
     int gen = 0;
+    // geometry generation (every rs_scene_update_positions; not a rebuild: same positions) and the
+    // generation the a_* copy (+ a_tri_nrm when those normals differ) holds as the previous geometry --
+    // a tile's temporal pass rebuilds a previous-frame G element against the previous frame's geometry
+    uint32_t geo_gen = 0, a_geo = 0xffffffffu;
+    float4* a_tri_nrm = nullptr;
+    bool a_nrm = false;
     hipEvent_t update_ev = nullptr;        // the last pipelined update (every later frame waits for it)
     bool update_recorded = false;
     float* d_nrm_stage = nullptr;
@@ -85,6 +91,16 @@ struct rs_scene {
         S.tri_uv = d_uv; S.tri_tan = d_tan; S.tex = d_tex; S.texd = d_texd; S.sky = sky;
         S.wnodes = wide_on ? wide.nodes : nullptr; S.wtris = wide.tris; S.n_wnodes = wide_on ? wide.n_nodes : 0u;
         return S;
+    }
+    // the geometry of generation `g` if this scene still holds it (current, or the a_* copy of g == a_geo)
+    bool dev_of(uint32_t g, DevScene& S) const {
+        S = dev();
+        if (g == geo_gen) return true;
+        if (g != a_geo || !a_nodes) return false;
+        S.nodes = a_nodes; S.tris = a_tris;
+        if (a_nrm) S.tri_nrm = a_tri_nrm;
+        S.wnodes = nullptr; S.n_wnodes = 0u;       // the refit binary tree of that generation
+        return true;
     }
 };
 
@@ -165,9 +181,18 @@ struct rs_context {
     const rs_scene* lane_scene[kLanes] = {};
     int lane_gen[kLanes] = {};
     hipEvent_t lane_done[kLanes] = {};
+    bool lane_prevgeo[kLanes] = {};        // the lane's last frame rebuilt G elements from the a_* geometry copy
+    // geometry generation of the last finished frame / the frame in progress (a tile's temporal rebuild of
+    // a previous-frame G element traces the previous frame's geometry, rs_scene::dev_of)
+    const rs_scene* geo_last_scene = nullptr;
+    uint32_t geo_last = 0, geo_prev = 0;
+    const rs_scene* geo_prev_scene = nullptr;
+    bool prevgeo_read = false;
+    uint64_t prevgeo_missing = 0;          // rebuilds that had to use the current geometry (two updates between frames)
     const rs_scene* frame_scene = nullptr;   // the frame in progress: scene and copy generation
     int frame_gen = 0;
     int trav = TRAV_LOCKSTEP;
+    bool twide = false;                    // the frame's scene has its 8-wide tree live (kernel template bit)
     bool tuning = false;
     hipEvent_t tune_ev[16] = {};           // tuning frame: events around each spatial kernel (halo exchanges excluded)
     int tune_n = 0;
@@ -739,9 +764,10 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     sync_all(c);                                // frames in flight, pipelined updates
     if (hipStreamSynchronize(st) != hipSuccess) { err = "stream sync failed"; return -1; }
     {
-        void* alt[] = {s->a_nodes, s->a_tris, s->a_emis, s->a_cdf, s->a_cdf_guide};
+        void* alt[] = {s->a_nodes, s->a_tris, s->a_emis, s->a_cdf, s->a_cdf_guide, s->a_tri_nrm};
         for (void* p : alt) if (p) hipFree(p);
-        s->a_nodes = s->a_tris = s->a_emis = nullptr; s->a_cdf = nullptr; s->a_cdf_guide = nullptr;
+        s->a_nodes = s->a_tris = s->a_emis = s->a_tri_nrm = nullptr; s->a_cdf = nullptr; s->a_cdf_guide = nullptr;
+        s->a_geo = 0xffffffffu; s->a_nrm = false;
         s->update_recorded = false;
     }
     void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide, s->d_emis_tri,
@@ -772,7 +798,7 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     hipEventRecord(e0, st);
     std::string berr;
     int rc = build_bvh(s->d_pos, n, st, &s->d_nodes, &s->n_nodes, &s->d_tris, &s->wide, berr);
-    s->wide_on = rc == 0 && s->wide.n_nodes > 0;   // deeper than the walk's stack: overflow falls back (rs_scene.h)
+    s->wide_on = rc == 0 && s->wide.n_nodes > 0 && s->wide.depth <= kWideStack;   // deeper: the skip pointers
     hipEventRecord(e1, st);
     if (rc == 0 && hipStreamSynchronize(st) == hipSuccess) hipEventElapsedTime(&s->build_ms, e0, e1);
     else { err = "BVH build failed: " + berr; rc = -1; }
@@ -934,31 +960,44 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
     float4 *nodes = s->d_nodes, *tris = s->d_tris, *em = s->d_emis;
     float* cdf = s->d_cdf;
     int* guide = s->d_cdf_guide;
+    const size_t bn = 2 * ((size_t)s->n_nodes + 1) * sizeof(float4), bt = 3 * (size_t)s->n_tris * sizeof(float4),
+                 be = 8 * (size_t)s->n_emis * sizeof(float4), bc = (size_t)std::max(1u, s->n_emis) * sizeof(float),
+                 bg = (kCdfGuide + 1) * sizeof(int), bnrm = 3 * (size_t)s->n_tris * sizeof(float4);
+    if (!s->a_nodes) {                           // the second copy, on first use: topology and tables copied
+        sync_all(c);
+        HIPCHK(c, hipMalloc(&s->a_nodes, bn));
+        HIPCHK(c, hipMalloc(&s->a_tris, bt));
+        HIPCHK(c, hipMalloc(&s->a_emis, std::max<size_t>(be, sizeof(float4))));
+        HIPCHK(c, hipMalloc(&s->a_cdf, bc));
+        HIPCHK(c, hipMalloc(&s->a_cdf_guide, bg));
+        HIPCHK(c, hipMemcpyAsync(s->a_nodes, s->d_nodes, bn, hipMemcpyDeviceToDevice, st));
+        HIPCHK(c, hipMemcpyAsync(s->a_tris, s->d_tris, bt, hipMemcpyDeviceToDevice, st));
+        if (be) HIPCHK(c, hipMemcpyAsync(s->a_emis, s->d_emis, be, hipMemcpyDeviceToDevice, st));
+        HIPCHK(c, hipMemcpyAsync(s->a_cdf, s->d_cdf, bc, hipMemcpyDeviceToDevice, st));
+        HIPCHK(c, hipMemcpyAsync(s->a_cdf_guide, s->d_cdf_guide, bg, hipMemcpyDeviceToDevice, st));
+    }
     if (pipelined) {
-        const size_t bn = 2 * ((size_t)s->n_nodes + 1) * sizeof(float4), bt = 3 * (size_t)s->n_tris * sizeof(float4),
-                     be = 8 * (size_t)s->n_emis * sizeof(float4), bc = (size_t)std::max(1u, s->n_emis) * sizeof(float),
-                     bg = (kCdfGuide + 1) * sizeof(int);
-        if (!s->a_nodes) {                       // the second copy, on first use: topology and tables copied
-            sync_all(c);
-            HIPCHK(c, hipMalloc(&s->a_nodes, bn));
-            HIPCHK(c, hipMalloc(&s->a_tris, bt));
-            HIPCHK(c, hipMalloc(&s->a_emis, std::max<size_t>(be, sizeof(float4))));
-            HIPCHK(c, hipMalloc(&s->a_cdf, bc));
-            HIPCHK(c, hipMalloc(&s->a_cdf_guide, bg));
-            HIPCHK(c, hipMemcpyAsync(s->a_nodes, s->d_nodes, bn, hipMemcpyDeviceToDevice, st));
-            HIPCHK(c, hipMemcpyAsync(s->a_tris, s->d_tris, bt, hipMemcpyDeviceToDevice, st));
-            if (be) HIPCHK(c, hipMemcpyAsync(s->a_emis, s->d_emis, be, hipMemcpyDeviceToDevice, st));
-            HIPCHK(c, hipMemcpyAsync(s->a_cdf, s->d_cdf, bc, hipMemcpyDeviceToDevice, st));
-            HIPCHK(c, hipMemcpyAsync(s->a_cdf_guide, s->d_cdf_guide, bg, hipMemcpyDeviceToDevice, st));
-        }
-        // every frame that read the copy about to be written has finished (a lane's frames in stream order)
+        // every frame that read the copy about to be written has finished (a lane's frames in stream order):
+        // the frames of that generation, and tile frames that rebuilt elements from it as the previous one
         for (int l = 0; l < kLanes; ++l)
-            if (c->lane_scene[l] == s && ((s->gen - c->lane_gen[l]) & 1) && c->lane_done[l])
+            if (c->lane_scene[l] == s && (((s->gen - c->lane_gen[l]) & 1) || c->lane_prevgeo[l]) && c->lane_done[l])
                 HIPCHK(c, hipStreamWaitEvent(st, c->lane_done[l], 0));
         nodes = s->a_nodes; tris = s->a_tris; em = s->a_emis; cdf = s->a_cdf; guide = s->a_cdf_guide;
+        s->a_nrm = false;
     } else {
         c->join_next = true;                     // the next frame's initial pass must see the new geometry
+        // in place (after every enqueued frame): the current geometry becomes the a_* copy first, so a
+        // tile's next temporal pass can still trace the previous frame's geometry
+        HIPCHK(c, hipMemcpyAsync(s->a_nodes, s->d_nodes, bn, hipMemcpyDeviceToDevice, st));
+        HIPCHK(c, hipMemcpyAsync(s->a_tris, s->d_tris, bt, hipMemcpyDeviceToDevice, st));
+        s->a_nrm = normals != nullptr;
+        if (s->a_nrm) {
+            if (!s->a_tri_nrm) HIPCHK(c, hipMalloc(&s->a_tri_nrm, bnrm));
+            HIPCHK(c, hipMemcpyAsync(s->a_tri_nrm, s->d_tri_nrm, bnrm, hipMemcpyDeviceToDevice, st));
+        }
     }
+    s->a_geo = s->geo_gen;                       // after the update: a_* = this generation, d_* = the next
+    s->geo_gen++;
     HIPCHK(c, hipMemcpyAsync(s->d_pos, s->h_stage[k], nf * sizeof(float), hipMemcpyHostToDevice, st));
     if (normals) {
         s->h_nrm.assign(normals, normals + nf);
@@ -1116,7 +1155,7 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     if (s->ctx) sync_all(s->ctx);
     void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
                     s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage, s->d_tex, s->d_texd, s->d_uv,
-                    s->d_tan, s->wide.nodes, s->wide.tris, s->a_nodes, s->a_tris, s->a_emis,
+                    s->d_tan, s->wide.nodes, s->wide.tris, s->a_tri_nrm, s->a_nodes, s->a_tris, s->a_emis,
                     s->a_cdf, s->a_cdf_guide};
     for (void* p : ptrs) if (p) hipFree(p);
     for (int k = 0; k < 2; ++k) {
@@ -1143,17 +1182,20 @@ extern "C" int rs_scene_info(const rs_scene* s, uint32_t* n_tris, uint32_t* n_em
 static dim3 grid_rows(int W, int ya, int yb) { return dim3((W + 15) / 16, (yb - ya + 15) / 16); }
 
 // launch kernel<Trav> for the frame's traversal kind
-#define LAUNCH_TRAV_ON(c, st, kernel, grid, ...)                                               \
-    do {                                                                                       \
-        if ((c)->trav == TRAV_LANE) kernel<TRAV_LANE><<<(grid), 256, 0, (st)>>>(__VA_ARGS__);   \
-        else kernel<TRAV_LOCKSTEP><<<(grid), 256, 0, (st)>>>(__VA_ARGS__);                     \
+// the kernel instantiation of the frame: walk kind | TRAV_WIDE when the scene's 8-wide tree is live
+// (rs_scene.h Trav; c->twide is taken from the scene when the frame begins)
+#define LAUNCH_TRAV_BS_ON(c, st, kernel, grid, bs, ...)                                                     \
+    do {                                                                                                   \
+        switch ((c)->trav | ((c)->twide ? TRAV_WIDE : 0)) {                                                \
+            case TRAV_LANE | TRAV_WIDE: kernel<TRAV_LANE | TRAV_WIDE><<<(grid), (bs), 0, (st)>>>(__VA_ARGS__); break; \
+            case TRAV_LANE: kernel<TRAV_LANE><<<(grid), (bs), 0, (st)>>>(__VA_ARGS__); break;                  \
+            case TRAV_WIDE: kernel<TRAV_LOCKSTEP | TRAV_WIDE><<<(grid), (bs), 0, (st)>>>(__VA_ARGS__); break;  \
+            default: kernel<TRAV_LOCKSTEP><<<(grid), (bs), 0, (st)>>>(__VA_ARGS__); break;                     \
+        }                                                                                                  \
     } while (0)
+#define LAUNCH_TRAV_ON(c, st, kernel, grid, ...) LAUNCH_TRAV_BS_ON(c, st, kernel, grid, 256, __VA_ARGS__)
 #define LAUNCH_TRAV(c, kernel, grid, ...) LAUNCH_TRAV_ON(c, (c)->fs, kernel, grid, __VA_ARGS__)
-#define LAUNCH_TRAV_BS(c, kernel, grid, bs, ...)                                                  \
-    do {                                                                                       \
-        if ((c)->trav == TRAV_LANE) kernel<TRAV_LANE><<<(grid), (bs), 0, (c)->fs>>>(__VA_ARGS__); \
-        else kernel<TRAV_LOCKSTEP><<<(grid), (bs), 0, (c)->fs>>>(__VA_ARGS__);                   \
-    } while (0)
+#define LAUNCH_TRAV_BS(c, kernel, grid, bs, ...) LAUNCH_TRAV_BS_ON(c, (c)->fs, kernel, grid, bs, __VA_ARGS__)
 
 // fold a finished frame's pass times (event-ring slot s) into the running totals
 static void fold_slot(rs_context* c, int s) {
@@ -1383,6 +1425,7 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     // updates, ...) simply runs on that stream (it is ordered after every earlier frame there); the next
     // frame on its lane then waits for it
     pick_traversal(c, s);
+    c->twide = s->wide_on;
     if (!c->fbs[c->li]) {                       // a lane's framebuffer, on first use: cleared on the context's
         const size_t bytes = (size_t)c->W * c->H * 3 * sizeof(float);   // stream, so this frame runs there too
         HIPCHK(c, hipMalloc(&c->fbs[c->li], bytes));
@@ -1438,6 +1481,7 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     if (c->fs != c->stream && c->prev_begin) HIPCHK(c, hipStreamWaitEvent(c->fs, c->prev_begin, 0));
     if (s->update_recorded) HIPCHK(c, hipStreamWaitEvent(c->fs, s->update_ev, 0));   // the scene copy it reads
     c->frame_scene = s; c->frame_gen = s->gen;
+    c->geo_prev = c->geo_last; c->geo_prev_scene = c->geo_last_scene; c->prevgeo_read = false;
     c->join_next = false;
     // (the frame's Counters need no memset: k_reduce_counts stores rays/primary, and the initial pass
     // zeroes reproj_outside before the temporal pass can count -- one API call less per frame)
@@ -1513,8 +1557,17 @@ extern "C" int rs_tile_temporal(rs_context* c) {
         // the previous frame's final reservoirs and G-buffer (another lane may still be finishing it)
         if (c->prev_done && c->fs != c->stream) HIPCHK(c, hipStreamWaitEvent(c->fs, c->prev_done, 0));
         const size_t npx = (size_t)c->W * c->H;
+        // a tile rebuilds previous-frame G elements beyond its rows with the previous frame's geometry
+        DevScene Sp = S;
+        const bool partial = c->F.gy0 > 0 || c->F.gy1 < c->H;
+        if (partial && c->geo_prev_scene == c->scene && c->geo_prev != c->scene->geo_gen) {
+            if (c->scene->dev_of(c->geo_prev, Sp)) c->prevgeo_read = true;
+            else { Sp = S; c->prevgeo_missing++; }     // two updates between frames: the a_* copy moved on
+            // the scene moved, so its 8-wide tree is off and the kernels walk Sp's binary tree
+            if (c->twide) return fail(c, RS_E_INVALID, "rs_tile_temporal: moved scene with a live 8-wide tree");
+        }
         if (c->F.debug_reproj) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 2 * npx, c->fs));
-        LAUNCH_TRAV(c, k_temporal, gb, S, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]},
+        LAUNCH_TRAV(c, k_temporal, gb, S, Sp, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]},
                     ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
         HIPCHK(c, hipGetLastError());
         if (c->F.debug_reproj) {
@@ -1554,16 +1607,18 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
         const bool cm = c->F.mis == MIS_CONSTANT;
         const bool tev = c->tuning && c->tune_n + 2 <= (int)(sizeof(c->tune_ev) / sizeof(c->tune_ev[0]));
         if (tev) HIPCHK(c, hipEventRecord(c->tune_ev[c->tune_n], c->fs));
+#define SPATIAL(TK, CM, SM) k_spatial<TK, CM, SM><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs)
         if (c->trav == TRAV_LANE) {
-            if (cm) k_spatial<TRAV_LANE, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
-            else k_spatial<TRAV_LANE, 0><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+            if (c->twide) { if (cm) SPATIAL(TRAV_LANE | TRAV_WIDE, 1, 0); else SPATIAL(TRAV_LANE | TRAV_WIDE, 0, 0); }
+            else { if (cm) SPATIAL(TRAV_LANE, 1, 0); else SPATIAL(TRAV_LANE, 0, 0); }
         } else if (grid_waves(gb) < (size_t)2 * c->wave_slots) {   // a small launch: RS_SPATIAL_WAVES_SMALL budget
-            if (cm) k_spatial<TRAV_LOCKSTEP, 1, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
-            else k_spatial<TRAV_LOCKSTEP, 0, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+            if (c->twide) { if (cm) SPATIAL(TRAV_WIDE, 1, 1); else SPATIAL(TRAV_WIDE, 0, 1); }
+            else { if (cm) SPATIAL(TRAV_LOCKSTEP, 1, 1); else SPATIAL(TRAV_LOCKSTEP, 0, 1); }
         } else {
-            if (cm) k_spatial<TRAV_LOCKSTEP, 1><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
-            else k_spatial<TRAV_LOCKSTEP, 0><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+            if (c->twide) { if (cm) SPATIAL(TRAV_WIDE, 1, 0); else SPATIAL(TRAV_WIDE, 0, 0); }
+            else { if (cm) SPATIAL(TRAV_LOCKSTEP, 1, 0); else SPATIAL(TRAV_LOCKSTEP, 0, 0); }
         }
+#undef SPATIAL
         if (tev) {
             HIPCHK(c, hipEventRecord(c->tune_ev[c->tune_n + 1], c->fs));
             c->tune_n += 2;
@@ -1603,6 +1658,8 @@ extern "C" int rs_tile_finish(rs_context* c, const float** band_rgb, rs_pass_tim
     HIPCHK(c, hipEventRecord(c->ev[EV_DONE], c->fs));
     c->last_done = c->ev[EV_DONE];
     c->lane_scene[c->li] = c->frame_scene; c->lane_gen[c->li] = c->frame_gen; c->lane_done[c->li] = c->ev[EV_DONE];
+    c->lane_prevgeo[c->li] = c->prevgeo_read;
+    c->geo_last = c->frame_scene ? c->frame_scene->geo_gen : 0; c->geo_last_scene = c->frame_scene;
     if (c->fs == c->stream && c->ahead > 0) c->lane_wait[c->li] = c->ev[EV_DONE];
     if (c->fs != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev[EV_DONE], 0));   // sequential semantics
     record_traversal_time(c);
@@ -1701,6 +1758,7 @@ extern "C" int rs_render_direct_mis(rs_context* c, const rs_scene* s, const rs_c
     hipEvent_t e0 = c->ev_gt[0], e1 = c->ev_gt[1];
     HIPCHK(c, hipEventRecord(e0, c->stream));
     pick_traversal(c, s);
+    c->twide = s->wide_on;
     c->tuning = false;               // the ReSTIR frames own the per-scene traversal tuning
     LAUNCH_TRAV(c, k_direct_mis, g, S, F, (int)spp, c->fb, count_slot(c, g));
     HIPCHK(c, hipGetLastError());
@@ -2018,13 +2076,15 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
             }
         }
         if (act) { prim_out[i] = (int32_t)((visits << 16) | (tris & 0xffff)); t_out[i] = occ ? 1.0f : 0.0f; }
-    } else if (any == 1 || any == 3) {
+    } else if (any == 1 || any == 3) {         // per-lane: the scene's walk (8-wide when live)
         bool occ = any == 1 ? trace_any<TRAV_LOCKSTEP>(S, act, O, D, tn[i], tf[i])
-                            : trace_any<TRAV_LANE>(S, act, O, D, tn[i], tf[i]);
+                            : (S.n_wnodes ? trace_any<TRAV_LANE | TRAV_WIDE>(S, act, O, D, tn[i], tf[i])
+                                          : trace_any<TRAV_LANE>(S, act, O, D, tn[i], tf[i]));
         if (act) { prim_out[i] = occ ? 1 : 0; t_out[i] = 0.0f; }
     } else {
         Hit h = any == 0 ? trace_closest<TRAV_LOCKSTEP>(S, act, O, D, tn[i], tf[i])
-                         : trace_closest<TRAV_LANE>(S, act, O, D, tn[i], tf[i]);
+                         : (S.n_wnodes ? trace_closest<TRAV_LANE | TRAV_WIDE>(S, act, O, D, tn[i], tf[i])
+                                       : trace_closest<TRAV_LANE>(S, act, O, D, tn[i], tf[i]));
         if (act) { prim_out[i] = h.prim; t_out[i] = h.prim >= 0 ? h.t : -1.0f; }
     }
 }

@@ -70,13 +70,14 @@ __device__ __forceinline__ vec3 mis_sample(const MisSurf& h, Rng& rng, vec3& f_r
 
 // DirectMISIntegrator::evaluateBRDFSample (pg/DirectMISIntegrator.cpp:94-144).  BRDF rays are
 // incoherent: per-lane walk (as brdf_sample in the ReSTIR passes).
+template <int T>
 __device__ __forceinline__ vec3 mis_brdf_part(const DevScene& S, const FrameConst& F, const MisSurf& h, bool alive,
                                               Rng& rng, uint32_t& rays) {
     vec3 f_r;
     float pdf;
     vec3 wi = mis_sample(h, rng, f_r, pdf);
     rays += alive ? 1u : 0u;
-    SurfHit b = intersect<TRAV_LANE>(S, alive, h.pos + h.n * F.normal_off, wi, FLT_MIN + F.tnear_off);
+    SurfHit b = intersect<T | TRAV_LANE>(S, alive, h.pos + h.n * F.normal_off, wi, FLT_MIN + F.tnear_off);
     if (!b.hit) return mk(0, 0, 0);
     MatRec m = load_mat(S, b.mat);
     if (!(m.le.x + m.le.y + m.le.z > 0)) return mk(0, 0, 0);      // Material::isEmissive
@@ -150,7 +151,7 @@ __global__ void __launch_bounds__(256) k_direct_mis(DevScene S, FrameConst F, in
     Rng rng; rng.init(F.seed, F.frame, kPassMis, pix);
     vec3 acc = mk(0, 0, 0);
     for (int k = 0; k < spp; ++k) {
-        vec3 L = mk(0, 0, 0) + mis_brdf_part(S, F, h, surf, rng, rays);
+        vec3 L = mk(0, 0, 0) + mis_brdf_part<T>(S, F, h, surf, rng, rays);
         L = L + mis_light_part<T>(S, F, h, surf, rng, rays);
         acc = acc + (mk(0, 0, 0) + sanitize(L));                    // L_i_indirect (0) + L_i_direct
     }

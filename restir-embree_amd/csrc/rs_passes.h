@@ -46,7 +46,7 @@
 #ifndef RS_TEMPORAL_WAVES_LANE
 #define RS_TEMPORAL_WAVES_LANE RS_TEMPORAL_WAVES
 #endif
-#define RS_WAVES(T, lockstep, lane) ((T) == TRAV_LANE ? (lane) : (lockstep))
+#define RS_WAVES(T, lockstep, lane) (((T) & TRAV_LANE) ? (lane) : (lockstep))
 // area candidates whose shadow rays share one lockstep traversal (occluded_wave_multi); 4 measured on
 // C2 1080p: 694-698 frames/s at a 4-wave budget (700-704 with 2), 560 at 5 waves (register spills)
 #ifndef RS_RIS_BATCH
@@ -392,8 +392,7 @@ __device__ __forceinline__ Sample brdf_sample(const DevScene& S, const FrameCons
     rays += alive ? 1u : 0u;
     // BRDF-sampled directions are incoherent across a tile even when shadow rays are not: the
     // per-lane walk beats the lockstep union for them in either kind (C2: +3 %)
-    SurfHit h = intersect<TRAV_LANE>(S, alive, org, wi, FLT_MIN + F.tnear_off);
-    (void)T;
+    SurfHit h = intersect<T | TRAV_LANE>(S, alive, org, wi, FLT_MIN + F.tnear_off);
     W_out = 0.0f; mis_out = 0.0f;
     if (h.hit) {
         MatRec mr = load_mat(S, h.mat);
@@ -493,7 +492,7 @@ __device__ __forceinline__ Res initial_ris(const DevScene& S, const FrameConst& 
     if (__ballot(alive) == 0) return r;                                 // wave-uniform exit
     Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, pix);
     const bool tv = !F.do_vis_pass;
-    constexpr int kB = T == TRAV_LANE ? RS_RIS_BATCH_LANE : RS_RIS_BATCH;
+    constexpr int kB = trav_lane(T) ? RS_RIS_BATCH_LANE : RS_RIS_BATCH;
     float best_phat = 0.0f;
     if (F.m_area > 0) {
         // area candidates in batches of kB (area_batch: one walk per batch), then the reservoir updates
@@ -643,7 +642,7 @@ __global__ void __launch_bounds__(64 * kSplit, RS_WAVES(T, RS_INITIAL_WAVES, RS_
     const bool alive = pa.w != 0.0f;
     const int A = F.m_area, B = F.m_brdf, n = A + B;
     const bool tv = !F.do_vis_pass;
-    constexpr int kB = T == TRAV_LANE ? RS_RIS_BATCH_LANE : RS_RIS_BATCH;
+    constexpr int kB = trav_lane(T) ? RS_RIS_BATCH_LANE : RS_RIS_BATCH;
     int lo, hi;
     split_range(n, g, lo, hi);
     if (__ballot(alive) != 0) {                                         // wave-uniform
@@ -747,7 +746,9 @@ __device__ __forceinline__ bool reproject(const GCam& c, vec3 ws, int W, int H, 
 // temporalReusePass (pg/ReSTIRIntegrator.cpp:625-732).  The previous reservoir is read at the
 // CURRENT pixel (:641), the previous G-buffer at the reprojected pixel (:652).
 template <int T>
-__global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORAL_WAVES_LANE)) k_temporal(DevScene S, FrameConst F, GBuf G, GBuf Gp, ResBuf Rr, ResBuf Rl,
+// Sp: the previous frame's geometry (== S unless the scene moved since; rs_scene::dev_of), traced when a tile
+// rebuilds a previous-frame G element beyond its rows
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORAL_WAVES_LANE)) k_temporal(DevScene S, DevScene Sp, FrameConst F, GBuf G, GBuf Gp, ResBuf Rr, ResBuf Rl,
                                                   ResBuf Rw, CountSlot C) {
     const uint64_t t0 = wave_clock();
     int x, y;
@@ -768,7 +769,7 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
     const size_t q = ok && !q_out ? (size_t)qy * F.W + qx : p;
     GElem prev = Gp.load(q);
     if (__ballot(q_out) != 0) {
-        const GElem alt = gbuffer_fill_cam<T>(S, F, F.camp, F.inv_view_prev, qx, qy, q_out);
+        const GElem alt = gbuffer_fill_cam<T>(Sp, F, F.camp, F.inv_view_prev, qx, qy, q_out);
         if (q_out) { prev = alt; rays += 1u; atomicAdd(C.outside, 1ull); }
     }
     if (ok) {

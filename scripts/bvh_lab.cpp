@@ -448,8 +448,14 @@ static int wide_rec(const Tree& T, int c, const std::vector<char>& leafify, int 
     std::vector<int> kids = {T.n[c].l, T.n[c].r};
     while ((int)kids.size() < k) {          // open the largest interior child
         int best = -1; float ba = -1;
-        for (int i = 0; i < (int)kids.size(); ++i)
-            if (!leafify[kids[i]] && T.n[kids[i]].b.half_area() > ba) { ba = T.n[kids[i]].b.half_area(); best = i; }
+        static const int wh = getenv("WH") ? atoi(getenv("WH")) : 0;   // 0 area, 1 area x count, 2 area x log count
+        for (int i = 0; i < (int)kids.size(); ++i) {
+            if (leafify[kids[i]]) continue;
+            float v = T.n[kids[i]].b.half_area();
+            if (wh == 1) v *= (float)T.n[kids[i]].cnt;
+            if (wh == 2) v *= std::log2((float)T.n[kids[i]].cnt + 1.0f);
+            if (v > ba) { ba = v; best = i; }
+        }
         if (best < 0) break;
         int x = kids[best];
         kids.erase(kids.begin() + best);
@@ -562,14 +568,14 @@ static int group_depth(const Wide& Wd, const Ray& r, bool any) {
 struct WEmu { int iters = 0, tris = 0, lost = 0, occ = 0; int prim = -1; float t = 0; int maxsp = 0; };
 static inline float u2f_(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 static uint32_t emu_hits(const uint32_t* w, V3 o, V3 inv, float tnear, float tfar) {
-    const uint32_t eb = w[3];
+    const uint32_t eb = w[15];
     const float s[3] = {u2f_((eb & 0xffu) << 23), u2f_(((eb >> 8) & 0xffu) << 23), u2f_(((eb >> 16) & 0xffu) << 23)};
     const float iv[3] = {inv.x, inv.y, inv.z}, org[3] = {o.x, o.y, o.z};
     float a[3], b[3];
-    for (int k = 0; k < 3; ++k) { a[k] = s[k] * iv[k]; b[k] = (u2f_(w[k]) - org[k]) * iv[k]; }
+    for (int k = 0; k < 3; ++k) { a[k] = s[k] * iv[k]; b[k] = (u2f_(w[12 + k]) - org[k]) * iv[k]; }
     const float E = 2.384185791015625e-07f * std::fmax(std::fmax(std::fabs(b[0]), std::fabs(b[1])), std::fabs(b[2]));
-    const uint32_t lo[3][2] = {{w[6], w[7]}, {w[8], w[9]}, {w[10], w[11]}};
-    const uint32_t hi[3][2] = {{w[12], w[13]}, {w[14], w[15]}, {w[16], w[17]}};
+    const uint32_t lo[3][2] = {{w[0], w[1]}, {w[2], w[3]}, {w[4], w[5]}};
+    const uint32_t hi[3][2] = {{w[6], w[7]}, {w[8], w[9]}, {w[10], w[11]}};
     const float lo_k = 1.0f - 4.0f * FLT_EPSILON, hi_k = 1.0f + 4.0f * FLT_EPSILON;
     uint32_t hits = 0;
     for (int c = 0; c < 8; ++c) {
@@ -584,7 +590,7 @@ static uint32_t emu_hits(const uint32_t* w, V3 o, V3 inv, float tnear, float tfa
         const float t1 = std::fmin(std::fmin(std::fmin(tfar, tf[0]), tf[1]), tf[2]);
         if (std::fma(t0, lo_k, -E) <= std::fma(t1, hi_k, E)) hits |= 1u << c;
     }
-    return hits & ((1u << (w[3] >> 28)) - 1u);
+    return hits & ((1u << (w[15] >> 28)) - 1u);
 }
 static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& prims, const Ray& r, bool any, int K) {
     WEmu e;
@@ -600,7 +606,7 @@ static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& pri
         e.maxsp = std::max(e.maxsp, (int)st.size());
         const uint32_t* w = &W[20 * (size_t)node];
         uint32_t hits = emu_hits(w, r.o, inv, r.tn, tf);
-        uint32_t ni = (w[3] >> 24) & 0xfu, tm = hits >> ni, tb = w[5];
+        uint32_t ni = (w[15] >> 24) & 0xfu, tm = hits >> ni, tb = w[17];
         while (tm && !(any && e.occ)) {
             uint32_t j = __builtin_ctz(tm); tm &= tm - 1; ++e.tris;
             float t; int p = prims[tb + j];
@@ -610,7 +616,7 @@ static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& pri
             }
         }
         uint32_t ngm = (any && e.occ) ? 0u : (hits & ((1u << ni) - 1u));
-        if (ngm) { gb = w[4]; gm = ngm; }
+        if (ngm) { gb = w[16]; gm = ngm; }
         else if (!st.empty() && !(any && e.occ)) { uint32_t top = st.back(); st.pop_back(); gb = top >> 8; gm = top & 0xff; }
         else gm = 0;
     }

@@ -1,4 +1,5 @@
-"""Diagnostic: BVH walk statistics on the GPU BVH (rs_debug_trace stats modes) for the scenes' primary
+"""Diagnostic: BVH walk statistics on the GPU BVHs (rs_debug_trace stats modes: the skip-pointer walk's node
+visits and the 8-wide walk's node fetches) for the scenes' primary
 rays (closest hit) and one shadow ray per pixel to a random point on a random emissive triangle
 (any hit), in 8x8-tile (wave) order.  Prints mean / p95 node visits and triangle tests per ray and
 the per-wave maximum (what a per-lane walk pays).  Usage (GPU box): python scripts/bvh_stats.py"""
@@ -29,6 +30,13 @@ def shadow_rays(sc, o, d, t, hit, seed=1):
     return p.astype(np.float32), sd.astype(np.float32), np.where(hit, dist - 0.001, -1.0).astype(np.float32)
 
 
+def report_wide(name, fetches, tris, lost, active):
+    f, tr = fetches[active], tris[active]
+    wf = np.where(active, fetches, 0)[: (fetches.size // 64) * 64].reshape(-1, 64).max(1)
+    print(f"  {name:8s} rays={active.sum():8d} 8-wide node fetches mean={f.mean():6.1f} p95={np.percentile(f, 95):6.0f} "
+          f"wave-max mean={wf.mean():6.1f} | tri tests mean={tr.mean():5.2f} | stack overflows {int((lost[active] > 0).sum())}")
+
+
 def report(name, visits, tris, active):
     v, tr = visits[active], tris[active]
     wv = np.where(active, visits, 0)[: (visits.size // 64) * 64].reshape(-1, 64).max(1)
@@ -53,6 +61,10 @@ def main():
         so, sd, tf = shadow_rays(sc, o, d, t, hit)
         vis, tri = r.debug_trace(gs, so, sd, 0.01, tf, any_hit=True, stats=True)
         report("shadow", vis, tri, hit)
+        fe, tr, lost = r.debug_trace(gs, o, d, 0.01, 3.0e38, any_hit=False, wide_stats=True)
+        report_wide("primary", fe, tr, lost, np.ones_like(hit))
+        fe, tr, lost = r.debug_trace(gs, so, sd, 0.01, tf, any_hit=True, wide_stats=True)
+        report_wide("shadow", fe, tr, lost, hit)
 
 
 if __name__ == "__main__":

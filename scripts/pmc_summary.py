@@ -1,5 +1,5 @@
 """Summarise rocprofv3 --pmc passes (gpurun_out/pmc_<cfg>_{FETCH_SIZE,WRITE_SIZE,SQ_WAVES}/) into
-profiles/r02_pmc_<cfg>.json: per pass kernel the per-launch mean HBM bytes and SQ counters, and per
+profiles/<round>_pmc_<cfg>.json (round from $ROUND, default r03): per pass kernel the per-launch mean HBM bytes and SQ counters, and per
 frame (one launch of every pass kernel) the HBM bytes and VALU wave-instructions that bench.py reports.
 Units and gfx950 correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB; FETCH_SIZE
 reads 1/2 of a wide streaming read's bytes on gfx950, so hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024
@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
 W, H = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (1920, 1080)
 src = os.path.join(ROOT, "gpurun_out")
-out = os.path.join(ROOT, "profiles", f"r02_pmc_{cfg}.json")
+ROUND = os.environ.get("ROUND", "r03")
+out = os.path.join(ROOT, "profiles", f"{ROUND}_pmc_{cfg}.json")
 px = W * H
 PASS = ("k_gbuffer_initial", "k_visibility", "k_temporal", "k_spatial", "k_shade")
 
@@ -35,7 +36,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
             if k in PASS:
                 vals[k][c].append(float(row["Counter_Value"]))
 res = {"config": f"{cfg}_{W}x{H}", "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE / --pmc SQ_* (separate "
-       f"runs), RESTIR_RUNAHEAD=0, bench.py --scene {cfg} --steps 3 --warmup 1 (scripts/gpu_profile_r02.sh)",
+       f"runs), RESTIR_RUNAHEAD=0, bench.py --scene {cfg} --steps 3 --warmup 1 (scripts/gpu_profile_{ROUND}.sh)",
        "kernels": {}}
 for k, d in vals.items():
     fe = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
@@ -53,6 +54,31 @@ if os.path.exists(sq_csv):   # SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* / SQ_WAIT_* are
     for k, d in sq.items():
         if k in res["kernels"]:
             res["kernels"][k]["sq"] = {c: round(sum(v) / len(v), 1) for c, v in d.items()}
+ta_csv = os.path.join(src, f"pmc_{cfg}_SQ_INSTS_VMEM_RD", "run_counter_collection.csv")
+if os.path.exists(ta_csv):   # vector-memory pipeline group: per-launch means, and derived ratios
+    ta = collections.defaultdict(lambda: collections.defaultdict(list))
+    with open(ta_csv) as f:
+        for row in csv.DictReader(f):
+            ta[kname(row)][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    for k, d in ta.items():
+        if k not in res["kernels"]:
+            continue
+        m = {c: sum(v) / len(v) for c, v in d.items()}
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS item): per-XCD active cycles
+        g = max(1.0, m.get("GRBM_GUI_ACTIVE", 0.0) / 8.0)
+        res["kernels"][k]["vmem"] = {c: round(v, 1) for c, v in m.items()}
+        # TA/TD busy are summed over the 256 CUs' units: per-unit fraction of the kernel's active cycles
+        cus = 256.0
+        res["kernels"][k]["vmem_derived"] = {
+            "ta_busy_frac": round(m.get("TA_TA_BUSY", 0.0) / cus / g, 4),
+            "td_busy_frac": round(m.get("TD_TD_BUSY", 0.0) / cus / g, 4),
+            "valu_issue_frac": round(m.get("SQ_INSTS_VALU", 0.0) / (1024.0 * g / 2.0), 4),
+            "cache_accesses_per_vmem_rd": round(m.get("TCP_TOTAL_CACHE_ACCESSES", 0.0) / max(1.0, m.get("SQ_INSTS_VMEM_RD", 0.0)), 2),
+            "tcp_tcc_read_req": m.get("TCP_TCC_READ_REQ"),
+            "wait_any_over_wave_cycles": round(m.get("SQ_WAIT_ANY", 0.0) / max(1.0, m.get("SQ_WAVE_CYCLES", 0.0)), 4),
+            "note": "busy fractions: TA_TA_BUSY / TD_TD_BUSY / 256 CUs / (GRBM_GUI_ACTIVE / 8 XCDs); VALU issue: "
+                    "SQ_INSTS_VALU / (1024 SIMDs x active cycles / 2 cycles per wave64 instruction); cache accesses per "
+                    "vector load instruction = TCP_TOTAL_CACHE_ACCESSES / SQ_INSTS_VMEM_RD"}
 # one frame = one launch of each pass kernel present
 res["frame_bytes"] = sum(v["hbm_bytes_corrected"] for v in res["kernels"].values())
 res["frame_valu"] = sum(v.get("sq", {}).get("SQ_INSTS_VALU", 0.0) for v in res["kernels"].values()) or None

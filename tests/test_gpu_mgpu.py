@@ -117,3 +117,49 @@ def test_local_mgpu_transfer_stats():
     assert st["halo_ms"] > 0 and st["gather_ms"] > 0
     assert m.stats()["frames"] == 0
     m.close()
+
+
+@pytest.mark.parametrize("pipelined", [True, False])
+def test_local_mgpu_moving_geometry_rebuilds_previous_geometry(pipelined):
+    """Tiles whose temporal reprojection falls beyond their rows rebuild the previous frame's G element --
+    against the PREVIOUS frame's geometry when the scene moved in between (rs_scene::dev_of: the a_* copy
+    of the pipelined update, or the copy an in-place update makes first).  The whole scene moves every
+    frame and the camera steps far with margin = halo, so rebuilds happen and every rebuilt element sees
+    moved geometry; frames must equal the single context's bit for bit.  pipelined=False: run-ahead 0
+    and updates with normals (the in-place path)."""
+    W, H, world = 96, 64, 4
+    sc = scenes.cornell_box(8)
+    prm = P.c3_params(m_area=6)
+    cams = [scenes.orbit_camera(sc.camera, 3 * f, 48, 0.6) for f in range(5)]
+    base = np.asarray(sc.positions, np.float32)
+    def pos(f):
+        p = base.reshape(-1, 3, 3).copy()
+        p[..., 2] += np.float32(0.02 * f)
+        p[..., 0] += np.float32(0.01 * f)
+        return p.reshape(-1, 9)
+    nrm = None if pipelined else sc.normals
+
+    def setup(r):
+        if not pipelined:
+            r.set_run_ahead(0)
+        r.set_traversal("lockstep")
+        return r
+    g = setup(Renderer(W, H))
+    gs = g.load_scene(sc)
+    ref = []
+    for f, c in enumerate(cams):
+        gs.update_positions(pos(f), nrm)
+        ref.append(g.produce_restir(gs, c, prm, f).copy())
+    rs = [setup(Renderer(W, H)) for _ in range(world)]
+    ss = [r.load_scene(sc) for r in rs]
+    m = MultiGpuFrame(rs)
+    for r in rs:
+        r.timing_totals(reset=True)
+    for f, c in enumerate(cams):
+        for s in ss:
+            s.update_positions(pos(f), nrm)
+        img = m.render(ss, c, prm, f, copy_out=True)
+        assert np.array_equal(img, ref[f]), f"frame {f}: {int(np.any(img != ref[f], -1).sum())} px differ"
+    outside = sum(int(r.timing_totals()[0].reproj_outside) for r in rs)
+    assert outside > 0
+    m.close()
