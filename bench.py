@@ -155,9 +155,11 @@ def baseline_threads(requested):
 def cpu_baseline(name, W, H, threads, budget_s=12.0):
     """The oracle (plain-C OpenMP restatement of the reference path, oracle/restir_oracle.c) timed on this
     host, on a bounded sample of the same workload: whole frames for C1/C2/C2V (median, after a warm-up
-    frame); for C3/C5 (~10-40 s per 1080p frame on 16 cores) a centred band of rows rendered through the
+    frame); for C3/C5 (seconds per 1080p frame) a centred quarter-frame band of rows rendered through the
     oracle's tile stages (G-buffer + initial + temporal + spatial + shade of the band; the first frame
-    only builds the temporal history), scaled to the full frame by rows."""
+    only builds the temporal history), scaled to the full frame by rows.  Ray queries walk the oracle's
+    8-wide tree with AVX2 box tests (or_scene_set_wide, SURVEY.md §8(d)'s SIMD-friendly traversal;
+    the same hits as its binary walk, tests/test_oracle.py)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     oracle_lib.build()
@@ -166,17 +168,18 @@ def cpu_baseline(name, W, H, threads, budget_s=12.0):
     L.or_set_num_threads(n_threads)
     sc, prm, camera, light_pos = workload(name)
     cam = camera or (lambda f: sc.camera)
-    osc = oracle_lib.OracleScene(sc)
+    osc = oracle_lib.OracleScene(sc, wide=True)
     times, rays, band_t, refr = [], [], [], []
     t_start = time.perf_counter()
     if name in ("C3", "C5"):
-        rows = max(8, H // (16 if name == "C3" else 8))
+        rows = max(8, H // 4)
         y0 = (H - rows) // 2
         be = oracle_lib.OracleTileBackend(W, H)
         halo = int(np.floor(np.sqrt(np.float32(prm.spatial_radius), dtype=np.float32)))
         for f in range(6):
             if light_pos is not None:
-                osc = oracle_lib.OracleScene(type(sc)(light_pos(f), sc.normals, sc.tri_material, sc.materials, sc.camera))
+                osc = oracle_lib.OracleScene(type(sc)(light_pos(f), sc.normals, sc.tri_material, sc.materials, sc.camera),
+                                             wide=True)
             t0 = time.perf_counter()
             be.begin(osc, cam(f), prm, f, y0, y0 + rows, halo, halo)
             be.temporal()
@@ -212,8 +215,10 @@ def cpu_baseline(name, W, H, threads, budget_s=12.0):
         mr = float(np.median([r / t for r, t in zip(rays, times)])) / 1e6
     dt = float(np.median(times))
     out = {"value": round(1.0 / dt, 5), "unit": "frames/s", "cores": n_threads, "kind": "port",
-           "sample": f"{sample}; oracle/restir_oracle.c (OpenMP, {n_threads} threads, scalar binary SAH BVH -- "
-                     f"not Embree's 4/8-wide SIMD BVH: the GPU/CPU ratio overstates the gap to an Embree-class CPU)",
+           "sample": f"{sample}; oracle/restir_oracle.c (OpenMP, {n_threads} threads; ray queries walk an 8-wide "
+                     f"tree with AVX2 box tests{'' if osc.wide else ' -- NOT available on this host: binary walk'}, "
+                     f"shading scalar)",
+           "traversal": "8-wide AVX2" if osc.wide else "binary scalar",
            "s_per_frame": round(dt, 4), "band": band, "host": host_cpu(),
            "timing_scope": "all passes of produceRestir (pg/simpleguidx11.cpp:361-486 totalFrameDuration), no post-frame"}
     if mr is not None:
@@ -240,6 +245,24 @@ def pmc_for(name, W, H):
             pmc["_path"] = f"profiles/{rnd}_pmc_{name}.json"
             return pmc
     return None
+
+
+def limiter_for(pmc, kernel):
+    """What bounds `kernel` by its committed PMC passes (scripts/pmc_summary.py vmem_derived): the busiest
+    of the texture-address (TA) and texture-data (TD) units and the VALU issue rate, each a fraction of
+    the kernel's active cycles, with the HBM fraction beside them (these walks are far from HBM-bound)."""
+    k = ((pmc or {}).get("kernels", {}) or {}).get(kernel) or {}
+    v = k.get("vmem_derived")
+    if not v:
+        return None
+    unit = {"ta_busy_frac": "TA (vector-memory address processing)",
+            "td_busy_frac": "TD (vector-memory data return)",
+            "valu_issue_frac": "VALU issue"}
+    fr = {u: float(v[u]) for u in unit if v.get(u) is not None}
+    top = max(fr, key=fr.get)
+    return {"kernel": kernel, "bound_by": unit[top], **{u: round(x, 4) for u, x in fr.items()},
+            "wait_any_over_wave_cycles": v.get("wait_any_over_wave_cycles"),
+            "cache_lines_per_vmem_load": v.get("cache_accesses_per_vmem_rd"), "source": pmc.get("_path")}
 
 
 # ---------------------------------------------------------------- one single-GPU config
@@ -311,6 +334,7 @@ def run_single(name, W, H, steps, warmup, device, stream, cpu_threads, with_cpu,
                             if pmc else None,
                             "timing": f"HIP events on the frame's stream, {kn} frames with one frame in flight"},
     }
+    out["limiter"] = limiter_for(pmc, PASS_KERNEL[dom])
     if pmc and pmc.get("frame_valu"):
         v = float(pmc["frame_valu"])
         out["valu_issue"] = {"scope": "frame", "valu_per_frame": v, "achieved": round(v / (ms_per_step * 1e-3) / 1e9, 2),

@@ -34,6 +34,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <float.h>
+#include <immintrin.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -254,6 +255,7 @@ typedef struct {
     float total_area;
     /* BVH */
     or_node* nodes; int n_nodes; uint32_t* tri_index;
+    struct or_wnode* wn; int n_wn;   /* 8-wide tree over the same leaves (or_scene_set_wide), or NULL */
     /* textures: per-material map slots (0-based, -1 none: diffuse, specular,
        shininess, normal), per-triangle uv (6) / tangents (9), textures in FreeImage layout, sky */
     int32_t* maps; float* uv; float* tan;
@@ -412,6 +414,7 @@ or_scene* or_scene_create(uint32_t n_tris, const float* pos, const float* nrm, c
 
 void or_scene_destroy(or_scene* s) {
     if (!s) return;
+    free(s->wn);
     free(s->p0); free(s->p1); free(s->p2); free(s->n0); free(s->n1); free(s->n2);
     free(s->mat); free(s->emis_id); free(s->mats); free(s->emis_tri); free(s->cdf);
     free(s->pick_pdf); free(s->area); free(s->nodes); free(s->tri_index);
@@ -586,9 +589,12 @@ static inline int box_hit(const or_node* n, v3 o, v3 inv, float tnear, float tfa
 
 typedef struct { int hit; float t, u, v; uint32_t prim; } or_hit;
 
+static or_hit closest_hit_wide(const or_scene* s, v3 o, v3 d, float tnear, float tfar);
+static int any_hit_wide(const or_scene* s, v3 o, v3 d, float tnear, float tfar);
 static or_hit closest_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
     or_hit h = {0, tfar, 0, 0, 0xffffffffu};
     if (!s->n_nodes) return h;
+    if (s->wn) return closest_hit_wide(s, o, d, tnear, tfar);
     v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     int stack[128]; int sp = 0; stack[sp++] = 0;
     while (sp) {
@@ -613,6 +619,7 @@ static or_hit closest_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar
 
 static int any_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
     if (!s->n_nodes) return 0;
+    if (s->wn) return any_hit_wide(s, o, d, tnear, tfar);
     v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     int stack[128]; int sp = 0; stack[sp++] = 0;
     while (sp) {
@@ -629,6 +636,134 @@ static int any_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
         }
     }
     return 0;
+}
+
+/* ---- 8-wide walks (the CPU baseline's SIMD traversal; not part of the restatement:
+ * any tree finds the same hits).  The binary tree collapsed like the product's wide tree (csrc/rs_wide.h:
+ * a wide node's up to 8 children come from opening the largest-area interior child), children kept as
+ * the binary nodes' exact boxes in SoA and tested 8 at a time with box_hit's float operations (fminf /
+ * fmaxf NaN rules included); leaf children are the binary leaves (<= 4 triangles each). */
+typedef struct or_wnode { float lo[3][8], hi[3][8]; int32_t kid[8]; uint32_t valid; } or_wnode;  /* kid < 0: leaf ~node */
+enum { OR_WSTACK = 512 };
+
+int or_scene_set_wide(or_scene* s, int on) {
+    free(s->wn); s->wn = NULL; s->n_wn = 0;
+    if (!on || !s->n_nodes || !__builtin_cpu_supports("avx2")) return 0;
+    or_wnode* W = calloc((size_t)s->n_nodes, sizeof(or_wnode));
+    int* q = malloc((size_t)s->n_nodes * sizeof(int));
+    int* lvl = malloc((size_t)s->n_nodes * sizeof(int));
+    int nq = 1, depth = 0;
+    q[0] = 0; lvl[0] = 0;
+    for (int qi = 0; qi < nq; ++qi) {
+        const or_node* b = &s->nodes[q[qi]];
+        int kids[8], nk = 0;
+        if (b->count) kids[nk++] = q[qi]; else { kids[nk++] = b->left; kids[nk++] = b->right; }
+        while (nk < 8) {
+            int best = -1; float ba = -1.0f;
+            for (int i = 0; i < nk; ++i) {
+                const or_node* k = &s->nodes[kids[i]];
+                aabb bb; memcpy(bb.lo, k->lo, sizeof bb.lo); memcpy(bb.hi, k->hi, sizeof bb.hi);
+                if (!k->count && bb_area(&bb) > ba) { ba = bb_area(&bb); best = i; }
+            }
+            if (best < 0) break;
+            const or_node* x = &s->nodes[kids[best]];
+            kids[best] = x->left; kids[nk++] = x->right;
+        }
+        or_wnode* w = &W[qi];
+        for (int c = 0; c < 8; ++c)
+            for (int a = 0; a < 3; ++a) { w->lo[a][c] = 0.0f; w->hi[a][c] = 0.0f; }
+        for (int c = 0; c < nk; ++c) {
+            const or_node* k = &s->nodes[kids[c]];
+            for (int a = 0; a < 3; ++a) { w->lo[a][c] = k->lo[a]; w->hi[a][c] = k->hi[a]; }
+            if (k->count) w->kid[c] = ~kids[c];
+            else { w->kid[c] = nq; lvl[nq] = lvl[qi] + 1; if (lvl[nq] > depth) depth = lvl[nq]; q[nq++] = kids[c]; }
+            w->valid |= 1u << c;
+        }
+    }
+    free(q); free(lvl);
+    if (7 * (depth + 1) + 1 > OR_WSTACK) { free(W); return 0; }   /* the walks' fixed stacks */
+    s->wn = W; s->n_wn = nq;
+    return 1;
+}
+
+/* box_hit for the 8 children: bit c = child c accepted; tentry[c] = its entry t */
+__attribute__((target("avx2"))) static inline uint32_t box8(const or_wnode* w, const __m256* O, const __m256* I,
+                                                              float tnear, float tfar, float* tentry) {
+    __m256 t0 = _mm256_set1_ps(tnear), t1 = _mm256_set1_ps(tfar);
+    for (int a = 0; a < 3; ++a) {
+        const __m256 ta = _mm256_mul_ps(_mm256_sub_ps(_mm256_loadu_ps(w->lo[a]), O[a]), I[a]);
+        const __m256 tb = _mm256_mul_ps(_mm256_sub_ps(_mm256_loadu_ps(w->hi[a]), O[a]), I[a]);
+        const __m256 nb = _mm256_cmp_ps(tb, tb, _CMP_UNORD_Q);
+        /* fminf / fmaxf(ta, tb): the non-NaN operand if one is NaN (min_ps/max_ps return tb then) */
+        const __m256 mn = _mm256_blendv_ps(_mm256_min_ps(ta, tb), ta, nb);
+        const __m256 mx = _mm256_blendv_ps(_mm256_max_ps(ta, tb), ta, nb);
+        t0 = _mm256_max_ps(mn, t0);   /* fmaxf(t0, mn): t0 when mn is NaN */
+        t1 = _mm256_min_ps(mx, t1);
+    }
+    _mm256_storeu_ps(tentry, t0);
+    const __m256 ok = _mm256_cmp_ps(_mm256_mul_ps(t0, _mm256_set1_ps(1.0f - 4.0f * FLT_EPSILON)),
+                                    _mm256_mul_ps(t1, _mm256_set1_ps(1.0f + 4.0f * FLT_EPSILON)), _CMP_LE_OQ);
+    return (uint32_t)_mm256_movemask_ps(ok) & w->valid;
+}
+
+__attribute__((target("avx2"))) static int any_hit_wide(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
+    const v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const __m256 O[3] = {_mm256_set1_ps(o.x), _mm256_set1_ps(o.y), _mm256_set1_ps(o.z)};
+    const __m256 I[3] = {_mm256_set1_ps(inv.x), _mm256_set1_ps(inv.y), _mm256_set1_ps(inv.z)};
+    int stack[OR_WSTACK]; int sp = 0; stack[sp++] = 0;
+    float te[8];
+    while (sp) {
+        const or_wnode* w = &s->wn[stack[--sp]];
+        uint32_t m = box8(w, O, I, tnear, tfar, te);
+        while (m) {
+            const int c = __builtin_ctz(m); m &= m - 1;
+            const int32_t k = w->kid[c];
+            if (k >= 0) { stack[sp++] = k; continue; }
+            const or_node* n = &s->nodes[~k];
+            for (int i = n->first; i < n->first + n->count; ++i) {
+                float tt, uu, vv;
+                if (tri_hit(s, s->tri_index[i], o, d, tnear, tfar, &tt, &uu, &vv)) return 1;
+            }
+        }
+    }
+    return 0;
+}
+
+/* closest hit: leaves tested when met, interior children pushed farthest first (nearest popped next, so
+ * the running t culls more of the rest) */
+__attribute__((target("avx2"))) static or_hit closest_hit_wide(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
+    or_hit h = {0, tfar, 0, 0, 0xffffffffu};
+    const v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const __m256 O[3] = {_mm256_set1_ps(o.x), _mm256_set1_ps(o.y), _mm256_set1_ps(o.z)};
+    const __m256 I[3] = {_mm256_set1_ps(inv.x), _mm256_set1_ps(inv.y), _mm256_set1_ps(inv.z)};
+    int stack[OR_WSTACK]; int sp = 0; stack[sp++] = 0;
+    float te[8];
+    while (sp) {
+        const or_wnode* w = &s->wn[stack[--sp]];
+        uint32_t m = box8(w, O, I, tnear, h.t, te);
+        int near[8]; int nn = 0;
+        while (m) {
+            const int c = __builtin_ctz(m); m &= m - 1;
+            const int32_t k = w->kid[c];
+            if (k >= 0) {   /* insertion by entry t, descending */
+                int j = nn++;
+                while (j > 0 && te[near[j - 1]] < te[c]) { near[j] = near[j - 1]; --j; }
+                near[j] = c;
+                continue;
+            }
+            const or_node* n = &s->nodes[~k];
+            for (int i = n->first; i < n->first + n->count; ++i) {
+                uint32_t t = s->tri_index[i]; float tt, uu, vv;
+                if (tri_hit(s, t, o, d, tnear, h.t, &tt, &uu, &vv)) {
+                    if (!h.hit || tt < h.t || (tt == h.t && t < h.prim)) {
+                        h.hit = 1; h.t = tt; h.u = uu; h.v = vv; h.prim = t;
+                    }
+                }
+            }
+        }
+        for (int j = 0; j < nn; ++j) stack[sp++] = w->kid[near[j]];
+    }
+    return h;
 }
 
 /* ------------------------------------------------------------------ params / buffers */

@@ -215,7 +215,7 @@ __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i,
 // 32-B node loads per C3 shadow ray, and the per-lane walks are bound by those lane-loads and the VALU of
 // one box test per step.  The 8-wide tree (rs_bvh_build.hip build_wide: 80-B nodes
 // holding the quantised boxes of up to 8 children) tests all children of a node per fetch: ~14 node
-// fetches per shadow ray (72 B each, 16-B aligned loads), i.e. about half the lane-loads, a fifth of the
+// fetches per shadow ray (5 x 16-B loads each), i.e. about half the lane-loads, a fifth of the
 // dependent-load chain, and 8 box tests per fetch that share the node's per-axis setup.
 // Traversal: a group = (first interior child node, mask of its hit slots still to visit); a step pops one
 // slot from the current group (pushing the rest on a short per-lane register stack), fetches that node,
@@ -259,16 +259,15 @@ struct WideStack {
     }
 };
 __device__ __forceinline__ float ubyte_f(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xffu); }
-// the 8 child boxes of a node (q words Q0..Q2, header H = origin + exponents/counts) against the ray;
-// bit c = slot c hit (valid slots only)
-__device__ __forceinline__ uint32_t wide_hits(uint4 Q0, uint4 Q1, uint4 Q2, uint4 H, vec3 o, vec3 inv, float tnear,
-                                              float tfar) {
-    const uint32_t eb = H.w;
+// the 8 child boxes of node (w0..w4) against the ray; bit c = slot c hit (valid slots only)
+__device__ __forceinline__ uint32_t wide_hits(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, vec3 o, vec3 inv,
+                                              float tnear, float tfar) {
+    const uint32_t eb = w0.w;
     const vec3 s = mk(__uint_as_float((eb & 0xffu) << 23), __uint_as_float(((eb >> 8) & 0xffu) << 23),
                       __uint_as_float(((eb >> 16) & 0xffu) << 23));
     const vec3 a = mk(s.x * inv.x, s.y * inv.y, s.z * inv.z);                 // exact (power-of-two scale)
-    const vec3 b = mk((__uint_as_float(H.x) - o.x) * inv.x, (__uint_as_float(H.y) - o.y) * inv.y,
-                      (__uint_as_float(H.z) - o.z) * inv.z);
+    const vec3 b = mk((__uint_as_float(w0.x) - o.x) * inv.x, (__uint_as_float(w0.y) - o.y) * inv.y,
+                      (__uint_as_float(w0.z) - o.z) * inv.z);
     // per axis the near (far) t lowered (raised) by 2^-22 |b|: the rounding of b and of b -+ that bound
     // (an axis the ray is almost parallel to has a huge |b| and widens only itself)
     const float ex = 2.384185791015625e-07f * fabsf(b.x), ey = 2.384185791015625e-07f * fabsf(b.y),
@@ -276,9 +275,9 @@ __device__ __forceinline__ uint32_t wide_hits(uint4 Q0, uint4 Q1, uint4 Q2, uint
     const vec3 bn = mk(b.x - ex, b.y - ey, b.z - ez), bf = mk(b.x + ex, b.y + ey, b.z + ez);
     // near / far planes per axis by the direction's sign (lo bytes near for a positive direction)
     const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
-    const uint32_t nx0 = px ? Q0.x : Q1.z, nx1 = px ? Q0.y : Q1.w, fx0 = px ? Q1.z : Q0.x, fx1 = px ? Q1.w : Q0.y;
-    const uint32_t ny0 = py ? Q0.z : Q2.x, ny1 = py ? Q0.w : Q2.y, fy0 = py ? Q2.x : Q0.z, fy1 = py ? Q2.y : Q0.w;
-    const uint32_t nz0 = pz ? Q1.x : Q2.z, nz1 = pz ? Q1.y : Q2.w, fz0 = pz ? Q2.z : Q1.x, fz1 = pz ? Q2.w : Q1.y;
+    const uint32_t nx0 = px ? w1.z : w3.x, nx1 = px ? w1.w : w3.y, fx0 = px ? w3.x : w1.z, fx1 = px ? w3.y : w1.w;
+    const uint32_t ny0 = py ? w2.x : w3.z, ny1 = py ? w2.y : w3.w, fy0 = py ? w3.z : w2.x, fy1 = py ? w3.w : w2.y;
+    const uint32_t nz0 = pz ? w2.z : w4.x, nz1 = pz ? w2.w : w4.y, fz0 = pz ? w4.x : w2.z, fz1 = pz ? w4.y : w2.w;
     const float lo_k = 1.0f - 4.0f * FLT_EPSILON, hi_k = 1.0f + 4.0f * FLT_EPSILON;
     uint32_t hits = 0u;
 #pragma unroll
@@ -294,16 +293,17 @@ __device__ __forceinline__ uint32_t wide_hits(uint4 Q0, uint4 Q1, uint4 Q2, uint
         const float t1 = fminf(fminf(fminf(tfar, tfx), tfy), tfz);
         hits |= (t0 * lo_k <= t1 * hi_k) ? (1u << c) : 0u;
     }
-    const uint32_t nv = eb >> 28;
+    const uint32_t nv = w0.w >> 28;
     return hits & ((1u << nv) - 1u);
 }
+// Stats (rs_debug_trace only): *stats = node fetches << 16 | triangle tests of this lane's walk
 template <bool Any, bool Stats = false, bool NoTri = false>
 __device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o, vec3 d, vec3 inv, float tnear,
                                           float tfar, Hit& h, uint32_t& occ, uint32_t& lost, uint32_t* stats = nullptr) {
     uint32_t gb = 0u, gm = active ? 1u : 0u;       // root group: node 0, slot 0
+    uint32_t n_fetch = 0u, n_tri = 0u;
     WideStack st;
     st.init();
-    uint32_t n_fetch = 0u, n_tri = 0u;
     while (__ballot(gm != 0u) != 0) {
         if (Stats) n_fetch += gm != 0u ? 1u : 0u;
         const bool live = gm != 0u;
@@ -312,13 +312,12 @@ __device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o
         const uint32_t rest = gm & (gm - 1u);
         st.push(live & (rest != 0u), (gb << 8) | rest);
         const uint4* P = S.wnodes + 5 * (size_t)node;
-        const uint4 Q0 = P[0], Q1 = P[1], Q2 = P[2], H = P[3];
-        const uint2 L = *(const uint2*)(P + 4);     // child_base, tri_base
+        const uint4 w0 = P[0], w1 = P[1], w2 = P[2], w3 = P[3], w4 = P[4];
         const float tf = Any ? tfar : h.t;
-        uint32_t hits = live ? wide_hits(Q0, Q1, Q2, H, o, inv, tnear, tf) : 0u;
-        const uint32_t ni = (H.w >> 24) & 0xfu;
+        uint32_t hits = live ? wide_hits(w0, w1, w2, w3, w4, o, inv, tnear, tf) : 0u;
+        const uint32_t ni = (w0.w >> 24) & 0xfu;
         uint32_t tm = NoTri ? 0u : hits >> ni;      // leaf slots ni.. -> triangles tri_base + (slot - ni)
-        const uint32_t tb = L.y;
+        const uint32_t tb = w1.y;
         while (__ballot(tm != 0u && (!Any || occ == 0u)) != 0) {
             const bool want = tm != 0u && (!Any || occ == 0u);
             if (Stats) n_tri += want ? 1u : 0u;
@@ -340,7 +339,7 @@ __device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o
         const uint32_t ngm = (Any && occ) ? 0u : (hits & ((1u << ni) - 1u));
         const bool pop = live & (ngm == 0u) & (st.n > 0) & !(Any && occ);
         const uint32_t top = st.pop(pop);
-        gb = !live ? gb : (ngm ? L.x : (pop ? top >> 8 : 0u));
+        gb = !live ? gb : (ngm ? w1.x : (pop ? top >> 8 : 0u));
         gm = !live ? 0u : (ngm ? ngm : (pop ? top & 0xffu : 0u));
         if (Any && occ) st.n = 0;
     }

@@ -16,12 +16,12 @@ namespace rs {
 // are 8 (Wald et al. 2008 / Ylitie et al. 2017's greedy collapse).  Leaves hold ONE triangle.  Layout
 // (breadth-first, so a node's interior children are consecutive nodes and its leaf triangles consecutive
 // wide-leaf triangles): interior children occupy slots 0..ni-1, leaf children slots ni..nv-1.
-// Node = 5 x uint4 (80 B), every load 16-B aligned (the walk loads 72 B: 4 x 16 B + 8 B):
-//   w0 = qlo.x[0..3], qlo.x[4..7], qlo.y[0..3], qlo.y[4..7]      (q: one byte per slot)
-//   w1 = qlo.z[0..3], qlo.z[4..7], qhi.x[0..3], qhi.x[4..7]
-//   w2 = qhi.y[0..3], qhi.y[4..7], qhi.z[0..3], qhi.z[4..7]
-//   w3 = origin o.xyz (float), ex | ey << 8 | ez << 16 | ni << 24 | nv << 28
-//   w4 = child_base, tri_base, 0, 0
+// Node = 5 x uint4 (80 B):
+//   w0 = origin o.xyz (float), ex | ey << 8 | ez << 16 | ni << 24 | nv << 28
+//   w1 = child_base, tri_base, qlo.x[0..3], qlo.x[4..7]      (q: one byte per slot)
+//   w2 = qlo.y[0..3], qlo.y[4..7], qlo.z[0..3], qlo.z[4..7]
+//   w3 = qhi.x[0..3], qhi.x[4..7], qhi.y[0..3], qhi.y[4..7]
+//   w4 = qhi.z[0..3], qhi.z[4..7], 0, 0
 // A child's box is o + q * s per axis, s = 2^(e - 127); o is a multiple of s, so every plane o + q*s is an
 // exact float, and the planes are rounded OUTWARD (lo down, hi up) from the exact child box: the walk's
 // box test is a superset of the exact one (results cannot change, rs_scene.h).
@@ -119,13 +119,13 @@ inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, 
             return (uint32_t)q[first] | ((uint32_t)q[first + 1] << 8) | ((uint32_t)q[first + 2] << 16) | ((uint32_t)q[first + 3] << 24);
         };
         const uint32_t w[20] = {
-            pack(qlo[0], 0), pack(qlo[0], 4), pack(qlo[1], 0), pack(qlo[1], 4),
-            pack(qlo[2], 0), pack(qlo[2], 4), pack(qhi[0], 0), pack(qhi[0], 4),
-            pack(qhi[1], 0), pack(qhi[1], 4), pack(qhi[2], 0), pack(qhi[2], 4),
             h_f2u(o[0]), h_f2u(o[1]), h_f2u(o[2]),
             (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16) | ((uint32_t)ni << 24) |
                 ((uint32_t)nv << 28),
-            child_base, tri_base, 0u, 0u};
+            child_base, tri_base, pack(qlo[0], 0), pack(qlo[0], 4),
+            pack(qlo[1], 0), pack(qlo[1], 4), pack(qlo[2], 0), pack(qlo[2], 4),
+            pack(qhi[0], 0), pack(qhi[0], 4), pack(qhi[1], 0), pack(qhi[1], 4),
+            pack(qhi[2], 0), pack(qhi[2], 4), 0u, 0u};
         out.insert(out.end(), w, w + 20);
         if (queue.size() >= (1u << 24)) { err = "wide BVH: too many nodes"; return -1; }
     }

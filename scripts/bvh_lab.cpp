@@ -568,14 +568,14 @@ static int group_depth(const Wide& Wd, const Ray& r, bool any) {
 struct WEmu { int iters = 0, tris = 0, lost = 0, occ = 0; int prim = -1; float t = 0; int maxsp = 0; };
 static inline float u2f_(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 static uint32_t emu_hits(const uint32_t* w, V3 o, V3 inv, float tnear, float tfar) {
-    const uint32_t eb = w[15];
+    const uint32_t eb = w[3];
     const float s[3] = {u2f_((eb & 0xffu) << 23), u2f_(((eb >> 8) & 0xffu) << 23), u2f_(((eb >> 16) & 0xffu) << 23)};
     const float iv[3] = {inv.x, inv.y, inv.z}, org[3] = {o.x, o.y, o.z};
     float a[3], b[3];
-    for (int k = 0; k < 3; ++k) { a[k] = s[k] * iv[k]; b[k] = (u2f_(w[12 + k]) - org[k]) * iv[k]; }
+    for (int k = 0; k < 3; ++k) { a[k] = s[k] * iv[k]; b[k] = (u2f_(w[k]) - org[k]) * iv[k]; }
     const float E = 2.384185791015625e-07f * std::fmax(std::fmax(std::fabs(b[0]), std::fabs(b[1])), std::fabs(b[2]));
-    const uint32_t lo[3][2] = {{w[0], w[1]}, {w[2], w[3]}, {w[4], w[5]}};
-    const uint32_t hi[3][2] = {{w[6], w[7]}, {w[8], w[9]}, {w[10], w[11]}};
+    const uint32_t lo[3][2] = {{w[6], w[7]}, {w[8], w[9]}, {w[10], w[11]}};
+    const uint32_t hi[3][2] = {{w[12], w[13]}, {w[14], w[15]}, {w[16], w[17]}};
     const float lo_k = 1.0f - 4.0f * FLT_EPSILON, hi_k = 1.0f + 4.0f * FLT_EPSILON;
     uint32_t hits = 0;
     for (int c = 0; c < 8; ++c) {
@@ -590,7 +590,7 @@ static uint32_t emu_hits(const uint32_t* w, V3 o, V3 inv, float tnear, float tfa
         const float t1 = std::fmin(std::fmin(std::fmin(tfar, tf[0]), tf[1]), tf[2]);
         if (std::fma(t0, lo_k, -E) <= std::fma(t1, hi_k, E)) hits |= 1u << c;
     }
-    return hits & ((1u << (w[15] >> 28)) - 1u);
+    return hits & ((1u << (w[3] >> 28)) - 1u);
 }
 static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& prims, const Ray& r, bool any, int K) {
     WEmu e;
@@ -606,7 +606,7 @@ static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& pri
         e.maxsp = std::max(e.maxsp, (int)st.size());
         const uint32_t* w = &W[20 * (size_t)node];
         uint32_t hits = emu_hits(w, r.o, inv, r.tn, tf);
-        uint32_t ni = (w[15] >> 24) & 0xfu, tm = hits >> ni, tb = w[17];
+        uint32_t ni = (w[3] >> 24) & 0xfu, tm = hits >> ni, tb = w[5];
         while (tm && !(any && e.occ)) {
             uint32_t j = __builtin_ctz(tm); tm &= tm - 1; ++e.tris;
             float t; int p = prims[tb + j];
@@ -616,7 +616,7 @@ static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& pri
             }
         }
         uint32_t ngm = (any && e.occ) ? 0u : (hits & ((1u << ni) - 1u));
-        if (ngm) { gb = w[16]; gm = ngm; }
+        if (ngm) { gb = w[4]; gm = ngm; }
         else if (!st.empty() && !(any && e.occ)) { uint32_t top = st.back(); st.pop_back(); gb = top >> 8; gm = top & 0xff; }
         else gm = 0;
     }
@@ -682,7 +682,7 @@ int main(int argc, char** argv) {
         float focal = (float)H / (2.0f * std::tan(fov / 2.0f));
         std::mt19937 rng(1);
         std::uniform_real_distribution<float> U(0.0f, 1.0f);
-        double it_p = 0, it_s = 0, tr_s = 0; long lost = 0, ns = 0, mism = 0; int maxsp = 0;
+        double it_p = 0, it_s = 0, tr_s = 0, it_b = 0, tr_p = 0, tr_b = 0; long lost = 0, ns = 0, nb = 0, mism = 0; int maxsp = 0;
         std::vector<int> wave_it(((W / 8) * (H / 8)), 0);
         for (int y = 0; y < H; ++y)
             for (int x = 0; x < W; ++x) {
@@ -693,9 +693,25 @@ int main(int argc, char** argv) {
                 WEmu a = emu_walk(WN, pr, pr_, false, 8);
                 Trace ref = walk(Fr, pr_, false);
                 mism += a.prim != ref.prim;
-                it_p += a.iters;
+                it_p += a.iters; tr_p += a.tris;
                 if (a.prim < 0) continue;
                 V3 o = eye + d * a.t;
+                {   // a cosine-distributed bounce off the hit triangle (the BRDF candidates' closest-hit rays)
+                    const Tri& ht = g_tris[a.prim];
+                    V3 nn = cross(ht.v1 - ht.v0, ht.v2 - ht.v0);
+                    nn = nn * (1.0f / std::sqrt(std::max(dot(nn, nn), 1e-30f)));
+                    if (dot(nn, d) > 0) nn = nn * -1.0f;
+                    V3 t1 = std::fabs(nn.x) > 0.5f ? V3{0, 1, 0} : V3{1, 0, 0};
+                    t1 = cross(nn, t1); t1 = t1 * (1.0f / std::sqrt(dot(t1, t1)));
+                    V3 t2 = cross(nn, t1);
+                    float u1 = U(rng), u2 = U(rng), rr = std::sqrt(u1), ph = 6.2831853f * u2;
+                    V3 bd = t1 * (rr * std::cos(ph)) + t2 * (rr * std::sin(ph)) + nn * std::sqrt(std::max(0.0f, 1 - u1));
+                    Ray br{o, bd, 0.01f, 3.0e38f, true};
+                    WEmu c = emu_walk(WN, pr, br, false, 8);
+                    Trace rb = walk(Fr, br, false);
+                    mism += c.prim != rb.prim;
+                    it_b += c.iters; tr_b += c.tris; ++nb;
+                }
                 int e = emis[rng() % ne];
                 float r1 = U(rng), r2 = U(rng), sr = std::sqrt(r1);
                 const Tri& t = g_tris[e];
@@ -711,8 +727,9 @@ int main(int argc, char** argv) {
                 if (y / 8 < H / 8 && x / 8 < W / 8) { int& wv = wave_it[(y / 8) * (W / 8) + x / 8]; wv = std::max(wv, b.iters); }
             }
         double wsum = 0; for (int v : wave_it) wsum += v;
-        printf("emu: primary iters %.2f | shadow iters %.2f tris %.2f lost %.4f max stack %d wave-max iters %.1f | mismatches %ld\n",
-               it_p / (W * H), it_s / ns, tr_s / ns, (double)lost / ns, maxsp, wsum / wave_it.size(), mism);
+        printf("emu: primary iters %.2f tris %.2f | bounce iters %.2f tris %.2f | shadow iters %.2f tris %.2f lost %.4f max stack %d wave-max iters %.1f | mismatches %ld | nodes %zu\n",
+               it_p / (W * H), tr_p / (W * H), it_b / std::max(nb, 1L), tr_b / std::max(nb, 1L), it_s / ns, tr_s / ns,
+               (double)lost / ns, maxsp, wsum / wave_it.size(), mism, WN.size() / 20);
         return 0;
     }
     const int wide_k = getenv("WIDE") ? atoi(getenv("WIDE")) : 0;

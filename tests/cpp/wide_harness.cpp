@@ -101,18 +101,18 @@ bool tri_test(const float* p, V o, V d, float tn, float tf, float& t) {
 
 // rs_scene.h wide_hits, the same float operations (fmaf = the device's v_fma_f32)
 uint32_t wide_hits(const uint32_t* w, V o, V inv, float tnear, float tfar) {
-    const uint32_t eb = w[15];
+    const uint32_t eb = w[3];
     const float s[3] = {u2f((eb & 0xffu) << 23), u2f(((eb >> 8) & 0xffu) << 23), u2f(((eb >> 16) & 0xffu) << 23)};
     const float iv[3] = {inv.x, inv.y, inv.z}, org[3] = {o.x, o.y, o.z};
     float a[3], b[3];
     float bn[3], bf[3];
     for (int k = 0; k < 3; ++k) {
-        a[k] = s[k] * iv[k]; b[k] = (u2f(w[12 + k]) - org[k]) * iv[k];
+        a[k] = s[k] * iv[k]; b[k] = (u2f(w[k]) - org[k]) * iv[k];
         const float e = 2.384185791015625e-07f * std::fabs(b[k]);
         bn[k] = b[k] - e; bf[k] = b[k] + e;
     }
-    const uint32_t lo[3][2] = {{w[0], w[1]}, {w[2], w[3]}, {w[4], w[5]}};
-    const uint32_t hi[3][2] = {{w[6], w[7]}, {w[8], w[9]}, {w[10], w[11]}};
+    const uint32_t lo[3][2] = {{w[6], w[7]}, {w[8], w[9]}, {w[10], w[11]}};
+    const uint32_t hi[3][2] = {{w[12], w[13]}, {w[14], w[15]}, {w[16], w[17]}};
     const float lo_k = 1.0f - 4.0f * FLT_EPSILON, hi_k = 1.0f + 4.0f * FLT_EPSILON;
     uint32_t hits = 0;
     for (int c = 0; c < 8; ++c) {
@@ -127,7 +127,7 @@ uint32_t wide_hits(const uint32_t* w, V o, V inv, float tnear, float tfar) {
         const float t1 = std::fmin(std::fmin(std::fmin(tfar, tf[0]), tf[1]), tf[2]);
         if (t0 * lo_k <= t1 * hi_k) hits |= 1u << c;
     }
-    const uint32_t nv = w[15] >> 28;
+    const uint32_t nv = w[3] >> 28;
     return hits & ((1u << nv) - 1u);
 }
 
@@ -136,11 +136,11 @@ void walk(const std::vector<uint32_t>& W, const std::vector<int>& prims, const S
           float tn, float& tf, int& prim, bool any, bool& occ) {
     const uint32_t* w = &W[20 * (size_t)node];
     const uint32_t hits = wide_hits(w, o, inv, tn, any ? tf : tf);
-    const uint32_t ni = (w[15] >> 24) & 0xfu;
+    const uint32_t ni = (w[3] >> 24) & 0xfu;
     for (uint32_t c = 0; c < 8 && !occ; ++c) {
         if (!((hits >> c) & 1u)) continue;
-        if (c < ni) { walk(W, prims, S, w[16] + c, o, d, inv, tn, tf, prim, any, occ); continue; }
-        const int p = prims[w[17] + c - ni];
+        if (c < ni) { walk(W, prims, S, w[4] + c, o, d, inv, tn, tf, prim, any, occ); continue; }
+        const int p = prims[w[5] + c - ni];
         float t;
         if (tri_test(&S.pos[9 * (size_t)p], o, d, tn, tf, t)) {
             if (any) { occ = true; return; }
@@ -172,12 +172,12 @@ int wide_check(int n, uint32_t seed, int* depth_out, char* msg, int msg_len) {
     uint32_t next_child = 1, next_tri = 0;
     for (size_t i = 0; i < nn; ++i) {
         const uint32_t* w = &W[20 * i];
-        const uint32_t ni = (w[15] >> 24) & 0xfu, nv = w[15] >> 28;
+        const uint32_t ni = (w[3] >> 24) & 0xfu, nv = w[3] >> 28;
         if (nv < 1 || nv > 8 || ni > nv) return fail("slot counts");
-        if (ni && w[16] != next_child) return fail("interior children not breadth-first contiguous");
-        if (nv > ni && w[17] != next_tri) return fail("leaf triangles not contiguous");
+        if (ni && w[4] != next_child) return fail("interior children not breadth-first contiguous");
+        if (nv > ni && w[5] != next_tri) return fail("leaf triangles not contiguous");
         next_child += ni; next_tri += nv - ni;
-        for (uint32_t c = 0; c < ni; ++c) { parent[w[16] + c] = (int)i; level[w[16] + c] = level[i] + 1; }
+        for (uint32_t c = 0; c < ni; ++c) { parent[w[4] + c] = (int)i; level[w[4] + c] = level[i] + 1; }
     }
     if (next_child != nn || next_tri != (uint32_t)n) return fail("layout totals");
     int md = 0;
@@ -185,23 +185,23 @@ int wide_check(int n, uint32_t seed, int* depth_out, char* msg, int msg_len) {
     if (md != depth) return fail("depth");
     for (size_t ii = nn; ii-- > 0;) {
         const uint32_t* w = &W[20 * ii];
-        const uint32_t ni = (w[15] >> 24) & 0xfu, nv = w[15] >> 28;
-        const uint32_t e[3] = {w[15] & 0xffu, (w[15] >> 8) & 0xffu, (w[15] >> 16) & 0xffu};
-        const uint32_t lo[3][2] = {{w[0], w[1]}, {w[2], w[3]}, {w[4], w[5]}};
-        const uint32_t hi[3][2] = {{w[6], w[7]}, {w[8], w[9]}, {w[10], w[11]}};
+        const uint32_t ni = (w[3] >> 24) & 0xfu, nv = w[3] >> 28;
+        const uint32_t e[3] = {w[3] & 0xffu, (w[3] >> 8) & 0xffu, (w[3] >> 16) & 0xffu};
+        const uint32_t lo[3][2] = {{w[6], w[7]}, {w[8], w[9]}, {w[10], w[11]}};
+        const uint32_t hi[3][2] = {{w[12], w[13]}, {w[14], w[15]}, {w[16], w[17]}};
         for (uint32_t c = 0; c < nv; ++c) {
             float clo[3], chi[3];
             if (c < ni) {
-                for (int a = 0; a < 3; ++a) { clo[a] = blo[3 * (w[16] + c) + a]; chi[a] = bhi[3 * (w[16] + c) + a]; }
+                for (int a = 0; a < 3; ++a) { clo[a] = blo[3 * (w[4] + c) + a]; chi[a] = bhi[3 * (w[4] + c) + a]; }
             } else {
-                const float* p = &S.pos[9 * (size_t)prims[w[17] + c - ni]];
+                const float* p = &S.pos[9 * (size_t)prims[w[5] + c - ni]];
                 for (int a = 0; a < 3; ++a) {
                     clo[a] = std::min(std::min(p[a], p[3 + a]), p[6 + a]);
                     chi[a] = std::max(std::max(p[a], p[3 + a]), p[6 + a]);
                 }
             }
             for (int a = 0; a < 3; ++a) {
-                const double s = std::ldexp(1.0, (int)e[a] - 127), o = (double)u2f(w[12 + a]);
+                const double s = std::ldexp(1.0, (int)e[a] - 127), o = (double)u2f(w[a]);
                 const double ql = (double)((lo[a][c >> 2] >> (8 * (c & 3))) & 0xffu), qh = (double)((hi[a][c >> 2] >> (8 * (c & 3))) & 0xffu);
                 if (o + ql * s > (double)clo[a] || o + qh * s < (double)chi[a]) return fail("plane not outward");
                 // and the planes are exact floats

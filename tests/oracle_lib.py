@@ -44,6 +44,7 @@ def lib():
         L.or_scene_create.restype = ctypes.c_void_p
         L.or_scene_create.argtypes = [ctypes.c_uint32, _f32p, _f32p, _u32p, ctypes.c_uint32, _f32p, _i32p]
         L.or_scene_destroy.argtypes = [ctypes.c_void_p]
+        L.or_scene_set_wide.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.or_ctx_create.restype = ctypes.c_void_p
         L.or_ctx_create.argtypes = [ctypes.c_int, ctypes.c_int]
         L.or_ctx_destroy.argtypes = [ctypes.c_void_p]
@@ -148,7 +149,9 @@ def _texdescs(textures):
 
 
 class OracleScene:
-    def __init__(self, scene):
+    """wide: walk the 8-wide AVX2 tree (or_scene_set_wide; same hits as the binary tree, faster) --
+    default on unless ORACLE_WIDE=0; False keeps the binary stack walk."""
+    def __init__(self, scene, wide=None):
         L = lib()
         self.scene = scene
         self._pos = np.ascontiguousarray(scene.positions, dtype=np.float32)
@@ -176,6 +179,9 @@ class OracleScene:
             descs, keep = _texdescs([scene.sky])
             if L.or_scene_set_sky(self.h, ctypes.cast(descs, ctypes.c_void_p)) != 0:
                 raise RuntimeError("or_scene_set_sky failed")
+        if wide is None:
+            wide = os.environ.get("ORACLE_WIDE", "1") != "0"
+        self.wide = bool(L.or_scene_set_wide(self.h, 1 if wide else 0))
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:

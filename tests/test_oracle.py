@@ -246,9 +246,13 @@ def _brute_closest(sc, o, d, tnear, tfar):
     return ts, prims
 
 
-def test_oracle_bvh_matches_brute_force():
+@pytest.mark.parametrize("wide", [False, True])
+def test_oracle_bvh_matches_brute_force(wide):
+    """Both oracle walks (the binary stack walk and the 8-wide AVX2 walk of the CPU baseline) find the
+    brute-force hits."""
     sc = scenes.cornell_many_lights(48)
-    os_ = O.OracleScene(sc)
+    os_ = O.OracleScene(sc, wide=wide)
+    assert os_.wide == wide
     rng = np.random.default_rng(3)
     n = 400
     o = rng.uniform([-0.9, -0.9, 0.1], [0.9, 0.9, 1.9], (n, 3)).astype(np.float32)
@@ -284,6 +288,22 @@ def _render(sc, W, H, prm, frames=1, threads=None, cam=None):
     for f in range(frames):
         img = r.render(os_, cam(f) if cam else sc.camera, prm, f)
     return img, r
+
+
+@pytest.mark.parametrize("name", ["cornell", "sponza"])
+def test_oracle_wide_walk_frames_identical(name):
+    """The CPU baseline's 8-wide walk renders the same frames as the binary walk (any tree, same hits)."""
+    sc = scenes.cornell_many_lights(64) if name == "cornell" else scenes.sponza_like(target_tris=20_000, n_lamps=64)
+    prm = P.default_params(m_area=8, m_brdf=1, do_spatial=1, spatial_neighbors=3, do_temporal=1)
+    cam = lambda f: scenes.orbit_camera(sc.camera, f, 24, 0.3)
+    imgs = []
+    for wide in (False, True):
+        os_ = O.OracleScene(sc, wide=wide)
+        assert os_.wide == wide
+        r = O.OracleRenderer(64, 48)
+        imgs.append([r.render(os_, cam(f), prm, f).copy() for f in range(3)])
+    for a, b in zip(*imgs):
+        assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("mis", [0, 1, 2, 3, 4])
