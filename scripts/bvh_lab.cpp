@@ -592,7 +592,8 @@ static uint32_t emu_hits(const uint32_t* w, V3 o, V3 inv, float tnear, float tfa
     }
     return hits & ((1u << (w[3] >> 28)) - 1u);
 }
-static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& prims, const Ray& r, bool any, int K) {
+static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& prims, const Ray& r, bool any, int K,
+                     std::vector<uint32_t>* seq = nullptr) {
     WEmu e;
     if (!r.active) return e;
     V3 inv{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
@@ -604,6 +605,7 @@ static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& pri
         uint32_t slot = __builtin_ctz(gm), node = gb + slot, rest = gm & (gm - 1);
         if (rest) { if ((int)st.size() == K) { st.erase(st.begin()); e.lost = 1; } st.push_back((gb << 8) | rest); }
         e.maxsp = std::max(e.maxsp, (int)st.size());
+        if (seq) seq->push_back(node);
         const uint32_t* w = &W[20 * (size_t)node];
         uint32_t hits = emu_hits(w, r.o, inv, r.tn, tf);
         uint32_t ni = (w[3] >> 24) & 0xfu, tm = hits >> ni, tb = w[5];
@@ -726,6 +728,68 @@ int main(int argc, char** argv) {
                 it_s += b.iters; tr_s += b.tris; lost += b.lost; ++ns; maxsp = std::max(maxsp, b.maxsp);
                 if (y / 8 < H / 8 && x / 8 < W / 8) { int& wv = wave_it[(y / 8) * (W / 8) + x / 8]; wv = std::max(wv, b.iters); }
             }
+        if (getenv("COHERENCE")) {
+            // per 16x16 workgroup and candidate: 256 shadow rays (pixel -> random emitter point) walked by
+            // 4 waves of 64.  Per wave: lockstep steps (its longest walk) and the node fetches the vector
+            // memory path processes, counted as distinct nodes among the lanes per step.  Groupings: the
+            // 8x8 pixel quadrants (the kernels' layout) vs the 256 rays sorted by a target key.
+            const int K = 8;
+            const char* names[4] = {"8x8 pixels", "sorted by emitter", "sorted by target Morton", "sorted by dir octant+Morton"};
+            double st[4] = {0, 0, 0, 0}, ds[4] = {0, 0, 0, 0}, lane_f = 0; long nwave = 0;
+            std::mt19937 rg2(5);
+            for (int ty = 0; ty + 16 <= H; ty += 16)
+                for (int tx = 0; tx + 16 <= W; tx += 16) {
+                    V3 org[256]; bool ok[256];
+                    for (int l = 0; l < 256; ++l) {
+                        int q4 = l >> 6, ll = l & 63;
+                        int x = tx + (q4 & 1) * 8 + (ll & 7), y = ty + (q4 >> 1) * 8 + (ll >> 3);
+                        V3 dc{(float)x - W / 2.0f, H / 2.0f - (float)y, -focal};
+                        V3 d = xc * dc.x + yc * dc.y + zc * dc.z;
+                        d = d * (1.0f / std::sqrt(dot(d, d)));
+                        WEmu a = emu_walk(WN, pr, Ray{eye, d, 0.01f, 3.0e38f, true}, false, 8);
+                        ok[l] = a.prim >= 0; org[l] = eye + d * a.t;
+                    }
+                    for (int k = 0; k < K; ++k) {
+                        std::vector<std::vector<uint32_t>> seq(256);
+                        uint64_t key[4][256];
+                        for (int l = 0; l < 256; ++l) {
+                            int e = emis[rg2() % ne];
+                            float r1 = U(rg2), r2 = U(rg2), sr = std::sqrt(r1);
+                            const Tri& t = g_tris[e];
+                            V3 q = t.v0 * (1 - sr) + t.v1 * (sr * (1 - r2)) + t.v2 * (sr * r2);
+                            auto qb = [](float v) { return (uint32_t)std::min(1023.0f, std::max(0.0f, (v + 20.0f) * 25.0f)); };
+                            uint32_t mx = qb(q.x), my = qb(q.y), mz = qb(q.z); uint64_t m = 0;
+                            for (int bb = 0; bb < 10; ++bb) m |= (uint64_t)((((mx >> bb) & 1) << (3 * bb)) | (((my >> bb) & 1) << (3 * bb + 1)) | (((mz >> bb) & 1) << (3 * bb + 2)));
+                            V3 sd = q - org[l];
+                            const uint64_t oct = (sd.x < 0) | ((sd.y < 0) << 1) | ((sd.z < 0) << 2);
+                            key[0][l] = l; key[1][l] = ((uint64_t)e << 8) | l; key[2][l] = (m << 8) | l; key[3][l] = (((oct << 30) | m) << 8) | l;
+                            if (!ok[l]) continue;
+                            float dist = std::sqrt(dot(sd, sd));
+                            sd = sd * (1.0f / std::max(dist, 1e-20f));
+                            emu_walk(WN, pr, Ray{org[l], sd, 0.01f, dist - 0.001f, true}, true, 8, &seq[l]);
+                            lane_f += seq[l].size();
+                        }
+                        for (int g = 0; g < 4; ++g) {
+                            std::sort(key[g], key[g] + 256);
+                            for (int w = 0; w < 4; ++w) {
+                                size_t T = 0;
+                                for (int i = 0; i < 64; ++i) T = std::max(T, seq[key[g][64 * w + i] & 255].size());
+                                st[g] += T;
+                                for (size_t t = 0; t < T; ++t) {
+                                    uint32_t v[64]; int nv = 0;
+                                    for (int i = 0; i < 64; ++i) { auto& q = seq[key[g][64 * w + i] & 255]; if (t < q.size()) v[nv++] = q[t]; }
+                                    std::sort(v, v + nv); ds[g] += std::unique(v, v + nv) - v;
+                                }
+                            }
+                        }
+                        nwave += 4;
+                    }
+                }
+            printf("coherence: lane fetches per ray %.2f\n", lane_f / (nwave * 64.0));
+            for (int g = 0; g < 4; ++g)
+                printf("  %-28s steps per wave %.1f, distinct node fetches per wave %.1f (per step %.1f)\n", names[g],
+                       st[g] / nwave, ds[g] / nwave, ds[g] / st[g]);
+        }
         double wsum = 0; for (int v : wave_it) wsum += v;
         printf("emu: primary iters %.2f tris %.2f | bounce iters %.2f tris %.2f | shadow iters %.2f tris %.2f lost %.4f max stack %d wave-max iters %.1f | mismatches %ld | nodes %zu\n",
                it_p / (W * H), tr_p / (W * H), it_b / std::max(nb, 1L), tr_b / std::max(nb, 1L), it_s / ns, tr_s / ns,

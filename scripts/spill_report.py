@@ -21,6 +21,76 @@ def flags():
     return out
 
 
+def cfg(body):
+    """Basic blocks of one kernel's assembly: [(first line, end line)] in layout order, and successor lists."""
+    starts = [0]
+    for k, l in enumerate(body):
+        t = l.strip()
+        if re.match(r"^\.LBB\d+_\d+:", t) or t.startswith("; %bb."):
+            starts.append(k)
+        elif re.match(r"s_(cbranch_\w+|branch|endpgm|setpc_b64)\b", t):
+            starts.append(k + 1)
+    starts = sorted(set(x for x in starts if x < len(body)))
+    order = [(a, b) for a, b in zip(starts, starts[1:] + [len(body)])]
+    label_block = {}
+    for bi, (a, b) in enumerate(order):
+        for k in range(a, b):
+            m = re.match(r"^(\.LBB\d+_\d+):", body[k].strip())
+            if m:
+                label_block[m.group(1)] = bi
+    succ = []
+    for bi, (a, b) in enumerate(order):
+        last = ""
+        for k in range(b - 1, a - 1, -1):
+            t = body[k].strip()
+            if t and not t.startswith((";", ".")):
+                last = t
+                break
+        out = []
+        m = re.match(r"s_(cbranch_\w+|branch) (\.LBB\d+_\d+)", last)
+        if m and m.group(2) in label_block:
+            out.append(label_block[m.group(2)])
+        if not (last.startswith("s_branch") or last.startswith("s_endpgm") or last.startswith("s_setpc")):
+            if bi + 1 < len(order):
+                out.append(bi + 1)
+        succ.append(out)
+    return succ, order
+
+
+def natural_loops(succ, order):
+    """Natural loops (back edge u -> h with h dominating u): [(set of blocks, size in lines)]."""
+    n = len(succ)
+    pred = [[] for _ in range(n)]
+    for u, vs in enumerate(succ):
+        for v in vs:
+            pred[v].append(u)
+    full = set(range(n))
+    dom = [full.copy() for _ in range(n)]
+    dom[0] = {0}
+    changed = True
+    while changed:
+        changed = False
+        for v in range(1, n):
+            ps = [dom[p] for p in pred[v]]
+            nd = (set.intersection(*ps) if ps else set()) | {v}
+            if nd != dom[v]:
+                dom[v] = nd
+                changed = True
+    loops = []
+    for u in range(n):
+        for h in succ[u]:
+            if h in dom[u]:
+                body, work = {h, u}, ([u] if u != h else [])
+                while work:
+                    x = work.pop()
+                    for p in pred[x]:
+                        if p not in body:
+                            body.add(p)
+                            work.append(p)
+                loops.append((body, sum(order[b][1] - order[b][0] for b in body)))
+    return loops
+
+
 def main():
     want = sys.argv[1:] or ["k_gbuffer_initial", "k_spatial", "k_temporal"]
     out = "/tmp/restir_capi.s"
@@ -33,15 +103,19 @@ def main():
             continue
         end = s.find(".Lfunc_end", m.end())
         body = s[m.end():end].splitlines()
-        labels = {l.split(":")[0]: k for k, l in enumerate(body) if re.match(r"^\.LBB\d+_\d+:", l)}
-        loops = []
-        for k, l in enumerate(body):
-            b = re.search(r"s_(?:cbranch_\w+|branch) (\.LBB\d+_\d+)", l)
-            if b and b.group(1) in labels and labels[b.group(1)] < k:
-                loops.append((labels[b.group(1)], k))
+        blocks, order = cfg(body)
+        loops = natural_loops(blocks, order)
         ops = [k for k, l in enumerate(body) if "scratch_load" in l or "scratch_store" in l]
-        inner = sorted(min(hi - lo for lo, hi in loops if lo <= k <= hi) for k in ops
-                       if any(lo <= k <= hi for lo, hi in loops))
+        owner = {}
+        for bi, (lo, hi) in enumerate(order):
+            for k in range(lo, hi):
+                owner[k] = bi
+        inner = []
+        for k in ops:
+            sizes = [sz for body_set, sz in loops if owner.get(k) in body_set]
+            if sizes:
+                inner.append(min(sizes))
+        inner.sort()
         vg = re.search(r"\.vgpr_count:\s+(\d+)", s[end:end + 200000])
         print(f"{name[:64]}: {len(ops)} scratch ops, {len(inner)} in loops (innermost loop lengths {inner[:16]})")
 
