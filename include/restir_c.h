@@ -413,8 +413,11 @@ int rs_mgpu_get_stats(rs_mgpu* m, rs_mgpu_stats* out, int reset);
 /* ---- test hook: raw BVH queries (rtcIntersect1 / rtcOccluded1 semantics) ----------------------
  * n rays, host arrays o[3n], d[3n], tnear[n], tfar[n].  any_hit=0: closest hit -> t_out[n] (-1 on miss),
  * prim_out[n] (original triangle index, -1 on miss); any_hit=1: prim_out[n] = 1 if occluded else 0.
- * Modes 0/1 use the lockstep traversal, 2/3 the same queries per-lane; 4 (closest) / 5 (any) return
- * per-ray walk statistics instead: prim_out[n] = node visits << 16 | triangle tests. */
+ * Modes 0/1 use the lockstep traversal, 2/3 the same queries per-lane (the 8-wide tree when the scene has
+ * one); 4 (closest) / 5 (any) return per-ray skip-pointer walk statistics instead: prim_out[n] = node
+ * visits << 16 | triangle tests; 6 (closest) / 7 (any) the 8-wide walk's: node fetches << 16 | triangle
+ * tests, t_out = 1 if its stack overflowed; 8 / 9 / 10 are timing probes of the 8-wide walk (closest;
+ * any-hit without triangle tests; any-hit).  Modes 6-10 return prim -1 / t -1 without a wide tree. */
 int rs_debug_trace(rs_context* ctx, const rs_scene* scene, uint32_t n, const float* o, const float* d,
                    const float* tnear, const float* tfar, int any_hit, float* t_out, int32_t* prim_out);
 

@@ -2031,6 +2031,10 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
     const bool act = i0 < n;
     const uint32_t i = act ? i0 : n - 1;
     vec3 O = mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), D = mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+    if (any >= 6 && any <= 10 && S.n_wnodes == 0u) {   // the 8-wide modes need the scene's wide tree
+        if (act) { prim_out[i] = -1; t_out[i] = -1.0f; }
+        return;
+    }
     if (any >= 8 && any <= 10) {  // timing probes of the 8-wide walk: 8 closest walk with the ray's tfar,
         const vec3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);   // 9 any-hit without triangle tests,
         Hit h; h.t = tf[i]; h.u = h.v = 0.0f; h.prim = -1;        // 10 any-hit with statistics off
@@ -2040,7 +2044,6 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
         else wide_walk<true>(S, act, O, D, inv, tn[i], tf[i], h, occ, lost);
         if (act) { prim_out[i] = any == 8 ? h.prim : (int32_t)occ; t_out[i] = (float)lost; }
     } else if (any == 6 || any == 7) {   // 8-wide walk statistics: node fetches << 16 | triangle tests; t = stack overflow
-        if (S.n_wnodes == 0u) { if (act) { prim_out[i] = -1; t_out[i] = -1.0f; } return; }
         const vec3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
         Hit h; h.t = tf[i]; h.u = h.v = 0.0f; h.prim = -1;
         uint32_t occ = 0u, lost = 0u, st = 0u;
