@@ -290,6 +290,9 @@ typedef struct {
     int32_t tonemap;           /* RenderParams::tonemap (default true) */
     int32_t gamma_correct;     /* Raytracer::gammaCorrect (default true) */
     int32_t max_acc_frames;    /* maxAccCount (<= 0: the reference's 300000) */
+    int32_t denoise;           /* RenderParams::denoise (default false, pg/RenderParams.h:13): display the
+                                  denoised accumulator (pg/simpleguidx11.cpp:277-280); needs a denoiser set
+                                  with rs_context_set_denoiser and a full frame (not a tile band) */
 } rs_post_params;
 typedef struct {
     double mean, variance;     /* accumulatorMean / accumulatorVariance over the rows processed */
@@ -304,6 +307,50 @@ int rs_post_frame(rs_context* ctx, const rs_post_params* params, const float** d
                   rs_post_stats* stats);
 /* accFrameCtr = 0 (the next rs_post_frame overwrites the accumulator with the frame). */
 int rs_post_reset(rs_context* ctx);
+
+/* ---- denoiser: the reference's Open Image Denoise "RT" filter ---------------------
+ * pg/simpleguidx11.cpp:52-75 (oidnNewDevice / oidnNewFilter("RT") / setImage color = accumulator, albedo =
+ * gBuffer.diffuseColorBuf, normal = gBuffer.wSpaceNormalBuf, output; hdr = true; quality High; commit) and
+ * :255-260 (execute every frame; errors printed).  Here: OIDN's UNet on the matrix cores (float16 storage,
+ * float32 accumulation; csrc/rs_denoise.hip), weights from an OIDN tensor archive (.tza; OIDN's trained
+ * rt_hdr_alb_nrm.tza is not shipped with the reference -- pass it, or any weights of the same topology).
+ * Errors: RS_E_INVALID for a malformed archive / topology mismatch (the message names the tensor),
+ * RS_E_UNSUPPORTED for hdr = false.  All execution is asynchronous on the context's stream. */
+typedef struct rs_denoiser rs_denoiser;
+typedef struct {
+    int32_t input_channels;    /* 3 colour only, 6 + albedo, 9 + normal (the reference's filter: 9) */
+    int32_t channels[16];      /* output channels of enc_conv0..5b, dec_conv4a..dec_conv0 */
+    uint64_t parameters;
+    double mac_per_pixel;      /* multiply-accumulates per (padded) input pixel */
+} rs_denoiser_info;
+typedef struct {
+    float input_scale;         /* oidn "inputScale": <= 0 or NaN = auto-exposure (OIDN's default) */
+    int32_t hdr;               /* oidn "hdr": must be 1 (the reference sets true) */
+} rs_denoise_params;
+/* Host only (no device work): parse + check an archive against the UNet topology. */
+int rs_denoiser_check_weights(const void* tza, size_t bytes, rs_denoiser_info* info);
+int rs_denoiser_create(rs_context* ctx, const void* tza, size_t bytes, rs_denoiser** out);
+int rs_denoiser_create_from_file(rs_context* ctx, const char* path, rs_denoiser** out);
+int rs_denoiser_info_get(const rs_denoiser* d, rs_denoiser_info* info);
+/* oidnFilter.execute on device images: colour / albedo / normal / output are W*H float3 rows (the
+ * reference's oidn::Format::Float3 shared buffers). */
+int rs_denoiser_execute(rs_denoiser* d, const float* color, const float* albedo, const float* normal,
+                        float* output, int32_t width, int32_t height, const rs_denoise_params* params);
+/* The reference's per-frame call: colour = the context's accumulator (after rs_post_frame), albedo / normal
+ * = the last frame's G-buffer diffuse colour / normal; *output_dptr = W*H float3 (owned by the denoiser). */
+int rs_denoise_frame(rs_context* ctx, rs_denoiser* d, const rs_denoise_params* params, const float** output_dptr);
+/* rs_post_frame with params->denoise runs rs_denoise_frame (auto-exposure) and tonemaps its output. */
+int rs_context_set_denoiser(rs_context* ctx, rs_denoiser* d);
+/* HIP-event time of the last execute (enable first; waits for it) and the input scale it used (waits). */
+int rs_denoiser_set_timing(rs_denoiser* d, int enable);
+int rs_denoiser_last_ms(rs_denoiser* d, float* ms);
+int rs_denoiser_get_scale(rs_denoiser* d, float* scale);
+/* Test hook: the float16 activation tensor `tensor` of the last execute (0 = network input, then the
+ * outputs of enc_conv0, pool(enc_conv1..4), enc_conv5a, enc_conv5b, dec_conv4a .. dec_conv1b) with its
+ * one-pixel zero border, NHWC: dims = {rows + 2, cols + 2, channel stride, real channels}; host (optional)
+ * receives dims[0] * dims[1] * dims[2] halves.  Synchronises. */
+int rs_denoiser_dump(rs_denoiser* d, int tensor, uint16_t* host, int32_t* dims);
+void rs_denoiser_destroy(rs_denoiser* d);
 
 /* ---- image export (SimpleGuiDX11::exportImage, pg/simpleguidx11.cpp:607-650) ------
  * Writes the display buffer of the last rs_post_frame as an 8-bit RGBA PNG -- every channel

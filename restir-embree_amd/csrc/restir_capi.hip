@@ -216,6 +216,7 @@ struct rs_context {
     uint32_t acc_frames = 0;
     uint64_t post_px = 0;                  // pixels the last rs_post_frame's statistics cover
     rs_camera cam_last = {};               // camera of the last frame (rs_export_png's sidecar)
+    rs_denoiser* denoiser = nullptr;       // rs_post_frame's RenderParams::denoise (rs_context_set_denoiser)
     // asynchronous framebuffer readback (rs_frame_readback): ticket ring, and per lane the readback its
     // framebuffer is under (that lane's next frame waits for it before writing)
     bool readback_kernel = false;          // DMA engine (default) or a copy kernel (env RESTIR_READBACK=kernel)
@@ -1934,6 +1935,15 @@ extern "C" int rs_post_frame(rs_context* c, const rs_post_params* pp, const floa
         HIPCHK(c, hipGetLastError());
     }
     c->post_px = nblk > 0 ? n : 0;
+    if (pp->denoise) {   // oidnFilter.execute on the accumulator, display = the denoised image (:255-280)
+        if (!c->denoiser) return fail(c, RS_E_INVALID, "rs_post_frame: denoise without a denoiser (rs_context_set_denoiser)");
+        if (y0 != 0 || y1 != c->H) return fail(c, RS_E_UNSUPPORTED, "rs_post_frame: denoise needs a full frame, not a tile band");
+        const float* den = nullptr;
+        const int rc = rs_denoise_frame(c, c->denoiser, nullptr, &den);
+        if (rc != RS_OK) return rc;
+        k_post_display<<<nblk, 256, 0, c->stream>>>(den, c->display, P);
+        HIPCHK(c, hipGetLastError());
+    }
     // accFrameCtr bookkeeping (pg/simpleguidx11.cpp:297-306)
     const uint32_t used = c->acc_frames;
     c->acc_frames++;
@@ -2013,6 +2023,30 @@ extern "C" int rs_image_encode_png(const char* path, uint32_t w, uint32_t h, uin
     if (!path || !px || !w || !h || ch < 1 || ch > 4) return fail(nullptr, RS_E_INVALID, "rs_image_encode_png: bad arguments");
     std::string err;
     if (write_png(path, (int)w, (int)h, (int)ch, px, err) != 0) return fail(nullptr, RS_E_IO, err);
+    return RS_OK;
+}
+
+// --------------------------------------------------------------------------- denoiser (§8f-4)
+extern "C" int rs_denoise_frame(rs_context* c, rs_denoiser* d, const rs_denoise_params* p, const float** out) {
+    if (!c || !d || !out) return fail(c, RS_E_INVALID, "rs_denoise_frame: null argument");
+    if (rs::denoiser_ctx(d) != c) return fail(c, RS_E_INVALID, "rs_denoise_frame: the denoiser belongs to another context");
+    if (c->active) return fail(c, RS_E_INVALID, "rs_denoise_frame: a frame is in flight (finish it first)");
+    if (!c->acc || !c->frames) return fail(c, RS_E_INVALID, "rs_denoise_frame: no accumulator yet (render a frame and call rs_post_frame)");
+    if (p && !p->hdr) return fail(c, RS_E_UNSUPPORTED, "rs_denoise_frame: only hdr = true (the reference's setting) is supported");
+    HIPCHK(c, enter(c));
+    float* o = rs::denoiser_frame_out(d, c->W, c->H);
+    if (!o) return fail(c, RS_E_HIP, "rs_denoise_frame: output allocation failed");
+    const GBuf& g = c->G[c->gcur];   // the last frame's G-buffer: albedo = kd (g2.xyz), normal = g1.xyz
+    const int rc = rs::denoise_run(d, c->stream, c->acc, 3, (const float*)g.g2, 4, (const float*)g.g1, 4, o, 3,
+                                   c->H, c->W, p ? p->input_scale : NAN);
+    if (rc != RS_OK) return rc;
+    *out = o;
+    return RS_OK;
+}
+extern "C" int rs_context_set_denoiser(rs_context* c, rs_denoiser* d) {
+    if (!c) return fail(nullptr, RS_E_INVALID, "rs_context_set_denoiser: null context");
+    if (d && rs::denoiser_ctx(d) != c) return fail(c, RS_E_INVALID, "rs_context_set_denoiser: the denoiser belongs to another context");
+    c->denoiser = d;
     return RS_OK;
 }
 

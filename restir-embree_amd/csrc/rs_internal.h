@@ -5,6 +5,7 @@
 #include <string>
 
 struct rs_context;
+struct rs_denoiser;
 
 namespace rs {
 // the context's own stream (ordered after every frame enqueued so far)
@@ -17,4 +18,11 @@ __attribute__((visibility("hidden"))) int ctx_height(const rs_context* c);
 __attribute__((visibility("hidden"))) int ctx_join(rs_context* c, hipStream_t st);
 // record an error message on the context (rs_last_error) and return `code`
 __attribute__((visibility("hidden"))) int ctx_fail(rs_context* c, int code, const std::string& msg);
+// rs_denoise.hip: the denoiser on device images (float3 rows at `*st` floats per pixel), enqueued on `st`;
+// input_scale <= 0 / NaN: auto-exposure.  The output buffer rs_denoise_frame writes; the owning context.
+__attribute__((visibility("hidden"))) int denoise_run(rs_denoiser* d, hipStream_t st, const float* color, int cst,
+                                                      const float* albedo, int ast, const float* normal, int nst,
+                                                      float* out, int ost, int H, int W, float input_scale);
+__attribute__((visibility("hidden"))) float* denoiser_frame_out(rs_denoiser* d, int W, int H);
+__attribute__((visibility("hidden"))) rs_context* denoiser_ctx(const rs_denoiser* d);
 }  // namespace rs

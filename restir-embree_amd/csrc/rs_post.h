@@ -64,6 +64,24 @@ __global__ void __launch_bounds__(256) k_post(const float* __restrict__ frame, f
     if (threadIdx.x == 0) part[blockIdx.x] = make_double2(ss[0], sq[0]);
 }
 
+// display from the denoised accumulator when RenderParams::denoise (pg/simpleguidx11.cpp:277-292)
+__global__ void __launch_bounds__(256) k_post_display(const float* __restrict__ img, float4* __restrict__ display,
+                                                      PostConst P) {
+    const size_t n = (size_t)(P.y1 - P.y0) * P.W;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const size_t p = (size_t)P.y0 * P.W + i;
+    float px[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float v = img[3 * p + k];
+        if (P.tonemap) v = post_aces(v);
+        if (P.gamma) v = post_compress(v);
+        px[k] = v;
+    }
+    display[p] = make_float4(px[0], px[1], px[2], 1.0f);
+}
+
 // one workgroup: partials -> (sum, sqr_sum), fixed order
 __global__ void __launch_bounds__(256) k_post_reduce(const double2* __restrict__ part, int n, double2* out) {
     __shared__ double ss[256], sq[256];

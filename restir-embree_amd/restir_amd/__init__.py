@@ -6,3 +6,4 @@ C ABI in include/restir_c.h; this package only marshals scenes/parameters and dr
 from . import params, scenes  # noqa: F401
 from .params import FrameParams, default_params, metric_params, c3_params  # noqa: F401
 from .renderer import Renderer, Scene, RestirError, load_library, LIB_PATH, EXPORTED_SYMBOLS  # noqa: F401
+from .denoise import Denoiser, check_weights  # noqa: F401

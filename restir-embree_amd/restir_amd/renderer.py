@@ -36,6 +36,9 @@ EXPORTED_SYMBOLS = [
     "rs_host_alloc", "rs_host_free", "rs_mgpu_unique_id", "rs_mgpu_create", "rs_mgpu_create_local",
     "rs_mgpu_destroy", "rs_mgpu_set_bands", "rs_mgpu_get_bands", "rs_mgpu_rebalance", "rs_mgpu_render_frame",
     "rs_mgpu_frame_device_ptr", "rs_mgpu_reset_history", "rs_mgpu_allreduce", "rs_mgpu_get_stats",
+    "rs_denoiser_check_weights", "rs_denoiser_create", "rs_denoiser_create_from_file", "rs_denoiser_info_get",
+    "rs_denoiser_execute", "rs_denoise_frame", "rs_context_set_denoiser", "rs_denoiser_set_timing",
+    "rs_denoiser_last_ms", "rs_denoiser_get_scale", "rs_denoiser_dump", "rs_denoiser_destroy",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -98,7 +101,7 @@ class PassTimes(ctypes.Structure):
 
 class PostParams(ctypes.Structure):
     _fields_ = [("accumulate", ctypes.c_int32), ("tonemap", ctypes.c_int32), ("gamma_correct", ctypes.c_int32),
-                ("max_acc_frames", ctypes.c_int32)]
+                ("max_acc_frames", ctypes.c_int32), ("denoise", ctypes.c_int32)]
 
 
 class PostStats(ctypes.Structure):
@@ -214,6 +217,19 @@ def load_library(path: str = LIB_PATH):
     L.rs_mgpu_reset_history.argtypes = [vp]
     L.rs_mgpu_allreduce.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i32, i32]
     L.rs_mgpu_get_stats.argtypes = [vp, vp, i32]
+    L.rs_denoiser_check_weights.argtypes = [vp, ctypes.c_size_t, vp]
+    L.rs_denoiser_create.argtypes = [vp, vp, ctypes.c_size_t, ctypes.POINTER(vp)]
+    L.rs_denoiser_create_from_file.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
+    L.rs_denoiser_info_get.argtypes = [vp, vp]
+    L.rs_denoiser_execute.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp]
+    L.rs_denoise_frame.argtypes = [vp, vp, vp, ctypes.POINTER(vp)]
+    L.rs_context_set_denoiser.argtypes = [vp, vp]
+    L.rs_denoiser_set_timing.argtypes = [vp, i32]
+    L.rs_denoiser_last_ms.argtypes = [vp, fp]
+    L.rs_denoiser_get_scale.argtypes = [vp, fp]
+    L.rs_denoiser_dump.argtypes = [vp, i32, vp, ctypes.POINTER(ctypes.c_int32)]
+    L.rs_denoiser_destroy.argtypes = [vp]
+    L.rs_denoiser_destroy.restype = None
     _lib = L
     return L
 
@@ -420,10 +436,11 @@ class Renderer:
         self._check(self.lib.rs_synchronize(self.h))
 
     def post_frame(self, accumulate: bool = False, tonemap: bool = True, gamma_correct: bool = True,
-                   max_acc_frames: int = 0, stats: bool = True):
+                   max_acc_frames: int = 0, stats: bool = True, denoise: bool = False):
         """Post-frame block of the reference's producer loop (rs_post_frame): accumulate, ACES + sRGB
-        display, accumulator mean/variance.  Returns (display device pointer, PostStats or None)."""
-        p = PostParams(int(accumulate), int(tonemap), int(gamma_correct), int(max_acc_frames))
+        display, accumulator mean/variance; denoise (RenderParams::denoise) displays the denoised
+        accumulator (needs set_denoiser).  Returns (display device pointer, PostStats or None)."""
+        p = PostParams(int(accumulate), int(tonemap), int(gamma_correct), int(max_acc_frames), int(denoise))
         dptr, st = ctypes.c_void_p(), PostStats()
         self._check(self.lib.rs_post_frame(self.h, ctypes.byref(p), ctypes.byref(dptr),
                                            ctypes.byref(st) if stats else None))
@@ -434,6 +451,11 @@ class Renderer:
         """SimpleGuiDX11::exportImage: the last post_frame's display as RGBA8 PNG (+ <path>.txt)."""
         p = ExportParams(float(render_time_s), 1 if sidecar else 0)
         self._check(self.lib.rs_export_png(self.h, os.fsencode(path), ctypes.byref(p)))
+
+    def set_denoiser(self, denoiser):
+        """rs_context_set_denoiser: the denoiser post_frame(denoise=True) runs (None clears it)."""
+        self._denoiser = denoiser
+        self._check(self.lib.rs_context_set_denoiser(self.h, denoiser.h if denoiser is not None else None))
 
     def post_reset(self):
         self._check(self.lib.rs_post_reset(self.h))

@@ -2,7 +2,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(ROOT, "restir-embree_amd"), os.path.join(ROOT, "tests"), ROOT):
+for p in (os.path.join(ROOT, "restir-embree_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"), ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 
