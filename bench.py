@@ -41,6 +41,7 @@ import numpy as np  # noqa: E402
 METRIC = "Mrays/s + frames/s at 1080p, 32 candidates, 4 spatial neighbours"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2   # wave64 VALU instr/ns: 1024 SIMDs, 2 cycles each, 2.4 GHz
+MFMA_F16_PEAK_TFLOPS = 2500.0  # dense f16/bf16 MFMA peak (MI355X_MICROARCH.md; no sparsity)
 C5_FRAMES = 240
 TUNE_FRAMES = 6                # RS_TRAVERSAL_AUTO tuning frames (2 kinds x kTuneRuns, restir_capi.hip)
 WORKLOADS = {
@@ -356,6 +357,99 @@ def run_single(name, W, H, steps, warmup, device, stream, cpu_threads, with_cpu,
     return out
 
 
+# ---------------------------------------------------------------- denoiser
+DN_LEVELS = [0, 0, 1, 2, 3, 4, 4, 3, 3, 2, 2, 1, 1, 0, 0, 0]     # pooling level of each convolution
+
+
+def run_denoise(W, H, steps, warmup, device, stream, cpu_threads, with_cpu):
+    """The reference's per-frame OIDN "RT" filter (pg/simpleguidx11.cpp:52-75, :255-256) on the C2 frame's
+    accumulator with the frame's G-buffer albedo / normal (rs_denoise_frame): one step = one execute at
+    W x H.  OIDN's trained weights are not shipped, so the weights are He-initialised ones of OIDN's UNet
+    shape (the cost does not depend on their values)."""
+    import torch
+    from restir_amd import Renderer, tza
+    from restir_amd.denoise import Denoiser, gflop_per_frame
+    sc, prm, camera, _ = workload("C2")
+    r = Renderer(W, H, device=device, stream=stream)
+    gs = r.load_scene(sc)
+    w = tza.random_unet_weights(seed=1)
+    d = Denoiser(r, w)
+    for f in range(2):
+        r.produce_restir(gs, sc.camera, prm, f, copy_out=False, timed=False)
+    r.post_frame(accumulate=False, stats=False)
+    for _ in range(warmup):
+        d.denoise_frame()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        d.denoise_frame()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    d.set_timing(True)
+    lay, tot = [], []
+    for _ in range(5):
+        d.denoise_frame()
+        lay.append(d.layer_ms())
+        tot.append(d.last_ms())
+    d.set_timing(False)
+    lay = np.median(np.array(lay), axis=0)
+    ms_ev = float(np.median(tot))
+    info = d.info()
+    gf = gflop_per_frame(info, W, H)
+    hp, wp = -(-H // 16) * 16, -(-W // 16) * 16
+    shapes = tza.unet_shapes(info.input_channels)
+    names = list(shapes)
+    lay_gf = [2.0 * shapes[n][0] * shapes[n][1] * 9 * (hp * wp) / 4 ** lv / 1e9 for n, lv in zip(names, DN_LEVELS)]
+    dom = int(np.argmax(lay[1:]))
+    dom_tf = lay_gf[dom] / float(lay[1 + dom])
+    out = {
+        "value": round(steps / dt, 3), "unit": "executes/s", "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps,
+        "warmup": warmup, "dtype": "f16 storage / f32 accumulation (MFMA 16x16x32 f16)",
+        "data": "synthetic: the C2 frame's accumulator + G-buffer albedo / normal; He-initialised weights of OIDN's UNet shape",
+        "config": {"workload": f"OIDN RT filter (hdr, auto-exposure) on a {W}x{H} frame", "width": W, "height": H,
+                   "parameters": int(info.parameters), "gflop_per_execute": round(gf, 2)},
+        "execute_ms_hip_events": round(ms_ev, 4),
+        "layer_ms": {"input_transform": round(float(lay[0]), 4),
+                     **{n: round(float(x), 4) for n, x in zip(names, lay[1:])}},
+        "roofline": {"bound": "mfma", "scope": "one execute (auto-exposure, input transform, 16 convolutions)",
+                     "achieved": round(gf / ms_ev, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(gf / ms_ev / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None},
+        "kernel_roofline": {"bound": "mfma", "kernel": f"k_conv3 {names[dom]}", "kernel_ms": round(float(lay[1 + dom]), 4),
+                            "gflop": round(lay_gf[dom], 2), "achieved": round(dom_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": round(dom_tf / MFMA_F16_PEAK_TFLOPS, 4),
+                            "timing": "HIP events on the context's stream around each convolution, median of 5 executes"},
+    }
+    if with_cpu:
+        frame = np.zeros((H, W, 3), np.float32)
+        r.produce_restir(gs, sc.camera, prm, 3, copy_out=True, timed=False)
+        frame[:] = r.frame_data
+        g = r.gbuffer()
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import denoise_ref
+        n_threads = baseline_threads(cpu_threads)
+        denoise_ref.denoise(frame[:64, :64], g[:64, :64, 6:9], g[:64, :64, 3:6], w, threads=n_threads)   # warm-up
+        ts = []
+        t_start = time.perf_counter()
+        for _ in range(3):
+            t0 = time.perf_counter()
+            denoise_ref.denoise(frame, g[..., 6:9], g[..., 3:6], w, threads=n_threads)
+            ts.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_start > 20.0:
+                break
+        cs = float(np.median(ts))
+        out["cpu_baseline"] = {"value": round(1.0 / cs, 4), "unit": "executes/s", "cores": n_threads, "kind": "port",
+                               "sample": f"median of {len(ts)} full {W}x{H} executes of oracle/denoise_ref.py (PyTorch CPU "
+                                         f"fp32 convolutions, {n_threads} threads; OIDN's own CPU path is not in the reference)",
+                               "s_per_execute": round(cs, 3), "host": host_cpu()}
+        out["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+    else:
+        out["cpu_baseline"] = None
+    d.close()
+    gs.close()
+    r.close()
+    return out
+
+
 def run_dropin(W, H, frames=120):
     """The drop-in path a reference user runs: C++ host code over include/restir.hpp (member names of
     SimpleGuiDX11) driving librestir_amd.so, the framebuffer landing in host memory every frame
@@ -418,6 +512,8 @@ def main():
                                not args.no_cpu_baseline)
                 e["data"] = f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX[name]}])"
                 extras[name] = e
+            extras["denoise"] = run_denoise(W, H, args.steps, args.warmup, local, stream, args.cpu_threads,
+                                            not args.no_cpu_baseline)
             out["configs"] = extras
             torch.cuda.synchronize()
             d = run_dropin(W, H)

@@ -67,6 +67,7 @@ public:
     ~Renderer() {
         if (ctx_) rs_synchronize(ctx_);
         if (scene_) rs_scene_destroy(scene_);
+        if (denoiser_) rs_denoiser_destroy(denoiser_);
         if (ctx_) rs_context_destroy(ctx_);
         for (auto b : ring_) rs_host_free(b);
     }
@@ -130,8 +131,18 @@ public:
 
     // The producer loop's post block after produceRestir (pg/simpleguidx11.cpp:246-333, OIDN excluded):
     // accumulate into the accumulator, ACES + sRGB into display_data(), accumulatorMean/Variance.
+    // SimpleGuiDX11::initOIDN (pg/simpleguidx11.cpp:52-75): the "RT" filter (hdr, auto-exposure) with
+    // the weights of an OIDN tensor archive; postFrame() then shows the denoised accumulator when
+    // `denoise` (RenderParams::denoise) is set.
+    void initOIDN(const std::string& weights_tza) {
+        rs_denoiser* d = nullptr;
+        check(rs_denoiser_create_from_file(ctx_, weights_tza.c_str(), &d), ctx_);
+        if (denoiser_) rs_denoiser_destroy(denoiser_);
+        denoiser_ = d;
+        check(rs_context_set_denoiser(ctx_, denoiser_), ctx_);
+    }
     void postFrame() {
-        rs_post_params pp{accumulate ? 1 : 0, tonemap ? 1 : 0, gammaCorrect ? 1 : 0, maxAccCount};
+        rs_post_params pp{accumulate ? 1 : 0, tonemap ? 1 : 0, gammaCorrect ? 1 : 0, maxAccCount, denoise ? 1 : 0};
         rs_post_stats st{};
         const float* dptr = nullptr;
         check(rs_post_frame(ctx_, &pp, &dptr, &st), ctx_);
@@ -160,6 +171,7 @@ public:
     // post block (SimpleGuiDX11 accumulate / maxAccCount / accFrameCtr, RenderParams::tonemap,
     // Raytracer::gammaCorrect, accumulatorMean / accumulatorVariance)
     bool accumulate = false, tonemap = true, gammaCorrect = true;
+    bool denoise = false;                       // RenderParams::denoise (pg/RenderParams.h:13), needs initOIDN
     int maxAccCount = 300000;
     uint32_t accFrameCtr = 0;
     double accumulatorMean = 0.0, accumulatorVariance = 0.0;
@@ -187,6 +199,7 @@ private:
     int width_, height_;
     rs_context* ctx_ = nullptr;
     rs_scene* scene_ = nullptr;
+    rs_denoiser* denoiser_ = nullptr;
 };
 
 // The N-GPU frame (rs_mgpu_*) with the same member surface: N row bands, one Renderer

@@ -344,6 +344,8 @@ int rs_context_set_denoiser(rs_context* ctx, rs_denoiser* d);
 /* HIP-event time of the last execute (enable first; waits for it) and the input scale it used (waits). */
 int rs_denoiser_set_timing(rs_denoiser* d, int enable);
 int rs_denoiser_last_ms(rs_denoiser* d, float* ms);
+/* ms[17]: the last timed execute's input transform (+ auto-exposure), then each of the 16 convolutions. */
+int rs_denoiser_layer_ms(rs_denoiser* d, float* ms);
 int rs_denoiser_get_scale(rs_denoiser* d, float* scale);
 /* Test hook: the float16 activation tensor `tensor` of the last execute (0 = network input, then the
  * outputs of enc_conv0, pool(enc_conv1..4), enc_conv5a, enc_conv5b, dec_conv4a .. dec_conv1b) with its

@@ -71,6 +71,8 @@ constexpr int kHaloPx = kHalo * kHalo;         // 324
 constexpr int kChunkBytes = kHaloPx * 64;      // one 32-channel float16 halo image: 20736 B
 constexpr int kMaxChunks = 12;
 constexpr int kStageRegs = (kHaloPx * 4 + 255) / 256;   // 16-B staging slots per thread (6)
+constexpr size_t kFillWorkgroups = 1024;                  // >= 4 workgroups per CU before splitting channels
+constexpr int kMaxNtw = 4;                                // n-tiles per workgroup: 16 x 4 accumulators per lane
 
 enum Post : int { POST_STORE = 0, POST_POOL = 1, POST_FINAL = 2 };
 
@@ -83,6 +85,7 @@ struct ConvArgs {
     int ch_src[kMaxChunks], ch_base[kMaxChunks], ch_w[kMaxChunks], ch_step[kMaxChunks];
     const half8* w;            // [k-step][n-tile][64 lanes] B fragments
     const float* bias;         // n-tiles * 16 (zero padded)
+    int nt_total;              // n-tiles of the layer; a workgroup computes NT of them from blockIdx.z * NT
     _Float16* dst;             // POST_STORE / POST_POOL: output tensor (bordered NHWC)
     int dcs;                   // its channel stride
     int h, w_;                 // this convolution's output-level interior size
@@ -130,21 +133,34 @@ __device__ __forceinline__ void stage_store(uint8_t* buf, int spp, const uint4 (
     }
 }
 
+// B fragments of the next k-step are loaded while this step's MFMAs run when they fit the register budget
+template <int NT> struct Prefetch { static constexpr bool on = NT <= kMaxNtw; };
+
 template <int NT>
 __device__ __forceinline__ void compute_chunk(const ConvArgs& a, int c, const uint8_t* buf, f32x4 (&acc)[4][NT],
-                                              int lane, int X, int Yb) {
+                                              int lane, int X, int Yb, int n0) {
     const int h = lane >> 4;
     const bool w32 = a.ch_w[c] == 32;
     const int nst = w32 ? 9 : 5;
-    const half8* wp = a.w + (size_t)a.ch_step[c] * NT * 64 + lane;
+    const int ntt = a.nt_total;
+    const half8* wp = a.w + ((size_t)a.ch_step[c] * ntt + n0) * 64 + lane;
+    half8 b[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) b[n] = wp[n * 64];
     for (int st = 0; st < nst; ++st) {
         int tap, sl;
         if (w32) { tap = st; sl = h; }
         else { tap = 2 * st + (h >> 1); tap = tap > 8 ? 8 : tap; sl = h & 1; }   // tap 9: zero weights
         const int ky = tap / 3, kx = tap - 3 * ky;
-        half8 b[NT];
+        half8 bn[NT];
+        if constexpr (Prefetch<NT>::on) {
+            if (st + 1 < nst)
 #pragma unroll
-        for (int n = 0; n < NT; ++n) b[n] = wp[(st * NT + n) * 64];
+                for (int n = 0; n < NT; ++n) bn[n] = wp[((st + 1) * ntt + n) * 64];
+        } else if (st > 0) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n) b[n] = wp[(st * ntt + n) * 64];
+        }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int hr = Yb + 2 * g + ky, hc = X + kx;
@@ -152,6 +168,9 @@ __device__ __forceinline__ void compute_chunk(const ConvArgs& a, int c, const ui
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[n], acc[g][n], 0, 0, 0);
         }
+        if constexpr (Prefetch<NT>::on)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) b[n] = bn[n];
     }
 }
 
@@ -166,6 +185,7 @@ template <int NT, int POST, bool RELU>
 __global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[ConvLds<NT, POST>::kBytes];
     const int tx0 = blockIdx.x * kTile, ty0 = blockIdx.y * kTile;
+    const int n0 = blockIdx.z * NT;            // first n-tile of this workgroup
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int wy = wv >> 1, wx = wv & 1;
     const int i = lane & 15, h = lane >> 4;
@@ -186,7 +206,7 @@ __global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
     for (int c = 0; c < a.nchunk; ++c) {
         const bool more = c + 1 < a.nchunk;
         if (more) stage_load(a, c + 1, tx0, ty0, st);          // in flight during the MFMAs
-        compute_chunk<NT>(a, c, lds + (c & 1) * kChunkBytes, acc, lane, X, Yb);
+        compute_chunk<NT>(a, c, lds + (c & 1) * kChunkBytes, acc, lane, X, Yb, n0);
         if (more) stage_store(lds + ((c + 1) & 1) * kChunkBytes, a.ch_w[c + 1] >> 3, st);
         __syncthreads();
     }
@@ -198,7 +218,7 @@ __global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
         _Float16* o = (_Float16*)lds;
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
-            const float bv = a.bias[16 * n + i];
+            const float bv = a.bias[16 * (n0 + n) + i];
 #pragma unroll
             for (int g = 0; g < 4; ++g)
 #pragma unroll
@@ -215,7 +235,7 @@ __global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
             const int px = q / PPP, pc = q - px * PPP;
             const int gy = ty0 + (px >> 4), gx = tx0 + (px & 15);
             if (gy < a.h && gx < a.w_)
-                *(uint4*)(a.dst + ((size_t)(gy + 1) * (size_t)(a.w_ + 2) + (size_t)(gx + 1)) * a.dcs + 8 * pc) =
+                *(uint4*)(a.dst + ((size_t)(gy + 1) * (size_t)(a.w_ + 2) + (size_t)(gx + 1)) * a.dcs + 16 * n0 + 8 * pc) =
                     *(const uint4*)(o + px * CS + 8 * pc);
         }
     } else if constexpr (POST == POST_POOL) {
@@ -223,7 +243,7 @@ __global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
         _Float16* o = (_Float16*)lds;
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
-            const float bv = a.bias[16 * n + i];
+            const float bv = a.bias[16 * (n0 + n) + i];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const f32x4 v4 = acc[g][n];
@@ -240,7 +260,7 @@ __global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
             const int px = q / PPP, pc = q - px * PPP;
             const int gy = (ty0 >> 1) + (px >> 3), gx = (tx0 >> 1) + (px & 7);
             if (gy < ph && gx < pw)
-                *(uint4*)(a.dst + ((size_t)(gy + 1) * (size_t)(pw + 2) + (size_t)(gx + 1)) * a.dcs + 8 * pc) =
+                *(uint4*)(a.dst + ((size_t)(gy + 1) * (size_t)(pw + 2) + (size_t)(gx + 1)) * a.dcs + 16 * n0 + 8 * pc) =
                     *(const uint4*)(o + px * CS + 8 * pc);
         }
     } else {   // POST_FINAL: dec_conv0 (linear) + the output transform, float3 at the caller's stride
@@ -337,19 +357,19 @@ __global__ void __launch_bounds__(256) k_dn_ae_bins(const float* color, int cst,
         binlog[b] = m > 1e-8f ? log2f(m) : __builtin_nanf("");
     }
 }
-__global__ void __launch_bounds__(256) k_dn_ae_final(const float* binlog, int nb, float* scale) {
-    __shared__ float s[256];
-    __shared__ int cn[256];
+__global__ void __launch_bounds__(1024) k_dn_ae_final(const float* binlog, int nb, float* scale) {
+    __shared__ float s[1024];
+    __shared__ int cn[1024];
     const int t = threadIdx.x;
     float a = 0.0f;
     int c = 0;
-    for (int b = t; b < nb; b += 256) {
+    for (int b = t; b < nb; b += 1024) {
         const float v = binlog[b];
         if (v == v) { a += v; ++c; }
     }
     s[t] = a; cn[t] = c;
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
+    for (int w = 512; w > 0; w >>= 1) {
         if (t < w) { s[t] += s[t + w]; cn[t] += cn[t + w]; }
         __syncthreads();
     }
@@ -567,6 +587,7 @@ struct rs_denoiser {
     float* d_out = nullptr;                     // rs_denoise_frame's output (W*H float3)
     int out_w = 0, out_h = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t evl[17] = {};                    // timed: after the input transform, after each convolution
     bool timed = false;
 };
 
@@ -619,7 +640,7 @@ bool dispatch(int nt, int post, bool relu, const ConvArgs& a, dim3 g, hipStream_
         return true;
     }
     switch (nt) {
-        RS_DN_CASE(1) RS_DN_CASE(2) RS_DN_CASE(3) RS_DN_CASE(4) RS_DN_CASE(5) RS_DN_CASE(6) RS_DN_CASE(7) RS_DN_CASE(8)
+        RS_DN_CASE(1) RS_DN_CASE(2) RS_DN_CASE(3) RS_DN_CASE(4)
         default: return false;
     }
 #undef RS_DN_CASE
@@ -652,6 +673,8 @@ int create_impl(rs_context* ctx, const void* tza, size_t bytes, rs_denoiser** ou
     if (rc == RS_OK && (hipMalloc(&d->d_scale, sizeof(float)) != hipSuccess || hipEventCreate(&d->ev0) != hipSuccess ||
                         hipEventCreate(&d->ev1) != hipSuccess))
         rc = rs::ctx_fail(ctx, RS_E_HIP, "rs_denoiser_create: allocation failed");
+    for (auto& e : d->evl)
+        if (rc == RS_OK && hipEventCreate(&e) != hipSuccess) rc = rs::ctx_fail(ctx, RS_E_HIP, "rs_denoiser_create: event");
     if (rc != RS_OK) { rs_denoiser_destroy(d); return rc; }
     *out = d;
     return RS_OK;
@@ -677,13 +700,14 @@ int denoise_run(rs_denoiser* d, hipStream_t st, const float* color, int cst, con
     } else {
         const int nbh = (H + 15) / 16, nbw = (W + 15) / 16;
         k_dn_ae_bins<<<nbh * nbw, 256, 0, st>>>(color, cst, H, W, nbh, nbw, d->d_binlog);
-        k_dn_ae_final<<<1, 256, 0, st>>>(d->d_binlog, nbh * nbw, d->d_scale);
+        k_dn_ae_final<<<1, 1024, 0, st>>>(d->d_binlog, nbh * nbw, d->d_scale);
     }
     const float norm = 1.0f / pu_forward(HDR_Y_MAX);
     InArgs ia{color, albedo, normal, cst, ast, nst, H, W, d->Hp, d->Wp, d->net.ic, d->d_scale, norm, d->buf[B_IN]};
     const size_t npx = (size_t)d->Hp * d->Wp;
     k_dn_input<<<(unsigned)((npx + 255) / 256), 256, 0, st>>>(ia);
     DCHK(d, hipGetLastError());
+    if (d->timed) DCHK(d, hipEventRecord(d->evl[0], st));
     for (int l = 0; l < 16; ++l) {
         const LayerDef& ld = kNet[l];
         const Layer& L = d->L[l];
@@ -710,9 +734,18 @@ int denoise_run(rs_denoiser* d, hipStream_t st, const float* color, int cst, con
             a.out = out; a.ostride = ost; a.H = H; a.W = W; a.scale = d->d_scale;
             a.inv_norm = pu_forward(HDR_Y_MAX);
         }
-        const dim3 g((unsigned)((a.w_ + kTile - 1) / kTile), (unsigned)((a.h + kTile - 1) / kTile));
-        if (!dispatch(L.nt, ld.post, ld.relu != 0, a, g, st)) return dfail(d, RS_E_UNSUPPORTED, "rs_denoise: unsupported layer width");
+        // n-tiles per workgroup: all of them, unless the layer's tiles cannot fill the chip (the coarse
+        // levels): then the output channels split over blockIdx.z (each split re-stages the input halo)
+        const unsigned gx = (unsigned)((a.w_ + kTile - 1) / kTile), gy = (unsigned)((a.h + kTile - 1) / kTile);
+        a.nt_total = L.nt;
+        int ntw = 1;
+        if (ld.post != POST_FINAL)
+            for (int k = L.nt < kMaxNtw ? L.nt : kMaxNtw; k >= 1; --k)
+                if (L.nt % k == 0) { ntw = k; if ((size_t)gx * gy * (L.nt / k) >= kFillWorkgroups) break; }
+        const dim3 g(gx, gy, (unsigned)(L.nt / ntw));
+        if (!dispatch(ntw, ld.post, ld.relu != 0, a, g, st)) return dfail(d, RS_E_UNSUPPORTED, "rs_denoise: unsupported layer width");
         DCHK(d, hipGetLastError());
+        if (d->timed) DCHK(d, hipEventRecord(d->evl[l + 1], st));
     }
     if (d->timed) DCHK(d, hipEventRecord(d->ev1, st));
     return RS_OK;
@@ -785,6 +818,15 @@ extern "C" int rs_denoiser_last_ms(rs_denoiser* d, float* ms) {
     return RS_OK;
 }
 
+extern "C" int rs_denoiser_layer_ms(rs_denoiser* d, float* ms) {
+    if (!d || !ms) return rs::ctx_fail(d ? d->ctx : nullptr, RS_E_INVALID, "rs_denoiser_layer_ms: null argument");
+    if (!d->timed) return dfail(d, RS_E_INVALID, "rs_denoiser_layer_ms: timing is off (rs_denoiser_set_timing)");
+    DCHK(d, hipEventSynchronize(d->ev1));
+    DCHK(d, hipEventElapsedTime(&ms[0], d->ev0, d->evl[0]));
+    for (int l = 0; l < 16; ++l) DCHK(d, hipEventElapsedTime(&ms[l + 1], d->evl[l], d->evl[l + 1]));
+    return RS_OK;
+}
+
 extern "C" int rs_denoiser_get_scale(rs_denoiser* d, float* scale) {
     if (!d || !scale) return rs::ctx_fail(d ? d->ctx : nullptr, RS_E_INVALID, "rs_denoiser_get_scale: null argument");
     hipStream_t st = rs::ctx_stream(d->ctx);
@@ -818,6 +860,7 @@ extern "C" void rs_denoiser_destroy(rs_denoiser* d) {
     if (d->d_out) hipFree(d->d_out);
     if (d->ev0) hipEventDestroy(d->ev0);
     if (d->ev1) hipEventDestroy(d->ev1);
+    for (auto e : d->evl) if (e) hipEventDestroy(e);
     delete d;
 }
 

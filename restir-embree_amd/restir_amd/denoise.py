@@ -132,6 +132,12 @@ class Denoiser:
         self.r._check(self.lib.rs_denoiser_last_ms(self.h, ctypes.byref(v)))
         return v.value
 
+    def layer_ms(self):
+        """[input transform, 16 convolutions] ms of the last timed execute (HIP events on its stream)."""
+        v = (ctypes.c_float * 17)()
+        self.r._check(self.lib.rs_denoiser_layer_ms(self.h, v))
+        return list(v)
+
     def scale(self) -> float:
         v = ctypes.c_float()
         self.r._check(self.lib.rs_denoiser_get_scale(self.h, ctypes.byref(v)))

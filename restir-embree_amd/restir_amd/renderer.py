@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = [
     "rs_mgpu_frame_device_ptr", "rs_mgpu_reset_history", "rs_mgpu_allreduce", "rs_mgpu_get_stats",
     "rs_denoiser_check_weights", "rs_denoiser_create", "rs_denoiser_create_from_file", "rs_denoiser_info_get",
     "rs_denoiser_execute", "rs_denoise_frame", "rs_context_set_denoiser", "rs_denoiser_set_timing",
-    "rs_denoiser_last_ms", "rs_denoiser_get_scale", "rs_denoiser_dump", "rs_denoiser_destroy",
+    "rs_denoiser_last_ms", "rs_denoiser_layer_ms", "rs_denoiser_get_scale", "rs_denoiser_dump", "rs_denoiser_destroy",
 ]
 
 # BVH traversal kinds (include/restir_c.h RS_TRAVERSAL_*)
@@ -226,6 +226,7 @@ def load_library(path: str = LIB_PATH):
     L.rs_context_set_denoiser.argtypes = [vp, vp]
     L.rs_denoiser_set_timing.argtypes = [vp, i32]
     L.rs_denoiser_last_ms.argtypes = [vp, fp]
+    L.rs_denoiser_layer_ms.argtypes = [vp, fp]
     L.rs_denoiser_get_scale.argtypes = [vp, fp]
     L.rs_denoiser_dump.argtypes = [vp, i32, vp, ctypes.POINTER(ctypes.c_int32)]
     L.rs_denoiser_destroy.argtypes = [vp]

@@ -5,7 +5,7 @@
 //
 //   restir_render [--obj file.obj] [--w 1920 --h 1080] [--frames 10] [--area 32] [--brdf 1]
 //                 [--spatial k] [--temporal] [--out frame.pfm] [--eye x y z --at x y z --fov deg]
-//                 [--bench] [--ranks N [--compare]]
+//                 [--bench] [--ranks N [--compare]] [--denoise weights.tza [--png display.png]]
 // --bench: the drop-in throughput -- frames/s of produceRestir with frame_data landing in host memory
 // every frame, pipelined (pipelineDepth 2 and 1: readbacks overlapping the next frames, timePasses off)
 // and with the reference's synchronous semantics; one JSON line.
@@ -38,7 +38,7 @@ static void write_pfm(const std::string& path, int W, int H, const float* rgb) {
 }
 
 int main(int argc, char** argv) {
-    std::string obj, out;
+    std::string obj, out, denoise_w, png;
     int W = 512, H = 512, frames = 5;
     bool bench = false, cam_set = false, compare = false;
     int ranks = 0;
@@ -60,6 +60,8 @@ int main(int argc, char** argv) {
         else if (a == "--bench") bench = true;
         else if (a == "--ranks") ranks = std::atoi(next());
         else if (a == "--compare") compare = true;
+        else if (a == "--denoise") denoise_w = next();
+        else if (a == "--png") png = next();
         else if (a == "--eye") { for (float& v : eye) v = (float)std::atof(next()); cam_set = true; }
         else if (a == "--at") { for (float& v : at) v = (float)std::atof(next()); cam_set = true; }
         else if (a == "--fov") fov = (float)std::atof(next());
@@ -150,6 +152,10 @@ int main(int argc, char** argv) {
             return 0;
         }
         r.accumulate = true;                 // the producer loop's progressive accumulation
+        if (!denoise_w.empty()) {            // SimpleGuiDX11::initOIDN + RenderParams::denoise
+            r.initOIDN(denoise_w);
+            r.denoise = true;
+        }
         for (int f = 0; f < frames; ++f) {
             r.produceRestir();
             r.postFrame();
@@ -161,6 +167,10 @@ int main(int argc, char** argv) {
         }
         r.finish();
         if (!out.empty()) write_pfm(out, W, H, r.frame_data());
+        if (!png.empty()) {                  // SimpleGuiDX11::exportImage of the (denoised) display
+            rs_export_params ep{0.0f, 1};
+            restir::check(rs_export_png(r.handle(), png.c_str(), &ep), r.handle());
+        }
     } catch (const restir::Error& e) {
         std::fprintf(stderr, "error %d: %s\n", e.code, e.what());
         return 1;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Denoiser GPU round: tests, timing probe, bench sub-line, rocprofv3 kernel stats (csv).
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_denoise.py -q -s --timeout 120 --timeout-method thread > gpurun_out/dn_tests.log 2>&1
+echo "tests rc=$?" >> gpurun_out/dn_tests.log
+timeout -k 10 120 python -u scripts/denoise_probe.py > gpurun_out/dn_probe.log 2>&1 || exit 1
+timeout -k 10 300 python -u scripts/bench_denoise.py > gpurun_out/dn_bench.log 2>&1 || exit 1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/dn_prof" -o dn -- \
+    python3 "$GRAFT_REPO_ROOT/scripts/denoise_probe.py" --iters 10 > "$GRAFT_REPO_ROOT/gpurun_out/dn_prof.log" 2>&1

@@ -25,6 +25,23 @@ def test_cpp_driver_renders(tmp_path):
     assert img.max() > 0.0                         # the light and lit walls
 
 
+def test_cpp_driver_denoised_display(tmp_path):
+    """restir.hpp initOIDN + `denoise` (pg/simpleguidx11.cpp:52-75, :277-280): the exported display is the
+    tonemapped denoised accumulator (weights from a .tza written by restir_amd.tza)."""
+    from restir_amd import tza
+    w = tmp_path / "w.tza"
+    w.write_bytes(tza.write_tza(tza.random_unet_weights(seed=2)))
+    png = tmp_path / "den.png"
+    p = subprocess.run([TOOL, "--w", "64", "--h", "48", "--frames", "2", "--area", "4", "--denoise", str(w),
+                        "--png", str(png)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    img = decode_image(png)
+    assert img.shape == (48, 64, 4) and img[..., 3].min() == 255
+    p = subprocess.run([TOOL, "--w", "64", "--h", "48", "--frames", "1", "--denoise", str(tmp_path / "missing.tza")],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1 and "cannot open" in p.stderr
+
+
 def test_cpp_driver_bench_pipelined_host_framebuffer():
     """restir_render --bench: produceRestir with frame_data in host memory every frame, pipelined (the
     readback of frame f overlaps frame f+1) and synchronous; one JSON line with both rates."""
