@@ -71,7 +71,9 @@ constexpr int kHaloPx = kHalo * kHalo;         // 324
 constexpr int kChunkBytes = kHaloPx * 64;      // one 32-channel float16 halo image: 20736 B
 constexpr int kMaxChunks = 12;
 constexpr int kStageRegs = (kHaloPx * 4 + 255) / 256;   // 16-B staging slots per thread (6)
-constexpr size_t kFillWorkgroups = 1024;                  // >= 4 workgroups per CU before splitting channels
+constexpr size_t kFillWorkgroups = 256;                   // one workgroup per CU before splitting channels
+                                                          // (splitting re-stages the halo: measured slower
+                                                          // at 1/4 resolution, faster only at 1/16)
 constexpr int kMaxNtw = 4;                                // n-tiles per workgroup: 16 x 4 accumulators per lane
 
 enum Post : int { POST_STORE = 0, POST_POOL = 1, POST_FINAL = 2 };
@@ -153,22 +155,31 @@ __device__ __forceinline__ void compute_chunk(const ConvArgs& a, int c, const ui
         else { tap = 2 * st + (h >> 1); tap = tap > 8 ? 8 : tap; sl = h & 1; }   // tap 9: zero weights
         const int ky = tap / 3, kx = tap - 3 * ky;
         half8 bn[NT];
-        if constexpr (Prefetch<NT>::on) {
+#if defined(RS_DN_DIAG_NOB)   // timing diagnostic only (wrong results): B fragments of step 0 for every step
+        constexpr bool kLoadB = false;
+#else
+        constexpr bool kLoadB = true;
+#endif
+        if constexpr (kLoadB && Prefetch<NT>::on) {
             if (st + 1 < nst)
 #pragma unroll
                 for (int n = 0; n < NT; ++n) bn[n] = wp[((st + 1) * ntt + n) * 64];
-        } else if (st > 0) {
+        } else if (kLoadB && st > 0) {
 #pragma unroll
             for (int n = 0; n < NT; ++n) b[n] = wp[(st * ntt + n) * 64];
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int hr = Yb + 2 * g + ky, hc = X + kx;
+#if defined(RS_DN_DIAG_NOA)   // timing diagnostic only (wrong results): one A read per chunk
+            const half8 av = *(const half8*)(buf + (lane << 4));
+#else
             const half8 av = *(const half8*)(buf + (hr * kHalo + hc) * 64 + ((sl ^ swz(hr, hc)) << 4));
+#endif
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[n], acc[g][n], 0, 0, 0);
         }
-        if constexpr (Prefetch<NT>::on)
+        if constexpr (kLoadB && Prefetch<NT>::on)
 #pragma unroll
             for (int n = 0; n < NT; ++n) b[n] = bn[n];
     }
