@@ -138,59 +138,88 @@ __device__ __forceinline__ void stage_store(uint8_t* buf, int spp, const uint4 (
     }
 }
 
-// B fragments of the next k-step are loaded while this step's MFMAs run when they fit the register budget
-template <int NT> struct Prefetch { static constexpr bool on = NT <= kMaxNtw; };
+// B fragments: all four waves of a workgroup multiply the same weights, so a chunk's B fragments are
+// staged once per workgroup into LDS ([step][n-tile][64 lanes] x 16 B, a wave's fragment read = 1 KB
+// contiguous: conflict-free) instead of each wave loading them from L2 -- the per-wave loads were 6x the
+// halo staging's vector-memory instructions and kept the texture data path 82 % busy (r03_pmc_denoise).
+// Halo and B buffers are single: loads of chunk c + 1 into registers overlap chunk c's MFMAs, then two
+// barriers around the LDS writes.
+// Only for NT <= 3: a 4-n-tile chunk's 36 KB of B would leave 2 workgroups per CU (measured slower on
+// dec_conv1a: 247 vs 219 us); those keep per-wave global B loads (next step's prefetched) and a
+// double-buffered halo.
+template <int NT> struct BStage { static constexpr bool lds = NT <= 3; static constexpr int kRegs = lds ? (9 * NT * 64 + 255) / 256 : 1; };
 
 template <int NT>
-__device__ __forceinline__ void compute_chunk(const ConvArgs& a, int c, const uint8_t* buf, f32x4 (&acc)[4][NT],
-                                              int lane, int X, int Yb, int n0) {
+__device__ __forceinline__ void bstage_load(const ConvArgs& a, int c, int n0, uint4 (&r)[BStage<NT>::kRegs]) {
+    const int nst = a.ch_w[c] == 32 ? 9 : 5;
+    const int n = nst * NT * 64;               // 16-B pieces: (step, n-tile, lane)
+    const uint4* w = (const uint4*)a.w;
+#pragma unroll
+    for (int k = 0; k < BStage<NT>::kRegs; ++k) {
+        const int q = (int)threadIdx.x + k * 256;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (q < n) {
+            const int st = q / (NT * 64), rem = q - st * (NT * 64);
+            v = w[((size_t)(a.ch_step[c] + st) * a.nt_total + n0) * 64 + rem];
+        }
+        r[k] = v;
+    }
+}
+template <int NT>
+__device__ __forceinline__ void bstage_store(uint8_t* bbuf, int nst, const uint4 (&r)[BStage<NT>::kRegs]) {
+    const int n = nst * NT * 64;
+#pragma unroll
+    for (int k = 0; k < BStage<NT>::kRegs; ++k) {
+        const int q = (int)threadIdx.x + k * 256;
+        if (q < n) *(uint4*)(bbuf + q * 16) = r[k];
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void compute_chunk(const ConvArgs& a, int c, const uint8_t* buf, const uint8_t* bbuf,
+                                              f32x4 (&acc)[4][NT], int lane, int X, int Yb, int n0) {
     const int h = lane >> 4;
     const bool w32 = a.ch_w[c] == 32;
     const int nst = w32 ? 9 : 5;
-    const int ntt = a.nt_total;
-    const half8* wp = a.w + ((size_t)a.ch_step[c] * ntt + n0) * 64 + lane;
-    half8 b[NT];
+    const half8* bp = (const half8*)bbuf + lane;                                      // BStage<NT>::lds
+    const half8* wp = a.w + ((size_t)a.ch_step[c] * a.nt_total + n0) * 64 + lane;     // otherwise
+    half8 bg[NT];
+    if constexpr (!BStage<NT>::lds)
 #pragma unroll
-    for (int n = 0; n < NT; ++n) b[n] = wp[n * 64];
+        for (int n = 0; n < NT; ++n) bg[n] = wp[n * 64];
     for (int st = 0; st < nst; ++st) {
         int tap, sl;
         if (w32) { tap = st; sl = h; }
         else { tap = 2 * st + (h >> 1); tap = tap > 8 ? 8 : tap; sl = h & 1; }   // tap 9: zero weights
         const int ky = tap / 3, kx = tap - 3 * ky;
-        half8 bn[NT];
-#if defined(RS_DN_DIAG_NOB)   // timing diagnostic only (wrong results): B fragments of step 0 for every step
-        constexpr bool kLoadB = false;
-#else
-        constexpr bool kLoadB = true;
-#endif
-        if constexpr (kLoadB && Prefetch<NT>::on) {
+        half8 b[NT], bn[NT];
+        if constexpr (BStage<NT>::lds) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n) b[n] = bp[(st * NT + n) * 64];
+        } else {
+#pragma unroll
+            for (int n = 0; n < NT; ++n) b[n] = bg[n];
             if (st + 1 < nst)
 #pragma unroll
-                for (int n = 0; n < NT; ++n) bn[n] = wp[((st + 1) * ntt + n) * 64];
-        } else if (kLoadB && st > 0) {
-#pragma unroll
-            for (int n = 0; n < NT; ++n) b[n] = wp[(st * ntt + n) * 64];
+                for (int n = 0; n < NT; ++n) bn[n] = wp[((st + 1) * a.nt_total + n) * 64];
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int hr = Yb + 2 * g + ky, hc = X + kx;
-#if defined(RS_DN_DIAG_NOA)   // timing diagnostic only (wrong results): one A read per chunk
-            const half8 av = *(const half8*)(buf + (lane << 4));
-#else
             const half8 av = *(const half8*)(buf + hr * kRowBytes + hc * 64 + (sl << 4));
-#endif
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[n], acc[g][n], 0, 0, 0);
         }
-        if constexpr (kLoadB && Prefetch<NT>::on)
+        if constexpr (!BStage<NT>::lds)
 #pragma unroll
-            for (int n = 0; n < NT; ++n) b[n] = bn[n];
+            for (int n = 0; n < NT; ++n) bg[n] = bn[n];
     }
 }
 
 template <int NT, int POST>
 struct ConvLds {
-    static constexpr int kIn = 2 * kChunkBytes;
+    static constexpr int kB = 9 * NT * 1024;   // one chunk's B fragments
+    static constexpr int kIn = BStage<NT>::lds ? kChunkBytes + kB : 2 * kChunkBytes;
     static constexpr int kOut = POST == POST_STORE ? 256 * (NT * 16 + 8) * 2 : POST == POST_POOL ? 64 * (NT * 16 + 8) * 2
                                                                                      : 256 * 17 * 4;
     static constexpr int kBytes = kIn > kOut ? kIn : kOut;
@@ -199,6 +228,7 @@ struct ConvLds {
 template <int NT, int POST, bool RELU>
 __global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[ConvLds<NT, POST>::kBytes];
+    uint8_t* const bbuf = lds + kChunkBytes;
     const int tx0 = blockIdx.x * kTile, ty0 = blockIdx.y * kTile;
     const int n0 = blockIdx.z * NT;            // first n-tile of this workgroup
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -215,15 +245,38 @@ __global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
         for (int n = 0; n < NT; ++n) acc[g][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
     uint4 st[kStageRegs];
-    stage_load(a, 0, tx0, ty0, st);
-    stage_store(lds, a.ch_w[0] >> 3, st);
-    __syncthreads();
-    for (int c = 0; c < a.nchunk; ++c) {
-        const bool more = c + 1 < a.nchunk;
-        if (more) stage_load(a, c + 1, tx0, ty0, st);          // in flight during the MFMAs
-        compute_chunk<NT>(a, c, lds + (c & 1) * kChunkBytes, acc, lane, X, Yb, n0);
-        if (more) stage_store(lds + ((c + 1) & 1) * kChunkBytes, a.ch_w[c + 1] >> 3, st);
+    if constexpr (BStage<NT>::lds) {           // single halo + B buffers, two barriers per chunk
+        uint4 bs[BStage<NT>::kRegs];
+        stage_load(a, 0, tx0, ty0, st);
+        bstage_load<NT>(a, 0, n0, bs);
+        stage_store(lds, a.ch_w[0] >> 3, st);
+        bstage_store<NT>(bbuf, a.ch_w[0] == 32 ? 9 : 5, bs);
         __syncthreads();
+        for (int c = 0; c < a.nchunk; ++c) {
+            const bool more = c + 1 < a.nchunk;
+            if (more) {                        // in flight during the MFMAs
+                stage_load(a, c + 1, tx0, ty0, st);
+                bstage_load<NT>(a, c + 1, n0, bs);
+            }
+            compute_chunk<NT>(a, c, lds, bbuf, acc, lane, X, Yb, n0);
+            __syncthreads();
+            if (more) {
+                stage_store(lds, a.ch_w[c + 1] >> 3, st);
+                bstage_store<NT>(bbuf, a.ch_w[c + 1] == 32 ? 9 : 5, bs);
+                __syncthreads();
+            }
+        }
+    } else {                                   // double-buffered halo, per-wave global B
+        stage_load(a, 0, tx0, ty0, st);
+        stage_store(lds, a.ch_w[0] >> 3, st);
+        __syncthreads();
+        for (int c = 0; c < a.nchunk; ++c) {
+            const bool more = c + 1 < a.nchunk;
+            if (more) stage_load(a, c + 1, tx0, ty0, st);      // in flight during the MFMAs
+            compute_chunk<NT>(a, c, lds + (c & 1) * kChunkBytes, nullptr, acc, lane, X, Yb, n0);
+            if (more) stage_store(lds + ((c + 1) & 1) * kChunkBytes, a.ch_w[c + 1] >> 3, st);
+            __syncthreads();
+        }
     }
 
     // epilogue.  C/D: lane holds column co = 16 n + i and rows 4 h + r (r = register): pixel
