@@ -39,3 +39,12 @@ gf = gflop_per_frame(d.info(), W, H)
 m = float(np.median(ms))
 print(f"denoise {W}x{H}: {m:.3f} ms/execute (HIP events, median of {a.iters}; wall {wall:.3f}), "
       f"{gf:.1f} GFLOP -> {gf / m:.1f} TFLOP/s = {gf / m / 2500:.3f} of 2.5 PF f16 dense")
+lm = np.zeros(17)
+for _ in range(5):
+    d.execute(col, alb, nrm, out)
+    lm += np.array(d.layer_ms())
+lm /= 5
+names = ["input+ae", "enc_conv0", "enc_conv1", "enc_conv2", "enc_conv3", "enc_conv4", "enc_conv5a", "enc_conv5b",
+         "dec_conv4a", "dec_conv4b", "dec_conv3a", "dec_conv3b", "dec_conv2a", "dec_conv2b", "dec_conv1a",
+         "dec_conv1b", "dec_conv0"]
+print("per-layer ms (HIP events, mean of 5): " + ", ".join(f"{n} {v:.4f}" for n, v in zip(names, lm)))
