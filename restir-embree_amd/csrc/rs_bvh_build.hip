@@ -466,6 +466,9 @@ __global__ void k_wide_tris(const float* __restrict__ pos, const int* __restrict
     tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
 }
 
+#ifndef RS_WIDE_COLLAPSE
+#define RS_WIDE_COLLAPSE 1        // rs_wide.h build_wide_host: 0 greedy, 1 SAH-optimal within kWideStack levels
+#endif
 // downloads the PLOC tree, collapses it on the host, uploads the wide nodes and gathers their triangles
 static int build_wide(const float* d_pos, const float4* nlo_d, const float4* nhi_d, int n, int root, hipStream_t st,
                       WideBvh* w, std::string& err) {
@@ -477,7 +480,8 @@ static int build_wide(const float* d_pos, const float4* nlo_d, const float4* nhi
     std::vector<uint32_t> nodes;
     std::vector<int> prims;
     int depth = 0;
-    if (build_wide_host((const float*)nlo.data(), (const float*)nhi.data(), n, root, nodes, prims, depth, err) != 0) return -1;
+    if (build_wide_host((const float*)nlo.data(), (const float*)nhi.data(), n, root, nodes, prims, depth, err,
+                        RS_WIDE_COLLAPSE, 1.0f, 0.3f, RS_WIDE_STACK) != 0) return -1;
     int* d_prims = nullptr;
     if (hipMalloc(&w->nodes, nodes.size() * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&w->tris, prims.size() * 3 * sizeof(float4)) != hipSuccess ||

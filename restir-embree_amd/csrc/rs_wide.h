@@ -8,6 +8,10 @@
 #include <string>
 #include <vector>
 
+#ifndef RS_WIDE_STACK
+#define RS_WIDE_STACK 8   // the walk's register stack (rs_scene.h kWideStack, same default): deepest tree walked
+#endif
+
 namespace rs {
 // ============================================================================================
 // 8-wide tree for the per-lane walks (rs_scene.h "8-wide per-lane walks").  Collapsed on the host from
@@ -65,10 +69,91 @@ inline bool wide_axis(float lo, float hi, const float* clo, const float* chi, in
 }  // namespace wide
 using namespace wide;
 
+// SAH-optimal collapse (Ylitie, Karras, Laine 2017, "Efficient incoherent ray traversal on GPUs through
+// compressed wide BVHs", §3.2), with one triangle per leaf slot and a bound on the wide tree's depth (the
+// walk's register stack holds one group per level: rs_scene.h kWideStack).  For binary node x, slot budget
+// k <= 8 and height budget g (a wide node placed in a slot may have at most g levels of wide nodes below it):
+//   triangle x:  S(x, k, g) = A(x) c_tri
+//   S(x, 1, g) = N(x, g) = A(x) c_node + D(x, 8, g - 1)       (x as a wide node; infeasible for g < 0)
+//   S(x, k, g) = min(S(x, k - 1, g), D(x, k, g)),  D(x, k, g) = min over a of S(l, a, g) + S(r, k - a, g)
+// The root is N(root, depth budget).  plan() fills the tables bottom-up; kids() expands a wide node's choice.
+struct SahCollapse {
+    static constexpr int kG = 10;                // g = -1 .. 8
+    int n = 0, gmax = 8;
+    std::vector<float> S;                        // per node [g + 1][k - 1]
+    std::vector<uint8_t> open, split;
+    size_t at(int x, int g, int k) const { return ((size_t)x * kG + (size_t)(g + 1)) * 8 + (size_t)(k - 1); }
+    bool plan(const float* nlo, const float* nhi, int n_, int root, float c_node, float c_tri, int depth_max) {
+        n = n_; gmax = depth_max;
+        if (gmax < 0 || gmax > kG - 2) return false;
+        const size_t total = 2 * (size_t)n - 1;
+        S.assign(total * kG * 8, 0.0f); open.assign(total * kG * 8, 0); split.assign(total * kG * 8, 0);
+        auto area = [&](int c) { const float* a = nlo + 4 * (size_t)c; const float* z = nhi + 4 * (size_t)c;
+            const float ex = z[0] - a[0], ey = z[1] - a[1], ez = z[2] - a[2]; return ex * ey + ey * ez + ez * ex; };
+        const float inf = 3.0e38f;
+        std::vector<std::pair<int, bool>> st = {{root, false}};   // post-order
+        while (!st.empty()) {
+            auto [x, done] = st.back();
+            st.pop_back();
+            if (x < n) { for (int g = -1; g <= gmax; ++g) for (int k = 1; k <= 8; ++k) S[at(x, g, k)] = area(x) * c_tri; continue; }
+            const int l = h_f2i(nlo[4 * (size_t)x + 3]), r = h_f2i(nhi[4 * (size_t)x + 3]);
+            if (l < 0 || r < 0 || (size_t)l >= total || (size_t)r >= total) return false;
+            if (!done) { st.push_back({x, true}); st.push_back({l, false}); st.push_back({r, false}); continue; }
+            float Dprev[8] = {};                     // D(x, ., g - 1)
+            for (int g = -1; g <= gmax; ++g) {
+                float D[8];
+                for (int k = 2; k <= 8; ++k) {       // D(x, k, g): a slots to the left child, k - a to the right
+                    float best = inf; int ba = 1;
+                    for (int a = 1; a < k; ++a) {
+                        const float v = S[at(l, g, a)] + S[at(r, g, k - a)];
+                        if (v < best) { best = v; ba = a; }
+                    }
+                    D[k - 1] = best; split[at(x, g, k)] = (uint8_t)ba;
+                }
+                // N(x, g) needs D(x, 8, g - 1): computed in the previous g iteration (g - 1 >= -1), else infeasible
+                float Nx = inf;
+                if (g >= 0) {
+                    const float d8 = Dprev[7];
+                    Nx = d8 < inf ? area(x) * c_node + d8 : inf;
+                }
+                S[at(x, g, 1)] = Nx;
+                for (int k = 2; k <= 8; ++k) {
+                    const float prev = S[at(x, g, k - 1)];
+                    const bool o = D[k - 1] < prev;
+                    S[at(x, g, k)] = o ? D[k - 1] : prev;
+                    open[at(x, g, k)] = o ? 1 : 0;
+                }
+                for (int k = 0; k < 8; ++k) Dprev[k] = D[k];
+            }
+        }
+        return S[at(root, gmax, 1)] < inf || root < n;
+    }
+    void expand(const float* nlo, const float* nhi, int x, int k, int g, std::vector<int>& out, std::vector<int>& hb) const {
+        while (x >= n && k > 1 && !open[at(x, g, k)]) --k;
+        if (x < n || k == 1) { out.push_back(x); hb.push_back(g); return; }
+        const int a = split[at(x, g, k)];
+        expand(nlo, nhi, h_f2i(nlo[4 * (size_t)x + 3]), a, g, out, hb);
+        expand(nlo, nhi, h_f2i(nhi[4 * (size_t)x + 3]), k - a, g, out, hb);
+    }
+    // children of wide node c built under height budget g; hb = each child's own height budget
+    std::vector<int> kids(const float* nlo, const float* nhi, int c, int g, std::vector<int>& hb) const {
+        std::vector<int> out;
+        hb.clear();
+        if (c < n) { out.push_back(c); hb.push_back(g); return out; }
+        const int a = split[at(c, g - 1, 8)];
+        expand(nlo, nhi, h_f2i(nlo[4 * (size_t)c + 3]), a, g - 1, out, hb);
+        expand(nlo, nhi, h_f2i(nhi[4 * (size_t)c + 3]), 8 - a, g - 1, out, hb);
+        return out;
+    }
+};
+
 // nlo / nhi: the PLOC nodes as 4 floats each (ids < n: primitives, hi.w = triangle index bits; ids >= n:
-// internal, lo.w / hi.w = left / right child id bits); out: 20 words per wide node
+// internal, lo.w / hi.w = left / right child id bits); out: 20 words per wide node.  collapse: 0 greedy
+// (open the largest-area interior child until 8), 1 SAH-optimal within max_depth levels (SahCollapse,
+// costs c_node / c_tri; falls back to greedy when it has no plan)
 inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, std::vector<uint32_t>& out,
-                           std::vector<int>& tri_prims, int& depth, std::string& err) {
+                           std::vector<int>& tri_prims, int& depth, std::string& err, int collapse = 0,
+                           float c_node = 1.0f, float c_tri = 0.3f, int max_depth = 8) {
     out.clear(); tri_prims.clear(); depth = 0;
     if (n <= 0) return 0;
     auto is_prim = [&](int c) { return c < n; };
@@ -76,28 +161,47 @@ inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, 
         for (int k = 0; k < 3; ++k) { b.lo[k] = a[k]; b.hi[k] = z[k]; } return b; };
     auto area = [&](int c) { const float* a = nlo + 4 * (size_t)c; const float* z = nhi + 4 * (size_t)c;
         const float ex = z[0] - a[0], ey = z[1] - a[1], ez = z[2] - a[2]; return ex * ey + ey * ez + ez * ex; };
-    std::vector<int> queue = {root}, level = {0};          // wide node i = PLOC node queue[i]
+    SahCollapse sah;
+    // the plan's tables take 480 B per binary node (0.24 GB at C3's 248 k triangles): above 2 M triangles,
+    // or without a plan inside the depth, the greedy collapse
+    if (collapse == 1 && (n > (1 << 21) || !sah.plan(nlo, nhi, n, root, c_node, c_tri, max_depth)))
+        collapse = 0;
+    std::vector<int> queue = {root}, level = {0}, budget = {max_depth};   // wide node i = PLOC node queue[i]
     for (size_t qi = 0; qi < queue.size(); ++qi) {
         const int c = queue[qi];
-        std::vector<int> kids;
-        if (is_prim(c)) kids = {c};
-        else kids = {h_f2i(nlo[4 * (size_t)c + 3]), h_f2i(nhi[4 * (size_t)c + 3])};
-        while (kids.size() < 8) {
-            int best = -1; float ba = -1.0f;
-            for (int i = 0; i < (int)kids.size(); ++i)
-                if (!is_prim(kids[i]) && area(kids[i]) > ba) { ba = area(kids[i]); best = i; }
-            if (best < 0) break;
-            const int x = kids[best];
-            kids.erase(kids.begin() + best);
-            kids.push_back(h_f2i(nlo[4 * (size_t)x + 3]));
-            kids.push_back(h_f2i(nhi[4 * (size_t)x + 3]));
+        std::vector<int> kids, hb;
+        if (collapse == 1) kids = sah.kids(nlo, nhi, c, budget[qi], hb);
+        else {
+            if (is_prim(c)) kids = {c};
+            else kids = {h_f2i(nlo[4 * (size_t)c + 3]), h_f2i(nhi[4 * (size_t)c + 3])};
+            while (kids.size() < 8) {
+                int best = -1; float ba = -1.0f;
+                for (int i = 0; i < (int)kids.size(); ++i)
+                    if (!is_prim(kids[i]) && area(kids[i]) > ba) { ba = area(kids[i]); best = i; }
+                if (best < 0) break;
+                const int x = kids[best];
+                kids.erase(kids.begin() + best);
+                kids.push_back(h_f2i(nlo[4 * (size_t)x + 3]));
+                kids.push_back(h_f2i(nhi[4 * (size_t)x + 3]));
+            }
         }
-        std::stable_partition(kids.begin(), kids.end(), [&](int k) { return !is_prim(k); });
+        if (collapse != 1) std::stable_partition(kids.begin(), kids.end(), [&](int k) { return !is_prim(k); });
+        if (collapse == 1) {                           // keep each slot's height budget with its child
+            std::vector<int> order(kids.size());
+            for (size_t i = 0; i < kids.size(); ++i) order[i] = (int)i;
+            std::stable_partition(order.begin(), order.end(), [&](int i) { return !is_prim(kids[i]); });
+            std::vector<int> k2, h2;
+            for (int i : order) { k2.push_back(kids[i]); h2.push_back(hb[i]); }
+            kids.swap(k2); hb.swap(h2);
+        }
         int ni = 0;
         while (ni < (int)kids.size() && !is_prim(kids[ni])) ++ni;
         const int nv = (int)kids.size();
         const uint32_t child_base = (uint32_t)queue.size(), tri_base = (uint32_t)tri_prims.size();
-        for (int i = 0; i < ni; ++i) { queue.push_back(kids[i]); level.push_back(level[qi] + 1); depth = std::max(depth, level[qi] + 1); }
+        for (int i = 0; i < ni; ++i) {
+            queue.push_back(kids[i]); level.push_back(level[qi] + 1); depth = std::max(depth, level[qi] + 1);
+            budget.push_back(collapse == 1 ? hb[i] : 0);
+        }
         for (int i = ni; i < nv; ++i) tri_prims.push_back(h_f2i(nhi[4 * (size_t)kids[i] + 3]));
         // quantisation frame from the union of the children (= the PLOC node's box)
         WBox u = box(kids[0]);

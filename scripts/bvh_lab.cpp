@@ -670,7 +670,10 @@ int main(int argc, char** argv) {
             std::memcpy(&a[3], &L, 4); std::memcpy(&b[3], &R, 4);
         }
         std::vector<uint32_t> WN; std::vector<int> pr; int depth = 0; std::string err;
-        int rc = rs::build_wide_host(lo.data(), hi.data(), n, id[T.root], WN, pr, depth, err);
+        const int coll = getenv("COLLAPSE") ? atoi(getenv("COLLAPSE")) : 0;
+        const float c_tri = getenv("C_TRI") ? (float)atof(getenv("C_TRI")) : 0.3f;
+        const int sl = getenv("MAX_DEPTH") ? atoi(getenv("MAX_DEPTH")) : 8;
+        int rc = rs::build_wide_host(lo.data(), hi.data(), n, id[T.root], WN, pr, depth, err, coll, 1.0f, c_tri, sl);
         printf("build_wide_host rc=%d err=%s nodes=%zu depth=%d\n", rc, err.c_str(), WN.size() / 20, depth);
         if (rc || !getenv("EMU")) return 0;
         Flat Fr = make_flat(T, 8, 1.0f, 1.0f, ORD_LEFT);

@@ -152,7 +152,7 @@ void walk(const std::vector<uint32_t>& W, const std::vector<int>& prims, const S
 
 extern "C" {
 // structure + conservativeness; returns the number of wide nodes (> 0) or a negative code, msg = reason
-int wide_check(int n, uint32_t seed, int* depth_out, char* msg, int msg_len) {
+int wide_check(int n, uint32_t seed, int* depth_out, char* msg, int msg_len, int collapse) {
     Scene S;
     make_scene(S, n, seed);
     std::vector<uint32_t> W;
@@ -160,7 +160,8 @@ int wide_check(int n, uint32_t seed, int* depth_out, char* msg, int msg_len) {
     int depth = 0;
     std::string err;
     auto fail = [&](const std::string& m) { if (msg) { std::strncpy(msg, m.c_str(), msg_len - 1); msg[msg_len - 1] = 0; } return -1; };
-    if (rs::build_wide_host(S.nlo.data(), S.nhi.data(), S.n, S.root, W, prims, depth, err) != 0) return fail(err);
+    if (rs::build_wide_host(S.nlo.data(), S.nhi.data(), S.n, S.root, W, prims, depth, err, collapse) != 0) return fail(err);
+    if (depth > 8) return fail("deeper than the walk's stack");
     const size_t nn = W.size() / 20;
     if ((int)prims.size() != n) return fail("triangle count");
     std::vector<int> seen(n, 0);
@@ -216,14 +217,14 @@ int wide_check(int n, uint32_t seed, int* depth_out, char* msg, int msg_len) {
 }
 
 // random queries: wide walk (restated) vs brute force; returns the number of rays checked or a negative code
-int wide_query(int n, uint32_t seed, int n_rays, int* n_hits) {
+int wide_query(int n, uint32_t seed, int n_rays, int* n_hits, int collapse) {
     Scene S;
     make_scene(S, n, seed);
     std::vector<uint32_t> W;
     std::vector<int> prims;
     int depth = 0;
     std::string err;
-    if (rs::build_wide_host(S.nlo.data(), S.nhi.data(), S.n, S.root, W, prims, depth, err) != 0) return -1;
+    if (rs::build_wide_host(S.nlo.data(), S.nhi.data(), S.n, S.root, W, prims, depth, err, collapse) != 0) return -1;
     std::mt19937 rng(seed * 7 + 1);
     std::uniform_real_distribution<float> U(-1.0f, 1.0f);
     int hits = 0;

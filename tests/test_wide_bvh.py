@@ -21,25 +21,28 @@ def _lib():
     if not os.path.exists(SO) or os.path.getmtime(SO) < max(os.path.getmtime(SRC), os.path.getmtime(HDR)):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", "-o", SO, SRC])
     L = ctypes.CDLL(SO)
-    L.wide_check.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
-    L.wide_query.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.wide_check.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int,
+                             ctypes.c_int]
+    L.wide_query.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     return L
 
 
+@pytest.mark.parametrize("collapse", [0, 1], ids=["greedy", "sah"])
 @pytest.mark.parametrize("n,seed", [(1, 1), (2, 2), (7, 3), (9, 4), (64, 5), (1000, 6), (20000, 7)])
-def test_wide_tree_structure_and_conservative_boxes(n, seed):
+def test_wide_tree_structure_and_conservative_boxes(n, seed, collapse):
     L = _lib()
     msg = ctypes.create_string_buffer(256)
     depth = ctypes.c_int(-1)
-    nn = L.wide_check(n, seed, ctypes.byref(depth), msg, 256)
+    nn = L.wide_check(n, seed, ctypes.byref(depth), msg, 256, collapse)
     assert nn > 0, msg.value.decode()
     assert depth.value >= 0 and (n <= 8 or depth.value >= 1)
 
 
+@pytest.mark.parametrize("collapse", [0, 1], ids=["greedy", "sah"])
 @pytest.mark.parametrize("n,seed", [(1, 11), (5, 12), (300, 13), (5000, 14)])
-def test_wide_walk_matches_brute_force(n, seed):
+def test_wide_walk_matches_brute_force(n, seed, collapse):
     L = _lib()
     hits = ctypes.c_int(0)
-    rc = L.wide_query(n, seed, 4000, ctypes.byref(hits))
+    rc = L.wide_query(n, seed, 4000, ctypes.byref(hits), collapse)
     assert rc == 4000, f"ray {-rc - 1000} differs from brute force"
     assert n < 100 or hits.value > 100
