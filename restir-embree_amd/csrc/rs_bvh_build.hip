@@ -466,6 +466,9 @@ __global__ void k_wide_tris(const float* __restrict__ pos, const int* __restrict
     tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
 }
 
+#ifndef RS_WIDE_SOURCE
+#define RS_WIDE_SOURCE 1          // the collapse's binary source tree: 0 the PLOC tree, 1 rs_wide.h build_sah_host
+#endif
 #ifndef RS_WIDE_COLLAPSE
 #define RS_WIDE_COLLAPSE 1        // rs_wide.h build_wide_host: 0 greedy, 1 SAH-optimal within kWideStack levels
 #endif
@@ -473,15 +476,23 @@ __global__ void k_wide_tris(const float* __restrict__ pos, const int* __restrict
 static int build_wide(const float* d_pos, const float4* nlo_d, const float4* nhi_d, int n, int root, hipStream_t st,
                       WideBvh* w, std::string& err) {
     const size_t total = 2 * (size_t)n - 1;
-    std::vector<float4> nlo(total), nhi(total);
-    if (hipMemcpyAsync(nlo.data(), nlo_d, total * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(nhi.data(), nhi_d, total * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) { err = "wide BVH: download failed"; return -1; }
+    std::vector<float> lo, hi;
+    if (RS_WIDE_SOURCE == 1 && n <= (1 << 21)) {   // the host SAH tree as the collapse's source
+        std::vector<float> pos(9 * (size_t)n);
+        if (hipMemcpyAsync(pos.data(), d_pos, pos.size() * sizeof(float), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) { err = "wide BVH: download failed"; return -1; }
+        root = build_sah_host(pos.data(), n, lo, hi);
+    } else {                                          // the PLOC tree
+        lo.resize(4 * total); hi.resize(4 * total);
+        if (hipMemcpyAsync(lo.data(), nlo_d, total * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(hi.data(), nhi_d, total * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) { err = "wide BVH: download failed"; return -1; }
+    }
     std::vector<uint32_t> nodes;
     std::vector<int> prims;
     int depth = 0;
-    if (build_wide_host((const float*)nlo.data(), (const float*)nhi.data(), n, root, nodes, prims, depth, err,
-                        RS_WIDE_COLLAPSE, 1.0f, 0.3f, RS_WIDE_STACK) != 0) return -1;
+    if (build_wide_host(lo.data(), hi.data(), n, root, nodes, prims, depth, err, RS_WIDE_COLLAPSE, 1.0f, 0.3f,
+                        RS_WIDE_STACK) != 0) return -1;
     int* d_prims = nullptr;
     if (hipMalloc(&w->nodes, nodes.size() * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&w->tris, prims.size() * 3 * sizeof(float4)) != hipSuccess ||

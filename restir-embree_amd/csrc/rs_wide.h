@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -68,6 +69,120 @@ inline bool wide_axis(float lo, float hi, const float* clo, const float* chi, in
 }
 }  // namespace wide
 using namespace wide;
+
+// Top-down SAH source tree for the collapse (the PLOC tree stays the binary walks' and the refit's): binned
+// SAH (32 bins per axis over the centroid bounds) above kSweepMax triangles, a full sweep over the sorted
+// centroids below (cost = the children's half areas x their triangle counts).  Output in the PLOC arrays'
+// shape: ids < n triangles (box, hi.w = triangle bits), ids >= n internal (lo.w / hi.w = child id bits).
+// pos: 9 floats per triangle.  Returns the root id.
+inline int build_sah_host(const float* pos, int n, std::vector<float>& nlo, std::vector<float>& nhi) {
+    constexpr int kSweepMax = 2048, kBins = 32;
+    const size_t total = 2 * (size_t)n - 1;
+    nlo.assign(4 * total, 0.0f); nhi.assign(4 * total, 0.0f);
+    std::vector<WBox> tb(n);
+    std::vector<float> cen(3 * (size_t)n);
+    for (int t = 0; t < n; ++t) {
+        const float* p = pos + 9 * (size_t)t;
+        for (int a = 0; a < 3; ++a) {
+            tb[t].lo[a] = std::min(std::min(p[a], p[3 + a]), p[6 + a]);
+            tb[t].hi[a] = std::max(std::max(p[a], p[3 + a]), p[6 + a]);
+            cen[3 * (size_t)t + a] = 0.5f * tb[t].lo[a] + 0.5f * tb[t].hi[a];
+            nlo[4 * (size_t)t + a] = tb[t].lo[a]; nhi[4 * (size_t)t + a] = tb[t].hi[a];
+        }
+        nlo[4 * (size_t)t + 3] = 0.0f; nhi[4 * (size_t)t + 3] = [&] { float f; std::memcpy(&f, &t, 4); return f; }();
+    }
+    if (n == 1) return 0;
+    auto grow = [](WBox& b, const WBox& c) {
+        for (int a = 0; a < 3; ++a) { b.lo[a] = std::min(b.lo[a], c.lo[a]); b.hi[a] = std::max(b.hi[a], c.hi[a]); }
+    };
+    auto empty = [] { WBox b; for (int a = 0; a < 3; ++a) { b.lo[a] = 3.0e38f; b.hi[a] = -3.0e38f; } return b; };
+    auto half_area = [](const WBox& b) {
+        const double x = (double)b.hi[0] - b.lo[0], y = (double)b.hi[1] - b.lo[1], z = (double)b.hi[2] - b.lo[2];
+        return x * y + y * z + z * x;
+    };
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; ++i) idx[i] = i;
+    std::vector<double> rarea(kSweepMax + 1);
+    int next = n;
+    struct Job { int first, count, id, parent, side; };
+    std::vector<Job> st = {{0, n, -1, -1, 0}};
+    int root = -1;
+    auto link = [&](const Job& j, int id) {
+        if (j.parent < 0) { root = id; return; }
+        float f; std::memcpy(&f, &id, 4);
+        (j.side ? nhi : nlo)[4 * (size_t)j.parent + 3] = f;
+    };
+    while (!st.empty()) {
+        Job j = st.back();
+        st.pop_back();
+        if (j.count == 1) { link(j, idx[j.first]); continue; }
+        const int id = next++;
+        link(j, id);
+        WBox nb = empty();
+        for (int i = j.first; i < j.first + j.count; ++i) grow(nb, tb[idx[i]]);
+        for (int a = 0; a < 3; ++a) { nlo[4 * (size_t)id + a] = nb.lo[a]; nhi[4 * (size_t)id + a] = nb.hi[a]; }
+        int* I = idx.data() + j.first;
+        int split = j.count / 2;
+        if (j.count > kSweepMax) {               // binned SAH
+            float clo[3] = {3.0e38f, 3.0e38f, 3.0e38f}, chi[3] = {-3.0e38f, -3.0e38f, -3.0e38f};
+            for (int i = 0; i < j.count; ++i)
+                for (int a = 0; a < 3; ++a) { clo[a] = std::min(clo[a], cen[3 * (size_t)I[i] + a]); chi[a] = std::max(chi[a], cen[3 * (size_t)I[i] + a]); }
+            double best = 1e300; int bax = -1, bb = 0;
+            for (int a = 0; a < 3; ++a) {
+                if (!(chi[a] > clo[a])) continue;
+                const double sc = kBins / ((double)chi[a] - clo[a]);
+                WBox bx[kBins]; int cnt[kBins] = {};
+                for (int b = 0; b < kBins; ++b) bx[b] = empty();
+                for (int i = 0; i < j.count; ++i) {
+                    const int b = std::min(kBins - 1, (int)(((double)cen[3 * (size_t)I[i] + a] - clo[a]) * sc));
+                    ++cnt[b]; grow(bx[b], tb[I[i]]);
+                }
+                double ra[kBins]; int rc[kBins];
+                WBox r = empty(); int c = 0;
+                for (int b = kBins - 1; b >= 1; --b) { grow(r, bx[b]); c += cnt[b]; ra[b] = c ? half_area(r) : 0.0; rc[b] = c; }
+                WBox l = empty(); c = 0;
+                for (int b = 1; b < kBins; ++b) {
+                    grow(l, bx[b - 1]); c += cnt[b - 1];
+                    if (!c || !rc[b]) continue;
+                    const double cost = half_area(l) * c + ra[b] * rc[b];
+                    if (cost < best) { best = cost; bax = a; bb = b; }
+                }
+            }
+            if (bax >= 0) {
+                const double sc = kBins / ((double)chi[bax] - clo[bax]);
+                int* mid = std::partition(I, I + j.count, [&](int t) {
+                    return std::min(kBins - 1, (int)(((double)cen[3 * (size_t)t + bax] - clo[bax]) * sc)) < bb;
+                });
+                split = (int)(mid - I);
+            }
+            if (split <= 0 || split >= j.count) split = j.count / 2;
+        } else {                                 // full sweep
+            double best = 1e300; int bax = 0, bs = j.count / 2;
+            auto by_axis = [&](int a) {
+                std::sort(I, I + j.count, [&](int p, int q) {
+                    const float cp = cen[3 * (size_t)p + a], cq = cen[3 * (size_t)q + a];
+                    return cp < cq || (cp == cq && p < q);
+                });
+            };
+            for (int a = 0; a < 3; ++a) {
+                by_axis(a);
+                WBox r = empty();
+                for (int i = j.count - 1; i >= 1; --i) { grow(r, tb[I[i]]); rarea[i] = half_area(r); }
+                WBox l = empty();
+                for (int i = 1; i < j.count; ++i) {
+                    grow(l, tb[I[i - 1]]);
+                    const double cost = half_area(l) * i + rarea[i] * (j.count - i);
+                    if (cost < best) { best = cost; bax = a; bs = i; }
+                }
+            }
+            if (bax != 2) by_axis(bax);
+            split = bs;
+        }
+        st.push_back({j.first + split, j.count - split, -1, id, 1});
+        st.push_back({j.first, split, -1, id, 0});
+    }
+    return root;
+}
 
 // SAH-optimal collapse (Ylitie, Karras, Laine 2017, "Efficient incoherent ray traversal on GPUs through
 // compressed wide BVHs", §3.2), with one triangle per leaf slot and a bound on the wide tree's depth (the

@@ -1,3 +1,4 @@
+#include <chrono>
 // bvh_lab.cpp -- offline BVH quality lab (analysis tooling, not product, not test).
 // Builds candidate trees on the CPU for a dumped scene and replays the walk the GPU's per-lane kernels
 // make (skip-pointer preorder, stackless, conservative slab test, leaf triangles tested in a wave-wide
@@ -669,11 +670,19 @@ int main(int argc, char** argv) {
             int L = B.l >= 0 ? id[B.l] : -1, R = B.r >= 0 ? id[B.r] : B.prims[0];
             std::memcpy(&a[3], &L, 4); std::memcpy(&b[3], &R, 4);
         }
+        int wroot = id[T.root];
+        if (getenv("HOST_SAH")) {                 // the product's host SAH source tree (rs_wide.h build_sah_host)
+            const auto t0 = std::chrono::steady_clock::now();
+            wroot = rs::build_sah_host((const float*)g_tris.data(), n, lo, hi);
+            printf("build_sah_host %.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        }
         std::vector<uint32_t> WN; std::vector<int> pr; int depth = 0; std::string err;
         const int coll = getenv("COLLAPSE") ? atoi(getenv("COLLAPSE")) : 0;
         const float c_tri = getenv("C_TRI") ? (float)atof(getenv("C_TRI")) : 0.3f;
         const int sl = getenv("MAX_DEPTH") ? atoi(getenv("MAX_DEPTH")) : 8;
-        int rc = rs::build_wide_host(lo.data(), hi.data(), n, id[T.root], WN, pr, depth, err, coll, 1.0f, c_tri, sl);
+        const auto tw = std::chrono::steady_clock::now();
+        int rc = rs::build_wide_host(lo.data(), hi.data(), n, wroot, WN, pr, depth, err, coll, 1.0f, c_tri, sl);
+        printf("build_wide_host %.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count());
         printf("build_wide_host rc=%d err=%s nodes=%zu depth=%d\n", rc, err.c_str(), WN.size() / 20, depth);
         if (rc || !getenv("EMU")) return 0;
         Flat Fr = make_flat(T, 8, 1.0f, 1.0f, ORD_LEFT);

@@ -1,6 +1,8 @@
 // TEST INFRASTRUCTURE: CPU checks of the 8-wide tree of the per-lane walks (restir-embree_amd/csrc/rs_wide.h,
 // the collapse rs_bvh_build.hip runs after every PLOC build) and of the walk's quantised box test
 // (rs_scene.h wide_hits, restated here with the same float operations).  Built by tests/test_wide_bvh.py.
+//   collapse: 0 greedy, 1 SAH-optimal (both over the random merge tree), 2 SAH-optimal over rs_wide.h
+//   build_sah_host's top-down SAH tree (the product's default)
 //   wide_check: structure (breadth-first layout, slots, every triangle exactly once, depth) and
 //               conservativeness (every dequantised child box contains the exact child box)
 //   wide_query: random rays (incl. axis-parallel directions and origins on box planes) through the wide walk
@@ -160,6 +162,7 @@ int wide_check(int n, uint32_t seed, int* depth_out, char* msg, int msg_len, int
     int depth = 0;
     std::string err;
     auto fail = [&](const std::string& m) { if (msg) { std::strncpy(msg, m.c_str(), msg_len - 1); msg[msg_len - 1] = 0; } return -1; };
+    if (collapse == 2) { S.root = rs::build_sah_host(S.pos.data(), S.n, S.nlo, S.nhi); collapse = 1; }   // host SAH source
     if (rs::build_wide_host(S.nlo.data(), S.nhi.data(), S.n, S.root, W, prims, depth, err, collapse) != 0) return fail(err);
     if (depth > 8) return fail("deeper than the walk's stack");
     const size_t nn = W.size() / 20;
@@ -224,6 +227,7 @@ int wide_query(int n, uint32_t seed, int n_rays, int* n_hits, int collapse) {
     std::vector<int> prims;
     int depth = 0;
     std::string err;
+    if (collapse == 2) { S.root = rs::build_sah_host(S.pos.data(), S.n, S.nlo, S.nhi); collapse = 1; }
     if (rs::build_wide_host(S.nlo.data(), S.nhi.data(), S.n, S.root, W, prims, depth, err, collapse) != 0) return -1;
     std::mt19937 rng(seed * 7 + 1);
     std::uniform_real_distribution<float> U(-1.0f, 1.0f);
