@@ -673,7 +673,7 @@ int main(int argc, char** argv) {
         int wroot = id[T.root];
         if (getenv("HOST_SAH")) {                 // the product's host SAH source tree (rs_wide.h build_sah_host)
             const auto t0 = std::chrono::steady_clock::now();
-            wroot = rs::build_sah_host((const float*)g_tris.data(), n, lo, hi);
+            wroot = rs::build_sah_host((const float*)g_tris.data(), n, lo, hi, getenv("SWEEP_MAX") ? atoi(getenv("SWEEP_MAX")) : 2048);
             printf("build_sah_host %.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         }
         std::vector<uint32_t> WN; std::vector<int> pr; int depth = 0; std::string err;
@@ -747,7 +747,7 @@ int main(int argc, char** argv) {
             // 8x8 pixel quadrants (the kernels' layout) vs the 256 rays sorted by a target key.
             const int K = 8;
             const char* names[4] = {"8x8 pixels", "sorted by emitter", "sorted by target Morton", "sorted by dir octant+Morton"};
-            double st[4] = {0, 0, 0, 0}, ds[4] = {0, 0, 0, 0}, lane_f = 0; long nwave = 0;
+            double st[4] = {0, 0, 0, 0}, ds[4] = {0, 0, 0, 0}, un[4] = {0, 0, 0, 0}, lane_f = 0; long nwave = 0;
             std::mt19937 rg2(5);
             for (int ty = 0; ty + 16 <= H; ty += 16)
                 for (int tx = 0; tx + 16 <= W; tx += 16) {
@@ -787,6 +787,11 @@ int main(int argc, char** argv) {
                                 size_t T = 0;
                                 for (int i = 0; i < 64; ++i) T = std::max(T, seq[key[g][64 * w + i] & 255].size());
                                 st[g] += T;
+                                {   // the union of the wave's walks: steps of a wave-lockstep wide walk
+                                    std::vector<uint32_t> u;
+                                    for (int i = 0; i < 64; ++i) { auto& q = seq[key[g][64 * w + i] & 255]; u.insert(u.end(), q.begin(), q.end()); }
+                                    std::sort(u.begin(), u.end()); un[g] += std::unique(u.begin(), u.end()) - u.begin();
+                                }
                                 for (size_t t = 0; t < T; ++t) {
                                     uint32_t v[64]; int nv = 0;
                                     for (int i = 0; i < 64; ++i) { auto& q = seq[key[g][64 * w + i] & 255]; if (t < q.size()) v[nv++] = q[t]; }
@@ -799,8 +804,8 @@ int main(int argc, char** argv) {
                 }
             printf("coherence: lane fetches per ray %.2f\n", lane_f / (nwave * 64.0));
             for (int g = 0; g < 4; ++g)
-                printf("  %-28s steps per wave %.1f, distinct node fetches per wave %.1f (per step %.1f)\n", names[g],
-                       st[g] / nwave, ds[g] / nwave, ds[g] / st[g]);
+                printf("  %-28s steps per wave %.1f, distinct node fetches per wave %.1f (per step %.1f), union %.1f\n", names[g],
+                       st[g] / nwave, ds[g] / nwave, ds[g] / st[g], un[g] / nwave);
         }
         double wsum = 0; for (int v : wave_it) wsum += v;
         printf("emu: primary iters %.2f tris %.2f | bounce iters %.2f tris %.2f | shadow iters %.2f tris %.2f lost %.4f max stack %d wave-max iters %.1f | mismatches %ld | nodes %zu\n",
