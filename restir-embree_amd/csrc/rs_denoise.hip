@@ -148,6 +148,38 @@ __device__ __forceinline__ void stage_store(uint8_t* buf, int spp, const uint4 (
 // dec_conv1a: 247 vs 219 us); those keep per-wave global B loads (next step's prefetched) and a
 // double-buffered halo.
 template <int NT> struct BStage { static constexpr bool lds = NT <= 3; static constexpr int kRegs = lds ? (9 * NT * 64 + 255) / 256 : 1; };
+// NT = 4: B staged through LDS in two stages per 32-channel chunk (steps 0-4, then 5-8: 20 KB at a time), so
+// the workgroup keeps the LDS budget of the per-wave-B form (3 per CU) without its per-wave B loads
+#ifndef RS_DN_HALFB
+#define RS_DN_HALFB 1
+#endif
+constexpr int kHalfSteps = 5;
+template <int NT> struct BHalf { static constexpr bool on = RS_DN_HALFB && NT == 4; static constexpr int kRegs = (kHalfSteps * NT * 64 + 255) / 256; };
+// B fragments of steps [s0, s0 + ns) of chunk c into registers / from registers into bbuf (step s0 first)
+template <int NT>
+__device__ __forceinline__ void bhalf_load(const ConvArgs& a, int c, int n0, int s0, int ns, uint4 (&r)[BHalf<NT>::kRegs]) {
+    const int n = ns * NT * 64;
+    const uint4* w = (const uint4*)a.w;
+#pragma unroll
+    for (int k = 0; k < BHalf<NT>::kRegs; ++k) {
+        const int q = (int)threadIdx.x + k * 256;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (q < n) {
+            const int st = q / (NT * 64), rem = q - st * (NT * 64);
+            v = w[((size_t)(a.ch_step[c] + s0 + st) * a.nt_total + n0) * 64 + rem];
+        }
+        r[k] = v;
+    }
+}
+template <int NT>
+__device__ __forceinline__ void bhalf_store(uint8_t* bbuf, int ns, const uint4 (&r)[BHalf<NT>::kRegs]) {
+    const int n = ns * NT * 64;
+#pragma unroll
+    for (int k = 0; k < BHalf<NT>::kRegs; ++k) {
+        const int q = (int)threadIdx.x + k * 256;
+        if (q < n) *(uint4*)(bbuf + q * 16) = r[k];
+    }
+}
 
 template <int NT>
 __device__ __forceinline__ void bstage_load(const ConvArgs& a, int c, int n0, uint4 (&r)[BStage<NT>::kRegs]) {
@@ -175,25 +207,27 @@ __device__ __forceinline__ void bstage_store(uint8_t* bbuf, int nst, const uint4
     }
 }
 
-template <int NT>
+// steps [s0, s1) of chunk c (s1 < 0: all); BL: B fragments from bbuf (step s0 first), else per wave from global
+template <int NT, bool BL = BStage<NT>::lds || BHalf<NT>::on>
 __device__ __forceinline__ void compute_chunk(const ConvArgs& a, int c, const uint8_t* buf, const uint8_t* bbuf,
-                                              f32x4 (&acc)[4][NT], int lane, int X, int Yb, int n0) {
+                                              f32x4 (&acc)[4][NT], int lane, int X, int Yb, int n0, int s0 = 0,
+                                              int s1 = -1) {
     const int h = lane >> 4;
     const bool w32 = a.ch_w[c] == 32;
-    const int nst = w32 ? 9 : 5;
-    const half8* bp = (const half8*)bbuf + lane;                                      // BStage<NT>::lds
+    const int nst = s1 >= 0 ? s1 : (w32 ? 9 : 5);
+    const half8* bp = (const half8*)bbuf + lane - s0 * NT * 64;                       // BL
     const half8* wp = a.w + ((size_t)a.ch_step[c] * a.nt_total + n0) * 64 + lane;     // otherwise
     half8 bg[NT];
-    if constexpr (!BStage<NT>::lds)
+    if constexpr (!BL)
 #pragma unroll
         for (int n = 0; n < NT; ++n) bg[n] = wp[n * 64];
-    for (int st = 0; st < nst; ++st) {
+    for (int st = s0; st < nst; ++st) {
         int tap, sl;
         if (w32) { tap = st; sl = h; }
         else { tap = 2 * st + (h >> 1); tap = tap > 8 ? 8 : tap; sl = h & 1; }   // tap 9: zero weights
         const int ky = tap / 3, kx = tap - 3 * ky;
         half8 b[NT], bn[NT];
-        if constexpr (BStage<NT>::lds) {
+        if constexpr (BL) {
 #pragma unroll
             for (int n = 0; n < NT; ++n) b[n] = bp[(st * NT + n) * 64];
         } else {
@@ -210,7 +244,7 @@ __device__ __forceinline__ void compute_chunk(const ConvArgs& a, int c, const ui
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[n], acc[g][n], 0, 0, 0);
         }
-        if constexpr (!BStage<NT>::lds)
+        if constexpr (!BL)
 #pragma unroll
             for (int n = 0; n < NT; ++n) bg[n] = bn[n];
     }
@@ -219,14 +253,15 @@ __device__ __forceinline__ void compute_chunk(const ConvArgs& a, int c, const ui
 template <int NT, int POST>
 struct ConvLds {
     static constexpr int kB = 9 * NT * 1024;   // one chunk's B fragments
-    static constexpr int kIn = BStage<NT>::lds ? kChunkBytes + kB : 2 * kChunkBytes;
+    static constexpr int kIn = BStage<NT>::lds ? kChunkBytes + kB
+                             : BHalf<NT>::on ? kChunkBytes + kHalfSteps * NT * 1024 : 2 * kChunkBytes;
     static constexpr int kOut = POST == POST_STORE ? 256 * (NT * 16 + 8) * 2 : POST == POST_POOL ? 64 * (NT * 16 + 8) * 2
                                                                                      : 256 * 17 * 4;
     static constexpr int kBytes = kIn > kOut ? kIn : kOut;
 };
 
 template <int NT, int POST, bool RELU>
-__global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
+__global__ void __launch_bounds__(256, BHalf<NT>::on ? 3 : 1) k_conv3(ConvArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[ConvLds<NT, POST>::kBytes];
     uint8_t* const bbuf = lds + kChunkBytes;
     const int tx0 = blockIdx.x * kTile, ty0 = blockIdx.y * kTile;
@@ -266,6 +301,34 @@ __global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
                 __syncthreads();
             }
         }
+    } else if constexpr (BHalf<NT>::on) {      // single halo buffer, B in two LDS stages per 32-channel chunk
+        uint4 bs[BHalf<NT>::kRegs];
+        auto nsteps = [&](int c) { return a.ch_w[c] == 32 ? 9 : 5; };
+        stage_load(a, 0, tx0, ty0, st);
+        bhalf_load<NT>(a, 0, n0, 0, kHalfSteps, bs);
+        stage_store(lds, a.ch_w[0] >> 3, st);
+        bhalf_store<NT>(bbuf, kHalfSteps, bs);
+        __syncthreads();
+        for (int c = 0; c < a.nchunk; ++c) {
+            const int nst = nsteps(c), nsg = nst > kHalfSteps ? 2 : 1;
+            const bool more = c + 1 < a.nchunk;
+            for (int sg = 0; sg < nsg; ++sg) {  // one compute call site: one inlined copy of the step loop
+                const bool last = sg + 1 == nsg;
+                if (!last) bhalf_load<NT>(a, c, n0, kHalfSteps, nst - kHalfSteps, bs);   // this chunk's second stage
+                else if (more) { stage_load(a, c + 1, tx0, ty0, st); bhalf_load<NT>(a, c + 1, n0, 0, kHalfSteps, bs); }
+                compute_chunk<NT, true>(a, c, lds, bbuf, acc, lane, X, Yb, n0, sg * kHalfSteps, last ? nst : kHalfSteps);
+                __syncthreads();
+                if (!last) {
+                    bhalf_store<NT>(bbuf, nst - kHalfSteps, bs);
+                    __syncthreads();
+                }
+            }
+            if (more) {
+                stage_store(lds, a.ch_w[c + 1] >> 3, st);
+                bhalf_store<NT>(bbuf, kHalfSteps, bs);
+                __syncthreads();
+            }
+        }
     } else {                                   // double-buffered halo, per-wave global B
         stage_load(a, 0, tx0, ty0, st);
         stage_store(lds, a.ch_w[0] >> 3, st);
@@ -273,7 +336,7 @@ __global__ void __launch_bounds__(256) k_conv3(ConvArgs a) {
         for (int c = 0; c < a.nchunk; ++c) {
             const bool more = c + 1 < a.nchunk;
             if (more) stage_load(a, c + 1, tx0, ty0, st);      // in flight during the MFMAs
-            compute_chunk<NT>(a, c, lds + (c & 1) * kChunkBytes, nullptr, acc, lane, X, Yb, n0);
+            compute_chunk<NT, false>(a, c, lds + (c & 1) * kChunkBytes, nullptr, acc, lane, X, Yb, n0);
             if (more) stage_store(lds + ((c + 1) & 1) * kChunkBytes, a.ch_w[c + 1] >> 3, st);
             __syncthreads();
         }
