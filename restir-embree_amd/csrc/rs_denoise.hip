@@ -147,14 +147,18 @@ __device__ __forceinline__ void stage_store(uint8_t* buf, int spp, const uint4 (
 // Only for NT <= 3: a 4-n-tile chunk's 36 KB of B would leave 2 workgroups per CU (measured slower on
 // dec_conv1a: 247 vs 219 us); those keep per-wave global B loads (next step's prefetched) and a
 // double-buffered halo.
-template <int NT> struct BStage { static constexpr bool lds = NT <= 3; static constexpr int kRegs = lds ? (9 * NT * 64 + 255) / 256 : 1; };
-// NT = 4: B staged through LDS in two stages per 32-channel chunk (steps 0-4, then 5-8: 20 KB at a time), so
-// the workgroup keeps the LDS budget of the per-wave-B form (3 per CU) without its per-wave B loads
 #ifndef RS_DN_HALFB
 #define RS_DN_HALFB 1
 #endif
+template <int NT> struct BStage { static constexpr bool lds = NT <= 3 && !(RS_DN_HALFB && NT == 2); static constexpr int kRegs = lds ? (9 * NT * 64 + 255) / 256 : 1; };
+// NT = 4 and 2: B staged through LDS in two stages per 32-channel chunk (steps 0-4, then 5-8: 5 NT KB at a
+// time): NT = 4 keeps the LDS budget of the per-wave-B form (3 workgroups per CU) without its per-wave B
+// loads, NT = 2 fits 4 workgroups per CU instead of 3 (whole-chunk staging).  NT = 1 and 3 gain nothing
+// from it (measured: equal; NT = 3 is register-bound at 3 waves)
 constexpr int kHalfSteps = 5;
-template <int NT> struct BHalf { static constexpr bool on = RS_DN_HALFB && NT == 4; static constexpr int kRegs = (kHalfSteps * NT * 64 + 255) / 256; };
+template <int NT> struct BHalf { static constexpr bool on = RS_DN_HALFB && (NT == 4 || NT == 2);
+                                 static constexpr int waves = NT == 4 ? 3 : 4;   // per SIMD (= workgroups per CU by LDS)
+                                 static constexpr int kRegs = (kHalfSteps * NT * 64 + 255) / 256; };
 // B fragments of steps [s0, s0 + ns) of chunk c into registers / from registers into bbuf (step s0 first)
 template <int NT>
 __device__ __forceinline__ void bhalf_load(const ConvArgs& a, int c, int n0, int s0, int ns, uint4 (&r)[BHalf<NT>::kRegs]) {
@@ -261,7 +265,7 @@ struct ConvLds {
 };
 
 template <int NT, int POST, bool RELU>
-__global__ void __launch_bounds__(256, BHalf<NT>::on ? 3 : 1) k_conv3(ConvArgs a) {
+__global__ void __launch_bounds__(256, BHalf<NT>::on ? BHalf<NT>::waves : 1) k_conv3(ConvArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[ConvLds<NT, POST>::kBytes];
     uint8_t* const bbuf = lds + kChunkBytes;
     const int tx0 = blockIdx.x * kTile, ty0 = blockIdx.y * kTile;
