@@ -155,10 +155,13 @@ template <int NT> struct BStage { static constexpr bool lds = NT <= 3 && !(RS_DN
 // time): NT = 4 keeps the LDS budget of the per-wave-B form (3 workgroups per CU) without its per-wave B
 // loads, NT = 2 fits 4 workgroups per CU instead of 3 (whole-chunk staging).  NT = 1 and 3 gain nothing
 // from it (measured: equal; NT = 3 is register-bound at 3 waves)
-constexpr int kHalfSteps = 5;
+#ifndef RS_DN_B4_STEPS
+#define RS_DN_B4_STEPS 5
+#endif
 template <int NT> struct BHalf { static constexpr bool on = RS_DN_HALFB && (NT == 4 || NT == 2);
-                                 static constexpr int waves = NT == 4 ? 3 : 4;   // per SIMD (= workgroups per CU by LDS)
-                                 static constexpr int kRegs = (kHalfSteps * NT * 64 + 255) / 256; };
+                                 static constexpr int steps = NT == 4 ? RS_DN_B4_STEPS : 5;   // k-steps per LDS stage
+                                 static constexpr int waves = NT == 4 && steps > 3 ? 3 : 4;   // per SIMD (= workgroups per CU by LDS)
+                                 static constexpr int kRegs = (steps * NT * 64 + 255) / 256; };
 // B fragments of steps [s0, s0 + ns) of chunk c into registers / from registers into bbuf (step s0 first)
 template <int NT>
 __device__ __forceinline__ void bhalf_load(const ConvArgs& a, int c, int n0, int s0, int ns, uint4 (&r)[BHalf<NT>::kRegs]) {
@@ -258,7 +261,7 @@ template <int NT, int POST>
 struct ConvLds {
     static constexpr int kB = 9 * NT * 1024;   // one chunk's B fragments
     static constexpr int kIn = BStage<NT>::lds ? kChunkBytes + kB
-                             : BHalf<NT>::on ? kChunkBytes + kHalfSteps * NT * 1024 : 2 * kChunkBytes;
+                             : BHalf<NT>::on ? kChunkBytes + BHalf<NT>::steps * NT * 1024 : 2 * kChunkBytes;
     static constexpr int kOut = POST == POST_STORE ? 256 * (NT * 16 + 8) * 2 : POST == POST_POOL ? 64 * (NT * 16 + 8) * 2
                                                                                      : 256 * 17 * 4;
     static constexpr int kBytes = kIn > kOut ? kIn : kOut;
@@ -305,31 +308,41 @@ __global__ void __launch_bounds__(256, BHalf<NT>::on ? BHalf<NT>::waves : 1) k_c
                 __syncthreads();
             }
         }
-    } else if constexpr (BHalf<NT>::on) {      // single halo buffer, B in two LDS stages per 32-channel chunk
+    } else if constexpr (BHalf<NT>::on) {      // single halo buffer, B in LDS stages of S k-steps
+        constexpr int S = BHalf<NT>::steps;
         uint4 bs[BHalf<NT>::kRegs];
         auto nsteps = [&](int c) { return a.ch_w[c] == 32 ? 9 : 5; };
         stage_load(a, 0, tx0, ty0, st);
-        bhalf_load<NT>(a, 0, n0, 0, kHalfSteps, bs);
+        bhalf_load<NT>(a, 0, n0, 0, S < nsteps(0) ? S : nsteps(0), bs);
         stage_store(lds, a.ch_w[0] >> 3, st);
-        bhalf_store<NT>(bbuf, kHalfSteps, bs);
+        bhalf_store<NT>(bbuf, S < nsteps(0) ? S : nsteps(0), bs);
         __syncthreads();
         for (int c = 0; c < a.nchunk; ++c) {
-            const int nst = nsteps(c), nsg = nst > kHalfSteps ? 2 : 1;
+            const int nst = nsteps(c), nsg = (nst + S - 1) / S;
             const bool more = c + 1 < a.nchunk;
             for (int sg = 0; sg < nsg; ++sg) {  // one compute call site: one inlined copy of the step loop
                 const bool last = sg + 1 == nsg;
-                if (!last) bhalf_load<NT>(a, c, n0, kHalfSteps, nst - kHalfSteps, bs);   // this chunk's second stage
-                else if (more) { stage_load(a, c + 1, tx0, ty0, st); bhalf_load<NT>(a, c + 1, n0, 0, kHalfSteps, bs); }
-                compute_chunk<NT, true>(a, c, lds, bbuf, acc, lane, X, Yb, n0, sg * kHalfSteps, last ? nst : kHalfSteps);
+                const int s0 = sg * S, s1 = last ? nst : s0 + S;
+                if (!last) {                     // this chunk's next stage
+                    const int e = s1 + S < nst ? s1 + S : nst;
+                    bhalf_load<NT>(a, c, n0, s1, e - s1, bs);
+                } else if (more) {
+                    const int nn = nsteps(c + 1);
+                    stage_load(a, c + 1, tx0, ty0, st);
+                    bhalf_load<NT>(a, c + 1, n0, 0, S < nn ? S : nn, bs);
+                }
+                compute_chunk<NT, true>(a, c, lds, bbuf, acc, lane, X, Yb, n0, s0, s1);
                 __syncthreads();
                 if (!last) {
-                    bhalf_store<NT>(bbuf, nst - kHalfSteps, bs);
+                    const int e = s1 + S < nst ? s1 + S : nst;
+                    bhalf_store<NT>(bbuf, e - s1, bs);
                     __syncthreads();
                 }
             }
             if (more) {
+                const int nn = nsteps(c + 1);
                 stage_store(lds, a.ch_w[c + 1] >> 3, st);
-                bhalf_store<NT>(bbuf, kHalfSteps, bs);
+                bhalf_store<NT>(bbuf, S < nn ? S : nn, bs);
                 __syncthreads();
             }
         }
