@@ -269,8 +269,10 @@ struct SahCollapse {
 // costs c_node / c_tri; falls back to greedy when it has no plan)
 inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, std::vector<uint32_t>& out,
                            std::vector<int>& tri_prims, int& depth, std::string& err, int collapse = 0,
-                           float c_node = 1.0f, float c_tri = 0.3f, int max_depth = 8) {
+                           float c_node = 1.0f, float c_tri = 0.3f, int max_depth = 8,
+                           std::vector<int>* slot_src = nullptr) {   // optional: 8 per node, the source node of each slot
     out.clear(); tri_prims.clear(); depth = 0;
+    if (slot_src) slot_src->clear();
     if (n <= 0) return 0;
     auto is_prim = [&](int c) { return c < n; };
     auto box = [&](int c) { WBox b; const float* a = nlo + 4 * (size_t)c; const float* z = nhi + 4 * (size_t)c;
@@ -347,6 +349,7 @@ inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, 
             pack(qhi[0], 0), pack(qhi[0], 4), pack(qhi[1], 0), pack(qhi[1], 4),
             pack(qhi[2], 0), pack(qhi[2], 4), 0u, 0u};
         out.insert(out.end(), w, w + 20);
+        if (slot_src) for (int i = 0; i < 8; ++i) slot_src->push_back(i < nv ? kids[i] : -1);
         if (queue.size() >= (1u << 24)) { err = "wide BVH: too many nodes"; return -1; }
     }
     return 0;

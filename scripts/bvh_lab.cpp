@@ -568,6 +568,23 @@ static int group_depth(const Wide& Wd, const Ray& r, bool any) {
 // the same group/stack logic and quantised box test; counts loop iterations, stack overflows, triangle tests
 struct WEmu { int iters = 0, tris = 0, lost = 0, occ = 0; int prim = -1; float t = 0; int maxsp = 0; };
 static inline float u2f_(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+static const std::vector<float>* g_exact_lo = nullptr;
+static const std::vector<float>* g_exact_hi = nullptr;
+static const std::vector<int>* g_slot_src = nullptr;
+static uint32_t emu_hits_exact(size_t node, const uint32_t* w, V3 o, V3 inv, float tnear, float tfar) {
+    uint32_t hits = 0;
+    const float iv[3] = {inv.x, inv.y, inv.z}, org[3] = {o.x, o.y, o.z};
+    for (int c = 0; c < (int)(w[3] >> 28); ++c) {
+        const int k = (*g_slot_src)[8 * node + c];
+        float t0 = tnear, t1 = tfar;
+        for (int a = 0; a < 3; ++a) {
+            const float x0 = ((*g_exact_lo)[4 * (size_t)k + a] - org[a]) * iv[a], x1 = ((*g_exact_hi)[4 * (size_t)k + a] - org[a]) * iv[a];
+            t0 = std::fmax(t0, std::fmin(x0, x1)); t1 = std::fmin(t1, std::fmax(x0, x1));
+        }
+        if (t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON)) hits |= 1u << c;
+    }
+    return hits;
+}
 static uint32_t emu_hits(const uint32_t* w, V3 o, V3 inv, float tnear, float tfar) {
     const uint32_t eb = w[3];
     const float s[3] = {u2f_((eb & 0xffu) << 23), u2f_(((eb >> 8) & 0xffu) << 23), u2f_(((eb >> 16) & 0xffu) << 23)};
@@ -608,7 +625,7 @@ static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& pri
         e.maxsp = std::max(e.maxsp, (int)st.size());
         if (seq) seq->push_back(node);
         const uint32_t* w = &W[20 * (size_t)node];
-        uint32_t hits = emu_hits(w, r.o, inv, r.tn, tf);
+        uint32_t hits = g_slot_src ? emu_hits_exact(node, w, r.o, inv, r.tn, tf) : emu_hits(w, r.o, inv, r.tn, tf);
         uint32_t ni = (w[3] >> 24) & 0xfu, tm = hits >> ni, tb = w[5];
         while (tm && !(any && e.occ)) {
             uint32_t j = __builtin_ctz(tm); tm &= tm - 1; ++e.tris;
@@ -681,7 +698,11 @@ int main(int argc, char** argv) {
         const float c_tri = getenv("C_TRI") ? (float)atof(getenv("C_TRI")) : 0.3f;
         const int sl = getenv("MAX_DEPTH") ? atoi(getenv("MAX_DEPTH")) : 8;
         const auto tw = std::chrono::steady_clock::now();
-        int rc = rs::build_wide_host(lo.data(), hi.data(), n, wroot, WN, pr, depth, err, coll, 1.0f, c_tri, sl);
+        std::vector<int> slot_src;
+        int rc = rs::build_wide_host(lo.data(), hi.data(), n, wroot, WN, pr, depth, err, coll, 1.0f, c_tri, sl, &slot_src);
+        if (getenv("EXACT_BOXES")) {   // LAB: the walk's box test on the exact child boxes instead of the quantised planes
+            g_exact_lo = &lo; g_exact_hi = &hi; g_slot_src = &slot_src;
+        }
         printf("build_wide_host %.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count());
         printf("build_wide_host rc=%d err=%s nodes=%zu depth=%d\n", rc, err.c_str(), WN.size() / 20, depth);
         if (rc || !getenv("EMU")) return 0;
