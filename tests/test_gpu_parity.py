@@ -643,3 +643,25 @@ def test_debug_reprojection_matches_oracle():
     assert seen == colours, seen
     with pytest.raises(RestirError):
         g.tile_begin(gs, cams[0], prm, 0, 0, H // 2, 8, 5)
+
+
+def test_wide_tree_live_on_c3():
+    """The C3 scene's 8-wide tree (host SAH tree, SAH-optimal collapse with the depth bound, rs_wide.h) must be
+    built and walked: a tree deeper than the walk's stack would silently fall back to the skip-pointer walks
+    (same results, 2x slower).  Checks that the wide walk runs (mode 6/7 returns -1 without a wide tree), never
+    overflows its stack, and stays within the fetch counts DESIGN §3.9 reports (12.7 shadow / 10.9 primary)."""
+    sc = scenes.by_name("C3")
+    g = Renderer(8, 8)
+    gs = g.load_scene(sc)
+    rng = np.random.default_rng(5)
+    n = 20000
+    lo = sc.positions.reshape(-1, 3).min(0)
+    hi = sc.positions.reshape(-1, 3).max(0)
+    o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    for any_hit in (False, True):
+        fetches, tris, lost = g.debug_trace(gs, o, d, 0.01, 3.0e38, any_hit=any_hit, wide_stats=True)
+        assert (fetches > 0).all(), "no 8-wide tree on the C3 scene (walks fell back to skip pointers)"
+        assert (lost == 0).all()
+        assert fetches.mean() < 40.0
