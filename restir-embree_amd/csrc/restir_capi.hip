@@ -217,6 +217,7 @@ struct rs_context {
     uint64_t post_px = 0;                  // pixels the last rs_post_frame's statistics cover
     rs_camera cam_last = {};               // camera of the last frame (rs_export_png's sidecar)
     rs_denoiser* denoiser = nullptr;       // rs_post_frame's RenderParams::denoise (rs_context_set_denoiser)
+    std::vector<rs_denoiser*> denoisers;   // every live denoiser created on this context (rs::ctx_track_denoiser)
     // asynchronous framebuffer readback (rs_frame_readback): ticket ring, and per lane the readback its
     // framebuffer is under (that lane's next frame waits for it before writing)
     bool readback_kernel = false;          // DMA engine (default) or a copy kernel (env RESTIR_READBACK=kernel)
@@ -485,6 +486,7 @@ extern "C" void rs_context_destroy(rs_context* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (auto st : c->lane) if (st) hipStreamSynchronize(st);
+    for (rs_denoiser* d : c->denoisers) rs::denoiser_detach(d);   // their rs_denoiser_destroy frees the rest
     for (auto e : c->rb_ev) if (e) hipEventDestroy(e);
     for (auto& q : c->qb) {
         void* ptrs[] = {q.ray, q.rid, q.cnt, q.cw, q.occ, q.brdf, q.bw};
@@ -1561,15 +1563,18 @@ extern "C" int rs_tile_temporal(rs_context* c) {
         // a tile rebuilds previous-frame G elements beyond its rows with the previous frame's geometry
         DevScene Sp = S;
         const bool partial = c->F.gy0 > 0 || c->F.gy1 < c->H;
+        const bool twide = c->twide;
         if (partial && c->geo_prev_scene == c->scene && c->geo_prev != c->scene->geo_gen) {
             if (c->scene->dev_of(c->geo_prev, Sp)) c->prevgeo_read = true;
             else { Sp = S; c->prevgeo_missing++; }     // two updates between frames: the a_* copy moved on
-            // the scene moved, so its 8-wide tree is off and the kernels walk Sp's binary tree
-            if (c->twide) return fail(c, RS_E_INVALID, "rs_tile_temporal: moved scene with a live 8-wide tree");
         }
+        // the kernel walks S and Sp with one traversal kind: when either lacks its 8-wide tree (a generation
+        // held without one), this launch walks both binary trees (same hits, rs_scene.h)
+        if (!S.wnodes || !Sp.wnodes) c->twide = false;
         if (c->F.debug_reproj) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 2 * npx, c->fs));
         LAUNCH_TRAV(c, k_temporal, gb, S, Sp, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]},
                     ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
+        c->twide = twide;
         HIPCHK(c, hipGetLastError());
         if (c->F.debug_reproj) {
             k_debug_reproj<<<(unsigned)((npx + 255) / 256), 256, 0, c->fs>>>(c->G[c->gcur], c->d_dbg, (uint32_t)npx);
@@ -1925,6 +1930,10 @@ extern "C" int rs_post_frame(rs_context* c, const rs_post_params* pp, const floa
     }
     // rows of the last rendered frame / band (rs_render_frame: all rows)
     const int y0 = c->frames ? c->F.y0 : 0, y1 = c->frames ? c->F.y1 : c->H;
+    // a denoised display is validated before the accumulator blends this frame (a rejected call leaves the
+    // accumulator and accFrameCtr as they were)
+    if (pp->denoise && !c->denoiser) return fail(c, RS_E_INVALID, "rs_post_frame: denoise without a denoiser (rs_context_set_denoiser)");
+    if (pp->denoise && (y0 != 0 || y1 != c->H)) return fail(c, RS_E_UNSUPPORTED, "rs_post_frame: denoise needs a full frame, not a tile band");
     PostConst P{c->W, y0, y1, 1.0f / (float)(c->acc_frames + 1), pp->tonemap ? 1 : 0, pp->gamma_correct ? 1 : 0};
     const size_t n = (size_t)(y1 - y0) * c->W;
     const int nblk = (int)((n + 255) / 256);
@@ -1935,21 +1944,20 @@ extern "C" int rs_post_frame(rs_context* c, const rs_post_params* pp, const floa
         HIPCHK(c, hipGetLastError());
     }
     c->post_px = nblk > 0 ? n : 0;
+    // accFrameCtr bookkeeping (pg/simpleguidx11.cpp:297-306): the frame is in the accumulator now, whatever
+    // the denoise step below returns
+    const uint32_t used = c->acc_frames;
+    c->acc_frames++;
+    const uint32_t max_acc = pp->max_acc_frames > 0 ? (uint32_t)pp->max_acc_frames : 300000u;
+    const bool accumulate = pp->accumulate && c->acc_frames <= max_acc;
+    if (!accumulate) c->acc_frames = 0;
     if (pp->denoise) {   // oidnFilter.execute on the accumulator, display = the denoised image (:255-280)
-        if (!c->denoiser) return fail(c, RS_E_INVALID, "rs_post_frame: denoise without a denoiser (rs_context_set_denoiser)");
-        if (y0 != 0 || y1 != c->H) return fail(c, RS_E_UNSUPPORTED, "rs_post_frame: denoise needs a full frame, not a tile band");
         const float* den = nullptr;
         const int rc = rs_denoise_frame(c, c->denoiser, nullptr, &den);
         if (rc != RS_OK) return rc;
         k_post_display<<<nblk, 256, 0, c->stream>>>(den, c->display, P);
         HIPCHK(c, hipGetLastError());
     }
-    // accFrameCtr bookkeeping (pg/simpleguidx11.cpp:297-306)
-    const uint32_t used = c->acc_frames;
-    c->acc_frames++;
-    const uint32_t max_acc = pp->max_acc_frames > 0 ? (uint32_t)pp->max_acc_frames : 300000u;
-    const bool accumulate = pp->accumulate && c->acc_frames <= max_acc;
-    if (!accumulate) c->acc_frames = 0;
     if (display_rgba_dptr) *display_rgba_dptr = (const float*)c->display;
     if (stats) {
         double2 h{0.0, 0.0};
@@ -2159,6 +2167,12 @@ int ctx_device(const rs_context* c) { return c->device; }
 int ctx_width(const rs_context* c) { return c->W; }
 int ctx_height(const rs_context* c) { return c->H; }
 int ctx_fail(rs_context* c, int code, const std::string& msg) { return fail(c, code, msg); }
+void ctx_track_denoiser(rs_context* c, rs_denoiser* d, bool add) {
+    auto& v = c->denoisers;
+    v.erase(std::remove(v.begin(), v.end(), d), v.end());
+    if (add) v.push_back(d);
+    else if (c->denoiser == d) c->denoiser = nullptr;
+}
 int ctx_join(rs_context* c, hipStream_t st) {
     HIPCHK(c, enter(c));
     if (st == c->stream) return RS_OK;

@@ -725,7 +725,8 @@ static void pack_layer(const Tensor& W, const Tensor& B, const Net& net, int l, 
 using namespace rs::dn;
 
 struct rs_denoiser {
-    rs_context* ctx = nullptr;
+    rs_context* ctx = nullptr;                  // null once the context is destroyed (rs::denoiser_detach)
+    int device = 0;
     Net net;
     Layer L[16];
     // activation tensors for the current image size
@@ -804,6 +805,7 @@ int create_impl(rs_context* ctx, const void* tza, size_t bytes, rs_denoiser** ou
     if (!parse_tza((const uint8_t*)tza, bytes, T, err)) return rs::ctx_fail(ctx, RS_E_INVALID, "rs_denoiser_create: " + err);
     rs_denoiser* d = new rs_denoiser();
     d->ctx = ctx;
+    d->device = rs::ctx_device(ctx);
     if (!check_net(T, d->net, err)) { delete d; return rs::ctx_fail(ctx, RS_E_INVALID, "rs_denoiser_create: " + err); }
     (void)hipGetLastError();
     if (hipSetDevice(rs::ctx_device(ctx)) != hipSuccess) { delete d; return rs::ctx_fail(ctx, RS_E_HIP, "rs_denoiser_create: hipSetDevice"); }
@@ -826,6 +828,7 @@ int create_impl(rs_context* ctx, const void* tza, size_t bytes, rs_denoiser** ou
     for (auto& e : d->evl)
         if (rc == RS_OK && hipEventCreate(&e) != hipSuccess) rc = rs::ctx_fail(ctx, RS_E_HIP, "rs_denoiser_create: event");
     if (rc != RS_OK) { rs_denoiser_destroy(d); return rc; }
+    rs::ctx_track_denoiser(ctx, d, true);
     *out = d;
     return RS_OK;
 }
@@ -836,6 +839,7 @@ namespace rs {
 int denoise_run(rs_denoiser* d, hipStream_t st, const float* color, int cst, const float* albedo, int ast,
                 const float* normal, int nst, float* out, int ost, int H, int W, float input_scale) {
     if (!d || !color || !out) return dfail(d, RS_E_INVALID, "rs_denoise: null image");
+    if (!d->ctx) return dfail(d, RS_E_INVALID, "rs_denoise: the denoiser's context was destroyed");
     if (H <= 0 || W <= 0) return dfail(d, RS_E_INVALID, "rs_denoise: empty image");
     if (d->net.ic >= 6 && !albedo) return dfail(d, RS_E_INVALID, "rs_denoise: the weights need an albedo image");
     if (d->net.ic >= 9 && !normal) return dfail(d, RS_E_INVALID, "rs_denoise: the weights need a normal image");
@@ -951,6 +955,7 @@ extern "C" int rs_denoiser_execute(rs_denoiser* d, const float* color, const flo
     if (!d) return rs::ctx_fail(nullptr, RS_E_INVALID, "rs_denoiser_execute: null denoiser");
     const float scale = p ? p->input_scale : NAN;
     if (p && !p->hdr) return dfail(d, RS_E_UNSUPPORTED, "rs_denoiser_execute: only hdr = true (the reference's setting) is supported");
+    if (!d->ctx) return dfail(d, RS_E_INVALID, "rs_denoiser_execute: the denoiser's context was destroyed");
     return rs::denoise_run(d, rs::ctx_stream(d->ctx), color, 3, albedo, 3, normal, 3, output, 3, height, width, scale);
 }
 
@@ -979,6 +984,7 @@ extern "C" int rs_denoiser_layer_ms(rs_denoiser* d, float* ms) {
 
 extern "C" int rs_denoiser_get_scale(rs_denoiser* d, float* scale) {
     if (!d || !scale) return rs::ctx_fail(d ? d->ctx : nullptr, RS_E_INVALID, "rs_denoiser_get_scale: null argument");
+    if (!d->ctx) return dfail(d, RS_E_INVALID, "rs_denoiser_get_scale: the denoiser's context was destroyed");
     hipStream_t st = rs::ctx_stream(d->ctx);
     DCHK(d, hipMemcpyAsync(scale, d->d_scale, sizeof(float), hipMemcpyDeviceToHost, st));
     DCHK(d, hipStreamSynchronize(st));
@@ -988,6 +994,7 @@ extern "C" int rs_denoiser_get_scale(rs_denoiser* d, float* scale) {
 extern "C" int rs_denoiser_dump(rs_denoiser* d, int tensor, uint16_t* host, int32_t* dims) {
     if (!d || tensor < 0 || tensor >= B_COUNT) return rs::ctx_fail(d ? d->ctx : nullptr, RS_E_INVALID, "rs_denoiser_dump: bad argument");
     if (!d->buf[tensor]) return dfail(d, RS_E_INVALID, "rs_denoiser_dump: nothing executed yet");
+    if (!d->ctx) return dfail(d, RS_E_INVALID, "rs_denoiser_dump: the denoiser's context was destroyed");
     const int lv = d->net.buflev[tensor];
     const int h = (d->Hp >> lv) + 2, w = (d->Wp >> lv) + 2, cs = d->net.bufcs[tensor];
     if (dims) { dims[0] = h; dims[1] = w; dims[2] = cs; dims[3] = d->net.bufc[tensor]; }
@@ -1001,8 +1008,11 @@ extern "C" int rs_denoiser_dump(rs_denoiser* d, int tensor, uint16_t* host, int3
 
 extern "C" void rs_denoiser_destroy(rs_denoiser* d) {
     if (!d) return;
-    (void)hipSetDevice(rs::ctx_device(d->ctx));
-    (void)hipStreamSynchronize(rs::ctx_stream(d->ctx));
+    (void)hipSetDevice(d->device);
+    if (d->ctx) {                               // still attached: its work is on the context's stream
+        (void)hipStreamSynchronize(rs::ctx_stream(d->ctx));
+        rs::ctx_track_denoiser(d->ctx, d, false);
+    }                                           // (detached: the context drained its streams when destroyed)
     free_bufs(d);
     for (auto& L : d->L) { if (L.dw) hipFree(L.dw); if (L.db) hipFree(L.db); }
     if (d->d_scale) hipFree(d->d_scale);
@@ -1026,4 +1036,5 @@ float* denoiser_frame_out(rs_denoiser* d, int W, int H) {
     return d->d_out;
 }
 rs_context* denoiser_ctx(const rs_denoiser* d) { return d->ctx; }
+void denoiser_detach(rs_denoiser* d) { d->ctx = nullptr; }
 }  // namespace rs

@@ -25,4 +25,9 @@ __attribute__((visibility("hidden"))) int denoise_run(rs_denoiser* d, hipStream_
                                                       float* out, int ost, int H, int W, float input_scale);
 __attribute__((visibility("hidden"))) float* denoiser_frame_out(rs_denoiser* d, int W, int H);
 __attribute__((visibility("hidden"))) rs_context* denoiser_ctx(const rs_denoiser* d);
+// denoiser lifetime: a context tracks the denoisers created on it; rs_denoiser_destroy unregisters one (and
+// clears the context's post-frame denoiser when it is that one); rs_context_destroy detaches the rest, which
+// then fail their calls with RS_E_INVALID and free only their own memory in rs_denoiser_destroy
+__attribute__((visibility("hidden"))) void ctx_track_denoiser(rs_context* c, rs_denoiser* d, bool add);
+__attribute__((visibility("hidden"))) void denoiser_detach(rs_denoiser* d);
 }  // namespace rs

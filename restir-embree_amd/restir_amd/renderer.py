@@ -359,6 +359,9 @@ class Renderer:
         return rc
 
     def close(self):
+        # an attached denoiser stays valid: rs_context_destroy detaches it (its close() then frees only its
+        # own memory); dropping the reference breaks the renderer <-> denoiser cycle
+        self._denoiser = None
         if getattr(self, "h", None):
             self.lib.rs_context_destroy(self.h)
             self.h = None

@@ -194,3 +194,38 @@ def test_denoise_frame_and_post_display():
         r.post_frame(denoise=True)                       # no denoiser set: loud error
     d.close()
     r.close()
+
+
+def test_denoiser_lifetime_and_rejected_post_frame():
+    """(1) a post_frame(denoise=True) that is rejected (no denoiser) leaves the accumulator and
+    accFrameCtr as they were; (2) destroying the attached denoiser clears the context's post-frame denoiser
+    (the next denoise=True call fails loudly instead of using freed memory); (3) destroying the context
+    first detaches its denoisers: their calls fail with an error, and their close() is still safe."""
+    W, H = 64, 48
+    sc = scenes.cornell_many_lights(64)
+    prm = metric_params(m_area=4)
+    r = Renderer(W, H)
+    s = r.load_scene(sc)
+    r.produce_restir(s, sc.camera, prm, 0)
+    _, st0 = r.post_frame(accumulate=True)
+    assert st0.acc_frames_used == 0
+    with pytest.raises(Exception):
+        r.post_frame(accumulate=True, denoise=True)      # rejected before the accumulator is touched
+    r.produce_restir(s, sc.camera, prm, 1)
+    _, st1 = r.post_frame(accumulate=True)
+    assert st1.acc_frames_used == 1, st1.acc_frames_used
+    d = Denoiser(r, tza.random_unet_weights(seed=3))
+    r.set_denoiser(d)
+    r.post_frame(accumulate=True, denoise=True)
+    d.close()                                            # attached: the context forgets it
+    with pytest.raises(Exception):
+        r.post_frame(accumulate=True, denoise=True)
+    d2 = Denoiser(r, tza.random_unet_weights(seed=4))
+    r.set_denoiser(d2)
+    s.close()
+    r.close()                                            # context first: d2 is detached, not freed
+    import torch
+    x = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+    with pytest.raises(Exception):
+        d2.execute(x, x, x)
+    d2.close()

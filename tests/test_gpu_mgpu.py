@@ -163,3 +163,47 @@ def test_local_mgpu_moving_geometry_rebuilds_previous_geometry(pipelined):
     outside = sum(int(r.timing_totals()[0].reproj_outside) for r in rs)
     assert outside > 0
     m.close()
+
+
+@pytest.mark.parametrize("traversal", ["lane", "lockstep"])
+def test_local_mgpu_update_then_rebuild(traversal):
+    """A tile frame after rs_scene_update_positions + rs_scene_rebuild: the rebuild brings the
+    8-wide tree back while the previous frame's geometry generation is still the updated one, so a tile's
+    temporal rebuild of a previous-frame G element traces a generation without (or with) its own wide tree;
+    the launch must not fail and the bands must equal the single context's frames bit for bit, over a
+    sequence of updates, rebuilds and plain frames."""
+    W, H, world = 96, 64, 3
+    sc = scenes.cornell_box(8)
+    prm = P.c3_params(m_area=6)
+    cams = [scenes.orbit_camera(sc.camera, 3 * f, 48, 0.6) for f in range(6)]
+    base = np.asarray(sc.positions, np.float32)
+
+    def pos(f):
+        p = base.reshape(-1, 3, 3).copy()
+        p[..., 2] += np.float32(0.02 * f)
+        return p.reshape(-1, 9)
+    ops = ["", "update+rebuild", "update", "rebuild", "update+rebuild", ""]
+
+    def apply(s, f):
+        if "update" in ops[f]:
+            s.update_positions(pos(f))
+        if "rebuild" in ops[f]:
+            s.rebuild()
+    g = Renderer(W, H)
+    g.set_traversal(traversal)
+    gs = g.load_scene(sc)
+    ref = []
+    for f, c in enumerate(cams):
+        apply(gs, f)
+        ref.append(g.produce_restir(gs, c, prm, f).copy())
+    rs = [Renderer(W, H) for _ in range(world)]
+    for r in rs:
+        r.set_traversal(traversal)
+    ss = [r.load_scene(sc) for r in rs]
+    m = MultiGpuFrame(rs)
+    for f, c in enumerate(cams):
+        for s in ss:
+            apply(s, f)
+        img = m.render(ss, c, prm, f, copy_out=True)
+        assert np.array_equal(img, ref[f]), f"frame {f} ({ops[f]}): {int(np.any(img != ref[f], -1).sum())} px differ"
+    m.close()
