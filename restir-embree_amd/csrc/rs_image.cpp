@@ -274,7 +274,7 @@ int load_image(const std::string& path, Image& img, std::string& err) {
     if (f.size() >= 8 && f[0] == 137 && f[1] == 'P' && f[2] == 'N' && f[3] == 'G') rc = decode_png(f, img, err);
     else if (f.size() >= 2 && f[0] == '#' && f[1] == '?') rc = decode_hdr(f, img, err);
     else if (f.size() >= 2 && f[0] == 'P') rc = decode_pnm(f, img, err);
-    else if (f.size() >= 2 && f[0] == 0xFF && f[1] == 0xD8) { err = "JPEG textures are not supported by this build (convert to PNG)"; rc = -3; }
+    else if (f.size() >= 2 && f[0] == 0xFF && f[1] == 0xD8) rc = decode_jpeg(f, img, err);
     else { err = "unknown image format"; rc = -1; }
     if (rc) err = path + ": " + err;
     return rc;

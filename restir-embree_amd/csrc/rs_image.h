@@ -1,6 +1,6 @@
 // rs_image.h -- texture file decoding for the scene loader (the reference uses FreeImage,
-// pg/Texture.cpp:9-57; not available here).  Formats: PNG (8-bit gray / gray+alpha / RGB / RGBA /
-// palette, non-interlaced; zlib inflate), Radiance .hdr (flat and RLE scanlines), .pfm, binary .ppm/.pgm.
+// pg/Texture.cpp:9-57; not available here).  Formats: JPEG (rs_jpeg.cpp), PNG (8-bit gray / gray+alpha / RGB /
+// RGBA / palette, non-interlaced; zlib inflate), Radiance .hdr (flat and RLE scanlines), .pfm, binary .ppm/.pgm.
 #pragma once
 #include "../../include/restir_c.h"
 
@@ -17,8 +17,12 @@ struct Image {
     std::vector<float> f32;
 };
 
-// 0 on success; -1 I/O or format error, -3 unsupported variant (JPEG, 16-bit / interlaced PNG)
+// 0 on success; -1 I/O or format error, -3 unsupported variant (arithmetic / lossless / 12-bit / CMYK JPEG,
+// 16-bit / interlaced PNG)
 int load_image(const std::string& path, Image& img, std::string& err);
+// rs_jpeg.cpp: baseline / extended / progressive Huffman JPEG, grey or 3 components, libjpeg-turbo's default
+// reconstruction (islow IDCT, fancy upsampling, fixed-point YCbCr -> RGB)
+int decode_jpeg(const std::vector<uint8_t>& file, Image& img, std::string& err);
 
 // 8-bit PNG writer (stbi_write_png's role in SimpleGuiDX11::exportImage, pg/simpleguidx11.cpp:607-627):
 // `channels` = 1..4 interleaved bytes, top row first; 0 on success, -1 I/O error
