@@ -7,14 +7,18 @@ temporal off, cap 20.  A "step" is one frame of the hot path (SimpleGuiDX11::pro
 pg/simpleguidx11.cpp:359-487): G-buffer + initial RIS, spatial reuse, shade.  Scene + buffers are
 resident in HBM before timing; the framebuffer stays in HBM (zero-copy, rs_get_frame_device_ptr).
 
-N=1 also measures, as extra keys of the same JSON line, the other single-GPU configs (C3 Sponza-like
-with temporal reuse, the full 240-frame C5 sequence, C2V = doVisibilityPass), each with its own
-ms_per_step, Mrays/s, rooflines and a bounded CPU baseline, and the drop-in C++ host path
-(include/restir.hpp through tools/restir_render, framebuffer copied to host memory every frame).
+N=1 also measures, under "configs" of the same JSON line, the other single-GPU configs (C3 Sponza-like
+with temporal reuse, the full 240-frame C5 sequence, C2V = doVisibilityPass, C4_1gpu = C3 at 3840x2160 on
+one GPU -- the denominator of the C4 speed-up), each with its own ms_per_step, Mrays/s, rooflines and a
+bounded CPU baseline, the denoiser and the drop-in C++ host path (include/restir.hpp through
+tools/restir_render, framebuffer copied to host memory every frame).  The printed line is compact (every
+config's value, ms_per_step, rooflines and CPU baseline); the full record (per-pass times, host, limiter
+details, per-layer denoiser times) goes to gpurun_out/bench_full.json.
 
 N>1 (torchrun): the frame is split into N row bands (strong scaling, one process per GPU); reservoir
 halo rows are exchanged over RCCL before each spatial pass and the band framebuffers are gathered to
-rank 0 (restir_amd/distributed.py).
+rank 0 (csrc/rs_mgpu.hip).  The line carries the headline config (C2) and, under "configs", C4 (BASELINE
+configs[3]: the C3 scene at 3840x2160 across the N GPUs), each with its per-rank band / halo / gather times.
 
 Frames are pipelined by the library (run-ahead lanes, up to 3 frames in flight); every frame is still
 rendered completely.  Rooflines (SURVEY.md §8(d) algorithmic bytes):
@@ -50,8 +54,10 @@ WORKLOADS = {
     "C2V": "C2 with doVisibilityPass (initial candidates without shadow rays, one visibility ray per pixel)",
     "C3": "Sponza-like ~250k tris, 4096 emissive triangles (2048 lamp quads), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
     "C5": "C2 scene, 240-frame camera orbit (r=0.3) + moving lights (light CDF recomputed + BVH refit on the GPU every frame), A=32 B=1, temporal + spatial k=4 P=1 R=30, cap 20",
+    "C4": "C3's Sponza-like scene and parameters at 3840x2160 (row bands across the GPUs)",
 }
-CONFIG_INDEX = {"C1": 0, "C2": 1, "C2V": 1, "C3": 2, "C5": 4}
+CONFIG_INDEX = {"C1": 0, "C2": 1, "C2V": 1, "C3": 2, "C4": 3, "C5": 4}
+RES = {"C4": (3840, 2160)}      # configs quoted at another resolution than --width/--height
 
 
 # SURVEY.md §8(d) algorithmic bytes per pixel-frame: G write 69, initial (G + R) 117, visibility 28,
@@ -80,7 +86,7 @@ def workload(name):
         sc, prm = scenes.cornell_many_lights(1024), metric_params()
     elif name == "C2V":   # doVisibilityPass variant (1 shadow ray instead of A per pixel)
         sc, prm = scenes.cornell_many_lights(1024), metric_params(do_visibility_pass=1)
-    elif name == "C3":
+    elif name in ("C3", "C4"):
         sc, prm = scenes.sponza_like(), c3_params()
         camera = lambda f: scenes.orbit_camera(sc.camera, f % C5_FRAMES, C5_FRAMES, 0.3)
     else:   # C5: C2's scene, 240-frame camera orbit + moving lights, temporal reuse with M-cap 20
@@ -98,6 +104,10 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--scene", default="C2", choices=list(WORKLOADS))
+    ap.add_argument("--multi-configs", default="C4",
+                    help="N>1: further configs measured after --scene in the same run (comma list, '' for none)")
+    ap.add_argument("--full-out", default=os.path.join(ROOT, "gpurun_out", "bench_full.json"),
+                    help="the full record (the printed line is compact)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N=1: skip the C3/C5/C2V and drop-in lines")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -480,6 +490,40 @@ def run_dropin(W, H, frames=120):
     return {"error": (p.stderr or p.stdout)[-400:], "rc": p.returncode}
 
 
+def _compact_roofline(r, keep=("bound", "kernel", "kernel_ms", "bytes_per_px", "gflop", "achieved", "peak", "unit",
+                                  "frac", "traffic")):
+    return None if r is None else {k: r[k] for k in keep if k in r}
+
+
+def compact(e):
+    """The fields of a config that the printed line keeps (the rest goes to the full record)."""
+    out = {k: e[k] for k in ("value", "unit", "ms_per_step", "mrays_per_s", "gpu_over_cpu", "frac_of_zero_copy",
+                              "error") if k in e}
+    if "config" in e:
+        out["workload"] = e["config"].get("workload")
+    for k in ("roofline", "kernel_roofline"):
+        if e.get(k):
+            out[k] = _compact_roofline(e[k])
+    cb = e.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cb}
+    elif "cpu_baseline" in e:
+        out["cpu_baseline"] = None
+    if e.get("per_rank"):
+        out["per_rank"] = [{k: v for k, v in q.items() if k in ("rank", "band_rows", "band_ms", "halo_ms", "gather_ms")}
+                           for q in e["per_rank"]]
+    return out
+
+
+def write_full(path, rec):
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(rec, f, indent=1)
+    except OSError as ex:
+        print(f"warning: cannot write {path}: {ex}", file=sys.stderr)
+
+
 def main():
     args = parse()
     import torch
@@ -505,22 +549,43 @@ def main():
                "data": f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX[args.scene]}])"}
         head["config"]["parallelism"] = "1 GPU"
         out.update(head)
+        full = dict(out)
         if not args.no_extras and args.scene == "C2" and (W, H) == (1920, 1080):
             extras = {}
-            for name, steps in (("C3", 20), ("C5", C5_FRAMES), ("C2V", args.steps)):
-                e = run_single(name, W, H, steps, args.warmup, local, stream, args.cpu_threads,
-                               not args.no_cpu_baseline)
-                e["data"] = f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX[name]}])"
+            for name, steps, res in (("C3", 20, (W, H)), ("C5", C5_FRAMES, (W, H)), ("C2V", args.steps, (W, H)),
+                                     ("C4_1gpu", 10, RES["C4"])):
+                base = "C3" if name == "C4_1gpu" else name
+                e = run_single(base, res[0], res[1], steps, args.warmup, local, stream, args.cpu_threads,
+                               not args.no_cpu_baseline and name != "C4_1gpu")
+                e["data"] = f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX['C4' if name == 'C4_1gpu' else name]}])"
+                if name == "C4_1gpu":
+                    e["note"] = ("C4's scene and parameters on ONE GPU (the denominator of the N-GPU C4 speed-up); "
+                                 "CPU baseline: C3's (same per-pixel work at 1080p)")
                 extras[name] = e
             extras["denoise"] = run_denoise(W, H, args.steps, args.warmup, local, stream, args.cpu_threads,
                                             not args.no_cpu_baseline)
-            out["configs"] = extras
             torch.cuda.synchronize()
             d = run_dropin(W, H)
             if d is not None:
                 if "value" in d:
                     d["frac_of_zero_copy"] = round(d["value"] / out["value"], 4)
-                out["dropin_host_framebuffer"] = d
+                extras["dropin_host_framebuffer"] = d
+            full["configs"] = extras
+            out["configs"] = {k: compact(v) for k, v in extras.items()}
+        full["host"] = host_cpu()
+        write_full(args.full_out, full)
+        for k in ("pass_ms_one_frame_in_flight", "frame_ms_one_frame_in_flight", "frames_timed_by_events",
+                  "reference_rays_per_frame", "rays_per_frame"):
+            out.pop(k, None)
+        for k in ("roofline", "kernel_roofline"):
+            out[k] = _compact_roofline(out.get(k))
+        if out.get("cpu_baseline"):
+            out["cpu_baseline"] = {k: out["cpu_baseline"][k] for k in ("value", "unit", "cores", "kind", "sample")}
+        if out.get("limiter"):
+            out["limiter"] = {k: out["limiter"][k] for k in ("kernel", "bound_by", "source") if k in out["limiter"]}
+        if out.get("valu_issue"):
+            out["valu_issue"] = {k: out["valu_issue"][k] for k in ("achieved", "peak", "unit", "frac") if k in out["valu_issue"]}
+        out["full_record"] = os.path.relpath(args.full_out, ROOT)
         print(json.dumps(out), flush=True)
         return
     run_multi(args, world, rank, local, W, H)
@@ -529,19 +594,43 @@ def main():
 def run_multi(args, world, rank, local, W, H):
     """N>1: the native multi-GPU path behind the C ABI (rs_mgpu_*: RCCL point-to-point halo exchange and
     gather on each frame's stream, csrc/rs_mgpu.hip) with torch.distributed over gloo as the control
-    plane only (the RCCL id broadcast, barriers, max-over-ranks timing).  RESTIR_MGPU=python (or the
-    RESTIR_DIST_BACKEND=gloo rehearsal with ranks sharing a GPU) runs the Python orchestration
-    (restir_amd/distributed.py) instead."""
+    plane only (the RCCL id broadcast, barriers, max-over-ranks timing).  The headline config (--scene) and
+    then every --multi-configs entry (C4 by default) are measured in turn, one renderer at a time.
+    RESTIR_MGPU=python (or the RESTIR_DIST_BACKEND=gloo rehearsal with ranks sharing a GPU) runs the Python
+    orchestration (restir_amd/distributed.py) instead."""
     if os.environ.get("RESTIR_MGPU", "cabi") == "python" or os.environ.get("RESTIR_DIST_BACKEND") == "gloo":
         return run_multi_python(args, world, rank, local, W, H)
     import torch
     import torch.distributed as dist
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    names = [args.scene] + [c for c in args.multi_configs.split(",") if c and c != args.scene]
+    lines = {}
+    for name in names:
+        w, h = RES.get(name, (W, H))
+        lines[name] = run_multi_config(args, name, world, rank, local, w, h)
+    if rank == 0:
+        head = lines[args.scene]
+        full = dict(head)
+        if len(names) > 1:
+            full["configs"] = {n: lines[n] for n in names[1:]}
+            head["configs"] = {n: compact(lines[n]) for n in names[1:]}
+        full["host"] = host_cpu()
+        write_full(args.full_out, full)
+        head["per_rank"] = compact(head)["per_rank"]
+        head["full_record"] = os.path.relpath(args.full_out, ROOT)
+        print(json.dumps(head), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_multi_config(args, name, world, rank, local, W, H):
+    import torch
+    import torch.distributed as dist
     from restir_amd import Renderer
     from restir_amd.mgpu import MultiGpuFrame
-    dist.init_process_group("gloo")
-    sc, prm, camera, light_pos = workload(args.scene)
+    sc, prm, camera, light_pos = workload(name)
     cam = camera or (lambda f: sc.camera)
-    torch.cuda.set_device(local)
     r = Renderer(W, H, device=local)
     gs = r.load_scene(sc)
     uid = [MultiGpuFrame.unique_id() if rank == 0 else None]
@@ -557,7 +646,7 @@ def run_multi(args, world, rank, local, W, H):
         step(f)
     bands = m.rebalance([gs], cam(0), prm, 0, 2, 8)
     if rank == 0:
-        print(f"bands: {bands}", file=sys.stderr)
+        print(f"{name} bands: {bands}", file=sys.stderr)
     for f in range(args.warmup):
         step(f)
     r.synchronize()
@@ -587,8 +676,9 @@ def run_multi(args, world, rank, local, W, H):
     per_rank = [None] * world
     dist.all_gather_object(per_rank, mine)
     _, last_kind, _ = r.traversal(gs)
+    line = None
     if rank == 0:
-        line = multi_line(args, world, W, H, prm, dt, rays, outside, bands, last_kind,
+        line = multi_line(args, name, world, W, H, prm, dt, rays, outside, bands, last_kind,
                           "rs_mgpu (C ABI): RCCL point-to-point halo + gather")
         line["per_rank"] = [{"rank": q, "band_rows": bands[q][1] - bands[q][0], "band_ms": round(v[0], 4),
                              "halo_bytes_sent": int(v[1]), "halo_bytes_recv": int(v[2]), "halo_ms": round(v[3], 4),
@@ -596,21 +686,22 @@ def run_multi(args, world, rank, local, W, H):
                             for q, v in enumerate(per_rank)]
         line["per_rank_note"] = ("per frame; band_ms = the rank's pass kernels (HIP events, frames overlap); halo_ms / "
                                  "gather_ms = HIP-event span of the RCCL group on the frame's stream incl. waiting for peers")
-        print(json.dumps(line), flush=True)
     dist.barrier()
     m.close()
-    dist.destroy_process_group()
+    gs.close()
+    r.close()
+    return line
 
 
-def multi_line(args, world, W, H, prm, dt, rays, outside, bands, last_kind, path):
+def multi_line(args, name, world, W, H, prm, dt, rays, outside, bands, last_kind, path):
     ms = dt / args.steps * 1e3
     b_px = survey_bytes_per_px(prm)
     gbs = b_px * W * H / (ms * 1e-3) / 1e9
     return {"metric": METRIC, "value": round(args.steps / dt, 4), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX[args.scene]}])",
-            "config": {"workload": f"{args.scene}: {WORKLOADS[args.scene]}, {W}x{H}", "width": W, "height": H,
+            "data": f"synthetic (procedural scene, BASELINE.json configs[{CONFIG_INDEX[name]}])",
+            "config": {"workload": f"{name}: {WORKLOADS[name]}, {W}x{H}", "width": W, "height": H,
                        "parallelism": f"row-bands x{world}", "bands": bands, "multi_gpu_path": path,
                        "traversal": {0: "lockstep", 1: "lane"}.get(last_kind, str(last_kind)) + " (rank 0)",
                        "frames_in_flight": 3},
@@ -677,7 +768,7 @@ def run_multi_python(args, world, rank, local, W, H):
     dt, rays, outside = float(dmax[0]), int(sums[0]), int(sums[1])
     _, last_kind, _ = tr.be.r.traversal(gs)
     if rank == 0:
-        print(json.dumps(multi_line(args, world, W, H, prm, dt, rays, outside, bands, last_kind,
+        print(json.dumps(multi_line(args, args.scene, world, W, H, prm, dt, rays, outside, bands, last_kind,
                                     "restir_amd.distributed (Python): torch.distributed halo + gather")), flush=True)
     dist.barrier()
     dist.destroy_process_group()

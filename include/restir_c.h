@@ -470,6 +470,14 @@ int rs_mgpu_get_stats(rs_mgpu* m, rs_mgpu_stats* out, int reset);
 int rs_debug_trace(rs_context* ctx, const rs_scene* scene, uint32_t n, const float* o, const float* d,
                    const float* tnear, const float* tfar, int any_hit, float* t_out, int32_t* prim_out);
 
+/* ---- test hook: the scene's 8-wide tree (rs_wide.h layout, built on the GPU by rs_wide_build.hip and refit
+ * with the positions) ----------------------------------------------------------------------------------
+ * *n_nodes / *n_tris = its size (0 / 0: the scene has no wide tree; its walks take the skip pointers);
+ * *depth = its deepest level.  With words != NULL (20 * *n_nodes uint32) and prims != NULL (*n_tris int32)
+ * it also copies the node words and each wide-leaf triangle's original triangle index (synchronous). */
+int rs_debug_wide_tree(const rs_scene* scene, uint32_t* n_nodes, uint32_t* n_tris, int32_t* depth, uint32_t* words,
+                       int32_t* prims);
+
 #ifdef __cplusplus
 }
 #endif

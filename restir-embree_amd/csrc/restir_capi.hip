@@ -28,6 +28,7 @@ int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int*
                    std::vector<int>& lvl_off, std::string& err);
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
               const std::vector<int>& lvl_off, hipStream_t st, int* tail, std::string& err);
+void wide_free(WideBvh& w);
 }
 
 using namespace rs;
@@ -50,9 +51,10 @@ struct rs_scene {
     int* d_emis_tri = nullptr;
     int *d_refit_order = nullptr, *d_refit_lvl = nullptr;
     std::vector<int> refit_lvl;
-    // 8-wide tree of the per-lane walks (rs_scene.h); dropped (walks fall back to the skip pointers) once
-    // the positions move -- it is not refit
-    WideBvh wide;
+    // 8-wide tree of the per-lane walks (rs_scene.h), built on the GPU with the binary tree (rs_wide_build.hip)
+    // and refit with it when the positions move (rs_refit.h); a_wide = its second copy for pipelined updates
+    // and the previous geometry generation (like a_nodes below)
+    WideBvh wide, a_wide;
     bool wide_on = false;
     float* h_stage[2] = {nullptr, nullptr};
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
@@ -99,7 +101,8 @@ struct rs_scene {
         if (g != a_geo || !a_nodes) return false;
         S.nodes = a_nodes; S.tris = a_tris;
         if (a_nrm) S.tri_nrm = a_tri_nrm;
-        S.wnodes = nullptr; S.n_wnodes = 0u;       // the refit binary tree of that generation
+        const bool w = wide_on && a_wide.nodes;    // the refit trees of that generation
+        S.wnodes = w ? a_wide.nodes : nullptr; S.wtris = w ? a_wide.tris : nullptr; S.n_wnodes = w ? a_wide.n_nodes : 0u;
         return true;
     }
 };
@@ -769,13 +772,14 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     {
         void* alt[] = {s->a_nodes, s->a_tris, s->a_emis, s->a_cdf, s->a_cdf_guide, s->a_tri_nrm};
         for (void* p : alt) if (p) hipFree(p);
+        wide_free(s->a_wide);
         s->a_nodes = s->a_tris = s->a_emis = s->a_tri_nrm = nullptr; s->a_cdf = nullptr; s->a_cdf_guide = nullptr;
         s->a_geo = 0xffffffffu; s->a_nrm = false;
         s->update_recorded = false;
     }
     void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide, s->d_emis_tri,
-                   s->d_refit_order, s->d_refit_lvl, s->wide.nodes, s->wide.tris};
-    s->wide = WideBvh{}; s->wide_on = false;
+                   s->d_refit_order, s->d_refit_lvl};
+    wide_free(s->wide); s->wide_on = false;
     for (void* p : old) if (p) hipFree(p);
     s->d_pos = nullptr; s->d_nodes = nullptr; s->d_tris = nullptr; s->d_emis = nullptr; s->d_cdf = nullptr;
     s->d_cdf_guide = nullptr; s->d_emis_tri = nullptr; s->d_refit_order = nullptr; s->d_refit_lvl = nullptr;
@@ -906,18 +910,37 @@ __device__ __forceinline__ void light_table(const float* __restrict__ pos, const
     }
 }
 
-// one launch for the two independent single-workgroup jobs of an update: workgroup 0 the light
-// tables, workgroup 1 the last (small-level) refit batch
+// one launch for the three independent single-workgroup jobs of an update: workgroup 0 the light
+// tables, workgroup 1 the last (small-level) batch of the binary refit, workgroup 2 that of the 8-wide refit
 struct RefitArgs { float4* nodes; float4* tris; const float* pos; const int* order; const int* lvl_off; int l0, l1; };
 __global__ void __launch_bounds__(kLightBlock) k_scene_update(const float* __restrict__ pos, const float4* __restrict__ tri_nrm,
                                                               const float4* __restrict__ mats, const int* __restrict__ emis_tri,
-                                                              uint32_t ne, float4* em, float* cdf, int* guide, RefitArgs R) {
-    static_assert(kLightBlock == kRefitBlock, "one workgroup size for both jobs");
+                                                              uint32_t ne, float4* em, float* cdf, int* guide, RefitArgs R,
+                                                              WideRefitArgs W) {
+    static_assert(kLightBlock == kRefitBlock, "one workgroup size for every job");
     if (blockIdx.x == 0) {
         if (ne) light_table(pos, tri_nrm, mats, emis_tri, ne, em, cdf, guide);
-    } else {
+    } else if (blockIdx.x == 1) {
         refit_levels(R.nodes, R.tris, R.pos, R.order, R.lvl_off, R.l0, R.l1, 0, 1);
+    } else if (W.l_deep >= W.l_top) {
+        wide_refit_levels(W, 0, 1);
     }
+}
+__global__ void __launch_bounds__(kRefitBlock) k_wide_refit(WideRefitArgs W) { wide_refit_levels(W, blockIdx.x, gridDim.x); }
+
+// the 8-wide tree's second copy (same topology), allocated and filled on first use
+static int wide_copy(rs_context* c, const WideBvh& from, WideBvh& to, hipStream_t st) {
+    if (!to.nodes) {
+        to = from;
+        to.nodes = nullptr; to.tris = nullptr; to.box = nullptr;
+        HIPCHK(c, hipMalloc(&to.nodes, (size_t)5 * from.n_nodes * sizeof(uint4)));
+        HIPCHK(c, hipMalloc(&to.tris, (size_t)3 * from.n_tris * sizeof(float4)));
+        HIPCHK(c, hipMalloc(&to.box, (size_t)2 * from.n_nodes * sizeof(float4)));
+    }
+    HIPCHK(c, hipMemcpyAsync(to.nodes, from.nodes, (size_t)5 * from.n_nodes * sizeof(uint4), hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(to.tris, from.tris, (size_t)3 * from.n_tris * sizeof(float4), hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(to.box, from.box, (size_t)2 * from.n_nodes * sizeof(float4), hipMemcpyDeviceToDevice, st));
+    return RS_OK;
 }
 
 __global__ void k_set_normals(const float* __restrict__ nrm, uint32_t n, float4* tri_nrm) {
@@ -978,7 +1001,9 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
         if (be) HIPCHK(c, hipMemcpyAsync(s->a_emis, s->d_emis, be, hipMemcpyDeviceToDevice, st));
         HIPCHK(c, hipMemcpyAsync(s->a_cdf, s->d_cdf, bc, hipMemcpyDeviceToDevice, st));
         HIPCHK(c, hipMemcpyAsync(s->a_cdf_guide, s->d_cdf_guide, bg, hipMemcpyDeviceToDevice, st));
+        if (s->wide_on) if (int rc = wide_copy(c, s->wide, s->a_wide, st)) return rc;
     }
+    WideBvh* wt = &s->wide;                      // the 8-wide tree the refit writes
     if (pipelined) {
         // every frame that read the copy about to be written has finished (a lane's frames in stream order):
         // the frames of that generation, and tile frames that rebuilt elements from it as the previous one
@@ -986,6 +1011,7 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
             if (c->lane_scene[l] == s && (((s->gen - c->lane_gen[l]) & 1) || c->lane_prevgeo[l]) && c->lane_done[l])
                 HIPCHK(c, hipStreamWaitEvent(st, c->lane_done[l], 0));
         nodes = s->a_nodes; tris = s->a_tris; em = s->a_emis; cdf = s->a_cdf; guide = s->a_cdf_guide;
+        wt = &s->a_wide;
         s->a_nrm = false;
     } else {
         c->join_next = true;                     // the next frame's initial pass must see the new geometry
@@ -993,6 +1019,7 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
         // tile's next temporal pass can still trace the previous frame's geometry
         HIPCHK(c, hipMemcpyAsync(s->a_nodes, s->d_nodes, bn, hipMemcpyDeviceToDevice, st));
         HIPCHK(c, hipMemcpyAsync(s->a_tris, s->d_tris, bt, hipMemcpyDeviceToDevice, st));
+        if (s->wide_on) if (int rc = wide_copy(c, s->wide, s->a_wide, st)) return rc;
         s->a_nrm = normals != nullptr;
         if (s->a_nrm) {
             if (!s->a_tri_nrm) HIPCHK(c, hipMalloc(&s->a_tri_nrm, bnrm));
@@ -1010,19 +1037,30 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
         k_set_normals<<<(s->n_tris + 255) / 256, 256, 0, st>>>(s->d_nrm_stage, s->n_tris, s->d_tri_nrm);
     }
     HIPCHK(c, hipEventRecord(s->stage_ev[k], st));
-    s->wide_on = false;                          // later frames walk the refit binary tree (S.n_wnodes = 0)
     std::string err;
     int tail[2];
     if (bvh_refit(nodes, tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, s->refit_lvl, st, tail, err) != 0)
         return fail(c, RS_E_HIP, "rs_scene_update_positions: " + err);
     RefitArgs R{nodes, tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, tail[0], tail[1]};
-    k_scene_update<<<2, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, em, cdf, guide, R);
+    // the 8-wide tree keeps its topology and is refit too (rs_refit.h): large levels alone, the last run of
+    // small levels up to the root in the fused launch's third workgroup
+    WideRefitArgs W = wide_refit_args(*wt, s->d_pos, -1, 0);
+    if (s->wide_on) {
+        const std::vector<WideBatch> wb = wide_refit_batches(*wt);
+        for (size_t i = 0; i < wb.size(); ++i) {
+            if (i + 1 == wb.size() && wb[i].blocks == 1) { W.l_deep = wb[i].l_deep; W.l_top = wb[i].l_top; break; }
+            WideRefitArgs A = wide_refit_args(*wt, s->d_pos, wb[i].l_deep, wb[i].l_top);
+            k_wide_refit<<<wb[i].blocks, kRefitBlock, 0, st>>>(A);
+        }
+    }
+    k_scene_update<<<3, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, em, cdf, guide, R, W);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(s->update_ev, st));
     s->update_recorded = true;
     if (pipelined) {                             // later frames read the new copy
         std::swap(s->d_nodes, s->a_nodes); std::swap(s->d_tris, s->a_tris); std::swap(s->d_emis, s->a_emis);
         std::swap(s->d_cdf, s->a_cdf); std::swap(s->d_cdf_guide, s->a_cdf_guide);
+        std::swap(s->wide, s->a_wide);
         s->gen++;
     }
     return RS_OK;
@@ -1158,9 +1196,10 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     if (s->ctx) sync_all(s->ctx);
     void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
                     s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage, s->d_tex, s->d_texd, s->d_uv,
-                    s->d_tan, s->wide.nodes, s->wide.tris, s->a_tri_nrm, s->a_nodes, s->a_tris, s->a_emis,
-                    s->a_cdf, s->a_cdf_guide};
+                    s->d_tan, s->a_tri_nrm, s->a_nodes, s->a_tris, s->a_emis, s->a_cdf, s->a_cdf_guide};
     for (void* p : ptrs) if (p) hipFree(p);
+    wide_free(s->wide);
+    wide_free(s->a_wide);
     for (int k = 0; k < 2; ++k) {
         if (s->h_stage[k]) hipHostFree(s->h_stage[k]);
         if (s->stage_ev[k]) hipEventDestroy(s->stage_ev[k]);
@@ -1169,6 +1208,30 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     {
     }
     delete s;
+}
+
+extern "C" int rs_debug_wide_tree(const rs_scene* s, uint32_t* n_nodes, uint32_t* n_tris, int32_t* depth, uint32_t* words,
+                                  int32_t* prims) {
+    if (!s || !n_nodes || !n_tris) return fail(s ? s->ctx : nullptr, RS_E_INVALID, "rs_debug_wide_tree: null argument");
+    rs_context* c = s->ctx;
+    HIPCHK(c, enter(c));
+    const WideBvh& w = s->wide;
+    const bool on = s->wide_on && w.nodes;
+    *n_nodes = on ? w.n_nodes : 0u;
+    *n_tris = on ? w.n_tris : 0u;
+    if (depth) *depth = on ? w.depth : -1;
+    if (!on || (!words && !prims)) return RS_OK;
+    if (s->update_recorded) HIPCHK(c, hipStreamWaitEvent(c->stream, s->update_ev, 0));
+    if (words) HIPCHK(c, hipMemcpyAsync(words, w.nodes, (size_t)w.n_nodes * 5 * sizeof(uint4), hipMemcpyDeviceToHost, c->stream));
+    std::vector<float4> t;
+    if (prims) {
+        t.resize(3 * (size_t)w.n_tris);
+        HIPCHK(c, hipMemcpyAsync(t.data(), w.tris, t.size() * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (prims)
+        for (uint32_t k = 0; k < w.n_tris; ++k) std::memcpy(&prims[k], &t[3 * (size_t)k].w, 4);
+    return RS_OK;
 }
 
 extern "C" int rs_scene_info(const rs_scene* s, uint32_t* n_tris, uint32_t* n_emissive, uint32_t* n_nodes,

@@ -454,62 +454,6 @@ __global__ void k_ploc_emit(const float4* nlo, const float4* nhi, const int* par
 }
 
 
-// wide-leaf triangles (v0, prim) (e1) (e2) in tri_prims order, like k_leaf_tris
-__global__ void k_wide_tris(const float* __restrict__ pos, const int* __restrict__ prims, uint32_t n, float4* tris) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const int prim = prims[k];
-    const float* p = pos + 9 * (size_t)prim;
-    const float v0x = p[0], v0y = p[1], v0z = p[2];
-    tris[3 * k] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
-    tris[3 * k + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
-    tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
-}
-
-#ifndef RS_WIDE_SOURCE
-#define RS_WIDE_SOURCE 1          // the collapse's binary source tree: 0 the PLOC tree, 1 rs_wide.h build_sah_host
-#endif
-#ifndef RS_WIDE_COLLAPSE
-#define RS_WIDE_COLLAPSE 1        // rs_wide.h build_wide_host: 0 greedy, 1 SAH-optimal within kWideStack levels
-#endif
-// downloads the PLOC tree, collapses it on the host, uploads the wide nodes and gathers their triangles
-static int build_wide(const float* d_pos, const float4* nlo_d, const float4* nhi_d, int n, int root, hipStream_t st,
-                      WideBvh* w, std::string& err) {
-    const size_t total = 2 * (size_t)n - 1;
-    std::vector<float> lo, hi;
-    if (RS_WIDE_SOURCE == 1 && n <= (1 << 21)) {   // the host SAH tree as the collapse's source
-        std::vector<float> pos(9 * (size_t)n);
-        if (hipMemcpyAsync(pos.data(), d_pos, pos.size() * sizeof(float), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) { err = "wide BVH: download failed"; return -1; }
-        root = build_sah_host(pos.data(), n, lo, hi);
-    } else {                                          // the PLOC tree
-        lo.resize(4 * total); hi.resize(4 * total);
-        if (hipMemcpyAsync(lo.data(), nlo_d, total * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipMemcpyAsync(hi.data(), nhi_d, total * sizeof(float4), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) { err = "wide BVH: download failed"; return -1; }
-    }
-    std::vector<uint32_t> nodes;
-    std::vector<int> prims;
-    int depth = 0;
-    if (build_wide_host(lo.data(), hi.data(), n, root, nodes, prims, depth, err, RS_WIDE_COLLAPSE, 1.0f, 0.3f,
-                        RS_WIDE_STACK) != 0) return -1;
-    int* d_prims = nullptr;
-    if (hipMalloc(&w->nodes, nodes.size() * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&w->tris, prims.size() * 3 * sizeof(float4)) != hipSuccess ||
-        hipMalloc(&d_prims, prims.size() * sizeof(int)) != hipSuccess) { err = "wide BVH: hipMalloc failed"; hipFree(d_prims); return -1; }
-    if (hipMemcpyAsync(w->nodes, nodes.data(), nodes.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_prims, prims.data(), prims.size() * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
-        err = "wide BVH: upload failed"; hipFree(d_prims); return -1;
-    }
-    k_wide_tris<<<((uint32_t)prims.size() + 255) / 256, 256, 0, st>>>(d_pos, d_prims, (uint32_t)prims.size(), w->tris);
-    const bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
-    hipFree(d_prims);
-    if (!ok) { err = "wide BVH: triangle gather failed"; return -1; }
-    w->n_nodes = (uint32_t)(nodes.size() / 20);
-    w->depth = depth;
-    return 0;
-}
-
 #define PLOC_CHECK(x)                                                                  \
     do {                                                                               \
         hipError_t e_ = (x);                                                           \
@@ -517,7 +461,7 @@ static int build_wide(const float* d_pos, const float4* nlo_d, const float4* nhi
     } while (0)
 
 int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes,
-                   float4** d_tris, WideBvh* wide, std::string& err) {
+                   float4** d_tris, std::string& err) {
     *d_nodes = nullptr; *d_tris = nullptr; *n_nodes = 0;
     if (n == 0) return 0;
     if (n >= (1u << 27)) { err = "too many triangles for the leaf index"; return -1; }
@@ -614,7 +558,6 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
     k_ploc_emit<<<(total + B - 1) / B, B, 0, st>>>(nlo, nhi, parent, cnt, kept, collapsed, (int)n, d_pos, nodes, tris);
     PLOC_CHECK(hipGetLastError());
     PLOC_CHECK(hipStreamSynchronize(st));
-    if (wide && build_wide(d_pos, nlo, nhi, (int)n, root, st, wide, err) != 0) goto fail;
     *d_nodes = nodes; *d_tris = tris; *n_nodes = (uint32_t)kept_root;
     nodes = nullptr; tris = nullptr;
 fail: {
@@ -680,15 +623,28 @@ int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_
     return 0;
 }
 
-// builder selection: PLOC by default; RESTIR_BVH=lbvh selects the Karras LBVH (kept for comparison)
-// (RESTIR_WIDE=off: no wide tree, the per-lane walks use the skip pointers)
+// builder selection: PLOC by default; RESTIR_BVH=lbvh selects the Karras LBVH (kept for comparison).  Then the
+// 8-wide tree of the per-lane walks from the positions alone (rs_wide_build.hip); it is optional: when it does
+// not apply (non-finite positions, no plan within the walk's depth) or its build fails, the scene keeps the
+// binary tree and the walks take the skip pointers (RESTIR_WIDE=off: never built).
+int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::string& err);
+void wide_free(WideBvh& w) {
+    void* p[] = {w.nodes, w.tris, w.box};
+    for (void* q : p) if (q) hipFree(q);
+    w = WideBvh{};
+}
 int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes, float4** d_tris,
               WideBvh* wide, std::string& err) {
     const char* e = getenv("RESTIR_BVH");
     const char* w = getenv("RESTIR_WIDE");
     if (w && std::string(w) == "off") wide = nullptr;
-    if (e && std::string(e) == "lbvh") return build_bvh_lbvh(d_pos, n, st, d_nodes, n_nodes, d_tris, err);
-    return build_bvh_ploc(d_pos, n, st, d_nodes, n_nodes, d_tris, wide, err);
+    const int rc = (e && std::string(e) == "lbvh") ? build_bvh_lbvh(d_pos, n, st, d_nodes, n_nodes, d_tris, err)
+                                                   : build_bvh_ploc(d_pos, n, st, d_nodes, n_nodes, d_tris, err);
+    if (rc != 0 || !wide) return rc;
+    std::string werr;
+    if (build_wide_gpu(d_pos, (int)n, st, wide, werr) != 0) wide_free(*wide);   // optional: binary walks
+    (void)hipGetLastError();
+    return 0;
 }
 
 }  // namespace rs

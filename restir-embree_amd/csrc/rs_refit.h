@@ -13,20 +13,32 @@
 // topology on the host (bvh_refit_plan); large levels get a multi-workgroup launch each, runs of small
 // levels share one single-workgroup launch with a workgroup barrier between levels (one CU: global
 // writes are visible to the workgroup after the barrier).
+//
+// The 8-wide tree (rs_wide.h layout) is refit the same way: its topology (breadth-first levels, each node's
+// slots) stays, every node's 8 child boxes are recomputed bottom-up from the new positions -- triangle slots
+// from their vertices, interior slots from the child node's EXACT box (kept beside the tree, `box`, so that
+// the outward rounding does not compound level over level) -- and re-quantised with the builder's own
+// encoder (rs_wide.h wide_encode: outward, exact), so the walk's box test stays a superset of the exact one.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <vector>
+#include "rs_wide.h"
 
 namespace rs {
 
-// 8-wide tree of the per-lane walks (built by rs_bvh_build.hip build_wide, walked by rs_scene.h; layout
-// there).  Device allocations owned by the scene.
+constexpr int kWideLevels = RS_WIDE_STACK + 1;   // a tree walked by the 8-entry stack has <= 9 levels
+
+// 8-wide tree of the per-lane walks (built on the GPU by rs_wide_build.hip, walked by rs_scene.h; layout
+// in rs_wide.h).  Device allocations owned by the scene.
 struct WideBvh {
     uint4* nodes = nullptr;      // 5 per node
     float4* tris = nullptr;      // 3 per wide-leaf triangle
+    float4* box = nullptr;       // 2 per node: its exact box (lo, hi), the refit's input for the parent
     uint32_t n_nodes = 0;
+    uint32_t n_tris = 0;
     int depth = 0;               // deepest level (root = 0)
+    int lvl[kWideLevels + 1] = {};   // breadth-first level offsets: level L = nodes [lvl[L], lvl[L + 1])
 };
 
 constexpr int kRefitBlock = 1024;
@@ -93,6 +105,76 @@ inline std::vector<RefitBatch> refit_batches(const std::vector<int>& lvl_off) {
         }
     }
     return out;
+}
+
+
+// ---------------------------------------------------------------- 8-wide tree refit
+struct WideRefitArgs {
+    uint4* nodes; float4* tris; float4* box; const float* pos;
+    int lvl[kWideLevels + 1];
+    int l_deep, l_top;           // levels l_deep down to l_top (inclusive), deepest first; l_deep < l_top: none
+};
+__device__ __forceinline__ void wide_refit_node(const WideRefitArgs& A, uint32_t j) {
+    const uint4 w0 = A.nodes[5 * (size_t)j], w1 = A.nodes[5 * (size_t)j + 1];
+    const int ni = (int)((w0.w >> 24) & 0xfu), nv = (int)(w0.w >> 28);
+    const uint32_t cb = w1.x, tb = w1.y;
+    WBox kb[8];
+    for (int i = 0; i < nv; ++i) {
+        if (i < ni) {
+            const float4 l = A.box[2 * (size_t)(cb + i)], h = A.box[2 * (size_t)(cb + i) + 1];
+            kb[i] = WBox{{l.x, l.y, l.z}, {h.x, h.y, h.z}};
+        } else {
+            const size_t t = tb + (uint32_t)(i - ni);
+            const int prim = __float_as_int(A.tris[3 * t].w);
+            const float* p = A.pos + 9 * (size_t)prim;
+            for (int a = 0; a < 3; ++a) {
+                kb[i].lo[a] = w_min(w_min(p[a], p[3 + a]), p[6 + a]);
+                kb[i].hi[a] = w_max(w_max(p[a], p[3 + a]), p[6 + a]);
+            }
+            const float v0x = p[0], v0y = p[1], v0z = p[2];
+            A.tris[3 * t] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
+            A.tris[3 * t + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
+            A.tris[3 * t + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
+        }
+    }
+    uint32_t w[20];
+    WBox u;
+    // a non-finite box has no quantisation frame: the node keeps its previous planes (the binary tree's
+    // boxes are NaN / infinite there too; neither walk promises anything for non-finite geometry)
+    if (!wide_encode(kb, nv, ni, cb, tb, w, &u)) return;
+    uint4* P = A.nodes + 5 * (size_t)j;
+    for (int k = 0; k < 5; ++k) P[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    A.box[2 * (size_t)j] = make_float4(u.lo[0], u.lo[1], u.lo[2], 0.0f);
+    A.box[2 * (size_t)j + 1] = make_float4(u.hi[0], u.hi[1], u.hi[2], 0.0f);
+}
+// levels l_deep .. l_top by `nblocks` workgroups of kRefitBlock threads (one workgroup: barriers between levels)
+__device__ __forceinline__ void wide_refit_levels(const WideRefitArgs& A, int block, int nblocks) {
+    for (int lv = A.l_deep; lv >= A.l_top; --lv) {
+        for (int q = A.lvl[lv] + block * kRefitBlock + (int)threadIdx.x; q < A.lvl[lv + 1]; q += nblocks * kRefitBlock)
+            wide_refit_node(A, (uint32_t)q);
+        if (lv > A.l_top) __syncthreads();
+    }
+}
+// launch batches, deepest first: a level with more than kRefitSmall nodes alone over many workgroups, runs
+// of small levels in one workgroup
+struct WideBatch { int l_deep, l_top, blocks; };
+inline std::vector<WideBatch> wide_refit_batches(const WideBvh& w) {
+    std::vector<WideBatch> out;
+    int l = w.depth;
+    while (l >= 0) {
+        const int n = w.lvl[l + 1] - w.lvl[l];
+        if (n > kRefitSmall) { out.push_back({l, l, (n + kRefitBlock - 1) / kRefitBlock}); --l; continue; }
+        int e = l;
+        while (e - 1 >= 0 && w.lvl[e] - w.lvl[e - 1] <= kRefitSmall) --e;
+        out.push_back({l, e, 1});
+        l = e - 1;
+    }
+    return out;
+}
+inline WideRefitArgs wide_refit_args(const WideBvh& w, const float* pos, int l_deep, int l_top) {
+    WideRefitArgs A{w.nodes, w.tris, w.box, pos, {}, l_deep, l_top};
+    for (int i = 0; i <= kWideLevels; ++i) A.lvl[i] = w.lvl[i];
+    return A;
 }
 
 }  // namespace rs

@@ -1,5 +1,8 @@
-// rs_wide.h -- host-side collapse of the PLOC tree into the 8-wide tree of the per-lane walks (plain C++:
-// rs_bvh_build.hip calls it after a build; tests/cpp/wide_harness.cpp checks its invariants on the CPU).
+// rs_wide.h -- the 8-wide tree of the per-lane walks: its node encoding (shared by the host restatement and
+// the GPU builder / refit, rs_wide_build.hip) and the host restatement of the build -- a top-down SAH source
+// tree and the SAH-optimal collapse -- that the GPU builder reproduces bit for bit (tests/test_wide_bvh.py,
+// tests/test_gpu_parity.py::test_wide_tree_gpu_equals_host).  Plain C++ apart from RS_HD: the header is also
+// compiled by g++ for tests/cpp/wide_harness.cpp.
 #pragma once
 #include <algorithm>
 #include <cmath>
@@ -11,6 +14,11 @@
 
 #ifndef RS_WIDE_STACK
 #define RS_WIDE_STACK 8   // the walk's register stack (rs_scene.h kWideStack, same default): deepest tree walked
+#endif
+#if defined(__HIP__)
+#define RS_HD __host__ __device__
+#else
+#define RS_HD
 #endif
 
 namespace rs {
@@ -33,31 +41,34 @@ namespace rs {
 // ============================================================================================
 namespace wide {
 struct WBox { float lo[3], hi[3]; };
+inline double exp2i(int e) { return std::ldexp(1.0, e); }
 inline int h_f2i(float f) { int i; std::memcpy(&i, &f, 4); return i; }
 inline uint32_t h_f2u(float f) { uint32_t i; std::memcpy(&i, &f, 4); return i; }
-inline double exp2i(int e) { return std::ldexp(1.0, e); }
+RS_HD inline bool w_finite(float x) { return x - x == 0.0f; }
+RS_HD inline float w_min(float a, float b) { return b < a ? b : a; }   // std::min / std::max
+RS_HD inline float w_max(float a, float b) { return a < b ? b : a; }
 // quantisation frame of one axis: s = 2^e >= extent / 255 and >= the float spacing at the box, o = a float
 // multiple of s <= lo with o + 255 s >= hi; every child box [clo, chi] quantises OUTWARD to bytes ql, qh with
 // o + ql s <= clo and o + qh s >= chi, all checked in double, where o, s and q are exact (the first k that
-// satisfies every check is taken)
-inline bool wide_axis(float lo, float hi, const float* clo, const float* chi, int nv, int& e, float& o, uint8_t* ql,
-                      uint8_t* qh) {
+// satisfies every check is taken).  Host and device run the same double operations.
+RS_HD inline bool wide_axis(float lo, float hi, const float* clo, const float* chi, int nv, int& e, float& o, uint8_t* ql,
+                            uint8_t* qh) {
     const double ext = (double)hi - (double)lo;
     int k = -126;
-    if (ext > 0) { int x; std::frexp(ext / 255.0, &x); k = std::max(-126, x); }   // ext / 255 < 2^x
-    const float big = std::max(std::fabs(lo), std::fabs(hi));
-    if (big > 0) { int x; std::frexp((double)big, &x); k = std::max(k, x - 24); }  // ulp(big) <= 2^(x-24)
+    if (ext > 0) { int x; frexp(ext / 255.0, &x); k = x > -126 ? x : -126; }   // ext / 255 < 2^x
+    const float big = w_max(fabsf(lo), fabsf(hi));
+    if (big > 0) { int x; frexp((double)big, &x); k = k > x - 24 ? k : x - 24; }  // ulp(big) <= 2^(x-24)
     for (; k <= 127; ++k) {
-        const double sd = exp2i(k);
-        const float of = (float)(std::floor((double)lo / sd) * sd);
+        const double sd = ldexp(1.0, k);
+        const float of = (float)(floor((double)lo / sd) * sd);
         const double od = (double)of;
-        if (od > (double)lo || od + 255.0 * sd < (double)hi || std::floor(od / sd) * sd != od) continue;
+        if (od > (double)lo || od + 255.0 * sd < (double)hi || floor(od / sd) * sd != od) continue;
         bool ok = true;
         for (int i = 0; i < nv && ok; ++i) {
             // estimate in double (the difference chi - od may round), then step to the exact outward byte:
             // od + q * sd is a multiple of sd no larger than the box, exact in double, so the tests are exact
-            double a = std::floor(((double)clo[i] - od) / sd), b = std::ceil(((double)chi[i] - od) / sd);
-            a = std::max(0.0, std::min(255.0, a)); b = std::max(0.0, std::min(255.0, b));
+            double a = floor(((double)clo[i] - od) / sd), b = ceil(((double)chi[i] - od) / sd);
+            a = a < 0.0 ? 0.0 : (a > 255.0 ? 255.0 : a); b = b < 0.0 ? 0.0 : (b > 255.0 ? 255.0 : b);
             while (a > 0.0 && od + a * sd > (double)clo[i]) a -= 1.0;
             while (b < 255.0 && od + b * sd < (double)chi[i]) b += 1.0;
             ok = od + a * sd <= (double)clo[i] && od + b * sd >= (double)chi[i];
@@ -67,12 +78,44 @@ inline bool wide_axis(float lo, float hi, const float* clo, const float* chi, in
     }
     return false;
 }
+// one wide node from its nv <= 8 child boxes (slots 0..ni-1 interior, ni..nv-1 triangles): the 20 words of
+// the layout above; *u = the union of the child boxes.  false: a non-finite box, or no conservative frame.
+RS_HD inline bool wide_encode(const WBox* kb, int nv, int ni, uint32_t child_base, uint32_t tri_base, uint32_t* w, WBox* u) {
+    WBox b = kb[0];
+    for (int i = 1; i < nv; ++i)
+        for (int a = 0; a < 3; ++a) { b.lo[a] = w_min(b.lo[a], kb[i].lo[a]); b.hi[a] = w_max(b.hi[a], kb[i].hi[a]); }
+    *u = b;
+    int e[3] = {0, 0, 0};
+    float o[3] = {0.0f, 0.0f, 0.0f};
+    uint8_t qlo[3][8] = {}, qhi[3][8] = {};
+    for (int a = 0; a < 3; ++a) {
+        if (!w_finite(b.lo[a]) || !w_finite(b.hi[a])) return false;
+        float clo[8], chi[8];
+        for (int i = 0; i < nv; ++i) { clo[i] = kb[i].lo[a]; chi[i] = kb[i].hi[a]; }
+        if (!wide_axis(b.lo[a], b.hi[a], clo, chi, nv, e[a], o[a], qlo[a], qhi[a])) return false;
+    }
+    auto pack = [](const uint8_t* q, int first) {
+        return (uint32_t)q[first] | ((uint32_t)q[first + 1] << 8) | ((uint32_t)q[first + 2] << 16) | ((uint32_t)q[first + 3] << 24);
+    };
+    auto bits = [](float f) { union { float f; uint32_t u; } x; x.f = f; return x.u; };
+    w[0] = bits(o[0]); w[1] = bits(o[1]); w[2] = bits(o[2]);
+    w[3] = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16) | ((uint32_t)ni << 24) |
+           ((uint32_t)nv << 28);
+    w[4] = child_base; w[5] = tri_base; w[6] = pack(qlo[0], 0); w[7] = pack(qlo[0], 4);
+    w[8] = pack(qlo[1], 0); w[9] = pack(qlo[1], 4); w[10] = pack(qlo[2], 0); w[11] = pack(qlo[2], 4);
+    w[12] = pack(qhi[0], 0); w[13] = pack(qhi[0], 4); w[14] = pack(qhi[1], 0); w[15] = pack(qhi[1], 4);
+    w[16] = pack(qhi[2], 0); w[17] = pack(qhi[2], 4); w[18] = 0u; w[19] = 0u;
+    return true;
+}
 }  // namespace wide
 using namespace wide;
 
 // Top-down SAH source tree for the collapse (the PLOC tree stays the binary walks' and the refit's): binned
 // SAH (32 bins per axis over the centroid bounds) above kSweepMax triangles, a full sweep over the sorted
-// centroids below (C3 lab: thresholds 256 / 2048 / 8192 give the same walk counts; 256 builds in 0.4 s) (cost = the children's half areas x their triangle counts).  Output in the PLOC arrays'
+// centroids below (C3 lab: thresholds 256 / 2048 / 8192 give the same walk counts) (cost = the children's
+// half areas x their triangle counts).  Every choice is a function of the node's triangle SET (ties: axis,
+// then position, then triangle index), so the tree does not depend on the order of the arrays -- the GPU
+// builder (rs_wide_build.hip) builds the same tree level by level.  Output in the PLOC arrays'
 // shape: ids < n triangles (box, hi.w = triangle bits), ids >= n internal (lo.w / hi.w = child id bits).
 // pos: 9 floats per triangle.  Returns the root id.
 inline int build_sah_host(const float* pos, int n, std::vector<float>& nlo, std::vector<float>& nhi,
@@ -155,8 +198,12 @@ inline int build_sah_host(const float* pos, int n, std::vector<float>& nlo, std:
                     return std::min(kBins - 1, (int)(((double)cen[3 * (size_t)t + bax] - clo[bax]) * sc)) < bb;
                 });
                 split = (int)(mid - I);
+            } else {                             // every centroid equal: split at the middle of the triangle-index
+                int mn = I[0], mx = I[0];        // range (a rule on the set, not on the array's order; both sides
+                for (int i = 1; i < j.count; ++i) { mn = std::min(mn, I[i]); mx = std::max(mx, I[i]); }   // non-empty)
+                const int mid = mn + (mx - mn) / 2;
+                split = (int)(std::partition(I, I + j.count, [&](int t) { return t <= mid; }) - I);
             }
-            if (split <= 0 || split >= j.count) split = j.count / 2;
         } else {                                 // full sweep
             double best = 1e300; int bax = 0, bs = j.count / 2;
             auto by_axis = [&](int a) {
@@ -321,33 +368,15 @@ inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, 
             budget.push_back(collapse == 1 ? hb[i] : 0);
         }
         for (int i = ni; i < nv; ++i) tri_prims.push_back(h_f2i(nhi[4 * (size_t)kids[i] + 3]));
-        // quantisation frame from the union of the children (= the PLOC node's box)
-        WBox u = box(kids[0]);
-        for (int i = 1; i < nv; ++i) {
-            const WBox b = box(kids[i]);
-            for (int a = 0; a < 3; ++a) { u.lo[a] = std::min(u.lo[a], b.lo[a]); u.hi[a] = std::max(u.hi[a], b.hi[a]); }
+        WBox kb[8], u;
+        for (int i = 0; i < nv; ++i) kb[i] = box(kids[i]);
+        uint32_t w[20];
+        if (!wide_encode(kb, nv, ni, child_base, tri_base, w, &u)) {
+            bool fin = true;
+            for (int a = 0; a < 3; ++a) fin = fin && w_finite(u.lo[a]) && w_finite(u.hi[a]);
+            err = fin ? "wide BVH: no conservative quantisation" : "wide BVH: non-finite box";
+            return -1;
         }
-        int e[3]; float o[3];
-        uint8_t qlo[3][8] = {}, qhi[3][8] = {};
-        for (int a = 0; a < 3; ++a) {
-            if (!std::isfinite(u.lo[a]) || !std::isfinite(u.hi[a])) { err = "wide BVH: non-finite box"; return -1; }
-            float clo[8], chi[8];
-            for (int i = 0; i < nv; ++i) { const WBox b = box(kids[i]); clo[i] = b.lo[a]; chi[i] = b.hi[a]; }
-            if (!wide_axis(u.lo[a], u.hi[a], clo, chi, nv, e[a], o[a], qlo[a], qhi[a])) {
-                err = "wide BVH: no conservative quantisation"; return -1;
-            }
-        }
-        auto pack = [](const uint8_t* q, int first) {
-            return (uint32_t)q[first] | ((uint32_t)q[first + 1] << 8) | ((uint32_t)q[first + 2] << 16) | ((uint32_t)q[first + 3] << 24);
-        };
-        const uint32_t w[20] = {
-            h_f2u(o[0]), h_f2u(o[1]), h_f2u(o[2]),
-            (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16) | ((uint32_t)ni << 24) |
-                ((uint32_t)nv << 28),
-            child_base, tri_base, pack(qlo[0], 0), pack(qlo[0], 4),
-            pack(qlo[1], 0), pack(qlo[1], 4), pack(qlo[2], 0), pack(qlo[2], 4),
-            pack(qhi[0], 0), pack(qhi[0], 4), pack(qhi[1], 0), pack(qhi[1], 4),
-            pack(qhi[2], 0), pack(qhi[2], 4), 0u, 0u};
         out.insert(out.end(), w, w + 20);
         if (slot_src) for (int i = 0; i < 8; ++i) slot_src->push_back(i < nv ? kids[i] : -1);
         if (queue.size() >= (1u << 24)) { err = "wide BVH: too many nodes"; return -1; }

@@ -27,7 +27,8 @@ EXPORTED_SYMBOLS = [
     "rs_context_create", "rs_context_destroy", "rs_last_error", "rs_scene_create", "rs_scene_load_obj",
     "rs_scene_destroy", "rs_scene_info", "rs_render_frame", "rs_get_frame_device_ptr", "rs_reset_history",
     "rs_synchronize", "rs_dump_gbuffer", "rs_dump_reservoirs", "rs_tile_begin", "rs_tile_halo_ptr",
-    "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_context_set_traversal",
+    "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_debug_wide_tree",
+    "rs_context_set_traversal",
     "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions", "rs_post_frame",
     "rs_post_reset", "rs_scene_rebuild", "rs_render_direct_mis", "rs_scene_create_textured", "rs_scene_set_sky",
     "rs_scene_load_sky", "rs_image_decode", "rs_context_set_initial_split", "rs_context_get_initial_split",
@@ -170,6 +171,7 @@ def load_library(path: str = LIB_PATH):
     L.rs_tile_spatial.argtypes = [vp, i32]
     L.rs_tile_finish.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(PassTimes)]
     L.rs_debug_trace.argtypes = [vp, vp, u32, fp, fp, fp, fp, i32, fp, ctypes.POINTER(ctypes.c_int32)]
+    L.rs_debug_wide_tree.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_int32), vp, vp]
     L.rs_context_set_traversal.argtypes = [vp, i32]
     ip = ctypes.POINTER(ctypes.c_int32)
     L.rs_context_get_traversal.argtypes = [vp, vp, ip, ip, ip]
@@ -321,6 +323,20 @@ class Scene:
         r._check(r.lib.rs_scene_info(self.h, ctypes.byref(n_tris), ctypes.byref(n_emis), ctypes.byref(n_nodes),
                                      ctypes.byref(ms)))
         self.n_nodes, self.build_ms = n_nodes.value, ms.value
+
+    def wide_tree(self):
+        """Test hook (rs_debug_wide_tree): the scene's 8-wide tree as (words (n_nodes, 20) uint32, leaf-triangle
+        ids int32, depth), or None when the scene has none (its walks take the skip pointers)."""
+        r = self.renderer
+        nn, nt, dp = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int32()
+        r._check(r.lib.rs_debug_wide_tree(self.h, ctypes.byref(nn), ctypes.byref(nt), ctypes.byref(dp), None, None))
+        if nn.value == 0:
+            return None
+        words = np.zeros((nn.value, 20), np.uint32)
+        prims = np.zeros(nt.value, np.int32)
+        r._check(r.lib.rs_debug_wide_tree(self.h, ctypes.byref(nn), ctypes.byref(nt), ctypes.byref(dp),
+                                          words.ctypes.data_as(ctypes.c_void_p), prims.ctypes.data_as(ctypes.c_void_p)))
+        return words, prims, dp.value
 
     def close(self):
         if self.h:

@@ -153,6 +153,27 @@ void walk(const std::vector<uint32_t>& W, const std::vector<int>& prims, const S
 }  // namespace
 
 extern "C" {
+// the host restatement of the product's build (build_sah_host + SAH-optimal collapse within the walk's depth)
+// over caller positions: returns the number of wide nodes (words: 20 each) or -1; *n_prims = leaf triangles.
+// The GPU builder (rs_wide_build.hip) must produce the same words (tests/test_gpu_parity.py).
+int wide_build_host(const float* pos, int n, uint32_t* words, int cap_nodes, int* prims, int* n_prims, int* depth_out) {
+    std::vector<float> nlo, nhi;
+    const int root = rs::build_sah_host(pos, n, nlo, nhi);
+    rs::SahCollapse sah;
+    if (n > 1 && !sah.plan(nlo.data(), nhi.data(), n, root, 1.0f, 0.3f, 8)) return -2;   // the GPU builds no tree
+    std::vector<uint32_t> W;
+    std::vector<int> P;
+    int depth = 0;
+    std::string err;
+    if (rs::build_wide_host(nlo.data(), nhi.data(), n, root, W, P, depth, err, 1) != 0) return -1;
+    const int nn = (int)(W.size() / 20);
+    if (nn > cap_nodes) return -3;
+    std::memcpy(words, W.data(), W.size() * sizeof(uint32_t));
+    std::memcpy(prims, P.data(), P.size() * sizeof(int));
+    *n_prims = (int)P.size();
+    *depth_out = depth;
+    return nn;
+}
 // structure + conservativeness; returns the number of wide nodes (> 0) or a negative code, msg = reason
 int wide_check(int n, uint32_t seed, int* depth_out, char* msg, int msg_len, int collapse) {
     Scene S;

@@ -207,3 +207,29 @@ def test_local_mgpu_update_then_rebuild(traversal):
         img = m.render(ss, c, prm, f, copy_out=True)
         assert np.array_equal(img, ref[f]), f"frame {f} ({ops[f]}): {int(np.any(img != ref[f], -1).sum())} px differ"
     m.close()
+
+
+@pytest.mark.parametrize("world,temporal", [(2, 0), (4, 1)])
+def test_rccl_branch_threads_on_one_gpu(tmp_path, world, temporal):
+    """the RCCL branch of rs_mgpu (rs_mgpu_create + ncclCommSplit per lane, NcclLink halo exchanges
+    and gathers issued with frames in flight, rs_mgpu_rebalance's ncclAllReduce) with world 2 and 4 as threads of
+    one process on this one GPU, linked against a stand-in librccl (tests/cpp/rccl_stub.cpp: sends and receives
+    paired per communicator / sender / receiver in issue order and turned into device copies; every pair's byte
+    counts equal, nothing left unpaired).  Every gathered frame (before and after a rebalance) is bit-identical
+    to one context's frame."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "_build", "mgpu_rccl_driver")
+    assert os.path.exists(exe), "build it first: make -C tests/cpp (run by __graft_entry__.build())"
+    sc = scenes.cornell_many_lights(256)
+    obj = tmp_path / "c2.obj"
+    scenes.write_obj(sc, str(obj))
+    c = sc.camera
+    cmd = [exe, str(obj), "96", "64", str(world), "4", *map(str, c.eye), *map(str, c.at), str(c.fov_y), str(temporal)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and line, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    r = json.loads(line[-1])
+    print(f"[rccl-stub] {r}")
+    assert r["bad_frames"] == 0 and r["mismatches"] == 0 and r["unpaired"] == 0 and r["pairs"] > 0 and r["allreduces"] >= 1
