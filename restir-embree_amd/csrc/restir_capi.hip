@@ -49,6 +49,7 @@ struct rs_scene {
     std::vector<rs_material_desc> h_mats;
     // rs_scene_update_positions: emissive triangle ids, refit plan, pinned upload ring (2 slots)
     int* d_emis_tri = nullptr;
+    uint8_t* d_ebucket = nullptr;          // per emitter: its Morton bucket (the sorted initial pass's ray key)
     int *d_refit_order = nullptr, *d_refit_lvl = nullptr;
     std::vector<int> refit_lvl;
     // 8-wide tree of the per-lane walks (rs_scene.h), built on the GPU with the binary tree (rs_wide_build.hip)
@@ -92,6 +93,7 @@ struct rs_scene {
         S.n_nodes = n_nodes; S.n_tris = n_tris; S.n_emis = n_emis; S.n_mats = n_mats;
         S.tri_uv = d_uv; S.tri_tan = d_tan; S.tex = d_tex; S.texd = d_texd; S.sky = sky;
         S.wnodes = wide_on ? wide.nodes : nullptr; S.wtris = wide.tris; S.n_wnodes = wide_on ? wide.n_nodes : 0u;
+        S.ebucket = d_ebucket;
         return S;
     }
     // the geometry of generation `g` if this scene still holds it (current, or the a_* copy of g == a_geo)
@@ -239,6 +241,7 @@ struct rs_context {
     size_t q_slots[kLanes] = {}, q_px[kLanes] = {}, q_waves[kLanes] = {};
     int q_A[kLanes] = {}, q_B[kLanes] = {};
     int cus = 256;
+    bool sort_on = true;                   // wave-sorted initial pass for per-lane wide walks (RESTIR_SORT=off)
 };
 
 // --------------------------------------------------------------------------- helpers
@@ -399,6 +402,8 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         else if (!std::strcmp(t, "off")) c->queue_mode = RS_SPLIT_OFF;
         else if (!std::strcmp(t, "auto")) c->queue_mode = RS_SPLIT_AUTO;
     }
+    if (const char* t = std::getenv("RESTIR_SORT"))            // on (default) | off: wave-sorted initial pass
+        c->sort_on = std::string(t) != "off";
     if (const char* t = std::getenv("RESTIR_TILE_ORDER"))      // cost (default) | off (row-major)
         c->order_on = std::strcmp(t, "off") != 0;
     if (const char* t = std::getenv("RESTIR_READBACK"))        // sdma (default) | kernel
@@ -760,6 +765,36 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
         em[8 * e + 6] = make_float4(area[e], inv_area, 0.0f, 0.0f);
         em[8 * e + 7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
+    // emitter buckets for the sorted initial pass (performance only: any bucketing gives the same frames):
+    // the emitters' centroids in Morton order over their bounds, cut into 64 equal runs
+    std::vector<uint8_t> ebucket(std::max(ne, 1u), 0);
+    if (ne) {
+        float lo[3] = {3.0e38f, 3.0e38f, 3.0e38f}, hi[3] = {-3.0e38f, -3.0e38f, -3.0e38f};
+        std::vector<float> cen(3 * (size_t)ne);
+        for (uint32_t e = 0; e < ne; ++e) {
+            const float* p = &pos[9 * (size_t)emis_tri[e]];
+            for (int a = 0; a < 3; ++a) {
+                const float v = (p[a] + p[3 + a] + p[6 + a]) * (1.0f / 3.0f);
+                cen[3 * (size_t)e + a] = std::isfinite(v) ? v : 0.0f;
+                lo[a] = std::min(lo[a], cen[3 * (size_t)e + a]); hi[a] = std::max(hi[a], cen[3 * (size_t)e + a]);
+            }
+        }
+        std::vector<std::pair<uint64_t, uint32_t>> ord(ne);
+        for (uint32_t e = 0; e < ne; ++e) {
+            uint64_t m = 0;
+            uint32_t q[3];
+            for (int a = 0; a < 3; ++a) {
+                const float ext = hi[a] - lo[a];
+                const float t = ext > 0.0f ? (cen[3 * (size_t)e + a] - lo[a]) / ext : 0.0f;
+                q[a] = (uint32_t)std::min(1023.0f, std::max(0.0f, t * 1024.0f));
+            }
+            for (int b = 0; b < 10; ++b)
+                for (int a = 0; a < 3; ++a) m |= (uint64_t)((q[a] >> b) & 1u) << (3 * b + a);
+            ord[e] = {m, e};
+        }
+        std::sort(ord.begin(), ord.end());
+        for (uint32_t i = 0; i < ne; ++i) ebucket[ord[i].second] = (uint8_t)(((uint64_t)i * 64u) / ne);
+    }
     std::vector<int> guide(kCdfGuide + 1);     // guide[j] = lower_bound(cdf, j / kCdfGuide)
     for (int j = 0; j <= kCdfGuide; ++j) {
         float key = (float)j / (float)kCdfGuide;
@@ -778,7 +813,8 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
         s->update_recorded = false;
     }
     void* old[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_emis, s->d_cdf, s->d_cdf_guide, s->d_emis_tri,
-                   s->d_refit_order, s->d_refit_lvl};
+                   s->d_refit_order, s->d_refit_lvl, s->d_ebucket};
+    s->d_ebucket = nullptr;
     wide_free(s->wide); s->wide_on = false;
     for (void* p : old) if (p) hipFree(p);
     s->d_pos = nullptr; s->d_nodes = nullptr; s->d_tris = nullptr; s->d_emis = nullptr; s->d_cdf = nullptr;
@@ -795,6 +831,8 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     hipMemcpyAsync(s->d_cdf, cdf.data(), cdf.size() * sizeof(float), hipMemcpyHostToDevice, st);
     if (hipMalloc(&s->d_cdf_guide, guide.size() * sizeof(int)) != hipSuccess) { err = "hipMalloc(guide) failed"; return -1; }
     hipMemcpyAsync(s->d_cdf_guide, guide.data(), guide.size() * sizeof(int), hipMemcpyHostToDevice, st);
+    if (hipMalloc(&s->d_ebucket, ebucket.size()) != hipSuccess) { err = "hipMalloc(emitter buckets) failed"; return -1; }
+    hipMemcpyAsync(s->d_ebucket, ebucket.data(), ebucket.size(), hipMemcpyHostToDevice, st);
     if (ne) {
         if (hipMalloc(&s->d_emis_tri, ne * sizeof(int)) != hipSuccess) { err = "hipMalloc(emis ids) failed"; return -1; }
         hipMemcpyAsync(s->d_emis_tri, emis_tri.data(), ne * sizeof(int), hipMemcpyHostToDevice, st);
@@ -1196,7 +1234,7 @@ extern "C" void rs_scene_destroy(rs_scene* s) {
     if (s->ctx) sync_all(s->ctx);
     void* ptrs[] = {s->d_pos, s->d_nodes, s->d_tris, s->d_tri_nrm, s->d_mats, s->d_emis, s->d_cdf, s->d_cdf_guide,
                     s->d_emis_tri, s->d_refit_order, s->d_refit_lvl, s->d_nrm_stage, s->d_tex, s->d_texd, s->d_uv,
-                    s->d_tan, s->a_tri_nrm, s->a_nodes, s->a_tris, s->a_emis, s->a_cdf, s->a_cdf_guide};
+                    s->d_tan, s->a_tri_nrm, s->a_nodes, s->a_tris, s->a_emis, s->a_cdf, s->a_cdf_guide, s->d_ebucket};
     for (void* p : ptrs) if (p) hipFree(p);
     wide_free(s->wide);
     wide_free(s->a_wide);
@@ -1571,6 +1609,9 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
         HIPCHK(c, hipGetLastError());
         k_q_resolve<<<gb, 256, 0, c->fs>>>(S, F, c->G[gnew], Q, ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                                            count_slot(c, gb));
+    } else if (c->sort_on && P->m_area > 0 && s->n_emis < (1u << 21)) {
+        LAUNCH_TRAV(c, k_gbuffer_initial_sorted, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
+                    count_slot(c, gg));
     } else {
         LAUNCH_TRAV(c, k_gbuffer_initial, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                     count_slot(c, gg));

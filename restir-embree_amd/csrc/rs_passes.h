@@ -581,6 +581,239 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
     }
     count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u, t0, y);
 }
+// ---------------------------------------------------------------- wave-sorted initial pass (per-lane wide walks)
+// The per-lane walks of incoherent scenes (C3) are bound by the vector-memory data path returning a wave's
+// divergent node loads (TD busy 0.92): every load instruction touches as many cache lines as its lanes visit
+// distinct nodes.  Lane = pixel and candidate by candidate, a wave's 64 shadow rays aim at 64 random lights.
+// This kernel regroups them: per chunk of kSortChunk area candidates a wave (an 8x8 pixel tile)
+//   A  samples each candidate of its 64 pixels (lane = pixel): a needed shadow ray (its slot = candidate,
+//      pixel) takes a rank in one of 64 buckets by its light (S.ebucket: the Morton order of the emitter
+//      centroids; one LDS atomic), and its light and rank are kept in the slot's LDS word;
+//   then a 64-lane scan turns the bucket counts into offsets and every slot index is scattered to its place:
+//      the chunk's rays are in LDS bucket by bucket (a counting sort);
+//   B  traces them 64 at a time in that order (lane = ray): each lane re-forms its ray from the slot -- the
+//      pixel's surface point from LDS, the candidate's RNG draws, the light record -- with the operations
+//      area_sample_at / evaluate_f_pre use, so it is bit for bit the ray the pixel would trace, walks the
+//      tree (per lane: the 8-wide tree; lockstep: the wave steps through the union of its rays' binary
+//      paths, which the grouping shrinks) and sets the pixel's occlusion bit;
+//   C  re-draws each candidate (lane = pixel) for its RIS weight and runs the reference's addSample stream
+//      over the chunk in candidate order.  (Re-drawing costs one more sampling pass; keeping the weights
+//      would take 4 B per slot of LDS and cost occupancy.)
+// Rays aimed at neighbouring lights share their upper tree paths, so a load instruction touches fewer lines
+// (CPU lab, scripts/bvh_lab.cpp COHERENCE_WAVE, C3: distinct node fetches per wave -39 %, lockstep steps
+// -13 % for 32 candidates in 64 buckets).  The results do not depend on the order rays are traced in:
+// frames are bit-identical to k_gbuffer_initial (tests/test_gpu_parity.py).
+#ifndef RS_SORT_CHUNK
+#define RS_SORT_CHUNK 16
+#endif
+#ifndef RS_INITIAL_WAVES_SORT
+#define RS_INITIAL_WAVES_SORT 5              // per-lane walks (LDS: 29 KB per workgroup -> 5 workgroups per CU)
+#endif
+#ifndef RS_INITIAL_WAVES_SORT_LOCKSTEP
+#define RS_INITIAL_WAVES_SORT_LOCKSTEP 5
+#endif
+constexpr int kSortChunk = RS_SORT_CHUNK;   // area candidates per sort round
+static_assert(kSortChunk >= 1 && kSortChunk <= 32, "one occlusion word per pixel; 11-bit ranks");
+struct SortLds {                            // one wave's region (7.3 KB at 16 candidates)
+    uint32_t slot[kSortChunk * 64];         // slot k * 64 + lane: light | rank in its bucket << 21
+    uint16_t e[kSortChunk * 64];            // the slots of the chunk's rays, bucket by bucket
+    uint32_t cur[64];                       // bucket counts, then bucket offsets
+    uint32_t occ[64];                       // per pixel: the chunk's occlusion bits
+    float px[64], py[64], pz[64];           // per pixel: its surface point
+};
+// cross-lane LDS hand-off inside one wave: LDS requests of a wave complete in order, so a fence against
+// compiler reordering is all that is needed
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+// the pixel index of lane `l` of this thread's wave tile (pixel_of's layout, unclamped)
+__device__ __forceinline__ uint32_t tile_pixel(const FrameConst& F, int ya, int yb, int l) {
+    int bx, by;
+    tile_of(F, ya, yb, bx, by);
+    const int wave = threadIdx.x >> 6;
+    const int x = bx * 16 + (wave & 1) * 8 + (l & 7), y = ya + by * 16 + (wave >> 1) * 8 + (l >> 3);
+    return (uint32_t)y * (uint32_t)F.W + (uint32_t)x;
+}
+// the bucket of a shadow ray: RS_SORT_KEY 1 (default) = the direction's octant x the top 3 bits of the
+// light's Morton bucket; 0 = the light's Morton bucket alone (CPU lab, scripts/bvh_lab.cpp COHERENCE_WAVE,
+// 32 candidates: octant x light 3 bits -- C2 binary lockstep union -45 %, C3 wide-walk distinct fetches -30 %;
+// light bucket alone -- C2 -6 %, C3 -39 %)
+#ifndef RS_SORT_KEY
+#define RS_SORT_KEY 1
+#endif
+__device__ __forceinline__ uint32_t ray_bucket(const DevScene& S, uint32_t pick, vec3 d) {
+    const uint32_t eb = S.ebucket[pick];
+    if (RS_SORT_KEY == 0) return eb;
+    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    return (oct << 3) | (eb >> 3);
+}
+// candidate c of a pixel: area_batch's sample and unoccluded evaluation (pick, weights, shadow ray need)
+struct AreaCand { uint32_t pick, bucket; float wu; bool ok, need, wo_nan; };
+__device__ __forceinline__ AreaCand area_cand(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
+                                              Rng& rng, int c, bool tv, bool alive, float inv_ma) {
+    AreaCand a;
+    a.pick = area_pick(S, rng, c);
+    float Wc, mis;
+    rng.n = cand_slot(c) + 1u;
+    const Sample s = area_sample_at(S, F, pos, sf, rng, a.pick, Wc, mis);
+    const FPre pr = evaluate_f_pre(F, s, pos, false, sf, tv, alive);
+    a.bucket = ray_bucket(S, a.pick, pr.dir);
+    const float m = F.m_brdf > 0 ? mis : inv_ma;
+    a.wu = m * length(pr.L) * Wc;
+    const float wo = m * 0.0f * Wc;             // +-0 (the same reservoir update) or NaN
+    a.wo_nan = wo != wo;
+    a.ok = pr.ok;
+    a.need = pr.need;
+    return a;
+}
+
+template <int T>
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES_SORT_LOCKSTEP, RS_INITIAL_WAVES_SORT))
+k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int fuse_shade, CountSlot C) {
+    const uint64_t t0 = wave_clock();
+    if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
+    __shared__ SortLds lds[4];
+    SortLds& L = lds[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    int x, y;
+    uint32_t rays = 0;
+    const bool in = pixel_of(F, F.gy0, F.gy1, x, y);
+    const size_t p = (size_t)y * F.W + x;
+    {
+        const GElem g = gbuffer_fill<T>(S, F, x, y, in);
+        if (in) G.store(p, g);
+        L.px[lane] = g.pos.x; L.py[lane] = g.pos.y; L.pz[lane] = g.pos.z;
+    }
+    const bool ris = in && y >= F.y0 && y < F.y1;
+    const vec3 cam = F.cam.pos;
+    Res r = res_empty();
+    vec3 f_sel = mk(0, 0, 0);
+    // (the G element is re-read where it is needed: nothing of it stays live across the walks)
+    const bool alive = ris && !any_pos(G.load(p).le) && S.n_emis > 0;          // :238-244
+    if (__ballot(alive) != 0) {
+        Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, (uint32_t)p);
+        const bool tv = !F.do_vis_pass;
+        float best_phat = 0.0f;
+        if (F.m_area > 0) {
+            int sel = -1;
+            const float inv_ma = 1.0f / (float)F.m_area;
+            for (int c0 = 0; c0 < F.m_area; c0 += kSortChunk) {
+                const int nk = F.m_area - c0 < kSortChunk ? F.m_area - c0 : kSortChunk;
+                // ---- A: the chunk's samples (lane = pixel); needed rays take a rank in their light's bucket
+                L.cur[lane] = 0u;
+                L.occ[lane] = 0u;
+                wave_lds_sync();
+                uint32_t needm = 0u;
+                uint32_t bkt[(kSortChunk + 3) / 4] = {};                // the needed rays' buckets, 8 bits each
+                {
+                    const GElem g = G.load(p);
+                    const ShadeFrame sf = make_frame(g, cam);
+                    for (int k = 0; k < nk; ++k) {
+                        const AreaCand a = area_cand(S, F, g.pos, sf, rng, c0 + k, tv, alive, inv_ma);
+                        if (a.need) {
+                            const uint32_t rank = atomicAdd(&L.cur[a.bucket], 1u);
+                            L.slot[k * 64 + lane] = a.pick | (rank << 21);
+                            bkt[k >> 2] |= a.bucket << (8 * (k & 3));
+                            needm |= 1u << k;
+                        }
+                    }
+                }
+                wave_lds_sync();
+                const uint32_t cnt = L.cur[lane];                       // lane = bucket: exclusive scan
+                uint32_t incl = cnt;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t v = __shfl_up(incl, o);
+                    incl += lane >= o ? v : 0u;
+                }
+                const uint32_t n_rays = __shfl(incl, 63);
+                L.cur[lane] = incl - cnt;
+                wave_lds_sync();
+#pragma unroll
+                for (int k = 0; k < kSortChunk; ++k)
+                    if ((needm >> k) & 1u) {
+                        const uint32_t b = (bkt[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                        L.e[L.cur[b] + (L.slot[k * 64 + lane] >> 21)] = (uint16_t)(k * 64 + lane);
+                    }
+                wave_lds_sync();
+                // ---- B: the chunk's shadow rays in bucket order (lane = ray)
+                for (uint32_t j0 = 0; j0 < n_rays; j0 += 64u) {
+                    const uint32_t j = j0 + (uint32_t)lane;
+                    const bool act = j < n_rays;
+                    const uint32_t sl = L.e[act ? j : 0u];
+                    const uint32_t pick = L.slot[sl] & 0x1fffffu, k = sl >> 6, src = sl & 63u;
+                    const vec3 o = mk(L.px[src], L.py[src], L.pz[src]);
+                    Rng q;
+                    q.init(F.seed, F.frame, PASS_INITIAL, tile_pixel(F, F.gy0, F.gy1, (int)src));
+                    q.n = cand_slot(c0 + (int)k) + 1u;
+                    const float r1 = q.range(0, 1), r2 = q.range(0, 1);    // area_sample_at's draws
+                    const float4* E = S.emis + 8 * (size_t)pick;
+                    const vec3 p0 = xyz(E[0]), p1 = xyz(E[1]), p2 = xyz(E[2]);
+                    const float sr = sqrtf(r1);
+                    const float bx = 1.0f - sr, by = sr * (1.0f - r2), bz = sr * r2;
+                    const vec3 pt = (p0 * bx + p1 * by) + p2 * bz;
+                    vec3 ld = pt - o;                                        // evaluate_f_pre's ray
+                    const float r2s = dot(ld, ld);
+                    ld = normalize(ld);
+                    const float tfar = sqrtf(r2s) - F.tfar_off;
+                    const bool occ = trace_any<T>(S, act, o, ld, FLT_MIN + F.tnear_off, tfar);
+                    rays += act ? 1u : 0u;
+                    if (act && occ) atomicOr(&L.occ[src], 1u << k);
+                }
+                wave_lds_sync();
+                // ---- C: re-drawn weights, the reservoir stream in candidate order (lane = pixel)
+                const uint32_t occm = L.occ[lane];
+                const GElem g = G.load(p);
+                const ShadeFrame sf = make_frame(g, cam);
+                for (int k = 0; k < nk; ++k) {
+                    const int c = c0 + k;
+                    const AreaCand a = area_cand(S, F, g.pos, sf, rng, c, tv, alive, inv_ma);
+                    const bool use_u = a.ok && !(a.need && ((occm >> k) & 1u));
+                    const float w = use_u ? a.wu : (a.wo_nan ? __int_as_float(0x7fc00000) : 0.0f);
+                    rng.n = cand_slot(c) + 3u;
+                    if (alive && res_add_w(r, w, 0, rng)) sel = c;
+                }
+            }
+            if (sel >= 0) {
+                const GElem g = G.load(p);
+                const Sample s = area_redraw(S, F, g.pos, make_frame(g, cam), rng, sel, tv, f_sel);
+                best_phat = length(f_sel);
+                r.p = s.p; r.n = s.n; r.li = s.li;
+            }
+        }
+        if (F.m_brdf > 0) {
+            const GElem g = G.load(p);
+            const ShadeFrame sf = make_frame(g, cam);
+            const float inv_mb = 1.0f / (float)F.m_brdf;
+            for (int i = 0; i < F.m_brdf; ++i) {
+                float Wc, mis;
+                rng.n = cand_slot(F.m_area + i);
+                Sample s = brdf_sample<T>(S, F, g.pos, sf, alive, rng, Wc, mis, rays);
+                vec3 f = evaluate_f<T>(S, F, s, g.pos, false, sf, tv, alive, rays);
+                float ph = length(f);
+                float w = F.m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
+                rng.n = cand_slot(F.m_area + i) + 3u;
+                if (alive && res_add(r, s, w, 0, rng)) { best_phat = ph; f_sel = f; }
+            }
+        }
+        if (alive) {                                                    // as initial_ris's epilogue
+            r.conf = F.m_area + F.m_brdf;
+            const float ph = smp_valid(smp_of(r)) ? best_phat : 0.0f;
+            r.W = ph > 0.0f ? 1.0f / ph * r.wsum : 0.0f;
+            res_cap(r, F.cap);
+        } else {
+            r = res_empty();
+            f_sel = mk(0, 0, 0);
+        }
+    }
+    if (ris) {
+        Rw.store(p, r);
+        if (fuse_shade) store_rgb(fb, p, shade_px(r, f_sel, G.load(p).le));
+    }
+    count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u, t0, y);
+}
+
 // ---------------------------------------------------------------- candidate-split initial pass
 // The same G-buffer + initialRenderPass with the candidates of a pixel spread over kSplit waves: a
 // workgroup is ONE 8x8 tile, wave g evaluates candidate group g of its 64 pixels.  A pixel's

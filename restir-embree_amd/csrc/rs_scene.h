@@ -40,6 +40,9 @@ struct DevScene {
     const uint4* wnodes;      // 5 per node
     const float4* wtris;      // 3 per wide-leaf triangle: (v0, prim) (e1) (e2)
     uint32_t n_wnodes;
+    // per emissive triangle: its bucket (0..63) in the Morton order of the emitters' centroids -- the key
+    // the wave-sorted initial pass groups its shadow rays by (rs_passes.h k_gbuffer_initial_sorted)
+    const uint8_t* ebucket;
 };
 constexpr int kCdfGuide = 1024;
 

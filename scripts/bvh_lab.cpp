@@ -384,7 +384,7 @@ static inline bool tri_hit(int p, V3 o, V3 d, float tn, float tf, float& t) {
 struct Ray { V3 o, d; float tn, tf; bool active; };
 // per-lane walk; records per step (node index or -1 done) and the leaf count tested at each step
 struct Trace { int visits = 0, tris = 0; std::vector<int> step_cnt; float t = -1; int prim = -1; bool occ = false; };
-static Trace walk(const Flat& F, const Ray& r, bool any) {
+static Trace walk(const Flat& F, const Ray& r, bool any, std::vector<int>* vis = nullptr) {
     Trace tr;
     if (!r.active) return tr;
     V3 inv{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
@@ -393,6 +393,7 @@ static Trace walk(const Flat& F, const Ray& r, bool any) {
     while (i < n) {
         const FNode& N = F.n[i];
         ++tr.visits;
+        if (vis) vis->push_back(i);
         bool hit = box_test(N.b, r.o, inv, r.tn, tf);
         int cnt = 0;
         if (hit && N.cnt > 0) {
@@ -827,6 +828,98 @@ int main(int argc, char** argv) {
             for (int g = 0; g < 4; ++g)
                 printf("  %-28s steps per wave %.1f, distinct node fetches per wave %.1f (per step %.1f), union %.1f\n", names[g],
                        st[g] / nwave, ds[g] / nwave, ds[g] / st[g], un[g] / nwave);
+        }
+        if (getenv("COHERENCE_WAVE")) {
+            // one wave = an 8x8 pixel tile with K area candidates per pixel (64 K shadow rays).  As the kernels
+            // run them: candidate by candidate (lane = pixel).  Regrouped: the wave's 64 K rays sorted by a key
+            // and traced 64 at a time in sorted order (lane = sorted position).  Per wave: lockstep steps (sum
+            // over the K groups of the longest walk) and the distinct nodes per step (the lines the vector
+            // memory path returns), summed.
+            const int K = getenv("K") ? atoi(getenv("K")) : 32;
+            const int RB = getenv("RANK_BITS") ? atoi(getenv("RANK_BITS")) : 12;   // buckets of the emitter's spatial rank
+            const char* names[4] = {"per candidate (kernel)", "by emitter spatial rank (bucketed)", "sorted by target Morton", "sorted by octant+Morton"};
+            // each emitter's rank in the Morton order of the emitter centroids (a per-scene table)
+            std::vector<uint32_t> erank(g_tris.size(), 0);
+            {
+                std::vector<std::pair<uint64_t, int>> order;
+                for (int e : emis) {
+                    const Tri& t = g_tris[e];
+                    V3 c = (t.v0 + t.v1 + t.v2) * (1.0f / 3.0f);
+                    auto qb = [](float v) { return (uint32_t)std::min(1023.0f, std::max(0.0f, (v + 20.0f) * 25.0f)); };
+                    uint32_t mx = qb(c.x), my = qb(c.y), mz = qb(c.z); uint64_t m = 0;
+                    for (int bb = 0; bb < 10; ++bb) m |= (uint64_t)((((mx >> bb) & 1) << (3 * bb)) | (((my >> bb) & 1) << (3 * bb + 1)) | (((mz >> bb) & 1) << (3 * bb + 2)));
+                    order.push_back({m, e});
+                }
+                std::sort(order.begin(), order.end());
+                for (size_t i = 0; i < order.size(); ++i) erank[order[i].second] = (uint32_t)((i << RB) / order.size());
+            }
+            double st[4] = {0, 0, 0, 0}, ds[4] = {0, 0, 0, 0}, bu[4] = {0, 0, 0, 0};
+            long nwave = 0;
+            std::mt19937 rg2(7);
+            const int stride = getenv("WSTRIDE") ? atoi(getenv("WSTRIDE")) : 4;   // every stride-th tile in x and y
+            for (int ty = 0; ty + 8 <= H; ty += 8 * stride)
+                for (int tx = 0; tx + 8 <= W; tx += 8 * stride) {
+                    V3 org[64]; bool ok[64];
+                    for (int l = 0; l < 64; ++l) {
+                        int x = tx + (l & 7), y = ty + (l >> 3);
+                        V3 dc{(float)x - W / 2.0f, H / 2.0f - (float)y, -focal};
+                        V3 d = xc * dc.x + yc * dc.y + zc * dc.z;
+                        d = d * (1.0f / std::sqrt(dot(d, d)));
+                        WEmu a = emu_walk(WN, pr, Ray{eye, d, 0.01f, 3.0e38f, true}, false, 8);
+                        ok[l] = a.prim >= 0; org[l] = eye + d * a.t;
+                    }
+                    const int R = 64 * K;
+                    std::vector<std::vector<uint32_t>> seq(R);
+                    std::vector<std::vector<int>> bvis(R);      // binary skip-pointer walk: visited nodes
+                    std::vector<uint64_t> key[4];
+                    for (int g = 0; g < 4; ++g) key[g].resize(R);
+                    for (int c = 0; c < K; ++c)
+                        for (int l = 0; l < 64; ++l) {
+                            const int r = c * 64 + l;
+                            int e = emis[rg2() % ne];
+                            float r1 = U(rg2), r2 = U(rg2), sr = std::sqrt(r1);
+                            const Tri& t = g_tris[e];
+                            V3 q = t.v0 * (1 - sr) + t.v1 * (sr * (1 - r2)) + t.v2 * (sr * r2);
+                            auto qb = [](float v) { return (uint32_t)std::min(1023.0f, std::max(0.0f, (v + 20.0f) * 25.0f)); };
+                            uint32_t mx = qb(q.x), my = qb(q.y), mz = qb(q.z); uint64_t m = 0;
+                            for (int bb = 0; bb < 10; ++bb) m |= (uint64_t)((((mx >> bb) & 1) << (3 * bb)) | (((my >> bb) & 1) << (3 * bb + 1)) | (((mz >> bb) & 1) << (3 * bb + 2)));
+                            V3 sd = q - org[l];
+                            const uint64_t oct = (sd.x < 0) | ((sd.y < 0) << 1) | ((sd.z < 0) << 2);
+                            static const int use_oct = getenv("OCT") ? atoi(getenv("OCT")) : 0;
+                            key[0][r] = (uint64_t)r; key[1][r] = ((((use_oct ? oct : 0) << RB) | (uint64_t)erank[e]) << 12) | r;
+                            key[2][r] = (m << 12) | r;
+                            key[3][r] = (((oct << 30) | m) << 12) | r;
+                            if (!ok[l]) continue;
+                            float dist = std::sqrt(dot(sd, sd));
+                            sd = sd * (1.0f / std::max(dist, 1e-20f));
+                            emu_walk(WN, pr, Ray{org[l], sd, 0.01f, dist - 0.001f, true}, true, 8, &seq[r]);
+                            walk(Fr, Ray{org[l], sd, 0.01f, dist - 0.001f, true}, true, &bvis[r]);
+                        }
+                    for (int g = 0; g < 4; ++g) {
+                        std::sort(key[g].begin(), key[g].end());
+                        for (int c = 0; c < K; ++c) {   // binary lockstep: the wave steps through the union of its lanes' visits
+                            std::vector<int> u;
+                            for (int i = 0; i < 64; ++i) { auto& q = bvis[key[g][64 * c + i] & 4095]; u.insert(u.end(), q.begin(), q.end()); }
+                            std::sort(u.begin(), u.end());
+                            bu[g] += std::unique(u.begin(), u.end()) - u.begin();
+                        }
+                        for (int c = 0; c < K; ++c) {
+                            size_t T = 0;
+                            for (int i = 0; i < 64; ++i) T = std::max(T, seq[key[g][64 * c + i] & 4095].size());
+                            st[g] += T;
+                            for (size_t s = 0; s < T; ++s) {
+                                uint32_t v[64]; int nv = 0;
+                                for (int i = 0; i < 64; ++i) { auto& q = seq[key[g][64 * c + i] & 4095]; if (s < q.size()) v[nv++] = q[s]; }
+                                std::sort(v, v + nv); ds[g] += std::unique(v, v + nv) - v;
+                            }
+                        }
+                    }
+                    ++nwave;
+                }
+            printf("wave coherence (8x8 tile, K=%d candidates, %ld waves):\n", K, nwave);
+            for (int g = 0; g < 4; ++g)
+                printf("  %-26s steps per wave %.1f, distinct node fetches per wave %.1f (per step %.2f) | binary lockstep union %.1f\n",
+                       names[g], st[g] / nwave, ds[g] / nwave, ds[g] / st[g], bu[g] / nwave);
         }
         double wsum = 0; for (int v : wave_it) wsum += v;
         printf("emu: primary iters %.2f tris %.2f | bounce iters %.2f tris %.2f | shadow iters %.2f tris %.2f lost %.4f max stack %d wave-max iters %.1f | mismatches %ld | nodes %zu\n",

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-3 profiles on the GPU box (after scripts/gpu_r03.sh): BVH walk statistics, rocprofv3 kernel-trace
+# Round-4 profiles on the GPU box (after scripts/gpu_r04.sh): BVH walk statistics, rocprofv3 kernel-trace
 # stats of C2 and C3 (frames in flight, and one frame in flight = the kernel averages bench.py's
 # kernel_roofline uses), then one --pmc pass per counter group with one frame in flight and the scene's
 # traversal kind pinned: FETCH_SIZE, WRITE_SIZE, SQ_* (issue / wait) and the vector-memory pipeline group
-# (TA/TD/TCP busy and requests).  scripts/pmc_summary.py turns the passes into profiles/r03_pmc_<cfg>.json.
+# (TA/TD/TCP busy and requests).  scripts/pmc_summary.py turns the passes into profiles/r04_pmc_<cfg>.json.
 # Stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

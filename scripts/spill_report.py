@@ -116,8 +116,11 @@ def main():
             if sizes:
                 inner.append(min(sizes))
         inner.sort()
-        vg = re.search(r"\.vgpr_count:\s+(\d+)", s[end:end + 200000])
-        print(f"{name[:64]}: {len(ops)} scratch ops, {len(inner)} in loops (innermost loop lengths {inner[:16]})")
+        hist = {}
+        for sz in inner:
+            hist[sz] = hist.get(sz, 0) + 1
+        print(f"{name[:64]}: {len(ops)} scratch ops, {len(inner)} in loops (innermost loop length: ops "
+              f"{dict(sorted(hist.items()))})")
 
 
 if __name__ == "__main__":

@@ -183,6 +183,12 @@ int wide_check(int n, uint32_t seed, int* depth_out, char* msg, int msg_len, int
     int depth = 0;
     std::string err;
     auto fail = [&](const std::string& m) { if (msg) { std::strncpy(msg, m.c_str(), msg_len - 1); msg[msg_len - 1] = 0; } return -1; };
+    if (collapse == 3) {                   // coincident triangles (the source tree's degenerate-centroid split)
+        // (a few dozen: the full sweep's ties peel identical boxes off one at a time, so hundreds of copies make
+        // a chain too deep for the walk's stack -- the product then builds no wide tree, tests/test_gpu_wide.py)
+        for (int t = 1; t < std::min(n / 2, 24); ++t) std::memcpy(&S.pos[9 * (size_t)t], &S.pos[0], 9 * sizeof(float));
+        collapse = 2;
+    }
     if (collapse == 2) { S.root = rs::build_sah_host(S.pos.data(), S.n, S.nlo, S.nhi); collapse = 1; }   // host SAH source
     if (rs::build_wide_host(S.nlo.data(), S.nhi.data(), S.n, S.root, W, prims, depth, err, collapse) != 0) return fail(err);
     if (depth > 8) return fail("deeper than the walk's stack");
@@ -248,6 +254,12 @@ int wide_query(int n, uint32_t seed, int n_rays, int* n_hits, int collapse) {
     std::vector<int> prims;
     int depth = 0;
     std::string err;
+    if (collapse == 3) {
+        // (a few dozen: the full sweep's ties peel identical boxes off one at a time, so hundreds of copies make
+        // a chain too deep for the walk's stack -- the product then builds no wide tree, tests/test_gpu_wide.py)
+        for (int t = 1; t < std::min(n / 2, 24); ++t) std::memcpy(&S.pos[9 * (size_t)t], &S.pos[0], 9 * sizeof(float));
+        collapse = 2;
+    }
     if (collapse == 2) { S.root = rs::build_sah_host(S.pos.data(), S.n, S.nlo, S.nhi); collapse = 1; }
     if (rs::build_wide_host(S.nlo.data(), S.nhi.data(), S.n, S.root, W, prims, depth, err, collapse) != 0) return -1;
     std::mt19937 rng(seed * 7 + 1);

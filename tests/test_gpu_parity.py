@@ -666,3 +666,33 @@ def test_wide_tree_live_on_c3():
         assert ((fetches > 0) & (fetches != 0xFFFF)).all(), "no 8-wide tree on the C3 scene (skip-pointer fallback)"
         assert (lost == 0).all()
         assert fetches.mean() < 100.0       # a broken tree (e.g. boxes opened for every ray) walks far more
+
+
+@pytest.mark.parametrize("which", ["c3", "c3_a37", "c2_lane"])
+def test_sorted_initial_pass_bit_identical(which, monkeypatch):
+    """The wave-sorted initial pass (rs_passes.h k_gbuffer_initial_sorted: per chunk of area candidates the
+    shadow rays of an 8x8 tile are counting-sorted by their light's Morton bucket and traced in that order)
+    renders the frames of the per-candidate kernel bit for bit (RESTIR_SORT=off), incl. a candidate count that
+    is not a multiple of the chunk, a visibility-pass frame (no shadow rays in the initial pass) and the
+    metric scene walked per lane."""
+    if which == "c2_lane":
+        sc, prm, W, H = scenes.cornell_many_lights(1024), P.metric_params(), 64, 48
+    else:
+        sc, W, H = scenes.sponza_like(target_tris=30_000, n_lamps=128), 64, 40
+        prm = P.c3_params(m_area=37 if which == "c3_a37" else 32)
+    cam = lambda f: scenes.orbit_camera(sc.camera, f, 240, 0.3)
+    out = {}
+    for sort in ("on", "off"):
+        monkeypatch.setenv("RESTIR_SORT", sort)
+        g = Renderer(W, H)
+        g.set_traversal("lane")
+        gs = g.load_scene(sc)
+        fr = [g.produce_restir(gs, cam(f), prm, f, timed=True).copy() for f in range(3)]
+        rays = int(g.last_times.rays)
+        vis = P.c3_params(m_area=8, do_visibility_pass=1)
+        fr.append(g.produce_restir(gs, cam(3), vis, 3).copy())
+        out[sort] = (fr, rays, g.reservoirs().copy())
+    for f, (a, b) in enumerate(zip(out["on"][0], out["off"][0])):
+        assert np.array_equal(a, b), f"{which} frame {f}: sorted != per-candidate"
+    assert out["on"][1] == out["off"][1]                # the same rays traced
+    assert np.array_equal(out["on"][2], out["off"][2])

@@ -27,7 +27,7 @@ def _lib():
     return L
 
 
-@pytest.mark.parametrize("collapse", [0, 1, 2], ids=["greedy", "sah", "sah-hostsah"])
+@pytest.mark.parametrize("collapse", [0, 1, 2, 3], ids=["greedy", "sah", "sah-hostsah", "hostsah-coincident"])
 @pytest.mark.parametrize("n,seed", [(1, 1), (2, 2), (7, 3), (9, 4), (64, 5), (1000, 6), (20000, 7)])
 def test_wide_tree_structure_and_conservative_boxes(n, seed, collapse):
     L = _lib()
@@ -38,7 +38,7 @@ def test_wide_tree_structure_and_conservative_boxes(n, seed, collapse):
     assert depth.value >= 0 and (n <= 8 or depth.value >= 1)
 
 
-@pytest.mark.parametrize("collapse", [0, 1, 2], ids=["greedy", "sah", "sah-hostsah"])
+@pytest.mark.parametrize("collapse", [0, 1, 2, 3], ids=["greedy", "sah", "sah-hostsah", "hostsah-coincident"])
 @pytest.mark.parametrize("n,seed", [(1, 11), (5, 12), (300, 13), (5000, 14)])
 def test_wide_walk_matches_brute_force(n, seed, collapse):
     L = _lib()
