@@ -50,6 +50,7 @@ struct rs_scene {
     // rs_scene_update_positions: emissive triangle ids, refit plan, pinned upload ring (2 slots)
     int* d_emis_tri = nullptr;
     uint8_t* d_ebucket = nullptr;          // per emitter: its Morton bucket (the sorted initial pass's ray key)
+    float ecen[3] = {0.0f, 0.0f, 0.0f};    // centre of the emitter centroids' bounds (the sorted spatial pass's key)
     int *d_refit_order = nullptr, *d_refit_lvl = nullptr;
     std::vector<int> refit_lvl;
     // 8-wide tree of the per-lane walks (rs_scene.h), built on the GPU with the binary tree (rs_wide_build.hip)
@@ -94,6 +95,7 @@ struct rs_scene {
         S.tri_uv = d_uv; S.tri_tan = d_tan; S.tex = d_tex; S.texd = d_texd; S.sky = sky;
         S.wnodes = wide_on ? wide.nodes : nullptr; S.wtris = wide.tris; S.n_wnodes = wide_on ? wide.n_nodes : 0u;
         S.ebucket = d_ebucket;
+        S.ecen = vec3{ecen[0], ecen[1], ecen[2]};
         return S;
     }
     // the geometry of generation `g` if this scene still holds it (current, or the a_* copy of g == a_geo)
@@ -241,7 +243,8 @@ struct rs_context {
     size_t q_slots[kLanes] = {}, q_px[kLanes] = {}, q_waves[kLanes] = {};
     int q_A[kLanes] = {}, q_B[kLanes] = {};
     int cus = 256;
-    bool sort_on = true;                   // wave-sorted initial pass for per-lane wide walks (RESTIR_SORT=off)
+    bool sort_on = true;                   // wave-sorted initial pass (RESTIR_SORT=off)
+    bool sort_spatial = true;              // wave-sorted spatial pass, CONSTANT MIS, k <= 8 (RESTIR_SORT_SPATIAL=off)
 };
 
 // --------------------------------------------------------------------------- helpers
@@ -404,6 +407,8 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
     }
     if (const char* t = std::getenv("RESTIR_SORT"))            // on (default) | off: wave-sorted initial pass
         c->sort_on = std::string(t) != "off";
+    if (const char* t = std::getenv("RESTIR_SORT_SPATIAL"))    // on (default) | off: wave-sorted spatial pass
+        c->sort_spatial = std::string(t) != "off";
     if (const char* t = std::getenv("RESTIR_TILE_ORDER"))      // cost (default) | off (row-major)
         c->order_on = std::strcmp(t, "off") != 0;
     if (const char* t = std::getenv("RESTIR_READBACK"))        // sdma (default) | kernel
@@ -794,6 +799,7 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
         }
         std::sort(ord.begin(), ord.end());
         for (uint32_t i = 0; i < ne; ++i) ebucket[ord[i].second] = (uint8_t)(((uint64_t)i * 64u) / ne);
+        for (int a = 0; a < 3; ++a) s->ecen[a] = 0.5f * lo[a] + 0.5f * hi[a];
     }
     std::vector<int> guide(kCdfGuide + 1);     // guide[j] = lower_bound(cdf, j / kCdfGuide)
     for (int j = 0; j <= kCdfGuide; ++j) {
@@ -1718,7 +1724,9 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
         const bool tev = c->tuning && c->tune_n + 2 <= (int)(sizeof(c->tune_ev) / sizeof(c->tune_ev[0]));
         if (tev) HIPCHK(c, hipEventRecord(c->tune_ev[c->tune_n], c->fs));
 #define SPATIAL(TK, CM, SM) k_spatial<TK, CM, SM><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs)
-        if (c->trav == TRAV_LANE) {
+        if (c->sort_spatial && cm && c->F.k + 1 <= kSpatialSortMax) {
+            LAUNCH_TRAV(c, k_spatial_sorted, gb, S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
+        } else if (c->trav == TRAV_LANE) {
             if (c->twide) { if (cm) SPATIAL(TRAV_LANE | TRAV_WIDE, 1, 0); else SPATIAL(TRAV_LANE | TRAV_WIDE, 0, 0); }
             else { if (cm) SPATIAL(TRAV_LANE, 1, 0); else SPATIAL(TRAV_LANE, 0, 0); }
         } else if (grid_waves(gb) < (size_t)2 * c->wave_slots) {   // a small launch: RS_SPATIAL_WAVES_SMALL budget

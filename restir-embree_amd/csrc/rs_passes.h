@@ -1288,6 +1288,146 @@ k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, 
     count_rays(C, rays, 0, t0, y);
 }
 
+// ---------------------------------------------------------------- wave-sorted spatial pass (CONSTANT MIS)
+// The same regrouping as k_gbuffer_initial_sorted for the spatial pass's k + 1 visibility rays per pixel (the
+// pixel to each listed neighbour's sample): per wave the rays are counting-sorted by octant x the target's cell
+// (one bit per axis of the emitters' bounds: the samples are light points) and traced 64 at a time in that
+// order; each lane re-forms its ray from the slot (list position, pixel) -- the pixel's surface point from the
+// G-buffer, the neighbour's sample from its reservoir -- with evaluate_f_pre's operations, and the reservoir
+// stream then runs per pixel in list order.  Bit-identical to k_spatial<T, 1> (tests/test_gpu_parity.py).
+// Lists of up to kSpatialSortMax entries (k <= 8); longer lists take k_spatial.
+constexpr int kSpatialSortMax = 9;
+struct SpatialSortLds {                     // one wave's region (2.9 KB)
+    uint16_t slot[kSpatialSortMax * 64];    // slot i * 64 + lane: rank in its bucket
+    uint16_t e[kSpatialSortMax * 64];       // the slots of the rays, bucket by bucket
+    uint32_t cur[64];                       // bucket counts, then offsets
+    uint32_t occ[64];                       // per pixel: occlusion bit of list position i
+};
+__device__ __forceinline__ uint32_t point_bucket(const DevScene& S, vec3 pt, vec3 d) {
+    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    const uint32_t cx = pt.x > S.ecen.x ? 1u : 0u, cy = pt.y > S.ecen.y ? 2u : 0u, cz = pt.z > S.ecen.z ? 4u : 0u;
+    return (oct << 3) | cx | cy | cz;
+}
+
+template <int T>
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_SPATIAL_WAVES, RS_SPATIAL_WAVES_LANE))
+k_spatial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, int fuse_shade, float* fb, CountSlot C) {
+    __shared__ uint32_t nbr[(kSpatialSortMax - 1) * 256];      // list position i >= 1 -> pixel
+    __shared__ SpatialSortLds lds[4];
+    SpatialSortLds& L = lds[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63, wbase = threadIdx.x & ~63;
+    const uint64_t t0 = wave_clock();
+    int x, y;
+    uint32_t rays = 0;
+    const bool in = pixel_of(F, F.y0, F.y1, x, y);
+    const size_t p = (size_t)y * F.W + x;
+    const vec3 cam = F.cam.pos;
+    GElem th = G.load(p);
+    const bool emissive = any_pos(th.le);
+    const bool alive = in && !emissive;
+    if (in && emissive) {                                  // :319-324
+        Res r = Rr.load(p);
+        Rw.store(p, r);
+        if (fuse_shade) store_rgb(fb, p, shade_px(r, mk(0, 0, 0), th.le));
+    }
+    if (__ballot(alive) != 0) {
+        Rng rng; rng.init(F.seed, F.frame, PASS_SPATIAL0 + (uint32_t)pass_idx, (uint32_t)p);
+        int M = 1;                                          // neighbour selection (:334-374), as k_spatial
+        for (int i = 0; i < F.k; ++i) {
+            size_t q = neighbor_px(F, rng, i, x, y);
+            if (any_pos(G.le(q))) continue;
+            if (F.reject) {
+                float4 nq = G.g1[q];
+                float ns = dot(xyz(nq), th.nrm);
+                if (ns < F.min_normal_sim) continue;
+                float nd = G.g0[q].w;
+                float dr = 0;
+                if (nd > 0) dr = th.depth / nd;
+                float hd = F.max_depth_diff * 0.5f;
+                if (dr < 1.0f - hd || dr > 1.0f + hd) continue;
+            }
+            nbr[(M - 1) * 256 + threadIdx.x] = (uint32_t)q;
+            M += 1;
+        }
+        rng.n = 2u * (uint32_t)F.k;
+        const int cnt = M, kk = F.k + 1;
+        const float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
+        auto list_q = [&](int i) -> size_t { return (i == 0 || i >= M) ? p : (size_t)nbr[(i - 1) * 256 + threadIdx.x]; };
+        const ShadeFrame sf = make_frame(th, cam);
+        // ---- A: every list entry's ray need and bucket rank (lane = pixel)
+        L.cur[lane] = 0u;
+        L.occ[lane] = 0u;
+        wave_lds_sync();
+        uint32_t needm = 0u, bkt[3] = {0u, 0u, 0u};         // 9 buckets x 6 bits -> 3 words of 3 x 10 bits
+        for (int i = 0; i < kk; ++i) {
+            const Res rr = Rr.load(list_q(i));
+            const FPre pre = evaluate_f_pre(F, smp_of(rr), th.pos, false, sf, true, alive && i < cnt);
+            if (pre.need) {
+                const uint32_t b = point_bucket(S, rr.p, pre.dir);
+                L.slot[i * 64 + lane] = (uint16_t)atomicAdd(&L.cur[b], 1u);
+                bkt[i / 3] |= b << (10 * (i % 3));
+                needm |= 1u << i;
+            }
+        }
+        wave_lds_sync();
+        const uint32_t cnt_b = L.cur[lane];
+        uint32_t incl = cnt_b;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o);
+            incl += lane >= o ? v : 0u;
+        }
+        const uint32_t n_rays = __shfl(incl, 63);
+        L.cur[lane] = incl - cnt_b;
+        wave_lds_sync();
+#pragma unroll
+        for (int i = 0; i < kSpatialSortMax; ++i)
+            if ((needm >> i) & 1u) {
+                const uint32_t b = (bkt[i / 3] >> (10 * (i % 3))) & 63u;
+                L.e[L.cur[b] + L.slot[i * 64 + lane]] = (uint16_t)(i * 64 + lane);
+            }
+        wave_lds_sync();
+        // ---- B: the rays in bucket order (lane = ray)
+        for (uint32_t j0 = 0; j0 < n_rays; j0 += 64u) {
+            const uint32_t j = j0 + (uint32_t)lane;
+            const bool act = j < n_rays;
+            const uint32_t sl = L.e[act ? j : 0u];
+            const uint32_t i = sl >> 6, src = sl & 63u;
+            const uint32_t psrc = tile_pixel(F, F.y0, F.y1, (int)src);
+            const size_t q = i == 0 ? (size_t)psrc : (size_t)nbr[(i - 1) * 256 + wbase + src];
+            const vec3 o = xyz(G.g0[psrc]);
+            const vec3 sp = xyz(Rr.r[3 * q]);
+            vec3 ld = sp - o;                                   // evaluate_f_pre's ray
+            const float r2 = dot(ld, ld);
+            ld = normalize(ld);
+            const float tfar = sqrtf(r2) - F.tfar_off;
+            const bool occ = trace_any<T>(S, act, o, ld, FLT_MIN + F.tnear_off, tfar);
+            rays += act ? 1u : 0u;
+            if (act && occ) atomicOr(&L.occ[src], 1u << i);
+        }
+        wave_lds_sync();
+        // ---- C: the reservoir stream in list order (lane = pixel)
+        const uint32_t occm = L.occ[lane];
+        Res res = res_empty();
+        vec3 f_sel = mk(0, 0, 0);
+        for (int i = 0; i < kk; ++i) {
+            const Res rr = Rr.load(list_q(i));
+            const FPre pre = evaluate_f_pre(F, smp_of(rr), th.pos, false, sf, true, alive && i < cnt);
+            const vec3 f = evaluate_f_post(pre, ((occm >> i) & 1u) != 0u);
+            const float rw = rcpM * length(f) * rr.W;
+            if (alive && i < cnt && res_add(res, smp_of(rr), rw, rr.conf, rng)) f_sel = f;
+        }
+        const float fph = smp_valid(smp_of(res)) ? length(f_sel) : 0.0f;  // :481
+        res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
+        res_cap(res, F.cap);
+        if (alive) {
+            Rw.store(p, res);
+            if (fuse_shade) store_rgb(fb, p, shade_px(res, f_sel, th.le));
+        }
+    }
+    count_rays(C, rays, 0, t0, y);
+}
+
 // shade loop (pg/simpleguidx11.cpp:447-472)
 template <int T>
 __global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G, ResBuf Rr, float* fb, CountSlot C) {

@@ -43,6 +43,7 @@ struct DevScene {
     // per emissive triangle: its bucket (0..63) in the Morton order of the emitters' centroids -- the key
     // the wave-sorted initial pass groups its shadow rays by (rs_passes.h k_gbuffer_initial_sorted)
     const uint8_t* ebucket;
+    vec3 ecen;                // centre of the emitters' centroid bounds (the sorted spatial pass's target cells)
 };
 constexpr int kCdfGuide = 1024;
 

@@ -60,7 +60,7 @@ def main():
     for N, rank in cases:
         y0, y1 = balanced_bands(costs, N, 8)[rank] if costs is not None else band_rows(H, rank, N)
         halo = halo_rows(prm) if N > 1 else 0
-        margin = max(halo, 64 if prm.do_temporal else 0) if N > 1 else 0
+        margin = halo          # rs_mgpu_render_frame's G-buffer margin (a temporal reprojection beyond it rebuilds)
 
         def frame(f):
             r, gs = rs[f % len(rs)], gss[f % len(rs)]

@@ -668,14 +668,15 @@ def test_wide_tree_live_on_c3():
         assert fetches.mean() < 100.0       # a broken tree (e.g. boxes opened for every ray) walks far more
 
 
-@pytest.mark.parametrize("which", ["c3", "c3_a37", "c2_lane"])
+@pytest.mark.parametrize("which", ["c3", "c3_a37", "c2_lane", "c2_lockstep"])
 def test_sorted_initial_pass_bit_identical(which, monkeypatch):
-    """The wave-sorted initial pass (rs_passes.h k_gbuffer_initial_sorted: per chunk of area candidates the
-    shadow rays of an 8x8 tile are counting-sorted by their light's Morton bucket and traced in that order)
-    renders the frames of the per-candidate kernel bit for bit (RESTIR_SORT=off), incl. a candidate count that
-    is not a multiple of the chunk, a visibility-pass frame (no shadow rays in the initial pass) and the
-    metric scene walked per lane."""
-    if which == "c2_lane":
+    """The wave-sorted initial and spatial passes (rs_passes.h k_gbuffer_initial_sorted / k_spatial_sorted: per
+    8x8 tile the shadow rays are counting-sorted by octant x light bucket and traced in that order) render the
+    frames of the per-candidate kernels bit for bit (RESTIR_SORT=off, RESTIR_SORT_SPATIAL=off), incl. a
+    candidate count that is not a multiple of the chunk, a visibility-pass frame (no shadow rays in the initial
+    pass), and both walk kinds on the metric scene."""
+    trav = "lockstep" if which == "c2_lockstep" else "lane"
+    if which.startswith("c2"):
         sc, prm, W, H = scenes.cornell_many_lights(1024), P.metric_params(), 64, 48
     else:
         sc, W, H = scenes.sponza_like(target_tris=30_000, n_lamps=128), 64, 40
@@ -684,8 +685,9 @@ def test_sorted_initial_pass_bit_identical(which, monkeypatch):
     out = {}
     for sort in ("on", "off"):
         monkeypatch.setenv("RESTIR_SORT", sort)
+        monkeypatch.setenv("RESTIR_SORT_SPATIAL", sort)
         g = Renderer(W, H)
-        g.set_traversal("lane")
+        g.set_traversal(trav)
         gs = g.load_scene(sc)
         fr = [g.produce_restir(gs, cam(f), prm, f, timed=True).copy() for f in range(3)]
         rays = int(g.last_times.rays)
