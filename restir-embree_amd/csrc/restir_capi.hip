@@ -96,6 +96,7 @@ struct rs_scene {
         S.wnodes = wide_on ? wide.nodes : nullptr; S.wtris = wide.tris; S.n_wnodes = wide_on ? wide.n_nodes : 0u;
         S.ebucket = d_ebucket;
         S.ecen = vec3{ecen[0], ecen[1], ecen[2]};
+        S.wtop = 0u; S.wtop_n = 0u;                    // set in a kernel that loads the LDS copy (wide_top_load)
         return S;
     }
     // the geometry of generation `g` if this scene still holds it (current, or the a_* copy of g == a_geo)
@@ -243,7 +244,7 @@ struct rs_context {
     size_t q_slots[kLanes] = {}, q_px[kLanes] = {}, q_waves[kLanes] = {};
     int q_A[kLanes] = {}, q_B[kLanes] = {};
     int cus = 256;
-    bool sort_on = true;                   // wave-sorted initial pass (RESTIR_SORT=off)
+    int sort_mode = RS_SPLIT_AUTO;         // wave-sorted initial pass (RESTIR_SORT=on|off; AUTO: per-lane walks)
     bool sort_spatial = true;              // wave-sorted spatial pass, CONSTANT MIS, k <= 8 (RESTIR_SORT_SPATIAL=off)
 };
 
@@ -405,8 +406,10 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         else if (!std::strcmp(t, "off")) c->queue_mode = RS_SPLIT_OFF;
         else if (!std::strcmp(t, "auto")) c->queue_mode = RS_SPLIT_AUTO;
     }
-    if (const char* t = std::getenv("RESTIR_SORT"))            // on (default) | off: wave-sorted initial pass
-        c->sort_on = std::string(t) != "off";
+    if (const char* t = std::getenv("RESTIR_SORT")) {          // auto (default) | on | off: wave-sorted initial pass
+        if (!std::strcmp(t, "on")) c->sort_mode = RS_SPLIT_ON;
+        else if (!std::strcmp(t, "off")) c->sort_mode = RS_SPLIT_OFF;
+    }
     if (const char* t = std::getenv("RESTIR_SORT_SPATIAL"))    // on (default) | off: wave-sorted spatial pass
         c->sort_spatial = std::string(t) != "off";
     if (const char* t = std::getenv("RESTIR_TILE_ORDER"))      // cost (default) | off (row-major)
@@ -1303,6 +1306,16 @@ static dim3 grid_rows(int W, int ya, int yb) { return dim3((W + 15) / 16, (yb - 
             default: kernel<TRAV_LOCKSTEP><<<(grid), (bs), 0, (st)>>>(__VA_ARGS__); break;                     \
         }                                                                                                  \
     } while (0)
+// the same with extra template bits X (a pass's own variant bits above the traversal kind's)
+#define LAUNCH_TRAV_X(c, X, kernel, grid, ...)                                                              \
+    do {                                                                                                   \
+        switch ((c)->trav | ((c)->twide ? TRAV_WIDE : 0)) {                                                \
+            case TRAV_LANE | TRAV_WIDE: kernel<TRAV_LANE | TRAV_WIDE | (X)><<<(grid), 256, 0, (c)->fs>>>(__VA_ARGS__); break; \
+            case TRAV_LANE: kernel<TRAV_LANE | (X)><<<(grid), 256, 0, (c)->fs>>>(__VA_ARGS__); break;                  \
+            case TRAV_WIDE: kernel<TRAV_LOCKSTEP | TRAV_WIDE | (X)><<<(grid), 256, 0, (c)->fs>>>(__VA_ARGS__); break;  \
+            default: kernel<TRAV_LOCKSTEP | (X)><<<(grid), 256, 0, (c)->fs>>>(__VA_ARGS__); break;                     \
+        }                                                                                                  \
+    } while (0)
 #define LAUNCH_TRAV_ON(c, st, kernel, grid, ...) LAUNCH_TRAV_BS_ON(c, st, kernel, grid, 256, __VA_ARGS__)
 #define LAUNCH_TRAV(c, kernel, grid, ...) LAUNCH_TRAV_ON(c, (c)->fs, kernel, grid, __VA_ARGS__)
 #define LAUNCH_TRAV_BS(c, kernel, grid, bs, ...) LAUNCH_TRAV_BS_ON(c, (c)->fs, kernel, grid, bs, __VA_ARGS__)
@@ -1426,6 +1439,13 @@ static CountSlot count_slot(rs_context* c, dim3 grid, int waves_per_block = 4) {
     return s;
 }
 // reserve slots for every launch of a frame: initial + visibility + temporal + P spatial + shade
+// the wave-sorted initial pass (rs_passes.h k_gbuffer_initial_sorted) for the per-lane walks: sorting a
+// tile's shadow rays by octant x light bucket cuts C3's initial pass 16.27 -> 15.25 ms; the lockstep walk
+// already shares one node stream per wave and loses to the sort's extra phases (C2: 1.31 -> 1.69 ms)
+static bool want_sorted(const rs_context* c, const rs_frame_params* P, const rs_scene* s) {
+    if (P->m_area <= 0 || s->n_emis >= (1u << 21) || c->sort_mode == RS_SPLIT_OFF) return false;
+    return c->sort_mode == RS_SPLIT_ON || c->trav == TRAV_LANE;
+}
 static dim3 grid_split(int W, int ya, int yb) { return dim3((W + 7) / 8, (yb - ya + 7) / 8); }
 // the initial pass runs candidate-split when asked, or (AUTO) when one thread per pixel would give the
 // launch too few rounds of the device's resident waves (a rank's band of a multi-GPU frame) and
@@ -1615,7 +1635,7 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
         HIPCHK(c, hipGetLastError());
         k_q_resolve<<<gb, 256, 0, c->fs>>>(S, F, c->G[gnew], Q, ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                                            count_slot(c, gb));
-    } else if (c->sort_on && P->m_area > 0 && s->n_emis < (1u << 21)) {
+    } else if (want_sorted(c, P, s)) {
         LAUNCH_TRAV(c, k_gbuffer_initial_sorted, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                     count_slot(c, gg));
     } else {
@@ -1682,8 +1702,12 @@ extern "C" int rs_tile_temporal(rs_context* c) {
         // held without one), this launch walks both binary trees (same hits, rs_scene.h)
         if (!S.wnodes || !Sp.wnodes) c->twide = false;
         if (c->F.debug_reproj) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 2 * npx, c->fs));
-        LAUNCH_TRAV(c, k_temporal, gb, S, Sp, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]},
-                    ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
+        if (partial)
+            LAUNCH_TRAV_X(c, TEMPORAL_BAND, k_temporal, gb, S, Sp, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]},
+                          ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
+        else
+            LAUNCH_TRAV(c, k_temporal, gb, S, Sp, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]},
+                        ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
         c->twide = twide;
         HIPCHK(c, hipGetLastError());
         if (c->F.debug_reproj) {

@@ -562,6 +562,8 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
                                                                             ResBuf Rw, float* fb, int fuse_shade,
                                                                             CountSlot C) {
     const uint64_t t0 = wave_clock();
+    __shared__ uint4 top_lds[kWideTopWords];
+    if constexpr (trav_wide(T) && kWideTop > 0) wide_top_load(S, top_lds);
     if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
     int x, y;
     uint32_t rays = 0;
@@ -672,6 +674,8 @@ template <int T>
 __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES_SORT_LOCKSTEP, RS_INITIAL_WAVES_SORT))
 k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int fuse_shade, CountSlot C) {
     const uint64_t t0 = wave_clock();
+    __shared__ uint4 top_lds[kWideTopWords];
+    if constexpr (trav_wide(T) && kWideTop > 0) wide_top_load(S, top_lds);
     if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
     __shared__ SortLds lds[4];
     SortLds& L = lds[threadIdx.x >> 6];
@@ -976,37 +980,61 @@ __device__ __forceinline__ bool reproject(const GCam& c, vec3 ws, int W, int H, 
     return true;
 }
 
+// k_temporal's per-thread state across its shadow walks: 20 words component-major (a wave's access to
+// one word is conflict-free), 20 KB per workgroup
+struct TemporalSlot {
+    static constexpr int kWords = 20;
+    float* base;
+    int t;
+    __device__ __forceinline__ void put(int c, float v) const { base[c * 256 + t] = v; }
+    __device__ __forceinline__ float get(int c) const { return base[c * 256 + t]; }
+    __device__ __forceinline__ void put3(int c, vec3 v) const { put(c, v.x); put(c + 1, v.y); put(c + 2, v.z); }
+    __device__ __forceinline__ vec3 get3(int c) const { return mk(get(c), get(c + 1), get(c + 2)); }
+};
+
 // temporalReusePass (pg/ReSTIRIntegrator.cpp:625-732).  The previous reservoir is read at the
 // CURRENT pixel (:641), the previous G-buffer at the reprojected pixel (:652).
+// T | TEMPORAL_BAND: the G-buffers hold only the tile's rows +- margin (a band of a multi-GPU frame, a
+// tile): the instantiation with the rare rebuilds below; a full-frame launch has none (their walks and the
+// state kept around them would otherwise cost every wave registers)
+constexpr int TEMPORAL_BAND = 4;
 template <int T>
 // Sp: the previous frame's geometry (== S unless the scene moved since; rs_scene::dev_of), traced when a tile
 // rebuilds a previous-frame G element beyond its rows
 __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORAL_WAVES_LANE)) k_temporal(DevScene S, DevScene Sp, FrameConst F, GBuf G, GBuf Gp, ResBuf Rr, ResBuf Rl,
                                                   ResBuf Rw, CountSlot C) {
+    constexpr bool kBand = (T & TEMPORAL_BAND) != 0;
     const uint64_t t0 = wave_clock();
+    __shared__ uint4 top_lds[kWideTopWords];
+    if constexpr (trav_wide(T) && kWideTop > 0) {
+        wide_top_load(S, top_lds);
+        Sp.wtop = S.wtop;
+        Sp.wtop_n = Sp.wnodes == S.wnodes ? S.wtop_n : 0u;        // the previous geometry's own tree: global only
+    }
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F, F.y0, F.y1, x, y);
     const size_t p = (size_t)y * F.W + x;
-    Res cr = Rr.load(p);
-    GElem cur = G.load(p);
+    const vec3 cpos = G.pos(p);
     int qx = x, qy = y, fx = x, fy = y;
-    bool ok = in && reproject(F.camp, cur.pos, F.W, F.H, qx, qy);
+    bool ok = in && reproject(F.camp, cpos, F.W, F.H, qx, qy);
     uint32_t dcode = (in && !ok) ? 1u : 0u;          // debugReprojection (pg/ReSTIRIntegrator.cpp:647-689)
     bool dfwd = false;
     // A tile holds the G-buffers of its rows +- margin only.  A reprojection beyond them (a miss
     // pixel's position is (0,0,0), which projects anywhere) rebuilds the element it needs from the
     // frame's camera -- gBufferFillPass is a function of (camera, pixel) -- so tiles stay bit-identical
     // to the full frame.  Rare (a few pixels per frame): counted in Counters::reproj_outside.
-    const bool q_out = ok && (qy < F.gy0 || qy >= F.gy1);
+    // Only positions live across these rebuilds' walks; the full elements are loaded after them (the
+    // previous one rebuilt once more for its lanes) so no G element is spilled around a walk.
+    const bool q_out = kBand && ok && (qy < F.gy0 || qy >= F.gy1);
     const size_t q = ok && !q_out ? (size_t)qy * F.W + qx : p;
-    GElem prev = Gp.load(q);
-    if (__ballot(q_out) != 0) {
+    vec3 ppos = Gp.pos(q);
+    if constexpr (kBand) if (__ballot(q_out) != 0) {
         const GElem alt = gbuffer_fill_cam<T>(Sp, F, F.camp, F.inv_view_prev, qx, qy, q_out);
-        if (q_out) { prev = alt; rays += 1u; atomicAdd(C.outside, 1ull); }
+        if (q_out) { ppos = alt.pos; rays += 1u; atomicAdd(C.outside, 1ull); }
     }
     if (ok) {
-        float cd = length(cur.pos - F.cam.pos), pd = length(prev.pos - F.camp.pos);
+        float cd = length(cpos - F.cam.pos), pd = length(ppos - F.camp.pos);
         float dr = cd > pd ? pd / cd : cd / pd;
         ok = !(dr < 0.9f);
         dcode = ok ? dcode : 2u;
@@ -1014,9 +1042,9 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
     vec3 pac = Gp.pos(p);
     const bool fok = ok && reproject(F.cam, pac, F.W, F.H, fx, fy);
     dcode = (ok && !fok) ? 3u : dcode;
-    const bool f_out = fok && (fy < F.gy0 || fy >= F.gy1);
+    const bool f_out = kBand && fok && (fy < F.gy0 || fy >= F.gy1);
     vec3 fw = G.pos(fok && !f_out ? (size_t)fy * F.W + fx : p);
-    if (__ballot(f_out) != 0) {
+    if constexpr (kBand) if (__ballot(f_out) != 0) {
         const GElem alt = gbuffer_fill_cam<T>(S, F, F.cam, F.inv_view, fx, fy, f_out);
         if (f_out) { fw = alt.pos; rays += 1u; atomicAdd(C.outside, 1ull); }
     }
@@ -1034,19 +1062,58 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
         if (dcode) F.dbg[p] = (uint8_t)dcode;
         if (dfwd) F.dbg[n + (size_t)fy * F.W + fx] = 1u;
     }
+    const bool any_ok = __ballot(ok) != 0;
+    float ph[4];
+    __shared__ float temporal_lds[TemporalSlot::kWords * 256];
+    const TemporalSlot ts{temporal_lds, (int)threadIdx.x};
+    if (any_ok) {
+        const GElem cur = G.load(p);
+        GElem prev = Gp.load(q);
+        if constexpr (kBand) if (__ballot(q_out && ok) != 0) {            // the rebuilt element again (its ray counted above)
+            const GElem alt = gbuffer_fill_cam<T>(Sp, F, F.camp, F.inv_view_prev, qx, qy, q_out && ok);
+            if (q_out) prev = alt;
+        }
+        // the four evaluateF calls (:700-717: the current and previous samples at the current and previous
+        // surfaces).  Their unoccluded f are evaluated first; what the shadow walks need afterwards -- the two
+        // origins and two targets, |L| and |L * 0| (the post-visibility lengths bit for bit, evaluate_f_post)
+        // -- goes to this thread's LDS slots (TemporalSlot), the need bits stay in a register, and the
+        // reservoirs are re-read after the walks (L2-resident), so the walks run with the whole register
+        // budget and nothing is spilled around them (r03: 219 scratch ops, the walk loops spill-free)
+        const Sample cs = smp_of(Rr.load(p)), ps = smp_of(Rl.load(p));
+        uint32_t nd = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const FPre e = evaluate_f_pre(F, k < 2 ? cs : ps, (k & 1) ? F.camp.pos : F.cam.pos, (k & 1) ? prev : cur,
+                                          true, ok);
+            ts.put(12 + k, e.ok ? length(e.L) : 0.0f);
+            ts.put(16 + k, e.ok ? length(e.L * 0.0f) : 0.0f);
+            nd |= e.need ? 1u << k : 0u;
+            rays += e.need ? 1u : 0u;
+        }
+        ts.put3(0, cur.pos); ts.put3(3, prev.pos); ts.put3(6, cs.p); ts.put3(9, ps.p);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            asm volatile("" ::: "memory");
+            const vec3 o = ts.get3(3 * (k & 1)), ld = ts.get3(6 + 3 * (k >> 1)) - o;   // evaluate_f_pre's ray
+            const bool need = (nd >> k) & 1u;
+            const bool oc = trace_any<T>(S, need, o, normalize(ld), FLT_MIN + F.tnear_off, sqrtf(dot(ld, ld)) - F.tfar_off);
+            asm volatile("" ::: "memory");
+            ph[k] = need && oc ? ts.get(16 + k) : ts.get(12 + k);
+        }
+    }
+    asm volatile("" ::: "memory");                      // re-read the reservoirs: nothing carried across the walks
+    const Res cr = Rr.load(p);
     Res out = cr;
-    if (__ballot(ok) != 0) {
-        Res pr = Rl.load(p);
+    if (any_ok) {
+        const Res pr = Rl.load(p);
         Rng rng; rng.init(F.seed, F.frame, PASS_TEMPORAL, (uint32_t)p);
         Res res = res_empty();
-        Sample cs = smp_of(cr), ps = smp_of(pr);
-        float p_cur = length(evaluate_f<T>(S, F, cs, F.cam.pos, cur, true, ok, rays));
-        float p_prev = length(evaluate_f<T>(S, F, cs, F.camp.pos, prev, true, ok, rays));
+        const Sample cs = smp_of(cr), ps = smp_of(pr);
+        const float p_cur = ph[0], p_prev = ph[1];
         float m_cur = p_cur * (float)cr.conf / (p_cur * (float)cr.conf + p_prev * (float)pr.conf);
         if (!(m_cur > 0)) m_cur = 0.0f;
         float ph_cur = p_cur;
-        float p_cur2 = length(evaluate_f<T>(S, F, ps, F.cam.pos, cur, true, ok, rays));
-        float p_prev2 = length(evaluate_f<T>(S, F, ps, F.camp.pos, prev, true, ok, rays));
+        const float p_cur2 = ph[2], p_prev2 = ph[3];
         if (ok) {
             bool took_cur = res_add(res, cs, m_cur * ph_cur * cr.W, cr.conf, rng);
             float m_prev = p_prev2 * (float)pr.conf / (p_cur2 * (float)cr.conf + p_prev2 * (float)pr.conf);

@@ -1,16 +1,21 @@
 #!/bin/bash
-# build_variant.sh NAME "EXTRA HIPCC FLAGS": librestir_amd built with the Makefile's flags plus extra -D flags
-# into _variants/NAME.so (A/B runs load it through RESTIR_LIB)
+# A/B builds of librestir_amd.so with changed compile-time switches (analysis tooling):
+#   scripts/build_variant.sh NAME "-DRS_X=1 -DRS_Y=2"   -> restir-embree_amd/_ab/lib_NAME.so
+# A -DNAME=v given here replaces the Makefile's own -DNAME=...; run with RESTIR_LIB=restir-embree_amd/_ab/lib_NAME.so.
 set -e
 cd "$(dirname "$0")/../restir-embree_amd"
-mkdir -p _variants/$1
-# the Makefile's HIPFLAGS (later -D flags override earlier ones)
-BASE=$(sed -n '/^HIPFLAGS ?=/,/^[^ ]/p' Makefile | sed 's/^HIPFLAGS ?=//; s/\\$//' | tr '\n' ' ' | sed 's/CSRC.*//; s/$(ARCH)/gfx950/')
-F="$BASE $2"
-/opt/rocm/bin/hipcc $F -c csrc/restir_capi.hip -o _variants/$1/capi.o
-/opt/rocm/bin/hipcc $F -c csrc/rs_bvh_build.hip -o _variants/$1/bvh.o
-/opt/rocm/bin/hipcc $F -c csrc/rs_mgpu.hip -o _variants/$1/mgpu.o
-/opt/rocm/bin/hipcc $F -c csrc/rs_denoise.hip -o _variants/$1/denoise.o
-/opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -c csrc/rs_obj_loader.cpp -o _variants/$1/obj.o
-/opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -ffp-contract=off -c csrc/rs_image.cpp -o _variants/$1/image.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o _variants/$1.so _variants/$1/*.o -lz -lrccl
+name=$1; shift
+flags=$(python3 - "$*" <<'PY'
+import re, sys
+mk = open("Makefile").read()
+f = re.search(r"HIPFLAGS \?=(.*?)\n(?!\s)", mk, re.S).group(1).replace("\\\n", " ").replace("$(ARCH)", "gfx950").split()
+extra = sys.argv[1].split()
+names = {e.split("=")[0] for e in extra}
+print(" ".join([x for x in f if x.split("=")[0] not in names] + extra))
+PY
+)
+mkdir -p _ab "_build_$name"
+cp -p _build/*.o "_build_$name/"
+rm -f "_build_$name/restir_capi.o"
+make -s OBJ="_build_$name" LIB="_ab/lib_$name.so" HIPFLAGS="$flags" "_ab/lib_$name.so"
+echo "built _ab/lib_$name.so: $flags"

@@ -720,13 +720,28 @@ int main(int argc, char** argv) {
         std::uniform_real_distribution<float> U(0.0f, 1.0f);
         double it_p = 0, it_s = 0, tr_s = 0, it_b = 0, tr_p = 0, tr_b = 0; long lost = 0, ns = 0, nb = 0, mism = 0; int maxsp = 0;
         std::vector<int> wave_it(((W / 8) * (H / 8)), 0);
+        // LEVELS: node fetches per breadth-first level (what an LDS copy of the top levels would serve)
+        const size_t NN = WN.size() / 20;
+        std::vector<int> lvl_of(NN, 0);
+        for (size_t j = 0; j < NN; ++j) {
+            const uint32_t ni = (WN[20 * j + 3] >> 24) & 0xfu;
+            for (uint32_t i = 0; i < ni; ++i) lvl_of[WN[20 * j + 4] + i] = lvl_of[j] + 1;
+        }
+        std::vector<double> lv_hist[3];
+        for (auto& h : lv_hist) h.assign(32, 0.0);
+        std::vector<size_t> lv_nodes(32, 0);
+        for (size_t j = 0; j < NN; ++j) lv_nodes[lvl_of[j]]++;
+        std::vector<uint32_t> lseq;
+        auto lv_add = [&](int k) { for (uint32_t v : lseq) lv_hist[k][lvl_of[v]] += 1; lseq.clear(); };
+        const bool levels = getenv("LEVELS") != nullptr;
         for (int y = 0; y < H; ++y)
             for (int x = 0; x < W; ++x) {
                 V3 dc{(float)x - W / 2.0f, H / 2.0f - (float)y, -focal};
                 V3 d = xc * dc.x + yc * dc.y + zc * dc.z;
                 d = d * (1.0f / std::sqrt(dot(d, d)));
                 Ray pr_{eye, d, 0.01f, 3.0e38f, true};
-                WEmu a = emu_walk(WN, pr, pr_, false, 8);
+                WEmu a = emu_walk(WN, pr, pr_, false, 8, levels ? &lseq : nullptr);
+                lv_add(0);
                 Trace ref = walk(Fr, pr_, false);
                 mism += a.prim != ref.prim;
                 it_p += a.iters; tr_p += a.tris;
@@ -743,7 +758,8 @@ int main(int argc, char** argv) {
                     float u1 = U(rng), u2 = U(rng), rr = std::sqrt(u1), ph = 6.2831853f * u2;
                     V3 bd = t1 * (rr * std::cos(ph)) + t2 * (rr * std::sin(ph)) + nn * std::sqrt(std::max(0.0f, 1 - u1));
                     Ray br{o, bd, 0.01f, 3.0e38f, true};
-                    WEmu c = emu_walk(WN, pr, br, false, 8);
+                    WEmu c = emu_walk(WN, pr, br, false, 8, levels ? &lseq : nullptr);
+                    lv_add(1);
                     Trace rb = walk(Fr, br, false);
                     mism += c.prim != rb.prim;
                     it_b += c.iters; tr_b += c.tris; ++nb;
@@ -756,12 +772,27 @@ int main(int argc, char** argv) {
                 float dist = std::sqrt(dot(sd, sd));
                 sd = sd * (1.0f / std::max(dist, 1e-20f));
                 Ray sh{o, sd, 0.01f, dist - 0.001f, true};
-                WEmu b = emu_walk(WN, pr, sh, true, 8);
+                WEmu b = emu_walk(WN, pr, sh, true, 8, levels ? &lseq : nullptr);
+                lv_add(2);
                 Trace rs_ = walk(Fr, sh, true);
                 mism += b.occ != (int)rs_.occ;
                 it_s += b.iters; tr_s += b.tris; lost += b.lost; ++ns; maxsp = std::max(maxsp, b.maxsp);
                 if (y / 8 < H / 8 && x / 8 < W / 8) { int& wv = wave_it[(y / 8) * (W / 8) + x / 8]; wv = std::max(wv, b.iters); }
             }
+        if (levels) {
+            const char* nm[3] = {"primary", "bounce", "shadow"};
+            for (int k = 0; k < 3; ++k) {
+                double tot = 0, cum = 0, bytes = 0;
+                for (double v : lv_hist[k]) tot += v;
+                printf("levels %-8s fetches/ray by level (cumulative share, nodes up to it, KB):", nm[k]);
+                size_t nodes = 0;
+                for (int l = 0; l < 8 && lv_hist[k][l] > 0; ++l) {
+                    cum += lv_hist[k][l]; nodes += lv_nodes[l]; bytes = nodes * 80.0;
+                    printf(" L%d %.0f%% (%zu, %.1f)", l, 100.0 * cum / tot, nodes, bytes / 1024.0);
+                }
+                printf("  [%.2f fetches/ray]\n", tot / (k == 0 ? (double)W * H : (k == 1 ? (double)nb : (double)ns)));
+            }
+        }
         if (getenv("COHERENCE")) {
             // per 16x16 workgroup and candidate: 256 shadow rays (pixel -> random emitter point) walked by
             // 4 waves of 64.  Per wave: lockstep steps (its longest walk) and the node fetches the vector

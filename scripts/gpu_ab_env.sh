@@ -12,8 +12,9 @@ fi
 for sc in ${SCENES:-C2 C3}; do
   for v in ${VARIANTS:-base}; do
     envs=""; [ "$v" != base ] && envs=$(echo $v | tr ',' ' ')
-    env $envs timeout -k 10 300 python bench.py --scene $sc --no-cpu-baseline --no-extras --steps ${STEPS:-20} --full-out gpurun_out/ab_${sc}_$v.full.json > gpurun_out/ab_${sc}_$v.json 2> gpurun_out/ab_${sc}_$v.err || { echo "bench $sc $v failed"; tail -5 gpurun_out/ab_${sc}_$v.err; exit 1; }
-    python - gpurun_out/ab_${sc}_$v.full.json "$sc $v" <<'PY'
+    tag=$(echo "$v" | tr '/,=' '_~-')
+    env $envs timeout -k 10 300 python bench.py --scene $sc --no-cpu-baseline --no-extras --steps ${STEPS:-20} --full-out gpurun_out/ab_${sc}_$tag.full.json > gpurun_out/ab_${sc}_$tag.json 2> gpurun_out/ab_${sc}_$tag.err || { echo "bench $sc $v failed"; tail -5 gpurun_out/ab_${sc}_$tag.err; exit 1; }
+    python - gpurun_out/ab_${sc}_$tag.full.json "$sc $v" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
 p = d.get("pass_ms_one_frame_in_flight") or {}
