@@ -96,7 +96,6 @@ struct rs_scene {
         S.wnodes = wide_on ? wide.nodes : nullptr; S.wtris = wide.tris; S.n_wnodes = wide_on ? wide.n_nodes : 0u;
         S.ebucket = d_ebucket;
         S.ecen = vec3{ecen[0], ecen[1], ecen[2]};
-        S.wtop = 0u; S.wtop_n = 0u;                    // set in a kernel that loads the LDS copy (wide_top_load)
         return S;
     }
     // the geometry of generation `g` if this scene still holds it (current, or the a_* copy of g == a_geo)

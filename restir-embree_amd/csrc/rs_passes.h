@@ -562,8 +562,6 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
                                                                             ResBuf Rw, float* fb, int fuse_shade,
                                                                             CountSlot C) {
     const uint64_t t0 = wave_clock();
-    __shared__ uint4 top_lds[kWideTopWords];
-    if constexpr (trav_wide(T) && kWideTop > 0) wide_top_load(S, top_lds);
     if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
     int x, y;
     uint32_t rays = 0;
@@ -674,8 +672,6 @@ template <int T>
 __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES_SORT_LOCKSTEP, RS_INITIAL_WAVES_SORT))
 k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int fuse_shade, CountSlot C) {
     const uint64_t t0 = wave_clock();
-    __shared__ uint4 top_lds[kWideTopWords];
-    if constexpr (trav_wide(T) && kWideTop > 0) wide_top_load(S, top_lds);
     if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
     __shared__ SortLds lds[4];
     SortLds& L = lds[threadIdx.x >> 6];
@@ -1005,12 +1001,6 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
                                                   ResBuf Rw, CountSlot C) {
     constexpr bool kBand = (T & TEMPORAL_BAND) != 0;
     const uint64_t t0 = wave_clock();
-    __shared__ uint4 top_lds[kWideTopWords];
-    if constexpr (trav_wide(T) && kWideTop > 0) {
-        wide_top_load(S, top_lds);
-        Sp.wtop = S.wtop;
-        Sp.wtop_n = Sp.wnodes == S.wnodes ? S.wtop_n : 0u;        // the previous geometry's own tree: global only
-    }
     int x, y;
     uint32_t rays = 0;
     const bool in = pixel_of(F, F.y0, F.y1, x, y);
@@ -1420,7 +1410,7 @@ k_spatial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pas
         const int cnt = M, kk = F.k + 1;
         const float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
         auto list_q = [&](int i) -> size_t { return (i == 0 || i >= M) ? p : (size_t)nbr[(i - 1) * 256 + threadIdx.x]; };
-        const ShadeFrame sf = make_frame(th, cam);
+        ShadeFrame sf = make_frame(th, cam);
         // ---- A: every list entry's ray need and bucket rank (lane = pixel)
         L.cur[lane] = 0u;
         L.occ[lane] = 0u;
@@ -1473,7 +1463,11 @@ k_spatial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pas
             if (act && occ) atomicOr(&L.occ[src], 1u << i);
         }
         wave_lds_sync();
-        // ---- C: the reservoir stream in list order (lane = pixel)
+        // ---- C: the reservoir stream in list order (lane = pixel).  The pixel's G element and frame are
+        // re-read / re-derived here rather than carried across B's walks (they would be spilled around them)
+        asm volatile("" ::: "memory");
+        th = G.load(p);
+        sf = make_frame(th, cam);
         const uint32_t occm = L.occ[lane];
         Res res = res_empty();
         vec3 f_sel = mk(0, 0, 0);

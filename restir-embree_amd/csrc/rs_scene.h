@@ -44,9 +44,6 @@ struct DevScene {
     // the wave-sorted initial pass groups its shadow rays by (rs_passes.h k_gbuffer_initial_sorted)
     const uint8_t* ebucket;
     vec3 ecen;                // centre of the emitters' centroid bounds (the sorted spatial pass's target cells)
-    // nodes [0, wtop_n) of this tree are served from the workgroup's LDS copy at LDS byte address wtop
-    // (wide_top_load); 0 from the host -- only a kernel that loaded the copy for this very tree sets it
-    uint32_t wtop, wtop_n;
 };
 constexpr int kCdfGuide = 1024;
 
@@ -303,27 +300,6 @@ __device__ __forceinline__ uint32_t wide_hits(uint4 w0, uint4 w1, uint4 w2, uint
     const uint32_t nv = w0.w >> 28;
     return hits & ((1u << nv) - 1u);
 }
-// The first kWideTop nodes of the 8-wide tree (breadth-first: its top three levels, 73 nodes = 5.8 KB) in
-// LDS, one copy per workgroup: they take 45 % of a C3 shadow ray's node fetches (scripts/bvh_lab.cpp
-// LEVELS: root 8 %, level 1 17 %, level 2 20 %), which then leave the texture path (TA/TD) the per-lane
-// walks are bound by.  A kernel calls wide_top_load on the scene it walks, with every thread of the
-// workgroup, before its first walk; walks of any other tree (S.wtop_n = 0) read global memory only.
-#ifndef RS_WIDE_TOP
-#define RS_WIDE_TOP 73
-#endif
-constexpr int kWideTop = RS_WIDE_TOP;
-constexpr int kWideTopWords = 5 * (kWideTop > 0 ? kWideTop : 1);   // a kernel's __shared__ uint4 array
-__device__ __forceinline__ void wide_top_load(DevScene& S, uint4* lds) {
-    const uint32_t n = S.wnodes ? (S.n_wnodes < (uint32_t)kWideTop ? S.n_wnodes : (uint32_t)kWideTop) : 0u;
-    const uint32_t nt = blockDim.x * blockDim.y;
-    for (uint32_t i = threadIdx.y * blockDim.x + threadIdx.x; i < 5u * n; i += nt) lds[i] = S.wnodes[i];
-    __syncthreads();
-    S.wtop = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)lds;
-    S.wtop_n = n;
-}
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(3))) u32x4_t lds_u32x4;
-__device__ __forceinline__ uint4 lds_u4(lds_u32x4* p) { const u32x4_t v = *p; return make_uint4(v.x, v.y, v.z, v.w); }
 // Stats (rs_debug_trace only): *stats = node fetches << 16 | triangle tests of this lane's walk
 template <bool Any, bool Stats = false, bool NoTri = false>
 __device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o, vec3 d, vec3 inv, float tnear,
@@ -339,14 +315,8 @@ __device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o
         const uint32_t node = live ? gb + slot : 0u;
         const uint32_t rest = gm & (gm - 1u);
         st.push(live & (rest != 0u), (gb << 8) | rest);
-        uint4 w0, w1, w2, w3, w4;
-        if (node < S.wtop_n) {
-            lds_u32x4* P = (lds_u32x4*)(uintptr_t)S.wtop + 5 * node;     // ds_read_b128
-            w0 = lds_u4(P); w1 = lds_u4(P + 1); w2 = lds_u4(P + 2); w3 = lds_u4(P + 3); w4 = lds_u4(P + 4);
-        } else {
-            const uint4* P = S.wnodes + 5 * (size_t)node;
-            w0 = P[0]; w1 = P[1]; w2 = P[2]; w3 = P[3]; w4 = P[4];
-        }
+        const uint4* P = S.wnodes + 5 * (size_t)node;
+        const uint4 w0 = P[0], w1 = P[1], w2 = P[2], w3 = P[3], w4 = P[4];
         const float tf = Any ? tfar : h.t;
         uint32_t hits = live ? wide_hits(w0, w1, w2, w3, w4, o, inv, tnear, tf) : 0u;
         const uint32_t ni = (w0.w >> 24) & 0xfu;

@@ -1,6 +1,6 @@
-"""Diagnostic: k_gbuffer_initial time on C2 1080p under parameter variations, to split its cost into
+"""Diagnostic: the initial pass's time at 1080p under parameter variations, to split its cost into
 primary ray / area sampling / shadow rays / BRDF ray.  Not a parity test; prints one line per config.
-Usage (GPU box): python scripts/initial_breakdown.py [--frames N]   (RESTIR_LIB selects a variant .so)"""
+Usage (GPU box): python scripts/initial_breakdown.py [--scene C2|C3] [--frames N]   (RESTIR_LIB selects a variant .so)"""
 import argparse
 import os
 import sys
@@ -15,14 +15,16 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--only", type=int, default=-1, help="run only config #N")
+    ap.add_argument("--scene", default="C2")
     a = ap.parse_args()
     import torch
     from restir_amd import Renderer, scenes
-    from restir_amd.params import metric_params
+    from restir_amd.params import metric_params, c3_params
 
     torch.cuda.set_stream(torch.cuda.Stream())
     r = Renderer(a.width, a.height, device=0, stream=torch.cuda.current_stream().cuda_stream)
-    sc = scenes.cornell_many_lights(1024)
+    sc = scenes.sponza_like() if a.scene == "C3" else scenes.cornell_many_lights(1024)
+    base = c3_params if a.scene == "C3" else metric_params
     gs = r.load_scene(sc)
     cfgs = [
         ("A32 B1 (metric)", {}),
@@ -38,7 +40,7 @@ def main():
     for i, (name, kw) in enumerate(cfgs):
         if a.only >= 0 and i != a.only:
             continue
-        prm = metric_params(**kw)
+        prm = base(**kw)
         for f in range(3):
             r.produce_restir(gs, sc.camera, prm, f, copy_out=False, timed=True)
         tot, rays = 0.0, 0
@@ -46,7 +48,7 @@ def main():
             r.produce_restir(gs, sc.camera, prm, 3 + f, copy_out=False, timed=True)
             tot += r.last_times.gbuffer_initial_ms
             rays += int(r.last_times.rays)
-        print(f"{lib:>10s} {name:48s} gbuffer_initial_ms={tot / a.frames:.3f} rays/frame={rays // a.frames}",
+        print(f"{a.scene} {lib:>10s} {name:48s} gbuffer_initial_ms={tot / a.frames:.3f} rays/frame={rays // a.frames}",
               flush=True)
 
 
