@@ -668,6 +668,21 @@ __device__ __forceinline__ AreaCand area_cand(const DevScene& S, const FrameCons
     return a;
 }
 
+// the sorted kernel's reservoir state around its BRDF candidates' walks: 14 words per lane in the wave's
+// slot[] region (word c at c * 64 + lane: conflict-free)
+static_assert(kSortChunk >= 14, "brdf_park needs 14 slot words per lane");
+__device__ __forceinline__ void brdf_park(uint32_t* sl, int lane, const Res& r, float bp, vec3 fs) {
+    const float v[14] = {r.p.x, r.p.y, r.p.z, r.n.x, r.n.y, r.n.z, r.li.x, r.li.y, r.li.z, r.wsum, bp, fs.x, fs.y, fs.z};
+#pragma unroll
+    for (int c = 0; c < 14; ++c) sl[c * 64 + lane] = __float_as_uint(v[c]);
+}
+__device__ __forceinline__ void brdf_unpark(const uint32_t* sl, int lane, Res& r, float& bp, vec3& fs) {
+    float v[14];
+#pragma unroll
+    for (int c = 0; c < 14; ++c) v[c] = __uint_as_float(sl[c * 64 + lane]);
+    r.p = mk(v[0], v[1], v[2]); r.n = mk(v[3], v[4], v[5]); r.li = mk(v[6], v[7], v[8]); r.wsum = v[9];
+    bp = v[10]; fs = mk(v[11], v[12], v[13]);
+}
 template <int T>
 __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES_SORT_LOCKSTEP, RS_INITIAL_WAVES_SORT))
 k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int fuse_shade, CountSlot C) {
@@ -783,14 +798,27 @@ k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb,
             }
         }
         if (F.m_brdf > 0) {
-            const GElem g = G.load(p);
-            const ShadeFrame sf = make_frame(g, cam);
+            // the BRDF candidates' two walks (closest hit, then the shadow ray) run with the reservoir state
+            // parked in this wave's LDS (slot[] is free after the area chunks) and the pixel's G element
+            // re-read around them, so only the sample in flight is live across a walk
             const float inv_mb = 1.0f / (float)F.m_brdf;
             for (int i = 0; i < F.m_brdf; ++i) {
+                brdf_park(L.slot, lane, r, best_phat, f_sel);
                 float Wc, mis;
                 rng.n = cand_slot(F.m_area + i);
-                Sample s = brdf_sample<T>(S, F, g.pos, sf, alive, rng, Wc, mis, rays);
-                vec3 f = evaluate_f<T>(S, F, s, g.pos, false, sf, tv, alive, rays);
+                Sample s;
+                {
+                    const GElem g = G.load(p);
+                    s = brdf_sample<T>(S, F, g.pos, make_frame(g, cam), alive, rng, Wc, mis, rays);
+                }
+                asm volatile("" ::: "memory");
+                vec3 f;
+                {
+                    const GElem g = G.load(p);
+                    f = evaluate_f<T>(S, F, s, g.pos, false, make_frame(g, cam), tv, alive, rays);
+                }
+                asm volatile("" ::: "memory");
+                brdf_unpark(L.slot, lane, r, best_phat, f_sel);
                 float ph = length(f);
                 float w = F.m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
                 rng.n = cand_slot(F.m_area + i) + 3u;
@@ -1408,7 +1436,6 @@ k_spatial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pas
         }
         rng.n = 2u * (uint32_t)F.k;
         const int cnt = M, kk = F.k + 1;
-        const float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
         auto list_q = [&](int i) -> size_t { return (i == 0 || i >= M) ? p : (size_t)nbr[(i - 1) * 256 + threadIdx.x]; };
         ShadeFrame sf = make_frame(th, cam);
         // ---- A: every list entry's ray need and bucket rank (lane = pixel)
@@ -1469,6 +1496,7 @@ k_spatial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pas
         th = G.load(p);
         sf = make_frame(th, cam);
         const uint32_t occm = L.occ[lane];
+        const float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
         Res res = res_empty();
         vec3 f_sel = mk(0, 0, 0);
         for (int i = 0; i < kk; ++i) {

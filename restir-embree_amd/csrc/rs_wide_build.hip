@@ -1,7 +1,7 @@
 // rs_wide_build.hip -- the 8-wide tree of the per-lane walks, built on the GPU (replaces, with the PLOC tree of
 // rs_bvh_build.hip, Embree's rtcCommitScene, pg/Scene.cpp:15).  It is the host restatement in rs_wide.h
 // (build_sah_host + SahCollapse + build_wide_host, collapse 1) run as data-parallel kernels, and produces the
-// same tree word for word (tests/test_gpu_parity.py::test_wide_tree_gpu_equals_host):
+// same tree word for word (tests/test_gpu_wide.py::test_wide_tree_gpu_equals_host):
 //
 //   1 k_tri_prep      triangle boxes and centroids (the host's float operations), the identity permutation,
 //                     a non-finite flag (no wide tree for non-finite geometry: the walks take the skip pointers)
