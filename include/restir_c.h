@@ -259,14 +259,16 @@ int rs_context_get_traversal(const rs_context* ctx, const rs_scene* scene, int* 
 int rs_context_set_initial_split(rs_context* ctx, int mode);
 /* mode: the requested mode; last: whether the last frame's initial pass ran split (0/1) */
 int rs_context_get_initial_split(const rs_context* ctx, int* mode, int* last);
-/* Frame pipelining (no reference counterpart): with depth D (0..2, default 2; env RESTIR_RUNAHEAD=D at
- * context creation) frames rotate over D+1 internal streams, so a frame's G-buffer + initial pass
+/* Frame pipelining (no reference counterpart): with depth D (0..rs_max_run_ahead(), default the maximum;
+ * env RESTIR_RUNAHEAD=D at context creation) frames rotate over D+1 internal streams, so a frame's G-buffer + initial pass
  * (which reads nothing of earlier frames) runs while up to D earlier frames still run their later
  * passes; only the temporal pass waits for the previous frame.  The context's stream waits for every
  * frame, so its semantics are unchanged; a frame's framebuffer pointer (rs_tile_finish,
  * rs_get_frame_device_ptr) stays valid for D+1 frames.  Work enqueued on the context's stream between
  * frames (geometry updates) is waited for by the next frame.  Frames are bit-identical for every D. */
 int rs_context_set_run_ahead(rs_context* ctx, int depth);
+/* the largest run-ahead depth this build supports (the default depth) */
+int rs_max_run_ahead(void);
 /* Framebuffer ring (no reference counterpart): n = 1 (default, one frame_data buffer, like
  * pg/simpleguidx11.h:152) or 2 -- consecutive frames alternate between two buffers, so a consumer
  * (the multi-GPU gather, an async copy) may still read frame f while frame f+1 renders. */

@@ -124,7 +124,7 @@ enum { EV_BEGIN, EV_INIT, EV_VIS, EV_TEMPORAL, EV_SPATIAL, EV_SHADE, EV_DONE, EV
 // its semantics are those of a sequential renderer.  D = 0 runs everything on the context's stream.
 // Work enqueued on the context's stream between frames (geometry updates, MIS frames, sky changes)
 // makes the next frame's lane wait for it.
-constexpr int kMaxAhead = 2, kLanes = kMaxAhead + 1, kGRing = kMaxAhead + 2, kRRing = 3 * kMaxAhead + 2;
+constexpr int kMaxAhead = RS_MAX_AHEAD, kLanes = kMaxAhead + 1, kGRing = kMaxAhead + 2, kRRing = 3 * kMaxAhead + 2;
 struct rs_context {
     int device = 0, W = 0, H = 0;
     hipStream_t stream = nullptr;
@@ -441,12 +441,13 @@ extern "C" int rs_context_set_initial_split(rs_context* c, int mode) {
     c->split_mode = mode;
     return RS_OK;
 }
+extern "C" int rs_max_run_ahead(void) { return kMaxAhead; }
 extern "C" int rs_context_set_run_ahead(rs_context* c, int depth) {
     if (!c) return fail(nullptr, RS_E_INVALID, "rs_context_set_run_ahead: null context");
     if (c->active) return fail(c, RS_E_INVALID, "rs_context_set_run_ahead: a frame is in flight");
     HIPCHK(c, enter(c));
     sync_all(c);                                 // frames in flight keep the buffers of the old depth
-    if (depth < 0 || depth > kMaxAhead) return fail(c, RS_E_INVALID, "rs_context_set_run_ahead: depth must be 0..2");
+    if (depth < 0 || depth > kMaxAhead) return fail(c, RS_E_INVALID, "rs_context_set_run_ahead: depth must be 0.." + std::to_string(kMaxAhead));
     c->ahead = depth;
     c->join_next = true;
     return RS_OK;

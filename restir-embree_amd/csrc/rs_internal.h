@@ -7,6 +7,12 @@
 struct rs_context;
 struct rs_denoiser;
 
+// run-ahead: the deepest frame pipeline a context supports (restir_capi.hip kMaxAhead; frames in flight =
+// depth + 1 lanes, each with its own stream, framebuffer and -- in rs_mgpu.hip -- communicator)
+#ifndef RS_MAX_AHEAD
+#define RS_MAX_AHEAD 2
+#endif
+
 namespace rs {
 // the context's own stream (ordered after every frame enqueued so far)
 __attribute__((visibility("hidden"))) hipStream_t ctx_stream(rs_context* c);

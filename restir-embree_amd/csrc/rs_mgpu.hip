@@ -26,7 +26,7 @@ using namespace rs;
 
 namespace {
 
-constexpr int kLanes = 3;   // run-ahead lanes of a context (restir_capi.hip kMaxAhead + 1)
+constexpr int kLanes = RS_MAX_AHEAD + 1;   // run-ahead lanes of a context (restir_capi.hip kMaxAhead + 1)
 
 // one rank's tile stages on its context (the interface rs::mgpu::render_frame drives)
 struct GpuRank {

@@ -670,7 +670,10 @@ __device__ __forceinline__ AreaCand area_cand(const DevScene& S, const FrameCons
 
 // the sorted kernel's reservoir state around its BRDF candidates' walks: 14 words per lane in the wave's
 // slot[] region (word c at c * 64 + lane: conflict-free)
-static_assert(kSortChunk >= 14, "brdf_park needs 14 slot words per lane");
+#ifndef RS_SORT_PARK
+#define RS_SORT_PARK 1
+#endif
+static_assert(kSortChunk >= 14 || !RS_SORT_PARK, "brdf_park needs 14 slot words per lane");
 __device__ __forceinline__ void brdf_park(uint32_t* sl, int lane, const Res& r, float bp, vec3 fs) {
     const float v[14] = {r.p.x, r.p.y, r.p.z, r.n.x, r.n.y, r.n.z, r.li.x, r.li.y, r.li.z, r.wsum, bp, fs.x, fs.y, fs.z};
 #pragma unroll
@@ -803,7 +806,7 @@ k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb,
             // re-read around them, so only the sample in flight is live across a walk
             const float inv_mb = 1.0f / (float)F.m_brdf;
             for (int i = 0; i < F.m_brdf; ++i) {
-                brdf_park(L.slot, lane, r, best_phat, f_sel);
+                if (RS_SORT_PARK) brdf_park(L.slot, lane, r, best_phat, f_sel);
                 float Wc, mis;
                 rng.n = cand_slot(F.m_area + i);
                 Sample s;
@@ -818,7 +821,7 @@ k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb,
                     f = evaluate_f<T>(S, F, s, g.pos, false, make_frame(g, cam), tv, alive, rays);
                 }
                 asm volatile("" ::: "memory");
-                brdf_unpark(L.slot, lane, r, best_phat, f_sel);
+                if (RS_SORT_PARK) brdf_unpark(L.slot, lane, r, best_phat, f_sel);
                 float ph = length(f);
                 float w = F.m_area > 0 ? mis * ph * Wc : inv_mb * ph * Wc;
                 rng.n = cand_slot(F.m_area + i) + 3u;

@@ -173,7 +173,10 @@ def balanced_bands(costs, world: int, min_rows: int = 1):
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
 
-LANES = 3   # run-ahead lanes of a context (kMaxAhead + 1 in restir_capi.hip)
+def run_ahead_lanes() -> int:
+    """Run-ahead lanes of a context: rs_max_run_ahead() + 1 (the library's build constant)."""
+    from .renderer import load_library
+    return int(load_library().rs_max_run_ahead()) + 1
 
 
 class TiledRenderer:
@@ -185,11 +188,12 @@ class TiledRenderer:
         self.group = group
         # one process group per run-ahead lane: frames in flight on different lanes exchange halos and
         # gather through independent communicators (one group's collectives run in issue order)
-        self.lane_groups = [group] * LANES
+        lanes = run_ahead_lanes()
+        self.lane_groups = [group] * lanes
         if world > 1:
             import torch.distributed as dist
             ranks = list(range(world)) if group is None else dist.get_process_group_ranks(group)
-            self.lane_groups = [group] + [dist.new_group(ranks=ranks) for _ in range(LANES - 1)]
+            self.lane_groups = [group] + [dist.new_group(ranks=ranks) for _ in range(lanes - 1)]
         if backend is None:
             from .renderer import Renderer
             backend = GpuTileBackend(Renderer(W, H, device=device, stream=stream))
@@ -198,8 +202,8 @@ class TiledRenderer:
         self.async_gather = async_gather and world > 1
         if self.async_gather:
             self.be.set_frame_ring(2)
-        self._inflight = [[] for _ in range(LANES)]   # gather works per lane (its framebuffer)
-        self._out = [None] * LANES                    # rank 0's full-frame buffers, per lane
+        self._inflight = [[] for _ in range(lanes)]   # gather works per lane (its framebuffer)
+        self._out = [None] * lanes                    # rank 0's full-frame buffers, per lane
         self._recv_ops = {}
 
     @property

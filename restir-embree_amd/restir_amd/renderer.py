@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = [
     "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions", "rs_post_frame",
     "rs_post_reset", "rs_scene_rebuild", "rs_render_direct_mis", "rs_scene_create_textured", "rs_scene_set_sky",
     "rs_scene_load_sky", "rs_image_decode", "rs_context_set_initial_split", "rs_context_get_initial_split",
-    "rs_context_set_frame_ring", "rs_context_set_run_ahead", "rs_tile_stream", "rs_export_png",
+    "rs_context_set_frame_ring", "rs_context_set_run_ahead", "rs_max_run_ahead", "rs_tile_stream", "rs_export_png",
     "rs_image_encode_png", "rs_context_track_row_costs", "rs_get_row_costs", "rs_frame_readback", "rs_frame_wait",
     "rs_host_alloc", "rs_host_free", "rs_mgpu_unique_id", "rs_mgpu_create", "rs_mgpu_create_local",
     "rs_mgpu_destroy", "rs_mgpu_set_bands", "rs_mgpu_get_bands", "rs_mgpu_rebalance", "rs_mgpu_render_frame",
@@ -179,6 +179,8 @@ def load_library(path: str = LIB_PATH):
     L.rs_context_get_initial_split.argtypes = [vp, ip, ip]
     L.rs_context_set_frame_ring.argtypes = [vp, i32]
     L.rs_context_set_run_ahead.argtypes = [vp, i32]
+    L.rs_max_run_ahead.argtypes = []
+    L.rs_max_run_ahead.restype = i32
     L.rs_tile_stream.argtypes = [vp, ctypes.POINTER(vp), ip]
     L.rs_export_png.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ExportParams)]
     L.rs_image_encode_png.argtypes = [ctypes.c_char_p, u32, u32, u32, ctypes.POINTER(ctypes.c_uint8)]

@@ -16,6 +16,6 @@ PY
 )
 mkdir -p _ab "_build_$name"
 cp -p _build/*.o "_build_$name/"
-rm -f "_build_$name/restir_capi.o"
+rm -f "_build_$name/restir_capi.o" "_build_$name/rs_mgpu.o"
 make -s OBJ="_build_$name" LIB="_ab/lib_$name.so" HIPFLAGS="$flags" "_ab/lib_$name.so"
 echo "built _ab/lib_$name.so: $flags"

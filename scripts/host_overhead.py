@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--width", type=int, default=128)
     ap.add_argument("--height", type=int, default=64)
     ap.add_argument("--light", action="store_true", help="1 area candidate: the GPU work per frame is tiny")
+    ap.add_argument("--mgpu", type=int, default=0, help="time rs_mgpu_render_frame over this many local ranks instead")
     a = ap.parse_args()
     import torch
     from restir_amd import Renderer, scenes
@@ -29,6 +30,22 @@ def main():
     r = Renderer(a.width, a.height, device=0, stream=st.cuda_stream)
     gs = r.load_scene(sc)
     H = a.height
+    if a.mgpu:
+        from restir_amd.mgpu import MultiGpuFrame
+        rs_ = [r] + [Renderer(a.width, a.height, device=0, stream=torch.cuda.Stream().cuda_stream) for _ in range(a.mgpu - 1)]
+        gss = [gs] + [x.load_scene(sc) for x in rs_[1:]]
+        m = MultiGpuFrame(rs_)
+        for f in range(a.steps + 10):
+            if f == 10:
+                torch.cuda.synchronize()
+                t_all = time.perf_counter()
+            m.render(gss, sc.camera, prm, f, gather=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t_all
+        print(f"{a.scene} {a.width}x{a.height} rs_mgpu_render_frame over {a.mgpu} local rank(s): "
+              f"{dt / a.steps * 1e6:.1f} us per frame, {dt / a.steps / a.mgpu * 1e6:.1f} us per rank-frame", flush=True)
+        m.close()
+        return
     acc = {"begin": 0.0, "temporal": 0.0, "spatial": 0.0, "finish": 0.0}
     for f in range(a.steps + 10):
         if f == 10:
