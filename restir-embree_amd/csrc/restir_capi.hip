@@ -1297,15 +1297,17 @@ static dim3 grid_rows(int W, int ya, int yb) { return dim3((W + 15) / 16, (yb - 
 // launch kernel<Trav> for the frame's traversal kind
 // the kernel instantiation of the frame: walk kind | TRAV_WIDE when the scene's 8-wide tree is live
 // (rs_scene.h Trav; c->twide is taken from the scene when the frame begins)
-#define LAUNCH_TRAV_BS_ON(c, st, kernel, grid, bs, ...)                                                     \
+#define LAUNCH_TRAV_BS_SH_ON(c, st, kernel, grid, bs, sh, ...)                                              \
     do {                                                                                                   \
         switch ((c)->trav | ((c)->twide ? TRAV_WIDE : 0)) {                                                \
-            case TRAV_LANE | TRAV_WIDE: kernel<TRAV_LANE | TRAV_WIDE><<<(grid), (bs), 0, (st)>>>(__VA_ARGS__); break; \
-            case TRAV_LANE: kernel<TRAV_LANE><<<(grid), (bs), 0, (st)>>>(__VA_ARGS__); break;                  \
-            case TRAV_WIDE: kernel<TRAV_LOCKSTEP | TRAV_WIDE><<<(grid), (bs), 0, (st)>>>(__VA_ARGS__); break;  \
-            default: kernel<TRAV_LOCKSTEP><<<(grid), (bs), 0, (st)>>>(__VA_ARGS__); break;                     \
+            case TRAV_LANE | TRAV_WIDE: kernel<TRAV_LANE | TRAV_WIDE><<<(grid), (bs), (sh), (st)>>>(__VA_ARGS__); break; \
+            case TRAV_LANE: kernel<TRAV_LANE><<<(grid), (bs), (sh), (st)>>>(__VA_ARGS__); break;                  \
+            case TRAV_WIDE: kernel<TRAV_LOCKSTEP | TRAV_WIDE><<<(grid), (bs), (sh), (st)>>>(__VA_ARGS__); break;  \
+            default: kernel<TRAV_LOCKSTEP><<<(grid), (bs), (sh), (st)>>>(__VA_ARGS__); break;                     \
         }                                                                                                  \
     } while (0)
+#define LAUNCH_TRAV_BS_ON(c, st, kernel, grid, bs, ...) LAUNCH_TRAV_BS_SH_ON(c, st, kernel, grid, bs, 0, __VA_ARGS__)
+#define LAUNCH_TRAV_BS_SH(c, kernel, grid, bs, sh, ...) LAUNCH_TRAV_BS_SH_ON(c, (c)->fs, kernel, grid, bs, sh, __VA_ARGS__)
 // the same with extra template bits X (a pass's own variant bits above the traversal kind's)
 #define LAUNCH_TRAV_X(c, X, kernel, grid, ...)                                                              \
     do {                                                                                                   \
@@ -1623,7 +1625,8 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     const dim3 gg = grid_rows(c->W, F.gy0, F.gy1), gb = grid_rows(c->W, F.y0, F.y1);
     if (c->split) {
         const dim3 gs = grid_split(c->W, F.gy0, F.gy1);
-        LAUNCH_TRAV_BS(c, k_gbuffer_initial_split, gs, 64 * kSplit, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
+        LAUNCH_TRAV_BS_SH(c, k_gbuffer_initial_split, gs, 64 * kSplit, split_lds_bytes(P->m_area + P->m_brdf, P->m_brdf),
+                          S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
                     c->shade_fused ? 1 : 0, count_slot(c, gs, kSplit));
     } else if (c->queue) {
         const QBuf& Q = c->qb[c->li];

@@ -865,11 +865,20 @@ k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb,
 constexpr int kSplit = RS_SPLIT_WAVES;    // waves (candidate groups) per 8x8 tile
 constexpr int kSplitMaxCand = 64;         // A + B the split kernel keeps in LDS
 constexpr int kSplitMaxBrdf = 2;          // B the split kernel keeps in LDS
+// LDS, sized at launch for the frame's candidate counts (split_lds_bytes): FrameSlot (5 x 64 float4) + (pos,
+// alive) per pixel, then w_c of candidate c at pixel lane (n x 64 floats), then BRDF candidate i's (p, f.x)
+// (n, f.y) (li, f.z).  C2's 33 candidates take 17.4 KB -- a fixed 64-candidate layout (34.5 KB) held the
+// kernel to 3 waves per SIMD
 struct SplitLds {
-    float4 frame[6 * 64];                 // FrameSlot (5 x 64) + (pos, alive) per pixel
-    float w[kSplitMaxCand * 64];          // w_c of candidate c, pixel lane
-    float4 brdf[kSplitMaxBrdf * 3 * 64];  // BRDF candidate i: (p, f.x) (n, f.y) (li, f.z)
+    float4* frame;
+    float* w;
+    float4* brdf;
+    __device__ __forceinline__ SplitLds(float4* base, int n)
+        : frame(base), w((float*)(base + 6 * 64)), brdf(base + 6 * 64 + 16 * n) {}
 };
+__host__ __device__ constexpr size_t split_lds_bytes(int n, int b) {
+    return (size_t)6 * 64 * 16 + (size_t)n * 64 * 4 + (size_t)b * 3 * 64 * 16;
+}
 // candidate range [lo, hi) of group g over the combined list (area 0..A-1, then BRDF A..A+B-1)
 __device__ __forceinline__ void split_range(int n, int g, int& lo, int& hi) {
     lo = (g * n) / kSplit; hi = ((g + 1) * n) / kSplit;
@@ -881,7 +890,8 @@ __global__ void __launch_bounds__(64 * kSplit, RS_WAVES(T, RS_INITIAL_WAVES, RS_
                                                                                   CountSlot C) {
     const uint64_t t0 = wave_clock();
     if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
-    __shared__ SplitLds L;
+    extern __shared__ float4 split_lds[];
+    const SplitLds L(split_lds, F.m_area + F.m_brdf);
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
     int x = blockIdx.x * 8 + (lane & 7), y = F.gy0 + blockIdx.y * 8 + (lane >> 3);
     const bool in = x < F.W && y < F.gy1;
@@ -1397,8 +1407,11 @@ __device__ __forceinline__ uint32_t point_bucket(const DevScene& S, vec3 pt, vec
     return (oct << 3) | cx | cy | cz;
 }
 
+#ifndef RS_SPATIAL_WAVES_SORT_LOCKSTEP
+#define RS_SPATIAL_WAVES_SORT_LOCKSTEP RS_SPATIAL_WAVES
+#endif
 template <int T>
-__global__ void __launch_bounds__(256, RS_WAVES(T, RS_SPATIAL_WAVES, RS_SPATIAL_WAVES_LANE))
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_SPATIAL_WAVES_SORT_LOCKSTEP, RS_SPATIAL_WAVES_LANE))
 k_spatial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, int fuse_shade, float* fb, CountSlot C) {
     __shared__ uint32_t nbr[(kSpatialSortMax - 1) * 256];      // list position i >= 1 -> pixel
     __shared__ SpatialSortLds lds[4];
