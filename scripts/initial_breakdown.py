@@ -25,6 +25,7 @@ def main():
     r = Renderer(a.width, a.height, device=0, stream=torch.cuda.current_stream().cuda_stream)
     sc = scenes.sponza_like() if a.scene == "C3" else scenes.cornell_many_lights(1024)
     base = c3_params if a.scene == "C3" else metric_params
+    r.set_traversal("lane" if a.scene == "C3" else "lockstep")   # pinned: AUTO's tuning frames alternate kinds
     gs = r.load_scene(sc)
     cfgs = [
         ("A32 B1 (metric)", {}),
