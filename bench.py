@@ -27,7 +27,7 @@ rendered completely.  Rooflines (SURVEY.md §8(d) algorithmic bytes):
                    its launch time measured with HIP events in a second window with one frame in
                    flight (RESTIR_RUNAHEAD=0 semantics), flagged when that exceeds ms_per_step (the
                    pipelined frame hides the kernel's ramp-up and tail behind its neighbours)
-  valu_issue       VALU wave-instructions per frame (rocprofv3 PMC, profiles/r02_pmc_<cfg>.json) /
+  valu_issue       VALU wave-instructions per frame (rocprofv3 PMC, profiles/r04_pmc_<cfg>.json) /
                    ms_per_step against 1024 SIMDs x 2.4 GHz / 2 cycles
 """
 import argparse

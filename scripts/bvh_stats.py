@@ -11,7 +11,25 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "restir-embree_amd"))
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
-from trace_bench import primary_rays  # noqa: E402
+
+
+def primary_rays(cam, W, H):
+    """Camera rays of a W x H frame in the kernels' wave order (8x8 tiles, row-major within a tile, tiles row-major)."""
+    eye, at, fov = np.array(cam.eye, np.float64), np.array(cam.at, np.float64), cam.fov_y
+    fwd = at - eye
+    fwd /= np.linalg.norm(fwd)
+    up = np.array([0.0, 0.0, 1.0])
+    right = np.cross(fwd, up)
+    right /= np.linalg.norm(right)
+    upv = np.cross(right, fwd)
+    focal = (H / 2.0) / np.tan(np.radians(fov) / 2.0)
+    ty, tx, iy, ix = np.meshgrid(np.arange(H // 8), np.arange(W // 8), np.arange(8), np.arange(8), indexing="ij")
+    x = (tx * 8 + ix).ravel().astype(np.float64)
+    y = (ty * 8 + iy).ravel().astype(np.float64)
+    d = (x - W / 2)[:, None] * right + (H / 2 - y)[:, None] * upv + focal * fwd
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    o = np.broadcast_to(eye, d.shape)
+    return o.astype(np.float32), d.astype(np.float32)
 
 
 def shadow_rays(sc, o, d, t, hit, seed=1):

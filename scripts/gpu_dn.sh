@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_denoise.py -q -s --timeout 120 --timeout-method thread > gpurun_out/dn_tests.log 2>&1
 echo "tests rc=$?" >> gpurun_out/dn_tests.log
-timeout -k 10 120 python -u scripts/denoise_probe.py > gpurun_out/dn_probe.log 2>&1 || exit 1
+timeout -k 10 120 python -u scripts/dn_trace_layers.py > gpurun_out/dn_probe.log 2>&1 || exit 1
 timeout -k 10 300 python -u scripts/bench_denoise.py > gpurun_out/dn_bench.log 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp
 # profiled: bench.py's own denoise leg (the C2 frame's accumulator and G-buffer), so the per-layer durations
