@@ -117,7 +117,8 @@ using namespace wide;
 // then position, then triangle index), so the tree does not depend on the order of the arrays -- the GPU
 // builder (rs_wide_build.hip) builds the same tree level by level.  Output in the PLOC arrays'
 // shape: ids < n triangles (box, hi.w = triangle bits), ids >= n internal (lo.w / hi.w = child id bits).
-// pos: 9 floats per triangle.  Returns the root id.
+// pos: 9 floats per triangle, all finite (callers check: NaN centroids would break the sorts' ordering;
+// the GPU builder and the test harness build no wide tree for non-finite geometry).  Returns the root id.
 inline int build_sah_host(const float* pos, int n, std::vector<float>& nlo, std::vector<float>& nhi,
                           int kSweepMax = 256) {
     constexpr int kBins = 32;

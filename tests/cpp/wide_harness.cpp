@@ -157,6 +157,8 @@ extern "C" {
 // over caller positions: returns the number of wide nodes (words: 20 each) or -1; *n_prims = leaf triangles.
 // The GPU builder (rs_wide_build.hip) must produce the same words (tests/test_gpu_parity.py).
 int wide_build_host(const float* pos, int n, uint32_t* words, int cap_nodes, int* prims, int* n_prims, int* depth_out) {
+    for (size_t i = 0; i < 9 * (size_t)n; ++i)
+        if (!rs::w_finite(pos[i])) return -2;          // non-finite geometry: the GPU builds no tree either
     std::vector<float> nlo, nhi;
     const int root = rs::build_sah_host(pos, n, nlo, nhi);
     rs::SahCollapse sah;

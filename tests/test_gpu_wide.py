@@ -59,6 +59,13 @@ def _soup(n, seed, dup=0):
     return p
 
 
+def _nonfinite():
+    p = _soup(800, 5)
+    p[17, 4] = np.nan                    # one NaN and one infinite coordinate
+    p[401, 0] = np.inf
+    return _scene_from_positions(p)
+
+
 CASES = {
     "c2": lambda: scenes.cornell_many_lights(1024),
     "c3": lambda: scenes.sponza_like(),
@@ -66,6 +73,7 @@ CASES = {
     "three": lambda: _scene_from_positions(_soup(3, 2)),
     "soup5k": lambda: _scene_from_positions(_soup(5000, 3)),
     "coincident": lambda: _scene_from_positions(_soup(1500, 4, dup=700)),
+    "nonfinite": _nonfinite,             # the wide tree is optional -- the scene loads without one
 }
 
 

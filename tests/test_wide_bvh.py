@@ -46,3 +46,21 @@ def test_wide_walk_matches_brute_force(n, seed, collapse):
     rc = L.wide_query(n, seed, 4000, ctypes.byref(hits), collapse)
     assert rc == 4000, f"ray {-rc - 1000} differs from brute force"
     assert n < 100 or hits.value > 100
+
+
+def test_nonfinite_geometry_builds_no_wide_tree():
+    """non-finite vertices leave the scene without a wide tree (the walks take the skip pointers)
+    instead of failing the load or sorting NaN centroids (tests/test_gpu_wide.py checks the GPU builder)."""
+    import numpy as np
+    L = _lib()
+    L.wide_build_host.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                  ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    rng = np.random.default_rng(2)
+    for bad in (np.nan, np.inf, -np.inf):
+        pos = rng.uniform(-1, 1, (300, 9)).astype(np.float32)
+        pos[123, 5] = bad
+        words = np.zeros((300, 20), np.uint32)
+        prims = np.zeros(300, np.int32)
+        npr, dep = ctypes.c_int(), ctypes.c_int()
+        assert L.wide_build_host(pos.ctypes.data, 300, words.ctypes.data, 300, prims.ctypes.data, ctypes.byref(npr),
+                                 ctypes.byref(dep)) == -2
