@@ -329,7 +329,8 @@ def run_single(name, W, H, steps, warmup, device, stream, cpu_threads, with_cpu,
         "value": round(steps / dt, 4), "unit": "frames/s", "ms_per_step": round(ms_per_step, 4), "steps": steps,
         "warmup": warmup, "frames_timed_by_events": n_timed,
         "config": {"workload": f"{name}: {WORKLOADS[name]}, {W}x{H}", "width": W, "height": H,
-                   "traversal": {0: "lockstep", 1: "lane"}.get(last_kind, str(last_kind)), "frames_in_flight": 3},
+                   "traversal": {0: "lockstep", 1: "lane"}.get(last_kind, str(last_kind)), "frames_in_flight": 3,
+                   "scene_build_ms": round(float(gs.build_ms), 2), "wide_tree": gs.wide_tree_nodes()},
         "mrays_per_s": round(rays / dt / 1e6, 2), "rays_per_frame": rays // max(1, steps),
         "pass_ms_one_frame_in_flight": {k: round(v, 4) for k, v in iso.items()},
         "frame_ms_one_frame_in_flight": round(iso_total, 4),

@@ -326,6 +326,13 @@ class Scene:
                                      ctypes.byref(ms)))
         self.n_nodes, self.build_ms = n_nodes.value, ms.value
 
+    def wide_tree_nodes(self) -> int:
+        """Nodes of the scene's 8-wide tree (0: none -- the per-lane walks take the skip pointers)."""
+        r = self.renderer
+        nn, nt, dp = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int32()
+        r._check(r.lib.rs_debug_wide_tree(self.h, ctypes.byref(nn), ctypes.byref(nt), ctypes.byref(dp), None, None))
+        return int(nn.value)
+
     def wide_tree(self):
         """Test hook (rs_debug_wide_tree): the scene's 8-wide tree as (words (n_nodes, 20) uint32, leaf-triangle
         ids int32, depth), or None when the scene has none (its walks take the skip pointers)."""
