@@ -497,17 +497,17 @@ def _compact_roofline(r, keep=("bound", "kernel", "kernel_ms", "bytes_per_px", "
 
 
 def compact(e):
-    """The fields of a config that the printed line keeps (the rest goes to the full record)."""
+    """The fields of a sub-config that the printed line keeps (workload text, samples, peaks and units of the
+    rooflines -- the head line's -- and the rest go to the full record), so the driver's stored tail keeps every
+    config's value."""
     out = {k: e[k] for k in ("value", "unit", "ms_per_step", "mrays_per_s", "gpu_over_cpu", "frac_of_zero_copy",
                               "error") if k in e}
-    if "config" in e:
-        out["workload"] = e["config"].get("workload")
     for k in ("roofline", "kernel_roofline"):
         if e.get(k):
-            out[k] = _compact_roofline(e[k])
+            out[k] = _compact_roofline(e[k], ("bound", "kernel", "kernel_ms", "achieved", "frac", "traffic"))
     cb = e.get("cpu_baseline")
     if cb:
-        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cb}
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind") if k in cb}
     elif "cpu_baseline" in e:
         out["cpu_baseline"] = None
     if e.get("per_rank"):

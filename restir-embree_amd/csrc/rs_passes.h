@@ -755,43 +755,29 @@ k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb,
                         L.e[L.cur[b] + (L.slot[k * 64 + lane] >> 21)] = (uint16_t)(k * 64 + lane);
                     }
                 wave_lds_sync();
-                // ---- B: the chunk's shadow rays in bucket order (lane = ray).  Per-lane walks take one ray per
-                // lane and step; the lockstep walk takes KB consecutive blocks of 64 sorted rays per walk (one
-                // union over 64 KB neighbouring rays, as k_gbuffer_initial's candidate batches)
-                constexpr int KB = trav_lane(T) ? 1 : RS_RIS_BATCH;
-                for (uint32_t j0 = 0; j0 < n_rays; j0 += 64u * KB) {
-                    bool act[KB], occ[KB];
-                    vec3 o[KB], ld[KB];
-                    float tfar[KB];
-                    uint32_t kk[KB], src[KB];
-#pragma unroll
-                    for (int m = 0; m < KB; ++m) {
-                        const uint32_t j = j0 + 64u * m + (uint32_t)lane;
-                        act[m] = j < n_rays;
-                        const uint32_t sl = L.e[act[m] ? j : 0u];
-                        const uint32_t pick = L.slot[sl] & 0x1fffffu;
-                        kk[m] = sl >> 6; src[m] = sl & 63u;
-                        o[m] = mk(L.px[src[m]], L.py[src[m]], L.pz[src[m]]);
-                        Rng q;
-                        q.init(F.seed, F.frame, PASS_INITIAL, tile_pixel(F, F.gy0, F.gy1, (int)src[m]));
-                        q.n = cand_slot(c0 + (int)kk[m]) + 1u;
-                        const float r1 = q.range(0, 1), r2 = q.range(0, 1);    // area_sample_at's draws
-                        const float4* E = S.emis + 8 * (size_t)pick;
-                        const vec3 p0 = xyz(E[0]), p1 = xyz(E[1]), p2 = xyz(E[2]);
-                        const float sr = sqrtf(r1);
-                        const float bx = 1.0f - sr, by = sr * (1.0f - r2), bz = sr * r2;
-                        const vec3 pt = (p0 * bx + p1 * by) + p2 * bz;
-                        vec3 dd = pt - o[m];                                  // evaluate_f_pre's ray
-                        const float r2s = dot(dd, dd);
-                        ld[m] = normalize(dd);
-                        tfar[m] = sqrtf(r2s) - F.tfar_off;
-                        rays += act[m] ? 1u : 0u;
-                    }
-                    if constexpr (KB == 1) occ[0] = trace_any<T>(S, act[0], o[0], ld[0], FLT_MIN + F.tnear_off, tfar[0]);
-                    else occluded_wave_multi_o<KB>(S, act, o, ld, FLT_MIN + F.tnear_off, tfar, occ);
-#pragma unroll
-                    for (int m = 0; m < KB; ++m)
-                        if (act[m] && occ[m]) atomicOr(&L.occ[src[m]], 1u << kk[m]);
+                // ---- B: the chunk's shadow rays in bucket order (lane = ray)
+                for (uint32_t j0 = 0; j0 < n_rays; j0 += 64u) {
+                    const uint32_t j = j0 + (uint32_t)lane;
+                    const bool act = j < n_rays;
+                    const uint32_t sl = L.e[act ? j : 0u];
+                    const uint32_t pick = L.slot[sl] & 0x1fffffu, k = sl >> 6, src = sl & 63u;
+                    const vec3 o = mk(L.px[src], L.py[src], L.pz[src]);
+                    Rng q;
+                    q.init(F.seed, F.frame, PASS_INITIAL, tile_pixel(F, F.gy0, F.gy1, (int)src));
+                    q.n = cand_slot(c0 + (int)k) + 1u;
+                    const float r1 = q.range(0, 1), r2 = q.range(0, 1);    // area_sample_at's draws
+                    const float4* E = S.emis + 8 * (size_t)pick;
+                    const vec3 p0 = xyz(E[0]), p1 = xyz(E[1]), p2 = xyz(E[2]);
+                    const float sr = sqrtf(r1);
+                    const float bx = 1.0f - sr, by = sr * (1.0f - r2), bz = sr * r2;
+                    const vec3 pt = (p0 * bx + p1 * by) + p2 * bz;
+                    vec3 ld = pt - o;                                        // evaluate_f_pre's ray
+                    const float r2s = dot(ld, ld);
+                    ld = normalize(ld);
+                    const float tfar = sqrtf(r2s) - F.tfar_off;
+                    const bool occ = trace_any<T>(S, act, o, ld, FLT_MIN + F.tnear_off, tfar);
+                    rays += act ? 1u : 0u;
+                    if (act && occ) atomicOr(&L.occ[src], 1u << k);
                 }
                 wave_lds_sync();
                 // ---- C: re-drawn weights, the reservoir stream in candidate order (lane = pixel)

@@ -425,12 +425,12 @@ __device__ __forceinline__ uint32_t next_min(bool full, bool descended, uint32_t
     return wave_min(full, lane_min_v);
 }
 
-// K any-hit rays per lane (origins o[k]: a pixel's shadow rays to K light samples share one; the wave-sorted
-// initial pass's rays come from different pixels), one lockstep walk: each lane keeps K cursors, the wave steps through the union of all 64*K paths; each step's node
+// K any-hit rays per lane sharing one origin (a pixel's shadow rays to K light samples), one lockstep
+// walk: each lane keeps K cursors, the wave steps through the union of all 64*K paths; each step's node
 // (and leaf triangles) is loaded once and tested against every ray whose cursor is on it.
 template <int K>
-__device__ __forceinline__ void occluded_wave_multi_o(const DevScene& S, const bool* active, const vec3* o, const vec3* d,
-                                                      float tnear, const float* tfar, bool* occ) {
+__device__ __forceinline__ void occluded_wave_multi(const DevScene& S, const bool* active, vec3 o, const vec3* d,
+                                                    float tnear, const float* tfar, bool* occ) {
     const bool full = __ballot(1) == ~0ull;
     vec3 inv[K];
     uint32_t cur[K];
@@ -454,7 +454,7 @@ __device__ __forceinline__ void occluded_wave_multi_o(const DevScene& S, const b
         const int leaf = __float_as_int(b.w);
         uint32_t hbb = 0u;
 #pragma unroll
-        for (int k = 0; k < K; ++k) hbb |= (cur[k] == m && box_test(a, b, o[k], inv[k], tnear, tfar[k])) ? (1u << k) : 0u;
+        for (int k = 0; k < K; ++k) hbb |= (cur[k] == m && box_test(a, b, o, inv[k], tnear, tfar[k])) ? (1u << k) : 0u;
         if (leaf >= 0) {                                      // wave-uniform
             const int first = leaf >> 3, cnt = (leaf & 7) + 1;
             for (int j = 0; j < cnt; ++j) {
@@ -466,7 +466,7 @@ __device__ __forceinline__ void occluded_wave_multi_o(const DevScene& S, const b
                 for (int k = 0; k < K; ++k) {
                     if (__ballot((want >> k) & 1u) != 0) {        // wave-uniform
                         float t, u, v;
-                        const bool hit = tri_test_nb(T0, T1, T2, o[k], d[k], tnear, tfar[k], t, u, v);
+                        const bool hit = tri_test_nb(T0, T1, T2, o, d[k], tnear, tfar[k], t, u, v);
                         occb |= (((want >> k) & 1u) && hit) ? (1u << k) : 0u;
                     }
                 }
@@ -483,15 +483,6 @@ __device__ __forceinline__ void occluded_wave_multi_o(const DevScene& S, const b
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) occ[k] = (occb >> k) & 1u;
-}
-// the K rays of a lane from one origin (a pixel's candidates)
-template <int K>
-__device__ __forceinline__ void occluded_wave_multi(const DevScene& S, const bool* active, vec3 o, const vec3* d,
-                                                    float tnear, const float* tfar, bool* occ) {
-    vec3 oa[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) oa[k] = o;
-    occluded_wave_multi_o<K>(S, active, oa, d, tnear, tfar, occ);
 }
 // one any-hit ray per lane (the K = 1 walk, written out: the leaf loop exits per lane)
 __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
