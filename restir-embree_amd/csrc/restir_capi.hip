@@ -245,6 +245,7 @@ struct rs_context {
     int cus = 256;
     int sort_mode = RS_SPLIT_AUTO;         // wave-sorted initial pass (RESTIR_SORT=on|off; AUTO: per-lane walks)
     bool sort_spatial = true;              // wave-sorted spatial pass, CONSTANT MIS, k <= 8 (RESTIR_SORT_SPATIAL=off)
+    int sort_temporal = RS_SPLIT_AUTO;     // wave-sorted temporal rays (RESTIR_SORT_TEMPORAL=on|off; AUTO: per-lane walks)
 };
 
 // --------------------------------------------------------------------------- helpers
@@ -408,6 +409,10 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
     if (const char* t = std::getenv("RESTIR_SORT")) {          // auto (default) | on | off: wave-sorted initial pass
         if (!std::strcmp(t, "on")) c->sort_mode = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->sort_mode = RS_SPLIT_OFF;
+    }
+    if (const char* t = std::getenv("RESTIR_SORT_TEMPORAL")) { // auto (default) | on | off: wave-sorted temporal rays
+        if (!std::strcmp(t, "on")) c->sort_temporal = RS_SPLIT_ON;
+        else if (!std::strcmp(t, "off")) c->sort_temporal = RS_SPLIT_OFF;
     }
     if (const char* t = std::getenv("RESTIR_SORT_SPATIAL"))    // on (default) | off: wave-sorted spatial pass
         c->sort_spatial = std::string(t) != "off";
@@ -1705,12 +1710,15 @@ extern "C" int rs_tile_temporal(rs_context* c) {
         // held without one), this launch walks both binary trees (same hits, rs_scene.h)
         if (!S.wnodes || !Sp.wnodes) c->twide = false;
         if (c->F.debug_reproj) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 2 * npx, c->fs));
-        if (partial)
-            LAUNCH_TRAV_X(c, TEMPORAL_BAND, k_temporal, gb, S, Sp, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]},
-                          ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
-        else
-            LAUNCH_TRAV(c, k_temporal, gb, S, Sp, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]},
-                        ResBuf{c->R[c->last]}, ResBuf{c->R[c->rb]}, count_slot(c, gb));
+        // the wave-sorted shadow rays (TEMPORAL_SORT) with the per-lane walks unless RESTIR_SORT_TEMPORAL says otherwise
+        const bool tsort = c->sort_temporal == RS_SPLIT_ON || (c->sort_temporal == RS_SPLIT_AUTO && c->trav == TRAV_LANE);
+#define RS_TEMPORAL_ARGS S, Sp, c->F, c->G[c->gcur], c->G[c->gprev], ResBuf{c->R[c->rcur]}, ResBuf{c->R[c->last]}, \
+                         ResBuf{c->R[c->rb]}, count_slot(c, gb)
+        if (partial && tsort) LAUNCH_TRAV_X(c, TEMPORAL_BAND | TEMPORAL_SORT, k_temporal, gb, RS_TEMPORAL_ARGS);
+        else if (partial) LAUNCH_TRAV_X(c, TEMPORAL_BAND, k_temporal, gb, RS_TEMPORAL_ARGS);
+        else if (tsort) LAUNCH_TRAV_X(c, TEMPORAL_SORT, k_temporal, gb, RS_TEMPORAL_ARGS);
+        else LAUNCH_TRAV(c, k_temporal, gb, RS_TEMPORAL_ARGS);
+#undef RS_TEMPORAL_ARGS
         c->twide = twide;
         HIPCHK(c, hipGetLastError());
         if (c->F.debug_reproj) {

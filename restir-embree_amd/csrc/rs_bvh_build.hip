@@ -52,10 +52,17 @@ __global__ void k_prim_bounds(const float* __restrict__ pos, uint32_t n, float4*
     if (i < n) {
         const float* p = pos + 9 * (size_t)i;
         float l[3], h[3];
+        bool fin = true;
         for (int a = 0; a < 3; ++a) {
             l[a] = fminf(fminf(p[a], p[3 + a]), p[6 + a]);
             h[a] = fmaxf(fmaxf(p[a], p[3 + a]), p[6 + a]);
+            fin = fin && isfinite(l[a]) && isfinite(h[a]);
         }
+        // a triangle with an infinite (or all-NaN) coordinate can never be hit (the triangle test's arithmetic
+        // turns NaN and fails); it enters the tree as a point box at the origin so that the centroid bounds,
+        // the Morton codes and PLOC's merge distances stay finite (Embree drops such primitives)
+        if (!fin)
+            for (int a = 0; a < 3; ++a) l[a] = h[a] = 0.0f;
         lo[i] = make_float4(l[0], l[1], l[2], 0.0f);
         hi[i] = make_float4(h[0], h[1], h[2], 0.0f);
         for (int a = 0; a < 3; ++a) {

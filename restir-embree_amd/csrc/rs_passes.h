@@ -1035,12 +1035,29 @@ struct TemporalSlot {
 // tile): the instantiation with the rare rebuilds below; a full-frame launch has none (their walks and the
 // state kept around them would otherwise cost every wave registers)
 constexpr int TEMPORAL_BAND = 4;
+// the bucket of a ray toward a light point: direction octant x the target's cell (one bit per axis against
+// the emitters' centroid centre) -- the sorted temporal and spatial passes' key
+__device__ __forceinline__ uint32_t point_bucket(const DevScene& S, vec3 pt, vec3 d) {
+    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    const uint32_t cx = pt.x > S.ecen.x ? 1u : 0u, cy = pt.y > S.ecen.y ? 2u : 0u, cz = pt.z > S.ecen.z ? 4u : 0u;
+    return (oct << 3) | cx | cy | cz;
+}
+// T | TEMPORAL_SORT: the four shadow rays of a wave's 64 pixels are counting-sorted by direction octant x
+// target cell (as k_spatial_sorted's) and traced 64 at a time in that order (lane = ray); bit-identical
+constexpr int TEMPORAL_SORT = 8;
+struct TemporalSortLds {                    // one wave's region (1.5 KB)
+    uint16_t slot[4 * 64];                  // slot k * 64 + lane: rank of ray k of pixel lane in its bucket
+    uint16_t e[4 * 64];                     // the slots, bucket by bucket
+    uint32_t cur[64];                       // bucket counts, then offsets
+    uint32_t occ[64];                       // per pixel: occlusion bit of ray k
+};
 template <int T>
 // Sp: the previous frame's geometry (== S unless the scene moved since; rs_scene::dev_of), traced when a tile
 // rebuilds a previous-frame G element beyond its rows
 __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORAL_WAVES_LANE)) k_temporal(DevScene S, DevScene Sp, FrameConst F, GBuf G, GBuf Gp, ResBuf Rr, ResBuf Rl,
                                                   ResBuf Rw, CountSlot C) {
     constexpr bool kBand = (T & TEMPORAL_BAND) != 0;
+    constexpr bool kSort = (T & TEMPORAL_SORT) != 0;
     const uint64_t t0 = wave_clock();
     int x, y;
     uint32_t rays = 0;
@@ -1122,14 +1139,64 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
             rays += e.need ? 1u : 0u;
         }
         ts.put3(0, cur.pos); ts.put3(3, prev.pos); ts.put3(6, cs.p); ts.put3(9, ps.p);
+        if constexpr (kSort) {
+            __shared__ TemporalSortLds sort_lds[4];
+            TemporalSortLds& L = sort_lds[threadIdx.x >> 6];
+            const int lane = threadIdx.x & 63, wbase = threadIdx.x & ~63;
+            // ---- A: each needed ray takes a rank in its bucket (lane = pixel)
+            L.cur[lane] = 0u;
+            L.occ[lane] = 0u;
+            wave_lds_sync();
+            uint32_t bk = 0u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            asm volatile("" ::: "memory");
-            const vec3 o = ts.get3(3 * (k & 1)), ld = ts.get3(6 + 3 * (k >> 1)) - o;   // evaluate_f_pre's ray
-            const bool need = (nd >> k) & 1u;
-            const bool oc = trace_any<T>(S, need, o, normalize(ld), FLT_MIN + F.tnear_off, sqrtf(dot(ld, ld)) - F.tfar_off);
-            asm volatile("" ::: "memory");
-            ph[k] = need && oc ? ts.get(16 + k) : ts.get(12 + k);
+            for (int k = 0; k < 4; ++k)
+                if ((nd >> k) & 1u) {
+                    const vec3 tg = ts.get3(6 + 3 * (k >> 1));
+                    const uint32_t b = point_bucket(S, tg, tg - ts.get3(3 * (k & 1)));
+                    L.slot[k * 64 + lane] = (uint16_t)atomicAdd(&L.cur[b], 1u);
+                    bk |= b << (8 * k);
+                }
+            wave_lds_sync();
+            const uint32_t cnt_b = L.cur[lane];
+            uint32_t incl = cnt_b;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = __shfl_up(incl, o);
+                incl += lane >= o ? v : 0u;
+            }
+            const uint32_t n_rays = __shfl(incl, 63);
+            L.cur[lane] = incl - cnt_b;
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((nd >> k) & 1u) L.e[L.cur[(bk >> (8 * k)) & 63u] + L.slot[k * 64 + lane]] = (uint16_t)(k * 64 + lane);
+            wave_lds_sync();
+            // ---- B: the rays in bucket order (lane = ray), re-formed from the pixel's LDS slot
+            for (uint32_t j0 = 0; j0 < n_rays; j0 += 64u) {
+                const uint32_t j = j0 + (uint32_t)lane;
+                const bool act = j < n_rays;
+                const uint32_t sl = L.e[act ? j : 0u];
+                const int k = (int)(sl >> 6), src = (int)(sl & 63u);
+                const TemporalSlot tq{temporal_lds, wbase + src};
+                const vec3 o = tq.get3(3 * (k & 1)), ld = tq.get3(6 + 3 * (k >> 1)) - o;   // evaluate_f_pre's ray
+                const bool oc = trace_any<T>(S, act, o, normalize(ld), FLT_MIN + F.tnear_off, sqrtf(dot(ld, ld)) - F.tfar_off);
+                if (act && oc) atomicOr(&L.occ[src], 1u << k);
+            }
+            wave_lds_sync();
+            // ---- C: the p-hats (lane = pixel)
+            const uint32_t occm = L.occ[lane];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ph[k] = ((nd & occm) >> k) & 1u ? ts.get(16 + k) : ts.get(12 + k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                asm volatile("" ::: "memory");
+                const vec3 o = ts.get3(3 * (k & 1)), ld = ts.get3(6 + 3 * (k >> 1)) - o;   // evaluate_f_pre's ray
+                const bool need = (nd >> k) & 1u;
+                const bool oc = trace_any<T>(S, need, o, normalize(ld), FLT_MIN + F.tnear_off, sqrtf(dot(ld, ld)) - F.tfar_off);
+                asm volatile("" ::: "memory");
+                ph[k] = need && oc ? ts.get(16 + k) : ts.get(12 + k);
+            }
         }
     }
     asm volatile("" ::: "memory");                      // re-read the reservoirs: nothing carried across the walks
@@ -1401,11 +1468,6 @@ struct SpatialSortLds {                     // one wave's region (2.9 KB)
     uint32_t cur[64];                       // bucket counts, then offsets
     uint32_t occ[64];                       // per pixel: occlusion bit of list position i
 };
-__device__ __forceinline__ uint32_t point_bucket(const DevScene& S, vec3 pt, vec3 d) {
-    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
-    const uint32_t cx = pt.x > S.ecen.x ? 1u : 0u, cy = pt.y > S.ecen.y ? 2u : 0u, cz = pt.z > S.ecen.z ? 4u : 0u;
-    return (oct << 3) | cx | cy | cz;
-}
 
 #ifndef RS_SPATIAL_WAVES_SORT_LOCKSTEP
 #define RS_SPATIAL_WAVES_SORT_LOCKSTEP RS_SPATIAL_WAVES

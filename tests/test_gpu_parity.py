@@ -670,9 +670,10 @@ def test_wide_tree_live_on_c3():
 
 @pytest.mark.parametrize("which", ["c3", "c3_a37", "c2_lane", "c2_lockstep"])
 def test_sorted_initial_pass_bit_identical(which, monkeypatch):
-    """The wave-sorted initial and spatial passes (rs_passes.h k_gbuffer_initial_sorted / k_spatial_sorted: per
-    8x8 tile the shadow rays are counting-sorted by octant x light bucket and traced in that order) render the
-    frames of the per-candidate kernels bit for bit (RESTIR_SORT=off, RESTIR_SORT_SPATIAL=off), incl. a
+    """The wave-sorted initial, temporal and spatial passes (rs_passes.h k_gbuffer_initial_sorted, k_temporal<T |
+    TEMPORAL_SORT>, k_spatial_sorted: per 8x8 tile the shadow rays are counting-sorted by octant x light bucket /
+    target cell and traced in that order) render the frames of the per-candidate kernels bit for bit
+    (RESTIR_SORT=off, RESTIR_SORT_SPATIAL=off, RESTIR_SORT_TEMPORAL=off), incl. a
     candidate count that is not a multiple of the chunk, a visibility-pass frame (no shadow rays in the initial
     pass), and both walk kinds on the metric scene."""
     trav = "lockstep" if which == "c2_lockstep" else "lane"
@@ -686,6 +687,7 @@ def test_sorted_initial_pass_bit_identical(which, monkeypatch):
     for sort in ("on", "off"):
         monkeypatch.setenv("RESTIR_SORT", sort)
         monkeypatch.setenv("RESTIR_SORT_SPATIAL", sort)
+        monkeypatch.setenv("RESTIR_SORT_TEMPORAL", sort)
         g = Renderer(W, H)
         g.set_traversal(trav)
         gs = g.load_scene(sc)

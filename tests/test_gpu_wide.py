@@ -86,6 +86,17 @@ def test_wide_tree_gpu_equals_host(case):
     want = _host_tree(sc.positions)
     if want is None:
         assert got is None
+        if case == "nonfinite":          # the scene still loads and its skip-pointer walks agree
+            rng = np.random.default_rng(3)
+            o = rng.uniform(-4, 4, (2000, 3)).astype(np.float32)
+            d = rng.normal(size=(2000, 3)).astype(np.float32)
+            d /= np.linalg.norm(d, axis=1, keepdims=True)
+            for any_hit in (False, True):
+                tl, pl = g.debug_trace(gs, o, d, 0.01, 3.0e38, any_hit=any_hit, lockstep=False)
+                tk, pk = g.debug_trace(gs, o, d, 0.01, 3.0e38, any_hit=any_hit, lockstep=True)
+                assert np.array_equal(pl, pk) and np.array_equal(tl, tk)
+                if not any_hit:
+                    assert (pl >= 0).any() and not np.isin(pl, [17, 401]).any()   # non-finite triangles: never hit
         return
     assert got is not None, f"{case}: the GPU built no wide tree"
     gw, gp, gd = got
