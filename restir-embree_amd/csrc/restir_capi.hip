@@ -244,7 +244,8 @@ struct rs_context {
     int q_A[kLanes] = {}, q_B[kLanes] = {};
     int cus = 256;
     int sort_mode = RS_SPLIT_AUTO;         // wave-sorted initial pass (RESTIR_SORT=on|off; AUTO: per-lane walks)
-    bool sort_spatial = true;              // wave-sorted spatial pass, CONSTANT MIS, k <= 8 (RESTIR_SORT_SPATIAL=off)
+    int sort_spatial = RS_SPLIT_AUTO;      // wave-sorted spatial pass, CONSTANT MIS, k <= 8 (RESTIR_SORT_SPATIAL=on|off;
+                                           // AUTO: per-lane walks -- C3 2.21 -> 1.87 ms; lockstep C5 0.228 -> 0.250)
     int sort_temporal = RS_SPLIT_AUTO;     // wave-sorted temporal rays (RESTIR_SORT_TEMPORAL=off: per-ray walks)
 };
 
@@ -414,8 +415,10 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->sort_temporal = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->sort_temporal = RS_SPLIT_OFF;
     }
-    if (const char* t = std::getenv("RESTIR_SORT_SPATIAL"))    // on (default) | off: wave-sorted spatial pass
-        c->sort_spatial = std::string(t) != "off";
+    if (const char* t = std::getenv("RESTIR_SORT_SPATIAL")) {  // auto (default) | on | off: wave-sorted spatial pass
+        if (!std::strcmp(t, "on")) c->sort_spatial = RS_SPLIT_ON;
+        else if (!std::strcmp(t, "off")) c->sort_spatial = RS_SPLIT_OFF;
+    }
     if (const char* t = std::getenv("RESTIR_TILE_ORDER"))      // cost (default) | off (row-major)
         c->order_on = std::strcmp(t, "off") != 0;
     if (const char* t = std::getenv("RESTIR_READBACK"))        // sdma (default) | kernel
@@ -1760,7 +1763,8 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
         const bool tev = c->tuning && c->tune_n + 2 <= (int)(sizeof(c->tune_ev) / sizeof(c->tune_ev[0]));
         if (tev) HIPCHK(c, hipEventRecord(c->tune_ev[c->tune_n], c->fs));
 #define SPATIAL(TK, CM, SM) k_spatial<TK, CM, SM><<<gb, 256, 0, c->fs>>>(S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs)
-        if (c->sort_spatial && cm && c->F.k + 1 <= kSpatialSortMax) {
+        const bool ssort = c->sort_spatial == RS_SPLIT_ON || (c->sort_spatial == RS_SPLIT_AUTO && c->trav == TRAV_LANE);
+        if (ssort && cm && c->F.k + 1 <= kSpatialSortMax) {
             LAUNCH_TRAV(c, k_spatial_sorted, gb, S, c->F, G, Rr, Rw, pass_index, fuse, c->fb, cs);
         } else if (c->trav == TRAV_LANE) {
             if (c->twide) { if (cm) SPATIAL(TRAV_LANE | TRAV_WIDE, 1, 0); else SPATIAL(TRAV_LANE | TRAV_WIDE, 0, 0); }
