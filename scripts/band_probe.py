@@ -2,11 +2,13 @@
 communication -- the compute + host-overhead floor of bench.py --gpus N.  For N in (1, 2, 4, 8) it renders
 the middle band of the frame (rank N//2, margin/halo as TiledRenderer sets them) K times through the
 tile ABI and reports wall ms/frame, GPU ms/frame (event ring) and host ms per render() call.
-Usage: python scripts/band_probe.py [--scene C2|C3|C5] [--steps K]"""
+Usage: python scripts/band_probe.py [--scene C2|C3|C5] [--steps K] [--balanced] [--all-ranks N [--refine R]]"""
 import argparse
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "restir-embree_amd"))
@@ -24,6 +26,9 @@ def main():
     ap.add_argument("--ahead", type=int, default=-1, help="run-ahead depth (default: the library's)")
     ap.add_argument("--only-n", type=int, default=0, help="only this N (rank N//2)")
     ap.add_argument("--all-ranks", type=int, default=0, help="time every rank of this N instead")
+    ap.add_argument("--refine", type=int, default=0,
+                    help="with --all-ranks: rounds of time-based rebalancing (each band's row costs rescaled to its "
+                         "measured time, bands balanced again; the rs_mgpu_rebalance refinement)")
     a = ap.parse_args()
     import torch
     from restir_amd import Renderer, scenes
@@ -57,8 +62,11 @@ def main():
         cases = [(a.only_n, a.only_n // 2)]
     if a.all_ranks:
         cases = [(a.all_ranks, k) for k in range(a.all_ranks)]
-    for N, rank in cases:
-        y0, y1 = balanced_bands(costs, N, 8)[rank] if costs is not None else band_rows(H, rank, N)
+    bands_of = {}
+    for N in {n for n, _ in cases}:
+        bands_of[N] = balanced_bands(costs, N, 8) if costs is not None else [band_rows(H, k, N) for k in range(N)]
+
+    def probe(N, rank, y0, y1, tag=""):
         halo = halo_rows(prm) if N > 1 else 0
         margin = halo          # rs_mgpu_render_frame's G-buffer margin (a temporal reprojection beyond it rebuilds)
 
@@ -89,10 +97,29 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         tot, n = r.timing_totals()
-        print(f"{a.scene} ahead={a.ahead} inflight={a.inflight} split={a.split}:{int(r.initial_split()[1])} N={N} rank={rank} rows={y1 - y0} margin={margin}: wall {dt / a.steps * 1e3:.4f} ms/frame, "
+        print(f"{tag}{a.scene} ahead={a.ahead} inflight={a.inflight} split={a.split}:{int(r.initial_split()[1])} N={N} rank={rank} rows={y1 - y0} margin={margin}: wall {dt / a.steps * 1e3:.4f} ms/frame, "
               f"gpu {tot.total_ms / n:.4f} ms (initial {tot.gbuffer_initial_ms / n:.4f}, spatial {tot.spatial_ms / n:.4f}, "
               f"temporal {tot.temporal_ms / n:.4f}), host {host / a.steps * 1e3:.4f} ms/call; "
               f"ideal (N=1 / N) -> efficiency bound", flush=True)
+        return dt / a.steps * 1e3
+
+    if a.all_ranks and a.refine and costs is not None:
+        N = a.all_ranks
+        c = np.asarray(costs, np.float64).copy()
+        bands = bands_of[N]
+        for it in range(a.refine + 1):
+            t = [probe(N, k, y0, y1, f"[round {it}] ") for k, (y0, y1) in enumerate(bands)]
+            print(f"[round {it}] bands {[y1 - y0 for y0, y1 in bands]}: max {max(t):.4f} mean {np.mean(t):.4f} ms",
+                  flush=True)
+            for (y0, y1), tk in zip(bands, t):          # each band's rows rescaled to its measured time
+                ck = c[y0:y1].sum()
+                if ck > 0:
+                    c[y0:y1] *= tk / ck
+            bands = balanced_bands(c, N, 8)
+        return
+    for N, rank in cases:
+        y0, y1 = bands_of[N][rank]
+        probe(N, rank, y0, y1)
 
 
 if __name__ == "__main__":
