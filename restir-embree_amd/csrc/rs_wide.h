@@ -314,7 +314,8 @@ struct SahCollapse {
 // nlo / nhi: the PLOC nodes as 4 floats each (ids < n: primitives, hi.w = triangle index bits; ids >= n:
 // internal, lo.w / hi.w = left / right child id bits); out: 20 words per wide node.  collapse: 0 greedy
 // (open the largest-area interior child until 8), 1 SAH-optimal within max_depth levels (SahCollapse,
-// costs c_node / c_tri; falls back to greedy when it has no plan)
+// costs c_node / c_tri; falls back to greedy when it has no plan).  The CPU restatement the GPU builder
+// (rs_wide_build.hip) is checked against (tests/cpp/wide_harness.cpp); no product path calls it.
 inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, std::vector<uint32_t>& out,
                            std::vector<int>& tri_prims, int& depth, std::string& err, int collapse = 0,
                            float c_node = 1.0f, float c_tri = 0.3f, int max_depth = 8,
@@ -328,8 +329,8 @@ inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, 
     auto area = [&](int c) { const float* a = nlo + 4 * (size_t)c; const float* z = nhi + 4 * (size_t)c;
         const float ex = z[0] - a[0], ey = z[1] - a[1], ez = z[2] - a[2]; return ex * ey + ey * ez + ez * ex; };
     SahCollapse sah;
-    // the plan's tables take 480 B per binary node (0.24 GB at C3's 248 k triangles): above 2 M triangles,
-    // or without a plan inside the depth, the greedy collapse
+    // the plan's tables take 480 B per binary node (0.24 GB at C3's 248 k triangles): above 2^21 triangles
+    // (~1 GB of tables), or without a plan inside the depth, the greedy collapse
     if (collapse == 1 && (n > (1 << 21) || !sah.plan(nlo, nhi, n, root, c_node, c_tri, max_depth)))
         collapse = 0;
     std::vector<int> queue = {root}, level = {0}, budget = {max_depth};   // wide node i = PLOC node queue[i]
