@@ -879,9 +879,24 @@ struct SplitLds {
 __host__ __device__ constexpr size_t split_lds_bytes(int n, int b) {
     return (size_t)6 * 64 * 16 + (size_t)n * 64 * 4 + (size_t)b * 3 * 64 * 16;
 }
-// candidate range [lo, hi) of group g over the combined list (area 0..A-1, then BRDF A..A+B-1)
-__device__ __forceinline__ void split_range(int n, int g, int& lo, int& hi) {
-    lo = (g * n) / kSplit; hi = ((g + 1) * n) / kSplit;
+// candidate range [lo, hi) of group g over the combined list (area 0..A-1, then BRDF A..A+B-1), cut at
+// equal estimated cost: a BRDF candidate (a per-lane closest-hit walk, then its shadow ray) counts as
+// RS_SPLIT_BRDF_W area candidates, so the last group -- the one holding the BRDF candidates -- takes fewer
+// area candidates and the workgroup's waves finish together (C2, 32 + 1 candidates: groups 8 / 9 / 9 / 6 + 1;
+// C2's 1/8 bands, every rank timed alone, two sessions: mean 0.2094-0.2108 vs 0.2154-0.2172 ms at weight 1,
+// weights 2 and 4 no better than 1: scripts/gpu_split_ab.sh)
+#ifndef RS_SPLIT_BRDF_W
+#define RS_SPLIT_BRDF_W 3
+#endif
+__device__ __forceinline__ int split_bound(int A, int B, int k) {
+    constexpr int wb = RS_SPLIT_BRDF_W;
+    const int e = (k * (A + B * wb)) / kSplit;           // in area-candidate units
+    if (e <= A) return e;
+    const int b = (e - A) / wb;
+    return A + (b < B ? b : B);
+}
+__device__ __forceinline__ void split_range(int A, int B, int g, int& lo, int& hi) {
+    lo = split_bound(A, B, g); hi = split_bound(A, B, g + 1);
 }
 
 template <int T>
@@ -918,7 +933,7 @@ __global__ void __launch_bounds__(64 * kSplit, RS_WAVES(T, RS_INITIAL_WAVES, RS_
     const bool tv = !F.do_vis_pass;
     constexpr int kB = trav_lane(T) ? RS_RIS_BATCH_LANE : RS_RIS_BATCH;
     int lo, hi;
-    split_range(n, g, lo, hi);
+    split_range(A, B, g, lo, hi);
     if (__ballot(alive) != 0) {                                         // wave-uniform
         Rng rng; rng.init(F.seed, F.frame, PASS_INITIAL, (uint32_t)p);
         const int ahi = hi < A ? hi : A;
