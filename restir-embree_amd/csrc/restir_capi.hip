@@ -1466,8 +1466,8 @@ static bool want_split(const rs_context* c, const rs_frame_params* P, int gy0, i
     if (c->split_mode == RS_SPLIT_ON) return true;
     if (c->split_mode == RS_SPLIT_OFF) return false;
     // with frames in flight the neighbouring frames fill a launch's tail: split only below one round
-    // (C2 1/4 band, 1.4 rounds: 0.38 ms/frame unsplit vs 0.44 split; 1/8 band, 0.7 rounds: 0.24 split
-    // vs 0.26); one frame at a time, below 3 rounds (1/8 band 0.64 -> 0.40 ms)
+    // (C2 1/4 band, 1.4 rounds: 0.363 ms/frame unsplit vs 0.411 split with the cost-weighted groups, r04;
+    // 1/8 band, 0.8 rounds: 0.209 split vs 0.26); one frame at a time, below 3 rounds (1/8 band 0.64 -> 0.40 ms)
     const size_t rounds = c->ahead > 0 ? 1 : 3;
     return c->trav == TRAV_LOCKSTEP && grid_waves(grid_rows(c->W, gy0, gy1)) < rounds * c->wave_slots;
 }
