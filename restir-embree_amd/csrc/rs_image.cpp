@@ -271,11 +271,15 @@ int load_image(const std::string& path, Image& img, std::string& err) {
     std::vector<uint8_t> f;
     if (!read_file(path, f)) { err = "cannot open " + path; return -1; }
     int rc;
-    if (f.size() >= 8 && f[0] == 137 && f[1] == 'P' && f[2] == 'N' && f[3] == 'G') rc = decode_png(f, img, err);
-    else if (f.size() >= 2 && f[0] == '#' && f[1] == '?') rc = decode_hdr(f, img, err);
-    else if (f.size() >= 2 && f[0] == 'P') rc = decode_pnm(f, img, err);
-    else if (f.size() >= 2 && f[0] == 0xFF && f[1] == 0xD8) rc = decode_jpeg(f, img, err);
-    else { err = "unknown image format"; rc = -1; }
+    try {   // a decoder's allocation failure is an error return, never an exception through the C ABI
+        if (f.size() >= 8 && f[0] == 137 && f[1] == 'P' && f[2] == 'N' && f[3] == 'G') rc = decode_png(f, img, err);
+        else if (f.size() >= 2 && f[0] == '#' && f[1] == '?') rc = decode_hdr(f, img, err);
+        else if (f.size() >= 2 && f[0] == 'P') rc = decode_pnm(f, img, err);
+        else if (f.size() >= 2 && f[0] == 0xFF && f[1] == 0xD8) rc = decode_jpeg(f, img, err);
+        else { err = "unknown image format"; rc = -1; }
+    } catch (const std::bad_alloc&) {
+        err = "out of memory decoding the image"; rc = -1;
+    }
     if (rc) err = path + ": " + err;
     return rc;
 }

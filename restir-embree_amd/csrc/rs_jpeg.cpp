@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -42,13 +43,13 @@ struct Huff {
         for (int l = 1; l <= 16; ++l) {
             valoff[l] = k - code;
             for (int i = 0; i < counts[l - 1]; ++i, ++k, ++code) {
+                if (code >= (1 << l)) return false;   // over-subscribed: checked before any table write
                 if (l <= 9) {
                     const int sh = 9 - l;
                     for (int f = 0; f < (1 << sh); ++f) { look_len[(code << sh) | f] = (uint8_t)l; look_val[(code << sh) | f] = v[k]; }
                 }
             }
             maxcode[l] = counts[l - 1] ? code - 1 : -1;
-            if (code > (1 << l)) return false;   // over-subscribed code lengths
             code <<= 1;
         }
         maxcode[17] = 0x7fffffff;
@@ -157,6 +158,10 @@ struct Decoder {
         const int nc = u8();
         if (prec != 8) return fail("only 8-bit JPEG is supported");
         if (W <= 0 || H <= 0 || W > 65535 || H > 65535) return fail("bad JPEG size");
+        // a header of a few bytes must not commit gigabytes: cap the image at 2^28 pixels, and at 4096 pixels
+        // per byte of the file (a real entropy stream codes far fewer; an all-DC 8x8 block still takes >= 1 bit)
+        if ((uint64_t)W * (uint64_t)H > (1ull << 28) || (uint64_t)W * (uint64_t)H > 4096ull * (uint64_t)n)
+            return fail("JPEG size exceeds the decoder's limit");
         if (nc != 1 && nc != 3) return fail("only grey and 3-component JPEG are supported");
         if (len != 8 + 3 * nc) return fail("bad SOF length");
         comp.assign(nc, Comp{});
@@ -595,7 +600,13 @@ int decode_jpeg(const std::vector<uint8_t>& file, Image& img, std::string& err) 
     Decoder d;
     d.f = file.data();
     d.n = file.size();
-    if (!d.parse() || !d.output(img)) {
+    bool ok = false;
+    try {
+        ok = d.parse() && d.output(img);
+    } catch (const std::bad_alloc&) {
+        d.fail("out of memory decoding JPEG");
+    }
+    if (!ok) {
         err = d.err;
         const bool unsup = err.find("not supported") != std::string::npos || err.find("only ") == 0 ||
                            err.find("unsupported") != std::string::npos;

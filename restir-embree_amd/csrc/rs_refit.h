@@ -127,10 +127,17 @@ __device__ __forceinline__ void wide_refit_node(const WideRefitArgs& A, uint32_t
             const size_t t = tb + (uint32_t)(i - ni);
             const int prim = __float_as_int(A.tris[3 * t].w);
             const float* p = A.pos + 9 * (size_t)prim;
+            bool fin = true;
             for (int a = 0; a < 3; ++a) {
                 kb[i].lo[a] = w_min(w_min(p[a], p[3 + a]), p[6 + a]);
                 kb[i].hi[a] = w_max(w_max(p[a], p[3 + a]), p[6 + a]);
+                fin = fin && isfinite(kb[i].lo[a]) && isfinite(kb[i].hi[a]);
             }
+            // a triangle with a non-finite vertex can never be hit (the triangle test's arithmetic turns NaN,
+            // DESIGN.md §3.9); like k_prim_bounds it gets a point box at the origin, so every node above it
+            // stays encodable and its planes stay a superset of the finite triangles below
+            if (!fin)
+                for (int a = 0; a < 3; ++a) kb[i].lo[a] = kb[i].hi[a] = 0.0f;
             const float v0x = p[0], v0y = p[1], v0z = p[2];
             A.tris[3 * t] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
             A.tris[3 * t + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
@@ -139,8 +146,8 @@ __device__ __forceinline__ void wide_refit_node(const WideRefitArgs& A, uint32_t
     }
     uint32_t w[20];
     WBox u;
-    // a non-finite box has no quantisation frame: the node keeps its previous planes (the binary tree's
-    // boxes are NaN / infinite there too; neither walk promises anything for non-finite geometry)
+    // every child box is finite now (point boxes above); encoding can only fail for coordinates near FLT_MAX
+    // (no power-of-two frame <= 2^127 spans them), where the node keeps its previous planes
     if (!wide_encode(kb, nv, ni, cb, tb, w, &u)) return;
     uint4* P = A.nodes + 5 * (size_t)j;
     for (int k = 0; k < 5; ++k) P[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);

@@ -101,6 +101,9 @@ class GpuTileBackend:
     def load_scene(self, scene):
         return self.r.load_scene(scene)
 
+    def run_ahead_lanes(self) -> int:
+        return run_ahead_lanes()
+
     def set_frame_ring(self, n):
         self.r.set_frame_ring(n)
 
@@ -173,6 +176,9 @@ def balanced_bands(costs, world: int, min_rows: int = 1):
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
 
+DEFAULT_LANES = 3   # lanes of a backend that does not say (the library's default run-ahead depth 2, + 1)
+
+
 def run_ahead_lanes() -> int:
     """Run-ahead lanes of a context: rs_max_run_ahead() + 1 (the library's build constant)."""
     from .renderer import load_library
@@ -186,18 +192,20 @@ class TiledRenderer:
         self.bands = [band_rows(H, r, world) for r in range(world)]
         self.temporal_margin = temporal_margin
         self.group = group
+        if backend is None:
+            from .renderer import Renderer
+            backend = GpuTileBackend(Renderer(W, H, device=device, stream=stream))
+        self.be = backend
         # one process group per run-ahead lane: frames in flight on different lanes exchange halos and
-        # gather through independent communicators (one group's collectives run in issue order)
-        lanes = run_ahead_lanes()
+        # gather through independent communicators (one group's collectives run in issue order).  The lane
+        # count is the backend's (a CPU backend never loads the HIP library for it -- ADVICE r4)
+        lanes_of = getattr(backend, "run_ahead_lanes", None)
+        lanes = int(lanes_of()) if callable(lanes_of) else DEFAULT_LANES
         self.lane_groups = [group] * lanes
         if world > 1:
             import torch.distributed as dist
             ranks = list(range(world)) if group is None else dist.get_process_group_ranks(group)
             self.lane_groups = [group] + [dist.new_group(ranks=ranks) for _ in range(lanes - 1)]
-        if backend is None:
-            from .renderer import Renderer
-            backend = GpuTileBackend(Renderer(W, H, device=device, stream=stream))
-        self.be = backend
         self.frame = None
         self.async_gather = async_gather and world > 1
         if self.async_gather:

@@ -130,6 +130,9 @@ def _check_conservative(words, prims, pos):
     ni, nv, cb, tb, lo, hi = _decode(words)
     p = pos.reshape(-1, 3, 3).astype(np.float64)
     tlo, thi = p.min(1), p.max(1)
+    bad = ~(np.isfinite(tlo).all(1) & np.isfinite(thi).all(1))   # non-finite triangles: point box at the origin
+    tlo[bad] = 0.0
+    thi[bad] = 0.0
     N = len(words)
     blo = np.full((N, 3), np.inf)
     bhi = np.full((N, 3), -np.inf)
@@ -172,6 +175,28 @@ def test_wide_refit_after_updates():
             assert np.array_equal(pl, pk) and np.array_equal(tl, tk), (f, any_hit)
         fetches, _, lost = g.debug_trace(gs, o, dr, 0.01, 3.0e38, any_hit=True, wide_stats=True)
         assert ((fetches > 0) & (fetches != 0xFFFF)).all() and (lost == 0).all()
+
+    # an update that moves vertices to NaN / inf on a live wide tree.  Those triangles get point boxes
+    # (never hittable anyway), every other node keeps exact outward planes, and the wide per-lane walk still
+    # equals the binary lockstep walk for the finite triangles that moved in the same update.
+    pos = scenes.moving_light_positions(sc, 77, 240, amplitude=0.2).copy()
+    plain = np.nonzero(~sc.emissive_mask())[0]               # not an emitter: the light tables stay finite
+    t_nan, t_inf = int(plain[1234]), int(plain[len(plain) // 2])
+    pos[t_nan, 4] = np.nan
+    pos[t_inf, 0] = np.inf
+    gs.update_positions(pos)
+    w, p, d = gs.wide_tree()
+    assert d == d0 and w.shape == w0.shape
+    _check_conservative(w, p, pos)
+    o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    dr = rng.normal(size=(n, 3)).astype(np.float32)
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    for any_hit in (False, True):
+        tl, pl = g.debug_trace(gs, o, dr, 0.01, 3.0e38, any_hit=any_hit, lockstep=False)
+        tk, pk = g.debug_trace(gs, o, dr, 0.01, 3.0e38, any_hit=any_hit, lockstep=True)
+        assert np.array_equal(pl, pk) and np.array_equal(tl, tk), ("nonfinite update", any_hit)
+        if not any_hit:
+            assert (pl >= 0).any() and not np.isin(pl, [t_nan, t_inf]).any()
 
 
 def test_c3_moving_lamps_on_live_wide_tree():

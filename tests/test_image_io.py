@@ -231,3 +231,76 @@ def test_jpeg_unsupported_variants_fail_loudly(tmp_path):
     bad.write_bytes(b"\xff\xd8\xff\xdb\x00")
     with pytest.raises(RestirError):
         decode_image(str(bad))
+
+
+def _jpeg_segments(data):
+    """(marker, offset of the length field, length) of every segment before the first SOS's entropy data."""
+    out, p = [], 2
+    while p + 4 <= len(data) and data[p] == 0xFF:
+        m = data[p + 1]
+        ln = (data[p + 2] << 8) | data[p + 3]
+        out.append((m, p + 2, ln))
+        if m == 0xDA:
+            break
+        p += 2 + ln
+    return out
+
+
+def test_jpeg_malformed_inputs_fail_cleanly(tmp_path):
+    """an over-subscribed DHT must be rejected before any lookahead-table write (it used to write
+    past the decoder's stack tables), an absurd SOF size must not commit gigabytes, and a garbage entropy
+    stream must decode to something or fail -- never crash.  Every failure is a clean RestirError (-1)."""
+    im = _jpeg_image(32, 32, "RGB", 7)
+    path = tmp_path / "ok.jpg"
+    im.save(path, "JPEG", quality=90)
+    good = bytearray(path.read_bytes())
+    segs = _jpeg_segments(good)
+
+    # 1. over-subscribed code lengths: three 1-bit codes (total count unchanged, so the segment stays well-formed)
+    bad = bytearray(good)
+    m, off, ln = next(s for s in segs if s[0] == 0xC4)
+    counts = off + 3                        # length (2) + table class/id (1)
+    take = 3
+    for i in range(15, 0, -1):
+        d = min(take, bad[counts + i])
+        bad[counts + i] -= d
+        take -= d
+        if not take:
+            break
+    assert take == 0
+    bad[counts] += 3
+    p1 = tmp_path / "oversub.jpg"
+    p1.write_bytes(bytes(bad))
+    with pytest.raises(RestirError, match="Huffman"):
+        decode_image(str(p1))
+
+    # 2. a 65535 x 65535 SOF in a file of a few hundred bytes
+    bad = bytearray(good)
+    m, off, ln = next(s for s in segs if s[0] in (0xC0, 0xC1, 0xC2))
+    bad[off + 3:off + 7] = b"\xff\xff\xff\xff"
+    p2 = tmp_path / "huge.jpg"
+    p2.write_bytes(bytes(bad))
+    with pytest.raises(RestirError, match="limit"):
+        decode_image(str(p2))
+
+    # 3. random entropy data after the SOS header (no 0xFF bytes, so no markers): any result, or a clean error
+    m, off, ln = segs[-1]
+    assert m == 0xDA
+    start = off + ln
+    rng = np.random.default_rng(3)
+    for trial in range(8):
+        junk = rng.integers(0, 255, size=len(good) - start - 2, dtype=np.uint8).tobytes()
+        p3 = tmp_path / f"junk{trial}.jpg"
+        p3.write_bytes(bytes(good[:start]) + junk + b"\xff\xd9")
+        try:
+            got = decode_image(str(p3))
+            assert got.size == 32 * 32 * 3
+        except RestirError:
+            pass
+    # 4. truncated right after the SOS header
+    p4 = tmp_path / "cut.jpg"
+    p4.write_bytes(bytes(good[:start + 3]))
+    try:
+        decode_image(str(p4))
+    except RestirError:
+        pass
