@@ -239,11 +239,13 @@ public:
               ranks_[0]->handle());
         ++frameCtr;
     }
-    // cost-balanced bands from n_frames of per-row wave times (resets the history)
-    void rebalance(int n_frames = 2, int min_rows = 8) {
+    // cost-balanced bands from n_frames of per-row wave times, then `refine` rounds of time-based refinement
+    // (-1: the library's default; resets the history)
+    void rebalance(int n_frames = 2, int min_rows = 8, int refine = -1) {
         produceRestir();                              // creates the group
         std::vector<const rs_scene*> scenes;
         for (auto* r : ranks_) scenes.push_back(r->scene_handle());
+        if (refine >= 0) check(rs_mgpu_set_rebalance_refine(m_, refine), ranks_[0]->handle());
         check(rs_mgpu_rebalance(m_, scenes.data(), &camera_, &params, frameCtr, n_frames, min_rows), ranks_[0]->handle());
         frameCtr = 0;
     }

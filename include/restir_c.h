@@ -439,6 +439,13 @@ int rs_mgpu_get_bands(const rs_mgpu* m, int32_t* bounds);
  * band >= max(min_rows, halo) rows; same split on every rank), resets the history. */
 int rs_mgpu_rebalance(rs_mgpu* m, const rs_scene* const* scenes, const rs_camera* camera,
                       const rs_frame_params* params, uint32_t first_frame, int n_frames, int min_rows);
+/* Then (rounds > 0, default 2) time-based refinement inside rs_mgpu_rebalance: each round renders frames with
+ * the current bands (gathered, frames in flight), all-reduces every rank's own time per frame (its frames'
+ * begin..shade span minus its halo exchanges, plus rank 0's gather), rescales each band's row costs to its
+ * time and balances again; the measured bands with the lowest maximum are kept.  rounds = 0: row costs only.
+ * rs_mgpu_rebalance_times: the last rebalance's measured ms per rank (world values) of measured round r. */
+int rs_mgpu_set_rebalance_refine(rs_mgpu* m, int rounds);
+int rs_mgpu_rebalance_times(const rs_mgpu* m, int round, double* ms);
 /* One frame.  gather != 0: bands -> rank 0's framebuffer; frame_rgb_host (rank 0, optional) receives it
  * (synchronous).  times (optional, synchronous): the first local rank's pass times. */
 int rs_mgpu_render_frame(rs_mgpu* m, const rs_scene* const* scenes, const rs_camera* camera,

@@ -2225,11 +2225,21 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
     const bool act = i0 < n;
     const uint32_t i = act ? i0 : n - 1;
     vec3 O = mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), D = mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    if (any >= 6 && any <= 10 && S.n_wnodes == 0u) {   // the 8-wide modes need the scene's wide tree
+    if (any >= 6 && any <= 12 && S.n_wnodes == 0u) {   // the 8-wide modes need the scene's wide tree
         if (act) { prim_out[i] = -1; t_out[i] = -1.0f; }
         return;
     }
-    if (any >= 8 && any <= 10) {  // timing probes of the 8-wide walk: 8 closest walk with the ray's tfar,
+    if (any == 11 || any == 12) {   // the wave-coherent walks over the 8-wide tree (rs_scene.h RS_WLOCK): 11 closest, 12 any
+        if (any == 11) {
+            const Hit h = closest_wlock(S, act, O, D, tn[i], tf[i]);
+            if (act) { prim_out[i] = h.prim; t_out[i] = h.prim >= 0 ? h.t : -1.0f; }
+        } else {
+            bool oc;
+            const float tni = tn[i], tfi = tf[i];
+            occluded_wlock_multi<1>(S, &act, O, &D, tni, &tfi, &oc);
+            if (act) { prim_out[i] = oc ? 1 : 0; t_out[i] = 0.0f; }
+        }
+    } else if (any >= 8 && any <= 10) {  // timing probes of the 8-wide walk: 8 closest walk with the ray's tfar,
         const vec3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);   // 9 any-hit without triangle tests,
         Hit h; h.t = tf[i]; h.u = h.v = 0.0f; h.prim = -1;        // 10 any-hit with statistics off
         uint32_t occ = 0u, lost = 0u;

@@ -88,6 +88,8 @@ struct rs_mgpu {
     ncclComm_t comm[kLanes] = {};
     // local mode: events ordering copies between the contexts' streams
     std::vector<hipEvent_t> ev_a, ev_b;
+    int refine = 2;                             // time-based refinement rounds of rs_mgpu_rebalance
+    std::vector<std::vector<double>> rebalance_ms;   // per measured round of the last rebalance: every rank's ms
     double* d_red = nullptr;                    // RCCL all-reduce scratch (rows of costs / a few scalars)
     size_t red_cap = 0;
     std::string err;
@@ -401,11 +403,50 @@ extern "C" int rs_mgpu_allreduce(rs_mgpu* m, double* values, int n, int op) {
     return m->allreduce(values, n, op);
 }
 
+extern "C" int rs_mgpu_set_rebalance_refine(rs_mgpu* m, int rounds) {
+    if (!m || rounds < 0 || rounds > 8) return RS_E_INVALID;
+    m->refine = rounds;
+    return RS_OK;
+}
+
+// Each rank's own time per frame with `bounds`: `warm` unmeasured frames (the history after a boundary move,
+// lazily grown buffers), then `n` frames with the gather.  A rank's time is its frames' begin..shade span
+// (rs_pass_times.total_ms, event ring, frames in flight as in production) minus the halo exchanges on its
+// stream (which include waiting for slower neighbours), plus -- on rank 0 -- the gather it receives.
+// All-reduced, so every rank sees the same vector and makes the same choice.
+static int measure_bands(rs_mgpu* m, const rs_scene* const* scenes, const rs_camera* cam, const rs_frame_params* P,
+                         uint32_t& frame, int warm, int n, std::vector<double>& t) {
+    if (int rc = rs_mgpu_reset_history(m)) return rc;   // the previous G-buffer rows of a moved band
+    for (int f = 0; f < warm; ++f)
+        if (int rc = rs_mgpu_render_frame(m, scenes, cam, P, frame++, 1, nullptr, nullptr)) return rc;
+    rs_pass_times sum{};
+    uint32_t nf = 0;
+    rs_mgpu_stats st{};
+    for (auto& g : m->ranks)
+        if (int rc = rs_get_timing_totals(g.ctx, &sum, &nf, 1)) return rc;
+    if (int rc = rs_mgpu_get_stats(m, &st, 1)) return rc;
+    for (int f = 0; f < n; ++f)
+        if (int rc = rs_mgpu_render_frame(m, scenes, cam, P, frame++, 1, nullptr, nullptr)) return rc;
+    if (int rc = rs_mgpu_get_stats(m, &st, 1)) return rc;
+    t.assign(m->world, 0.0);
+    for (size_t i = 0; i < m->ranks.size(); ++i) {
+        if (int rc = rs_get_timing_totals(m->ranks[i].ctx, &sum, &nf, 1)) return rc;
+        double v = sum.total_ms;
+        if (i == 0) {                           // the transfer spans are recorded on the first local rank's stream
+            v -= st.halo_ms;
+            if (m->rank_ids[0] == 0) v += st.gather_ms;
+        }
+        t[m->rank_ids[i]] = std::max(0.0, v) / std::max<uint32_t>(1, nf);
+    }
+    return m->allreduce(t.data(), m->world, 0);
+}
+
 extern "C" int rs_mgpu_rebalance(rs_mgpu* m, const rs_scene* const* scenes, const rs_camera* cam,
                                  const rs_frame_params* P, uint32_t first_frame, int n_frames, int min_rows) {
     if (!m || !cam || !P || n_frames < 1) return RS_E_INVALID;
     if (int rc = check_scenes(m, scenes)) return rc;
     if (m->world == 1) return RS_OK;
+    m->rebalance_ms.clear();
     for (auto& g : m->ranks) {
         if (int rc = rs_context_track_row_costs(g.ctx, 1)) return rc;
         std::vector<float> tmp(m->H);
@@ -423,8 +464,44 @@ extern "C" int rs_mgpu_rebalance(rs_mgpu* m, const rs_scene* const* scenes, cons
     if (int rc = m->allreduce(cost.data(), m->H, 0)) return rc;
     const int halo = mgpu::halo_rows(P->spatial_radius, P->do_spatial && P->spatial_passes > 0);
     std::vector<int> b;
-    if (!mgpu::balanced_bounds(cost, m->world, std::max(std::max(1, min_rows), halo), b))
+    const int rows = std::max(std::max(1, min_rows), halo);
+    if (!mgpu::balanced_bounds(cost, m->world, rows, b))
         return m->error(RS_E_INVALID, "rs_mgpu_rebalance: bands of min_rows do not fit");
     m->bounds = b;
+    // Time-based refinement: row costs predict a band's time only to about +-7 % (the per-row
+    // wave time misses what a band pays as a launch: rounds of waves, the split pass, halo and gather).  Each
+    // round measures every rank's time with the current bounds, rescales each band's row costs so that they sum
+    // to its measured time, and balances again; the bounds with the lowest measured maximum are kept.  (C4 at
+    // 8 ranks, every band timed alone on one MI355X: slowest band 9.09 -> 8.96 -> 8.80 ms over two rounds,
+    // profiles/r04_band_refine_C4_N8.txt.)
+    uint32_t frame = first_frame + (uint32_t)n_frames;
+    std::vector<int> best = b;
+    double best_max = 0.0;
+    const int n_meas = std::max(n_frames, 6);
+    for (int it = 0; it <= m->refine && m->refine > 0; ++it) {
+        std::vector<double> t;
+        if (int rc = measure_bands(m, scenes, cam, P, frame, 2, n_meas, t)) return rc;
+        const double mx = *std::max_element(t.begin(), t.end());
+        m->rebalance_ms.push_back(t);
+        if (it == 0 || mx < best_max) { best_max = mx; best = m->bounds; }
+        if (it == m->refine) break;
+        for (int r = 0; r < m->world; ++r) {    // band r's rows rescaled to its measured time
+            double c = 0.0;
+            for (int y = m->bounds[r]; y < m->bounds[r + 1]; ++y) c += cost[y];
+            if (c > 0.0 && t[r] > 0.0)
+                for (int y = m->bounds[r]; y < m->bounds[r + 1]; ++y) cost[y] *= t[r] / c;
+        }
+        std::vector<int> nb;
+        if (!mgpu::balanced_bounds(cost, m->world, rows, nb)) break;
+        if (nb == m->bounds) break;              // converged: nothing left to measure
+        m->bounds = nb;
+    }
+    m->bounds = best;
     return rs_mgpu_reset_history(m);   // the previous G-buffer rows of a moved band belong to another rank
+}
+
+extern "C" int rs_mgpu_rebalance_times(const rs_mgpu* m, int round, double* ms) {
+    if (!m || !ms || round < 0 || round >= (int)m->rebalance_ms.size()) return RS_E_INVALID;
+    for (int r = 0; r < m->world; ++r) ms[r] = m->rebalance_ms[round][r];
+    return RS_OK;
 }

@@ -83,11 +83,24 @@ class MultiGpuFrame:
         arr = (ctypes.c_int32 * (self.world + 1))(*b)
         self._check(self.lib.rs_mgpu_set_bands(self.h, arr))
 
-    def rebalance(self, scenes, camera, params, first_frame: int = 0, n_frames: int = 2, min_rows: int = 8):
+    def rebalance(self, scenes, camera, params, first_frame: int = 0, n_frames: int = 2, min_rows: int = 8,
+                  refine: int | None = None):
+        """Cost-balanced bands (rs_mgpu_rebalance): row costs, then `refine` rounds of time-based refinement
+        (None: the library's default, 2; 0: row costs only).  rebalance_times() has the measured rounds."""
+        if refine is not None:
+            self._check(self.lib.rs_mgpu_set_rebalance_refine(self.h, int(refine)))
         cam = camera_desc(camera)
         self._check(self.lib.rs_mgpu_rebalance(self.h, self._scenes(scenes), ctypes.byref(cam), ctypes.byref(params),
                                                int(first_frame), int(n_frames), int(min_rows)))
         return self.bands()
+
+    def rebalance_times(self):
+        """Every rank's measured ms per frame for each measured refinement round of the last rebalance."""
+        out = []
+        buf = (ctypes.c_double * self.world)()
+        while self.lib.rs_mgpu_rebalance_times(self.h, len(out), buf) == 0:
+            out.append([float(v) for v in buf])
+        return out
 
     def render(self, scenes, camera, params, frame_index: int, gather: bool = True, copy_out: bool = False,
                timed: bool = False):

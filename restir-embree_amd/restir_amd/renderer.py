@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = [
     "rs_host_alloc", "rs_host_free", "rs_mgpu_unique_id", "rs_mgpu_create", "rs_mgpu_create_local",
     "rs_mgpu_destroy", "rs_mgpu_set_bands", "rs_mgpu_get_bands", "rs_mgpu_rebalance", "rs_mgpu_render_frame",
     "rs_mgpu_frame_device_ptr", "rs_mgpu_reset_history", "rs_mgpu_allreduce", "rs_mgpu_get_stats",
+    "rs_mgpu_set_rebalance_refine", "rs_mgpu_rebalance_times",
     "rs_denoiser_check_weights", "rs_denoiser_create", "rs_denoiser_create_from_file", "rs_denoiser_info_get",
     "rs_denoiser_execute", "rs_denoise_frame", "rs_context_set_denoiser", "rs_denoiser_set_timing",
     "rs_denoiser_last_ms", "rs_denoiser_layer_ms", "rs_denoiser_get_scale", "rs_denoiser_dump", "rs_denoiser_destroy",
@@ -221,6 +222,8 @@ def load_library(path: str = LIB_PATH):
     L.rs_mgpu_reset_history.argtypes = [vp]
     L.rs_mgpu_allreduce.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i32, i32]
     L.rs_mgpu_get_stats.argtypes = [vp, vp, i32]
+    L.rs_mgpu_set_rebalance_refine.argtypes = [vp, i32]
+    L.rs_mgpu_rebalance_times.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double)]
     L.rs_denoiser_check_weights.argtypes = [vp, ctypes.c_size_t, vp]
     L.rs_denoiser_create.argtypes = [vp, vp, ctypes.c_size_t, ctypes.POINTER(vp)]
     L.rs_denoiser_create_from_file.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
@@ -582,10 +585,13 @@ class Renderer:
         return self.frame_data if copy_out else None
 
     def debug_trace(self, scene: Scene, o, d, tnear, tfar, any_hit: bool, lockstep: bool = True,
-                    stats: bool = False, wide_stats: bool = False):
+                    stats: bool = False, wide_stats: bool = False, wave_wide: bool = False):
         """Raw BVH queries.  stats=True: per-lane skip-pointer walk statistics instead -- returns
         (visits, triangle_tests) int arrays per ray; wide_stats=True: the 8-wide walk's (node fetches,
-        triangle tests, stack overflow flags)."""
+        triangle tests, stack overflow flags); wave_wide=True: the wave-coherent walk over the 8-wide tree
+        (rs_scene.h occluded_wlock_multi / closest_wlock; -1 results when the scene has no wide tree)."""
+        if wave_wide:
+            return self._debug_trace(scene, o, d, tnear, tfar, 12 if any_hit else 11)
         if wide_stats:
             t, prim = self._debug_trace(scene, o, d, tnear, tfar, 7 if any_hit else 6)
             p = prim.view(np.uint32)

@@ -884,7 +884,7 @@ int main(int argc, char** argv) {
                 std::sort(order.begin(), order.end());
                 for (size_t i = 0; i < order.size(); ++i) erank[order[i].second] = (uint32_t)((i << RB) / order.size());
             }
-            double st[4] = {0, 0, 0, 0}, ds[4] = {0, 0, 0, 0}, bu[4] = {0, 0, 0, 0};
+            double st[4] = {0, 0, 0, 0}, ds[4] = {0, 0, 0, 0}, bu[4] = {0, 0, 0, 0}, wu[4] = {0, 0, 0, 0};
             long nwave = 0;
             std::mt19937 rg2(7);
             const int stride = getenv("WSTRIDE") ? atoi(getenv("WSTRIDE")) : 4;   // every stride-th tile in x and y
@@ -934,6 +934,12 @@ int main(int argc, char** argv) {
                             std::sort(u.begin(), u.end());
                             bu[g] += std::unique(u.begin(), u.end()) - u.begin();
                         }
+                        for (int c = 0; c < K; ++c) {   // wide lockstep: the wave fetches the union of its lanes' wide nodes
+                            std::vector<uint32_t> u;
+                            for (int i = 0; i < 64; ++i) { auto& q = seq[key[g][64 * c + i] & 4095]; u.insert(u.end(), q.begin(), q.end()); }
+                            std::sort(u.begin(), u.end());
+                            wu[g] += std::unique(u.begin(), u.end()) - u.begin();
+                        }
                         for (int c = 0; c < K; ++c) {
                             size_t T = 0;
                             for (int i = 0; i < 64; ++i) T = std::max(T, seq[key[g][64 * c + i] & 4095].size());
@@ -949,8 +955,9 @@ int main(int argc, char** argv) {
                 }
             printf("wave coherence (8x8 tile, K=%d candidates, %ld waves):\n", K, nwave);
             for (int g = 0; g < 4; ++g)
-                printf("  %-26s steps per wave %.1f, distinct node fetches per wave %.1f (per step %.2f) | binary lockstep union %.1f\n",
-                       names[g], st[g] / nwave, ds[g] / nwave, ds[g] / st[g], bu[g] / nwave);
+                printf("  %-26s steps per wave %.1f, distinct node fetches per wave %.1f (per step %.2f) | binary lockstep union %.1f"
+                       " | wide lockstep union %.1f\n",
+                       names[g], st[g] / nwave, ds[g] / nwave, ds[g] / st[g], bu[g] / nwave, wu[g] / nwave);
         }
         double wsum = 0; for (int v : wave_it) wsum += v;
         printf("emu: primary iters %.2f tris %.2f | bounce iters %.2f tris %.2f | shadow iters %.2f tris %.2f lost %.4f max stack %d wave-max iters %.1f | mismatches %ld | nodes %zu\n",

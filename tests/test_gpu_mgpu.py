@@ -70,8 +70,12 @@ def test_local_mgpu_rebalance_and_frames_in_flight():
         r.set_traversal("lockstep")
     ss = [r.load_scene(sc) for r in rs]
     m = MultiGpuFrame(rs)
-    bands = m.rebalance(ss, cams[0], prm, 0, 2, 6)
+    m.rebalance(ss, cams[0], prm, 0, 2, 6, refine=0)              # row costs only: nothing measured
+    assert m.rebalance_times() == []
+    bands = m.rebalance(ss, cams[0], prm, 0, 2, 6)                 # + the default 2 time-based rounds
     assert bands != [(0, 24), (24, 48), (48, 72)] and all(b - a >= 6 for a, b in bands), bands
+    rounds = m.rebalance_times()                                   # every rank timed in every measured round
+    assert 1 <= len(rounds) <= 3 and all(len(t) == world and min(t) > 0 for t in rounds), rounds
     clones = []
     for f, c in enumerate(cams):
         m.render(ss, c, prm, f)

@@ -79,6 +79,16 @@ def test_bvh_queries_bit_exact(scene_fn):
         assert np.array_equal(t, tr)
         _, anyg = g.debug_trace(gs, o, d, np.full(n, 0.01, np.float32), tf, any_hit=True, lockstep=lockstep)
         assert np.array_equal(anyg, anyr)
+    if gs.wide_tree() is not None:          # the wave-coherent walk over the 8-wide tree (rs_scene.h RS_WLOCK)
+        t, prim = g.debug_trace(gs, o, d, 0.01, 3.0e38, any_hit=False, wave_wide=True)
+        assert np.array_equal(prim, pr) and np.array_equal(t, tr)
+        _, anyg = g.debug_trace(gs, o, d, np.full(n, 0.01, np.float32), tf, any_hit=True, wave_wide=True)
+        assert np.array_equal(anyg, anyr)
+        # coherent waves too: 64 rays from one point per wave (shadow rays of one pixel neighbourhood)
+        oc = np.repeat(o[:n // 64], 64, axis=0)
+        tc, pc = os_.trace_closest(oc, d[:len(oc)], 0.01, 3.0e38)
+        t, prim = g.debug_trace(gs, oc, d[:len(oc)], 0.01, 3.0e38, any_hit=False, wave_wide=True)
+        assert np.array_equal(prim, pc) and np.array_equal(t, tc)
 
 
 def test_bvh_degenerate_scenes():
