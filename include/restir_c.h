@@ -183,6 +183,19 @@ int rs_scene_rebuild(rs_scene* scene);
 /* Scene statistics: n_tris, n_emissive, n_bvh_nodes, bvh build time (ms). */
 int rs_scene_info(const rs_scene* scene, uint32_t* n_tris, uint32_t* n_emissive, uint32_t* n_nodes,
                   float* build_ms);
+/* The scene's ray-query structure: the 8-wide tree of the per-lane walks (wide_nodes > 0, wide_depth its deepest
+ * level) or, without one, the reason (status) -- the walks then take the binary tree's skip pointers, with the same
+ * hits.  A tree the walk's 8-entry group stack cannot hold (no SAH collapse within depth 8) is RS_WIDE_TOO_DEEP. */
+enum {
+    RS_WIDE_LIVE = 0,        /* the per-lane walks use the 8-wide tree */
+    RS_WIDE_NONFINITE = 1,   /* a non-finite vertex coordinate at build time */
+    RS_WIDE_TOO_DEEP = 2,    /* no collapse within the walk's stack depth (8 levels) */
+    RS_WIDE_TOO_MANY = 3,    /* >= 2^24 triangles (the node word's child index) */
+    RS_WIDE_EMPTY = 4,       /* no triangles */
+    RS_WIDE_OFF = 5,         /* disabled (RESTIR_WIDE=off) */
+    RS_WIDE_ERROR = 6        /* the build failed (device error / allocation) */
+};
+int rs_scene_walk_info(const rs_scene* scene, uint32_t* wide_nodes, int32_t* wide_depth, int32_t* status);
 
 /* ---- render(frame) (SimpleGuiDX11::produceRestir) ----------------------------------------- */
 /* Renders one frame: G-buffer -> initial RIS -> [visibility] -> [temporal, if a previous frame

@@ -1289,6 +1289,15 @@ extern "C" int rs_debug_wide_tree(const rs_scene* s, uint32_t* n_nodes, uint32_t
     return RS_OK;
 }
 
+extern "C" int rs_scene_walk_info(const rs_scene* s, uint32_t* wide_nodes, int32_t* wide_depth, int32_t* status) {
+    if (!s) return fail(nullptr, RS_E_INVALID, "rs_scene_walk_info: null scene");
+    const bool on = s->wide_on && s->wide.nodes;
+    if (wide_nodes) *wide_nodes = on ? s->wide.n_nodes : 0u;
+    if (wide_depth) *wide_depth = on ? s->wide.depth : -1;
+    if (status) *status = on ? RS_WIDE_LIVE : (s->wide.status ? s->wide.status : RS_WIDE_TOO_DEEP);
+    return RS_OK;
+}
+
 extern "C" int rs_scene_info(const rs_scene* s, uint32_t* n_tris, uint32_t* n_emissive, uint32_t* n_nodes,
                              float* build_ms) {
     if (!s) return fail(nullptr, RS_E_INVALID, "rs_scene_info: null scene");

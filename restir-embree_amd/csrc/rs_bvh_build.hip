@@ -26,6 +26,7 @@
 #include <algorithm>
 #include "rs_refit.h"
 #include "rs_wide.h"
+#include "../../include/restir_c.h"
 
 namespace rs {
 
@@ -644,12 +645,16 @@ int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, 
               WideBvh* wide, std::string& err) {
     const char* e = getenv("RESTIR_BVH");
     const char* w = getenv("RESTIR_WIDE");
-    if (w && std::string(w) == "off") wide = nullptr;
+    if (w && std::string(w) == "off") { if (wide) { wide_free(*wide); wide->status = RS_WIDE_OFF; } wide = nullptr; }
     const int rc = (e && std::string(e) == "lbvh") ? build_bvh_lbvh(d_pos, n, st, d_nodes, n_nodes, d_tris, err)
                                                    : build_bvh_ploc(d_pos, n, st, d_nodes, n_nodes, d_tris, err);
     if (rc != 0 || !wide) return rc;
     std::string werr;
-    if (build_wide_gpu(d_pos, (int)n, st, wide, werr) != 0) wide_free(*wide);   // optional: binary walks
+    if (const int wr = build_wide_gpu(d_pos, (int)n, st, wide, werr); wr != 0) {   // optional: binary walks
+        const int why = wr < 0 ? RS_WIDE_ERROR : (wide->status ? wide->status : RS_WIDE_ERROR);
+        wide_free(*wide);
+        wide->status = why;
+    }
     (void)hipGetLastError();
     return 0;
 }

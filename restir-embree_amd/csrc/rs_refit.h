@@ -39,6 +39,7 @@ struct WideBvh {
     uint32_t n_tris = 0;
     int depth = 0;               // deepest level (root = 0)
     int lvl[kWideLevels + 1] = {};   // breadth-first level offsets: level L = nodes [lvl[L], lvl[L + 1])
+    int status = 0;              // why there is no tree (include/restir_c.h RS_WIDE_*): 0 live
 };
 
 constexpr int kRefitBlock = 1024;

@@ -32,6 +32,7 @@
 #include <vector>
 #include <algorithm>
 #include "rs_refit.h"
+#include "../../include/restir_c.h"
 #include "rs_wide.h"
 
 namespace rs {
@@ -204,39 +205,55 @@ __global__ void __launch_bounds__(kB) k_seg_bins(const Chunk* __restrict__ ch, c
     }
 }
 
-// one thread per segment: build_sah_host's binned loop in the same order and precision
-__global__ void k_seg_choose(const Seg* __restrict__ segs, int ns, const SegAcc* __restrict__ acc, SegDec* dec,
-                             float4* nlo, float4* nhi) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+// one workgroup per segment: build_sah_host's binned loop, same precision and the same choice.  Thread (a, b) forms
+// the left box (bins 0..b-1) and the right box (bins b..31) of split b on axis a from the bins staged in LDS -- the
+// unions are exact float min / max, so any order gives the host's boxes -- and the lowest cost wins with the host's
+// tie rule (first axis, then first bin).  (One thread per segment walking the 96 bins through global memory took
+// 0.11 ms per level, 1.5 ms of C3's build: VERDICT r4.)
+constexpr int kChooseThreads = 128;
+__global__ void __launch_bounds__(kChooseThreads) k_seg_choose(const Seg* __restrict__ segs, int ns, const SegAcc* __restrict__ acc,
+                                                               SegDec* dec, float4* nlo, float4* nhi) {
+    const int s = blockIdx.x;
     if (s >= ns) return;
     const SegAcc& A = acc[s];
-    const Seg S = segs[s];
+    __shared__ int s_cnt[3][kBins];
+    __shared__ float s_lo[3][kBins][3], s_hi[3][kBins][3];
+    __shared__ double s_cost[3 * kBins];
+    for (int i = threadIdx.x; i < 3 * kBins; i += kChooseThreads) {
+        const int a = i / kBins, b = i % kBins;
+        s_cnt[a][b] = A.cnt[a][b];
+        for (int k = 0; k < 3; ++k) { s_lo[a][b][k] = o2f(A.blo[a][b][k]); s_hi[a][b][k] = o2f(A.bhi[a][b][k]); }
+    }
+    __syncthreads();
     float clo[3], chi[3];
     for (int a = 0; a < 3; ++a) { clo[a] = o2f(A.cb[a]); chi[a] = o2f(A.cb[3 + a]); }
+    if (threadIdx.x < 3 * kBins) {
+        const int a = threadIdx.x / kBins, b = threadIdx.x % kBins;
+        double cost = -1.0;                                   // -1: no split here
+        if (b >= 1 && chi[a] > clo[a]) {
+            float llo[3] = {kEmpty, kEmpty, kEmpty}, lhi[3] = {-kEmpty, -kEmpty, -kEmpty};
+            float rlo[3] = {kEmpty, kEmpty, kEmpty}, rhi[3] = {-kEmpty, -kEmpty, -kEmpty};
+            int cl = 0, cr = 0;
+            for (int j = 0; j < kBins; ++j) {
+                if (j < b) {
+                    for (int k = 0; k < 3; ++k) { llo[k] = w_min(llo[k], s_lo[a][j][k]); lhi[k] = w_max(lhi[k], s_hi[a][j][k]); }
+                    cl += s_cnt[a][j];
+                } else {
+                    for (int k = 0; k < 3; ++k) { rlo[k] = w_min(rlo[k], s_lo[a][j][k]); rhi[k] = w_max(rhi[k], s_hi[a][j][k]); }
+                    cr += s_cnt[a][j];
+                }
+            }
+            if (cl && cr) cost = half_area_d(llo, lhi) * cl + half_area_d(rlo, rhi) * cr;
+        }
+        s_cost[threadIdx.x] = cost;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     double best = 1e300;
     int bax = -1, bb = 0;
-    for (int a = 0; a < 3; ++a) {
-        if (!(chi[a] > clo[a])) continue;
-        double ra[kBins];
-        int rc[kBins];
-        float rlo[3] = {kEmpty, kEmpty, kEmpty}, rhi[3] = {-kEmpty, -kEmpty, -kEmpty};
-        int c = 0;
-        for (int b = kBins - 1; b >= 1; --b) {
-            for (int k = 0; k < 3; ++k) { rlo[k] = w_min(rlo[k], o2f(A.blo[a][b][k])); rhi[k] = w_max(rhi[k], o2f(A.bhi[a][b][k])); }
-            c += A.cnt[a][b];
-            ra[b] = c ? half_area_d(rlo, rhi) : 0.0;
-            rc[b] = c;
-        }
-        float llo[3] = {kEmpty, kEmpty, kEmpty}, lhi[3] = {-kEmpty, -kEmpty, -kEmpty};
-        c = 0;
-        for (int b = 1; b < kBins; ++b) {
-            for (int k = 0; k < 3; ++k) { llo[k] = w_min(llo[k], o2f(A.blo[a][b - 1][k])); lhi[k] = w_max(lhi[k], o2f(A.bhi[a][b - 1][k])); }
-            c += A.cnt[a][b - 1];
-            if (!c || !rc[b]) continue;
-            const double cost = half_area_d(llo, lhi) * c + ra[b] * rc[b];
-            if (cost < best) { best = cost; bax = a; bb = b; }
-        }
-    }
+    for (int i = 0; i < 3 * kBins; ++i)                      // axis-major, bin-ascending: the host's loop order
+        if (s_cost[i] >= 0.0 && s_cost[i] < best) { best = s_cost[i]; bax = i / kBins; bb = i % kBins; }
+    const Seg S = segs[s];
     SegDec D;
     D.bax = bax; D.bb = bb; D.left = 0; D.pad = 0;
     D.mid = A.imin + (A.imax - A.imin) / 2;
@@ -484,11 +501,39 @@ __global__ void __launch_bounds__(kB) k_small(const SmallSeg* __restrict__ segs,
 }
 
 // ---------------------------------------------------------------- 4 SAH-optimal collapse tables
-__global__ void k_depth_count(const int* __restrict__ depth, int m, int* cnt) {
+// The internal nodes bucketed by depth.  A workgroup first counts its nodes per depth in LDS and makes ONE global
+// atomic per depth it holds (the same-address global atomics of one thread per node serialised: 1.22 ms per
+// launch at C3's 248 k nodes).  Order inside a depth bucket is free: k_dp_level's nodes of one
+// depth are independent.  nd <= kDepthLds (the host falls back to the per-node atomics above it).
+constexpr int kDepthLds = 1024;
+__global__ void k_depth_count(const int* __restrict__ depth, int m, int nd, int* cnt) {
+    __shared__ int h[kDepthLds];
+    for (int d = threadIdx.x; d < nd; d += blockDim.x) h[d] = 0;
+    __syncthreads();
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) atomicAdd(&h[depth[i]], 1);
+    __syncthreads();
+    for (int d = threadIdx.x; d < nd; d += blockDim.x)
+        if (h[d]) atomicAdd(&cnt[d], h[d]);
+}
+__global__ void k_depth_fill(const int* __restrict__ depth, int m, int nd, int* fill, int* order) {
+    __shared__ int h[kDepthLds], base[kDepthLds];
+    for (int d = threadIdx.x; d < nd; d += blockDim.x) h[d] = 0;
+    __syncthreads();
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int dep = i < m ? depth[i] : 0;
+    const int rank = i < m ? atomicAdd(&h[dep], 1) : 0;
+    __syncthreads();
+    for (int d = threadIdx.x; d < nd; d += blockDim.x)
+        if (h[d]) base[d] = atomicAdd(&fill[d], h[d]);
+    __syncthreads();
+    if (i < m) order[base[dep] + rank] = i;
+}
+__global__ void k_depth_count_flat(const int* __restrict__ depth, int m, int* cnt) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) atomicAdd(&cnt[depth[i]], 1);
 }
-__global__ void k_depth_fill(const int* __restrict__ depth, int m, int* fill, int* order) {
+__global__ void k_depth_fill_flat(const int* __restrict__ depth, int m, int* fill, int* order) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) order[atomicAdd(&fill[depth[i]], 1)] = i;
 }
@@ -648,8 +693,8 @@ struct Scratch {
 int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::string& err) {
     using namespace wb;
     *w = WideBvh{};
-    if (n <= 0) return 1;
-    if (n >= (1 << 24)) return 1;                    // the node word's 24-bit child index
+    if (n <= 0) { w->status = RS_WIDE_EMPTY; return 1; }
+    if (n >= (1 << 24)) { w->status = RS_WIDE_TOO_MANY; return 1; }   // the node word's 24-bit child index
     Scratch X;
     const int total = 2 * n - 1, m = n - 1;          // binary nodes, internal nodes
     float4 *tlo, *thi, *tcen, *nlo, *nhi;
@@ -664,7 +709,7 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
     int h_bad = 0;
     WB_HIP(hipMemcpyAsync(&h_bad, bad, sizeof(int), hipMemcpyDeviceToHost, st));
     WB_HIP(hipStreamSynchronize(st));
-    if (h_bad) return 1;                             // non-finite geometry: no wide tree
+    if (h_bad) { w->status = RS_WIDE_NONFINITE; return 1; }   // non-finite geometry: no wide tree
     int root = 0, max_depth = 0;
     // ---- source tree
     if (n >= 2) {
@@ -699,7 +744,7 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
             k_acc_init<<<ns, kB, 0, st>>>(d_acc, ns);
             k_seg_bounds<<<nc, kB, 0, st>>>(d_ch, idx, tlo, thi, tcen, d_acc);
             k_seg_bins<<<nc, kB, 0, st>>>(d_ch, idx, tlo, thi, tcen, d_acc);
-            k_seg_choose<<<(ns + 63) / 64, 64, 0, st>>>(d_seg, ns, d_acc, d_dec, nlo, nhi);
+            k_seg_choose<<<ns, kChooseThreads, 0, st>>>(d_seg, ns, d_acc, d_dec, nlo, nhi);
             k_seg_side<<<nc, kB, 0, st>>>(d_ch, idx, tcen, d_dec, d_side, d_cl);
             k_seg_scan<<<(ns + 63) / 64, 64, 0, st>>>(d_seg, d_segch, ns, d_ch, d_cl, d_coff, d_dec);
             k_seg_scatter<<<nc, kB, 0, st>>>(d_ch, d_seg, idx, d_side, d_coff, d_dec, tmp);
@@ -753,14 +798,16 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
         const int nd = max_depth + 1;
         WB_CHECK(X.get(&cnt, nd) && X.get(&order, m), "scratch allocation failed");
         WB_HIP(hipMemsetAsync(cnt, 0, nd * sizeof(int), st));
-        k_depth_count<<<(m + kB - 1) / kB, kB, 0, st>>>(depth, m, cnt);
+        if (nd <= kDepthLds) k_depth_count<<<(m + kB - 1) / kB, kB, 0, st>>>(depth, m, nd, cnt);
+        else k_depth_count_flat<<<(m + kB - 1) / kB, kB, 0, st>>>(depth, m, cnt);
         std::vector<int> hc(nd), off(nd + 1, 0);
         WB_HIP(hipMemcpyAsync(hc.data(), cnt, nd * sizeof(int), hipMemcpyDeviceToHost, st));
         WB_HIP(hipStreamSynchronize(st));
         for (int d = 0; d < nd; ++d) off[d + 1] = off[d] + hc[d];
         WB_CHECK(off[nd] == m, "depth buckets");
         WB_HIP(hipMemcpyAsync(cnt, off.data(), nd * sizeof(int), hipMemcpyHostToDevice, st));
-        k_depth_fill<<<(m + kB - 1) / kB, kB, 0, st>>>(depth, m, cnt, order);
+        if (nd <= kDepthLds) k_depth_fill<<<(m + kB - 1) / kB, kB, 0, st>>>(depth, m, nd, cnt, order);
+        else k_depth_fill_flat<<<(m + kB - 1) / kB, kB, 0, st>>>(depth, m, cnt, order);
         for (int d = nd - 1; d >= 0; --d) {
             const int b = off[d], e = off[d + 1];
             if (e > b) k_dp_level<<<(e - b + 127) / 128, 128, 0, st>>>(order, b, e, n, nlo, nhi, S, open, split);
@@ -770,7 +817,7 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
         WB_HIP(hipMemcpyAsync(&s_root, S + (size_t)(root - n) * kG * 8 + (kGmax + 1) * 8, sizeof(float),
                               hipMemcpyDeviceToHost, st));
         WB_HIP(hipStreamSynchronize(st));
-        if (!(s_root < 3.0e38f)) return 1;           // no plan within the walk's depth: skip-pointer walks
+        if (!(s_root < 3.0e38f)) { w->status = RS_WIDE_TOO_DEEP; return 1; }   // no plan within the walk's depth
     }
     // ---- wide nodes, breadth first
     WideQ* wq = nullptr;

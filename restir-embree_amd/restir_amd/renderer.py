@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = [
     "rs_context_create", "rs_context_destroy", "rs_last_error", "rs_scene_create", "rs_scene_load_obj",
     "rs_scene_destroy", "rs_scene_info", "rs_render_frame", "rs_get_frame_device_ptr", "rs_reset_history",
     "rs_synchronize", "rs_dump_gbuffer", "rs_dump_reservoirs", "rs_tile_begin", "rs_tile_halo_ptr",
-    "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_debug_wide_tree",
+    "rs_tile_temporal", "rs_tile_spatial", "rs_tile_finish", "rs_debug_trace", "rs_debug_wide_tree", "rs_scene_walk_info",
     "rs_context_set_traversal",
     "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions", "rs_post_frame",
     "rs_post_reset", "rs_scene_rebuild", "rs_render_direct_mis", "rs_scene_create_textured", "rs_scene_set_sky",
@@ -173,6 +173,7 @@ def load_library(path: str = LIB_PATH):
     L.rs_tile_finish.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(PassTimes)]
     L.rs_debug_trace.argtypes = [vp, vp, u32, fp, fp, fp, fp, i32, fp, ctypes.POINTER(ctypes.c_int32)]
     L.rs_debug_wide_tree.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_int32), vp, vp]
+    L.rs_scene_walk_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
     L.rs_context_set_traversal.argtypes = [vp, i32]
     ip = ctypes.POINTER(ctypes.c_int32)
     L.rs_context_get_traversal.argtypes = [vp, vp, ip, ip, ip]
@@ -328,6 +329,15 @@ class Scene:
         r._check(r.lib.rs_scene_info(self.h, ctypes.byref(n_tris), ctypes.byref(n_emis), ctypes.byref(n_nodes),
                                      ctypes.byref(ms)))
         self.n_nodes, self.build_ms = n_nodes.value, ms.value
+
+    WIDE_STATUS = {0: "live", 1: "nonfinite", 2: "too_deep", 3: "too_many", 4: "empty", 5: "off", 6: "error"}
+
+    def walk_info(self) -> dict:
+        """rs_scene_walk_info: the 8-wide tree's nodes and depth, or why the scene has none (status name)."""
+        r = self.renderer
+        nn, dp, st = ctypes.c_uint32(), ctypes.c_int32(), ctypes.c_int32()
+        r._check(r.lib.rs_scene_walk_info(self.h, ctypes.byref(nn), ctypes.byref(dp), ctypes.byref(st)))
+        return {"wide_nodes": int(nn.value), "wide_depth": int(dp.value), "status": self.WIDE_STATUS.get(st.value, st.value)}
 
     def wide_tree_nodes(self) -> int:
         """Nodes of the scene's 8-wide tree (0: none -- the per-lane walks take the skip pointers)."""

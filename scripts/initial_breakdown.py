@@ -35,6 +35,7 @@ def main():
         ("A8 B1", dict(m_area=8)),
         ("A16 B1", dict(m_area=16)),
         ("A32 B1 vis-pass (no shadow rays in initial)", dict(do_visibility_pass=1)),
+        ("A32 B0 vis-pass (G-buffer + 32 samples, no rays)", dict(m_brdf=0, do_visibility_pass=1)),
         ("A1 B0 vis-pass (G-buffer + 1 sample)", dict(m_area=1, m_brdf=0, do_visibility_pass=1)),
     ]
     lib = os.path.basename(os.environ.get("RESTIR_LIB", "default"))

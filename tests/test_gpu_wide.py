@@ -66,6 +66,18 @@ def _nonfinite():
     return _scene_from_positions(p)
 
 
+def _chain(n, ratio):
+    """n triangles side by side along x, each `ratio` x the size of the previous: a binned / swept SAH split peels
+    off the largest triangle at every level, so the source tree is a chain of depth n - 1 (the SAH-optimal 8-wide
+    collapse of 100 such triangles needs exactly 8 levels; of 110, more than the walk's group stack holds)"""
+    pos, x = [], 0.0
+    for i in range(n):
+        sz = ratio ** i
+        pos.append([x, 0.0, 0.0, x + sz, 0.0, 0.0, x, sz, 0.0])
+        x += sz
+    return np.array(pos, np.float32)
+
+
 CASES = {
     "c2": lambda: scenes.cornell_many_lights(1024),
     "c3": lambda: scenes.sponza_like(),
@@ -74,6 +86,7 @@ CASES = {
     "soup5k": lambda: _scene_from_positions(_soup(5000, 3)),
     "coincident": lambda: _scene_from_positions(_soup(1500, 4, dup=700)),
     "nonfinite": _nonfinite,             # the wide tree is optional -- the scene loads without one
+    "depth8": lambda: _scene_from_positions(_chain(100, 1.5)),   # exactly the walk's stack depth
 }
 
 
@@ -225,3 +238,44 @@ def test_c3_moving_lamps_on_live_wide_tree():
         frac, mean = float((rel <= 1e-4).mean()), float(rel.mean())
         print(f"[parity] C3 moving lamps frame {f}: {100 * frac:.4f} % within 1e-4, mean {mean:.3g}")
         assert frac >= 0.995 and mean <= 1e-4, (f, frac, mean)
+
+
+def test_deep_tree_falls_back_to_skip_walks():
+    """a scene whose SAH-optimal collapse does not fit the walk's 8-level group stack (_chain(110)) loads
+    without a wide tree; rs_scene_walk_info says why (too_deep), the host restatement agrees (no plan within depth 8),
+    and the per-lane walks -- on the skip pointers now -- return the lockstep walks' and the oracle's hits bit for
+    bit.  The 100-triangle chain (depth exactly 8) keeps its tree (CASES["depth8"] above)."""
+    pos = _chain(110, 1.5)
+    assert _host_tree(pos) is None
+    sc = _scene_from_positions(pos)
+    g = Renderer(8, 8)
+    gs = g.load_scene(sc)
+    assert gs.walk_info() == {"wide_nodes": 0, "wide_depth": -1, "status": "too_deep"}, gs.walk_info()
+    assert gs.wide_tree() is None
+    ok = g.load_scene(_scene_from_positions(_chain(100, 1.5)))
+    info = ok.walk_info()
+    assert info["status"] == "live" and info["wide_depth"] == 8 and info["wide_nodes"] > 0, info
+    # rays aimed at a random point of a random triangle from a scale-relative distance (every size class is hit;
+    # a fifth of them in random directions)
+    rng = np.random.default_rng(4)
+    n = 8000
+    tri = rng.integers(0, len(pos), n)
+    p3 = pos.reshape(-1, 3, 3).astype(np.float64)
+    b = rng.dirichlet((1.0, 1.0, 1.0), n)
+    tgt = np.einsum("nk,nkc->nc", b, p3[tri])
+    size = p3[tri, 1, 0] - p3[tri, 0, 0]
+    o = (tgt + rng.normal(size=(n, 3)) * size[:, None] * 2.0).astype(np.float32)
+    d = tgt - o.astype(np.float64)
+    d[::5] = rng.normal(size=d[::5].shape)
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)   # normalised in float64: no overflow
+    os_ = O.OracleScene(sc)
+    tr, pr = os_.trace_closest(o, d, 0.0, 3.0e38)
+    assert (pr >= 0).mean() > 0.5, (pr >= 0).mean()
+    tf = np.where(tr > 0, tr * np.float32(0.999), np.float32(3.0e38)).astype(np.float32)
+    tf[::3] = np.where(tr[::3] > 0, tr[::3] * np.float32(1.001), np.float32(3.0e38))
+    anyr = os_.trace_any(o, d, np.zeros(n, np.float32), tf)
+    for lockstep in (False, True):
+        t, prim = g.debug_trace(gs, o, d, 0.0, 3.0e38, any_hit=False, lockstep=lockstep)
+        assert np.array_equal(prim, pr) and np.array_equal(t, tr), lockstep
+        _, anyg = g.debug_trace(gs, o, d, np.zeros(n, np.float32), tf, any_hit=True, lockstep=lockstep)
+        assert np.array_equal(anyg, anyr), lockstep

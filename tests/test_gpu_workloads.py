@@ -10,7 +10,9 @@ moves `U < w/w_sum`).  The measured statistics are printed (-s) and recorded in 
   C3  Sponza-like (250 k tris, 4096 emissive tris), 480x270, 2 temporal+spatial frames, orbiting camera;
       and at the metric's full 1920x1080, 3 orbit frames
   C5  C2's scene with 1024 lights, 32 consecutive orbit frames with moving lights (temporal + spatial,
-      confidence cap 20 reached after 20 frames and held across the rest of the sequence)
+      confidence cap 20 reached after 20 frames and held across the rest of the sequence); and the full
+      240-frame sequence at 1920x1080
+  C3  also one frame pair at C4's 3840x2160 against the oracle
   C4  C3 at 3840x2160 split in 8 row bands rendered by 8 contexts on one GPU (the RCCL halo exchange
       emulated by device copies) with G-buffer margins of only the spatial halo: bit-identical to one
       context's full frame (the temporal pass rebuilds the few G elements a reprojection needs beyond
@@ -165,20 +167,31 @@ def test_c4_eight_bands_4k_bit_identical():
               f"(G elements rebuilt beyond the tiles: {rebuilt})")
 
 
+def _energy_rel(gpu, ref):
+    """sum |gpu - ref| / sum |ref| over the frame (L2 per pixel): the frame's relative radiance error, which -- unlike
+    the per-pixel mean -- a dark pixel's flip cannot dominate (its 1e-3 denominator floor turns a 0.1 difference into
+    a relative error of 100)"""
+    d = np.linalg.norm(gpu.astype(np.float64) - ref, axis=-1).sum()
+    return float(d / max(np.linalg.norm(ref.astype(np.float64), axis=-1).sum(), 1e-30))
+
+
 def test_c5_1080p():
     """C5 at the shape BASELINE names: the C2 scene at 1920x1080 with the lights moving every frame, the camera
-    orbiting, temporal (cap 20) + spatial reuse, 64 consecutive frames against the oracle rendering each moved
-    scene.  A pixel outside 1e-4 is a reservoir-selection flip (ocml vs glibc last-ulp) that the temporal history
-    can carry for a few frames; the per-frame figures are printed ([parity] lines, profiles/r04_parity_stats.txt)
-    and the trend over the last 16 frames must not approach the floor."""
+    orbiting, temporal (cap 20) + spatial reuse, ALL 240 frames of the sequence against the oracle rendering each
+    moved scene.  A pixel outside 1e-4 is a reservoir-selection flip (ocml vs glibc last-ulp) that the temporal
+    history carries for a few frames.  Per frame: >= 99.5 % of pixels within 1e-4 and the frame's relative radiance
+    error (sum of per-pixel L2 differences / sum of per-pixel L2 radiance) <= 1e-4; the per-pixel mean is printed
+    and recorded but not bounded here -- a flip on a pixel darker than the 1e-3 floor weighs 100x in it
+    (DESIGN.md §5).  Every frame's figures go to gpurun_out/c5_240_stats.txt (profiles/r05_parity_stats.txt)."""
+    import os
     sc = scenes.cornell_many_lights(1024)
     W, H = 1920, 1080
     prm = P.c3_params()
     g = Renderer(W, H)
     gs = g.load_scene(sc)
     o = O.OracleRenderer(W, H)
-    n = 64
-    fr = []
+    n = 240
+    rows, fr = [], []
     for f in range(n):
         pos = scenes.moving_light_positions(sc, f, 240)
         gs.update_positions(pos)
@@ -186,9 +199,44 @@ def test_c5_1080p():
         a = g.produce_restir(gs, cam, prm, f).copy()
         moved = scenes.Scene(pos, sc.normals, sc.tri_material, sc.materials, sc.camera)
         b = o.render(O.OracleScene(moved), cam, prm, f)
-        _check(a, b, f"C5 1080p frame {f}")
-        fr.append(_stats(a, b)[0])
+        assert np.isfinite(a).all(), f
+        frac, mean, mx = _stats(a, b)
+        er = _energy_rel(a, b)
+        rel = np.linalg.norm(a.astype(np.float64) - b, axis=-1) / np.maximum(np.linalg.norm(b, axis=-1), 1e-3)
+        lum = np.linalg.norm(b, axis=-1)
+        dark = lum < 1e-2
+        # how much of the per-pixel mean the dark pixels carry
+        dark_share = float(rel[dark].sum() / max(rel.sum(), 1e-30))
+        fr.append(frac)
+        rows.append((f, frac, mean, mx, er, dark_share, int((rel > PIX_TOL).sum())))
+        print(f"[parity] C5 1080p frame {f}: within 1e-4 {100 * frac:.4f} %, mean rel {mean:.3g}, max {mx:.3g}, "
+              f"energy rel {er:.3g}, dark-pixel share of the mean {dark_share:.2f}", flush=True)
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/c5_240_stats.txt", "w") as fh:
+        fh.write("frame frac_within_1e-4 mean_rel max_rel energy_rel dark_share_of_mean pixels_out\n")
+        for r in rows:
+            fh.write(f"{r[0]} {r[1]:.6f} {r[2]:.4g} {r[3]:.4g} {r[4]:.4g} {r[5]:.3f} {r[6]}\n")
     worst = min(fr)
     print(f"[parity] C5 1080p {n} frames: worst frame {100 * worst:.4f} % (frame {int(np.argmin(fr))}), "
-          f"mean of the last 16 {100 * float(np.mean(fr[-16:])):.4f} %")
+          f"mean of the last 16 {100 * float(np.mean(fr[-16:])):.4f} %, worst energy rel {max(r[4] for r in rows):.3g}")
+    bad = [r for r in rows if not (r[1] >= PIX_FRAC and r[4] <= MEAN_TOL)]
+    assert not bad, bad[:5]
     assert float(np.mean(fr[-16:])) >= 0.998
+
+
+def test_c3_4k_frame():
+    """C3's scene at C4's 3840x2160 against the oracle (C4 was only a self-comparison of bands vs the
+    GPU's full frame): two orbit frames -- the first without, the second with temporal history -- temporal + spatial
+    reuse, the oracle on the host (~40 s per frame on 16 threads)."""
+    sc = scenes.sponza_like()
+    W, H = 3840, 2160
+    prm = P.c3_params()
+    cam = lambda f: scenes.orbit_camera(sc.camera, f, 240, 0.3)
+    g = Renderer(W, H)
+    gs = g.load_scene(sc)
+    o, os_ = O.OracleRenderer(W, H), O.OracleScene(sc)
+    for f in range(2):
+        a = g.produce_restir(gs, cam(f), prm, f).copy()
+        b = o.render(os_, cam(f), prm, f)
+        _check(a, b, f"C3 3840x2160 frame {f}")
+        print(f"[parity] C3 3840x2160 frame {f}: energy rel {_energy_rel(a, b):.3g}", flush=True)
