@@ -157,6 +157,9 @@ struct rs_context {
     Counters* d_tot = nullptr;             // running totals over frames (rs_get_timing_totals)
     ulonglong2* d_red = nullptr;           // k_reduce_counts partials + ticket (= reds[li])
     ulonglong2* reds[kLanes] = {};
+    uint32_t* qctr[kLanes] = {};           // persistent-wave tile queues (rs_passes.h TileQ): 4 words per lane
+    int persist_mode = RS_PERSIST ? RS_SPLIT_AUTO : RS_SPLIT_OFF;
+    int persist_wgs[4] = {};               // resident workgroups per CU of the persistent initial kernel, per kind
     // pass timing without a per-frame host sync: every frame records into its own slot of an event
     // ring; slots are folded into the running totals lazily (when reused, or on rs_get_timing_totals)
     static constexpr int kEvRing = 64;
@@ -381,6 +384,8 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (hipMalloc(&c->reds[i], (kReduceBlocks + 1) * sizeof(ulonglong2)) != hipSuccess) return bail("hipMalloc(partials) failed");
         hipMemsetAsync(c->reds[i], 0, (kReduceBlocks + 1) * sizeof(ulonglong2), c->stream);   // ticket = 0
         hipMemsetAsync(c->cnts[i], 0, sizeof(Counters), c->stream);
+        if (hipMalloc(&c->qctr[i], 4 * sizeof(uint32_t)) != hipSuccess) return bail("hipMalloc(tile queues) failed");
+        hipMemsetAsync(c->qctr[i], 0, 4 * sizeof(uint32_t), c->stream);
     }
     c->d_cnt = c->cnts[0]; c->d_red = c->reds[0];
     c->fs = c->stream;
@@ -406,6 +411,11 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->queue_mode = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->queue_mode = RS_SPLIT_OFF;
         else if (!std::strcmp(t, "auto")) c->queue_mode = RS_SPLIT_AUTO;
+    }
+    if (const char* t = std::getenv("RESTIR_PERSIST")) {       // persistent-wave initial pass: auto | on | off
+        if (!std::strcmp(t, "on")) c->persist_mode = RS_SPLIT_ON;
+        else if (!std::strcmp(t, "off")) c->persist_mode = RS_SPLIT_OFF;
+        else if (!std::strcmp(t, "auto")) c->persist_mode = RS_SPLIT_AUTO;
     }
     if (const char* t = std::getenv("RESTIR_SORT")) {          // auto (default) | on | off: wave-sorted initial pass
         if (!std::strcmp(t, "on")) c->sort_mode = RS_SPLIT_ON;
@@ -526,6 +536,7 @@ extern "C" void rs_context_destroy(rs_context* c) {
     if (c->d_rowcost) hipFree(c->d_rowcost);
     for (auto* p : c->cnts) if (p) hipFree(p);
     for (auto* p : c->reds) if (p) hipFree(p);
+    for (auto* p : c->qctr) if (p) hipFree(p);
     if (c->d_tot) hipFree(c->d_tot);
     void* post[] = {c->acc, c->display, c->post_part, c->post_out};
     for (void* p : post) if (p) hipFree(p);
@@ -1517,6 +1528,28 @@ static int ensure_queue(rs_context* c, int k, size_t n_waves, size_t px, int A, 
     q.A = A;
     return RS_OK;
 }
+// the persistent-wave initial pass (RESTIR_PERSIST / RS_PERSIST): AUTO = launches of more than one round of the
+// device's resident waves (a smaller launch starts every tile at once either way)
+static int persist_wgs(rs_context* c) {
+    const int kind = c->trav | (c->twide ? TRAV_WIDE : 0);
+    int& n = c->persist_wgs[kind];
+    if (!n) {                                   // resident workgroups per CU of the kernel the frame would launch
+        hipError_t e = hipSuccess;
+        switch (kind) {
+            case TRAV_LANE | TRAV_WIDE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_pq<TRAV_LANE | TRAV_WIDE>, 256, 0); break;
+            case TRAV_LANE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_pq<TRAV_LANE>, 256, 0); break;
+            case TRAV_WIDE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_pq<TRAV_WIDE>, 256, 0); break;
+            default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_pq<TRAV_LOCKSTEP>, 256, 0); break;
+        }
+        if (e != hipSuccess || n <= 0) n = RS_INITIAL_WAVES;
+    }
+    return n;
+}
+static bool want_persist(rs_context* c, dim3 grid) {
+    if (c->persist_mode == RS_SPLIT_OFF) return false;
+    if (c->persist_mode == RS_SPLIT_ON) return true;
+    return grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_wgs(c);
+}
 static bool reserve_count_slots(rs_context* c, int k, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
     size_t need = (c->split ? grid_waves(grid_split(c->W, gy0, gy1), kSplit) : grid_waves(grid_rows(c->W, gy0, gy1))) +
                   grid_waves(grid_rows(c->W, y0, y1)) * (4 + (size_t)std::max(0, P->spatial_passes));
@@ -1658,6 +1691,13 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     } else if (want_sorted(c, P, s)) {
         LAUNCH_TRAV(c, k_gbuffer_initial_sorted, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                     count_slot(c, gg));
+    } else if (want_persist(c, gg)) {
+        // persistent waves pulling 8x8 tiles (rs_passes.h k_gbuffer_initial_pq): about one device's worth of
+        // resident workgroups, never more than the tiles need
+        const uint32_t nt = gg.x * gg.y * 4u;
+        const dim3 gp((unsigned)std::min<size_t>((nt + 3) / 4, (size_t)c->cus * (size_t)persist_wgs(c)));
+        LAUNCH_TRAV(c, k_gbuffer_initial_pq, gp, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
+                    count_slot(c, gp), TileQ{c->qctr[c->li], nt});
     } else {
         LAUNCH_TRAV(c, k_gbuffer_initial, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                     count_slot(c, gg));

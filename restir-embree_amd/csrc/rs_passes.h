@@ -557,18 +557,63 @@ __device__ __forceinline__ void store_rgb(float* fb, size_t p, vec3 c) {
     fb[3 * p] = c.x; fb[3 * p + 1] = c.y; fb[3 * p + 2] = c.z;
 }
 
+// ---------------------------------------------------------------- persistent waves (per-wave tile queue)
+// A persistent launch has about one device's worth of resident workgroups; every WAVE pulls 8x8-pixel tiles from a
+// per-launch counter (one atomic per tile, lane 0) in the order a full grid would dispatch them -- the 4 waves of a
+// 16x16 tile in a row, the tile rows costliest first (tile_of) -- until the queue is empty.  A wave that finishes its
+// tile takes the next one at once, where a one-thread-per-pixel grid keeps a workgroup's four wave slots until its
+// slowest wave retires.  Counter words: [0] next tile, [1] waves exited; the last wave to exit re-arms both for the
+// lane's next launch.  Every pixel's work is independent of which wave does it: frames are bit-identical.
+struct TileQ { uint32_t* ctr; uint32_t n; };
+__device__ __forceinline__ uint32_t q_pull(const TileQ& Q) {
+    uint32_t t = 0u;
+    if ((threadIdx.x & 63) == 0) t = atomicAdd(Q.ctr, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+}
+__device__ __forceinline__ void q_exit(const TileQ& Q) {
+    if ((threadIdx.x & 63) != 0) return;
+    const uint32_t waves = gridDim.x * gridDim.y * (blockDim.x >> 6);
+    if (__hip_atomic_fetch_add(Q.ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == waves - 1) {
+        __hip_atomic_store(Q.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(Q.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+// 8x8 tile t of rows [ya, yb) in dispatch order (4 per 16x16 tile, 16-px rows by the context's cost order on full frames)
+__device__ __forceinline__ bool pixel_of_q(const FrameConst& F, int ya, int yb, uint32_t t, int& x, int& y) {
+    const int W = F.W, gx = (W + 15) / 16, gy = (yb - ya + 15) / 16;
+    const int q = (int)(t >> 2), w = (int)(t & 3u);
+    const int bx = q % gx;
+    int by = q / gx;
+    if (F.row_order && ya == 0 && yb == F.H && F.n_order == gy) by = order_row(F.row_order, (uint32_t)by);
+    const int lane = threadIdx.x & 63;
+    x = bx * 16 + (w & 1) * 8 + (lane & 7);
+    y = ya + by * 16 + (w >> 1) * 8 + (lane >> 3);
+    const bool in = x < W && y < yb;
+    x = x < W ? x : W - 1;
+    y = y < yb ? y : yb - 1;
+    return in;
+}
+// count_rays for a persistent wave: the slot of this wave once at the end; the per-row cost per tile
+__device__ __forceinline__ void count_store(CountSlot C, uint32_t rays, uint32_t primary) {
+    const uint32_t r = wave_sum(rays), p = wave_sum(primary);
+    if ((threadIdx.x & 63) == 0)
+        C.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)] = make_uint2(r, p);
+}
+__device__ __forceinline__ void row_cost_add(CountSlot C, uint64_t t0, int y) {
+    if (!C.row_cost) return;
+    const int yt = __builtin_amdgcn_readfirstlane(y);
+    if ((threadIdx.x & 63) == 0 && yt >= C.y0 && yt < C.y1) atomicAdd(C.row_cost + yt, (float)(wave_clock() - t0));
+}
+#ifndef RS_PERSIST
+#define RS_PERSIST 0           // 1: full-frame initial passes launch persistent waves (restir_capi.hip want_persist)
+#endif
+
+// G-buffer + initialRenderPass of one pixel (the body of k_gbuffer_initial)
 template <int T>
-__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_WAVES_LANE)) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G,
-                                                                            ResBuf Rw, float* fb, int fuse_shade,
-                                                                            CountSlot C) {
-    const uint64_t t0 = wave_clock();
-    if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
-    int x, y;
-    uint32_t rays = 0;
-    const bool in = pixel_of(F, F.gy0, F.gy1, x, y);
+__device__ __forceinline__ void gbuffer_initial_px(const DevScene& S, const FrameConst& F, const GBuf& G, const ResBuf& Rw,
+                                                   float* fb, int fuse_shade, const FrameSlot& fs, int x, int y, bool in,
+                                                   uint32_t& rays) {
     const size_t p = (size_t)y * F.W + x;
-    __shared__ float4 frame_lds[5 * 256];
-    const FrameSlot fs{frame_lds, (int)threadIdx.x, 256};
     GElem g = gbuffer_fill<T>(S, F, x, y, in);
     if (in) G.store(p, g);
     fs.store(make_frame(g, F.cam.pos));
@@ -579,7 +624,42 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
         Rw.store(p, r);
         if (fuse_shade) store_rgb(fb, p, shade_px(r, f, g.le));
     }
+}
+template <int T>
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_WAVES_LANE)) k_gbuffer_initial(DevScene S, FrameConst F, GBuf G,
+                                                                            ResBuf Rw, float* fb, int fuse_shade,
+                                                                            CountSlot C) {
+    const uint64_t t0 = wave_clock();
+    if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
+    int x, y;
+    uint32_t rays = 0;
+    const bool in = pixel_of(F, F.gy0, F.gy1, x, y);
+    __shared__ float4 frame_lds[5 * 256];
+    const FrameSlot fs{frame_lds, (int)threadIdx.x, 256};
+    gbuffer_initial_px<T>(S, F, G, Rw, fb, fuse_shade, fs, x, y, in, rays);
     count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u, t0, y);
+}
+// the same pass by persistent waves pulling 8x8 tiles (TileQ)
+template <int T>
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_WAVES_LANE))
+k_gbuffer_initial_pq(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int fuse_shade, CountSlot C, TileQ Q) {
+    if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;
+    __shared__ float4 frame_lds[5 * 256];
+    const FrameSlot fs{frame_lds, (int)threadIdx.x, 256};
+    uint32_t rays = 0, prim = 0;
+    for (;;) {
+        const uint32_t t = q_pull(Q);
+        if (t >= Q.n) break;
+        const uint64_t t0 = wave_clock();
+        int x, y;
+        const bool in = pixel_of_q(F, F.gy0, F.gy1, t, x, y);
+        gbuffer_initial_px<T>(S, F, G, Rw, fb, fuse_shade, fs, x, y, in, rays);
+        rays += in ? 1u : 0u;
+        prim += in ? 1u : 0u;
+        row_cost_add(C, t0, y);
+    }
+    count_store(C, rays, prim);
+    q_exit(Q);
 }
 // ---------------------------------------------------------------- wave-sorted initial pass (per-lane wide walks)
 // The per-lane walks of incoherent scenes (C3) are bound by the vector-memory data path returning a wave's
