@@ -247,6 +247,7 @@ struct rs_context {
     int q_A[kLanes] = {}, q_B[kLanes] = {};
     int cus = 256;
     int sort_mode = RS_SPLIT_AUTO;         // wave-sorted initial pass (RESTIR_SORT=on|off; AUTO: per-lane walks)
+    int spatial_split = RS_SPLIT_AUTO;     // candidate-split spatial pass for small launches (RESTIR_SPATIAL_SPLIT)
     int sort_spatial = RS_SPLIT_AUTO;      // wave-sorted spatial pass, CONSTANT MIS, k <= 8 (RESTIR_SORT_SPATIAL=on|off;
                                            // AUTO: per-lane walks -- C3 2.21 -> 1.87 ms; lockstep C5 0.228 -> 0.250)
     int sort_temporal = RS_SPLIT_AUTO;     // wave-sorted temporal rays (RESTIR_SORT_TEMPORAL=off: per-ray walks)
@@ -424,6 +425,10 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
     if (const char* t = std::getenv("RESTIR_SORT_TEMPORAL")) { // auto (default) | on | off: wave-sorted temporal rays
         if (!std::strcmp(t, "on")) c->sort_temporal = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->sort_temporal = RS_SPLIT_OFF;
+    }
+    if (const char* t = std::getenv("RESTIR_SPATIAL_SPLIT")) { // auto (default) | on | off
+        if (!std::strcmp(t, "on")) c->spatial_split = RS_SPLIT_ON;
+        else if (!std::strcmp(t, "off")) c->spatial_split = RS_SPLIT_OFF;
     }
     if (const char* t = std::getenv("RESTIR_SORT_SPATIAL")) {  // auto (default) | on | off: wave-sorted spatial pass
         if (!std::strcmp(t, "on")) c->sort_spatial = RS_SPLIT_ON;
@@ -1550,9 +1555,18 @@ static bool want_persist(rs_context* c, dim3 grid) {
     if (c->persist_mode == RS_SPLIT_ON) return true;
     return grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_wgs(c);
 }
+// the candidate-split spatial pass (rs_passes.h k_spatial_split): CONSTANT MIS, k <= 8, and (AUTO) a lockstep launch
+// of less than one round of the device's resident waves -- a rank's band (per-lane walks keep the sorted pass)
+static bool want_spatial_split(const rs_context* c, const rs_frame_params* P, int y0, int y1) {
+    if (c->spatial_split == RS_SPLIT_OFF || P->spatial_mis != MIS_CONSTANT || P->spatial_neighbors + 1 > kSpatialSortMax) return false;
+    if (c->spatial_split == RS_SPLIT_ON) return true;
+    return c->trav == TRAV_LOCKSTEP && grid_waves(grid_rows(c->W, y0, y1)) < (size_t)c->wave_slots;
+}
 static bool reserve_count_slots(rs_context* c, int k, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
+    const size_t spatial = want_spatial_split(c, P, y0, y1) ? grid_waves(grid_split(c->W, y0, y1), kSpatialSplit)
+                                                           : grid_waves(grid_rows(c->W, y0, y1));
     size_t need = (c->split ? grid_waves(grid_split(c->W, gy0, gy1), kSplit) : grid_waves(grid_rows(c->W, gy0, gy1))) +
-                  grid_waves(grid_rows(c->W, y0, y1)) * (4 + (size_t)std::max(0, P->spatial_passes));
+                  grid_waves(grid_rows(c->W, y0, y1)) * 4 + spatial * (size_t)std::max(0, P->spatial_passes);
     if (c->queue)
         need += grid_waves(grid_q_trace(c, grid_waves(grid_rows(c->W, gy0, gy1)))) + grid_waves(grid_rows(c->W, y0, y1));
     return use_parts(c, k, need);
@@ -1804,7 +1818,17 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
     int dst = (c->rcur == c->ra) ? c->rb : c->ra;
     int fuse = (pass_index == c->P.spatial_passes - 1) ? 1 : 0;
     const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
-    {
+    if (want_spatial_split(c, &c->P, c->F.y0, c->F.y1)) {
+        const dim3 gs = grid_split(c->W, c->F.y0, c->F.y1);
+        const bool tev = c->tuning && c->tune_n + 2 <= (int)(sizeof(c->tune_ev) / sizeof(c->tune_ev[0]));
+        if (tev) HIPCHK(c, hipEventRecord(c->tune_ev[c->tune_n], c->fs));
+        LAUNCH_TRAV_BS(c, k_spatial_split, gs, 64 * kSpatialSplit, S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]},
+                       ResBuf{c->R[dst]}, pass_index, fuse, c->fb, count_slot(c, gs, kSpatialSplit));
+        if (tev) {
+            HIPCHK(c, hipEventRecord(c->tune_ev[c->tune_n + 1], c->fs));
+            c->tune_n += 2;
+        }
+    } else {
         const CountSlot cs = count_slot(c, gb);
         const GBuf& G = c->G[c->gcur];
         const ResBuf Rr{c->R[c->rcur]}, Rw{c->R[dst]};

@@ -1690,6 +1690,114 @@ k_spatial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pas
     count_rays(C, rays, 0, t0, y);
 }
 
+// ---------------------------------------------------------------- candidate-split spatial pass (small launches)
+// A rank's band of a multi-GPU frame gives the spatial pass less than one round of waves (C2 1/8 band: 0.9), so the
+// launch takes as long as its slowest wave.  Here a workgroup is ONE 8x8 tile with kSpatialSplit waves: every wave
+// makes the pixel's neighbour selection itself (stateless RNG slots; the same list in every wave), traces the
+// visibility rays of its share of the list positions (i = g, g + kSpatialSplit, ...; a pixel's rays share one walk
+// two at a time, as k_spatial's) and sets the pixel's occlusion bits in LDS; wave 0 then runs k_spatial_sorted's
+// phase C -- every candidate re-evaluated with its bit, the reservoir stream in list order.  CONSTANT MIS, k <= 8.
+// The rays and the stream are k_spatial's: frames are bit-identical (tests/test_gpu_parity.py).
+#ifndef RS_SPATIAL_SPLIT
+#define RS_SPATIAL_SPLIT 3
+#endif
+constexpr int kSpatialSplit = RS_SPATIAL_SPLIT;
+template <int T>
+__global__ void __launch_bounds__(64 * kSpatialSplit, RS_WAVES(T, RS_SPATIAL_WAVES_SMALL, RS_SPATIAL_WAVES_LANE))
+k_spatial_split(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, int fuse_shade, float* fb, CountSlot C) {
+    __shared__ uint32_t occ_lds[64];
+    const uint64_t t0 = wave_clock();
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    int x = blockIdx.x * 8 + (lane & 7), y = F.y0 + blockIdx.y * 8 + (lane >> 3);
+    const bool in = x < F.W && y < F.y1;
+    x = x < F.W ? x : F.W - 1;
+    y = y < F.y1 ? y : F.y1 - 1;
+    const size_t p = (size_t)y * F.W + x;
+    uint32_t rays = 0;
+    const vec3 cam = F.cam.pos;
+    GElem th = G.load(p);
+    const bool emissive = any_pos(th.le);
+    const bool alive = in && !emissive;
+    if (g == 0) {
+        occ_lds[lane] = 0u;
+        if (in && emissive) {                              // :319-324
+            Res r = Rr.load(p);
+            Rw.store(p, r);
+            if (fuse_shade) store_rgb(fb, p, shade_px(r, mk(0, 0, 0), th.le));
+        }
+    }
+    __syncthreads();
+    Rng rng; rng.init(F.seed, F.frame, PASS_SPATIAL0 + (uint32_t)pass_idx, (uint32_t)p);
+    uint64_t acc = 0;                                      // neighbour selection (:334-374), as k_spatial
+    int M = 1;
+    if (__ballot(alive) != 0) {
+        for (int i = 0; i < F.k; ++i) {
+            size_t q = neighbor_px(F, rng, i, x, y);
+            if (any_pos(G.le(q))) continue;
+            if (F.reject) {
+                float4 nq = G.g1[q];
+                float ns = dot(xyz(nq), th.nrm);
+                if (ns < F.min_normal_sim) continue;
+                float nd = G.g0[q].w;
+                float dr = 0;
+                if (nd > 0) dr = th.depth / nd;
+                float hd = F.max_depth_diff * 0.5f;
+                if (dr < 1.0f - hd || dr > 1.0f + hd) continue;
+            }
+            acc |= 1ull << i;
+            M += 1;
+        }
+        const int cnt = M, kk = F.k + 1;
+        const ShadeFrame sf = make_frame(th, cam);
+        // this wave's list positions, two rays per walk
+        for (int i0 = g; i0 < kk; i0 += 2 * kSpatialSplit) {
+            FPre pre[2];
+            bool act[2], occ[2];
+            vec3 dir[2];
+            float tf[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int i = i0 + k * kSpatialSplit;
+                const Res rr = Rr.load(list_px(F, rng, acc, i < kk ? i : 0, x, y, p));
+                pre[k] = evaluate_f_pre(F, smp_of(rr), th.pos, false, sf, true, alive && i < cnt);
+                act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
+                rays += act[k] ? 1u : 0u;
+            }
+            trace_any_multi<T, 2>(S, act, th.pos, dir, FLT_MIN + F.tnear_off, tf, occ);
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (act[k] && occ[k]) atomicOr(&occ_lds[lane], 1u << (i0 + k * kSpatialSplit));
+        }
+    }
+    __syncthreads();
+    if (g != 0 || __ballot(alive) == 0) { count_rays(C, rays, 0, t0, y); return; }
+    // ---- wave 0: the reservoir stream in list order (k_spatial_sorted's phase C)
+    asm volatile("" ::: "memory");
+    th = G.load(p);
+    const ShadeFrame sf = make_frame(th, cam);
+    rng.n = 2u * (uint32_t)F.k;
+    const uint32_t occm = occ_lds[lane];
+    const int cnt = M, kk = F.k + 1;
+    const float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
+    Res res = res_empty();
+    vec3 f_sel = mk(0, 0, 0);
+    for (int i = 0; i < kk; ++i) {
+        const Res rr = Rr.load(list_px(F, rng, acc, i, x, y, p));
+        const FPre pre = evaluate_f_pre(F, smp_of(rr), th.pos, false, sf, true, alive && i < cnt);
+        const vec3 f = evaluate_f_post(pre, ((occm >> i) & 1u) != 0u);
+        const float rw = rcpM * length(f) * rr.W;
+        if (alive && i < cnt && res_add(res, smp_of(rr), rw, rr.conf, rng)) f_sel = f;
+    }
+    const float fph = smp_valid(smp_of(res)) ? length(f_sel) : 0.0f;  // :481
+    res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
+    res_cap(res, F.cap);
+    if (alive) {
+        Rw.store(p, res);
+        if (fuse_shade) store_rgb(fb, p, shade_px(res, f_sel, th.le));
+    }
+    count_rays(C, rays, 0, t0, y);
+}
+
 // shade loop (pg/simpleguidx11.cpp:447-472)
 template <int T>
 __global__ void __launch_bounds__(256) k_shade(DevScene S, FrameConst F, GBuf G, ResBuf Rr, float* fb, CountSlot C) {

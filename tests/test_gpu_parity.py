@@ -239,6 +239,39 @@ def test_initial_split_bit_identical(which):
     _assert_close(out["lane", "on"][0], o.render(os_, cam(0), prm, 0), f"{which} split vs oracle")
 
 
+@pytest.mark.parametrize("which", ["c2", "k8", "c3"])
+def test_spatial_split_bit_identical(which, monkeypatch):
+    """The candidate-split spatial pass (rs_passes.h k_spatial_split: an 8x8 tile's k + 1 visibility rays over three
+    waves, occlusion bits through LDS, the stream in wave 0) renders frames and ray counts bit-identical to the
+    one-thread-per-pixel pass, for both traversal kinds: the metric point (k = 4), k = 8 with the normal / depth
+    rejection on, and C3-like temporal + spatial frames; AUTO (small image, lockstep) uses it too."""
+    W, H = 72, 56
+    cam = lambda f: sc.camera
+    if which == "c2":
+        sc, prm = scenes.cornell_many_lights(1024), P.metric_params()
+    elif which == "k8":
+        sc, prm = scenes.cornell_many_lights(256), P.metric_params(spatial_neighbors=8, reject_dissimilar=1, spatial_passes=2)
+    else:
+        sc, prm = scenes.sponza_like(target_tris=30_000, n_lamps=128), P.c3_params(m_area=7)
+        cam = lambda f: scenes.orbit_camera(sc.camera, f, 240, 0.3)
+    out = {}
+    for trav in ("lockstep", "lane"):
+        for mode in ("off", "on", "auto"):
+            monkeypatch.setenv("RESTIR_SPATIAL_SPLIT", mode)
+            g = Renderer(W, H)
+            g.set_traversal(trav)
+            gs = g.load_scene(sc)
+            fr = []
+            for f in range(3):
+                fr.append(g.produce_restir(gs, cam(f), prm, f, timed=True).copy())
+                fr.append(int(g.last_times.rays))
+            out[trav, mode] = fr
+    ref = out["lockstep", "off"]
+    for k, v in out.items():
+        for i in range(len(ref)):
+            assert np.array_equal(ref[i], v[i]), f"{which} {k} item {i}"
+
+
 @pytest.mark.parametrize("which", ["c2", "c3", "c5", "c5mix", "fused"])
 def test_run_ahead_bit_identical(which):
     """Frame pipelining (initial pass of frame f+1 on the side stream, overlapping frame f's later
