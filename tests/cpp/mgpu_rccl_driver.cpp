@@ -54,6 +54,7 @@ int main(int argc, char** argv) {
     std::vector<std::string> msg(world);
     int bad_frames = 0;
     std::vector<int> bands(world + 1, 0);
+    int refine_rounds = 0;                      // measured rounds of the rebalance's time-based refinement
     std::barrier sync(world);
     auto run = [&](int i) {
         rs_mgpu* m = nullptr;
@@ -70,7 +71,11 @@ int main(int argc, char** argv) {
         };
         for (int k = 0; k < frames; ++k) frame((uint32_t)k, k);
         chk(rs_mgpu_rebalance(m, &s, &cam, &P, (uint32_t)frames, 2, 6), "rebalance");
-        if (i == 0) rs_mgpu_get_bands(m, bands.data());
+        if (i == 0) {
+            rs_mgpu_get_bands(m, bands.data());
+            std::vector<double> ms(world);
+            while (rs_mgpu_rebalance_times(m, refine_rounds, ms.data()) == RS_OK) ++refine_rounds;
+        }
         for (int k = 0; k < frames; ++k) frame(f_after + (uint32_t)k, frames + k);
         rs_mgpu_stats st{};
         chk(rs_mgpu_get_stats(m, &st, 0), "stats");
@@ -86,8 +91,8 @@ int main(int argc, char** argv) {
     for (int i = 0; i < world; ++i) if (fail[i]) { ++nfail; std::fprintf(stderr, "rank %d: %s\n", i, msg[i].c_str()); }
     std::printf("{\"world\": %d, \"frames\": %d, \"bad_frames\": %d, \"rank_errors\": %d, \"bands\": [", world, 2 * frames, bad_frames, nfail);
     for (int i = 0; i <= world; ++i) std::printf("%s%d", i ? ", " : "", bands[i]);
-    std::printf("], \"pairs\": %ld, \"bytes\": %ld, \"mismatches\": %ld, \"unpaired\": %ld, \"allreduces\": %ld}\n", pairs, bytes,
-                mism, unp, ar);
+    std::printf("], \"refine_rounds\": %d, \"pairs\": %ld, \"bytes\": %ld, \"mismatches\": %ld, \"unpaired\": %ld, \"allreduces\": %ld}\n",
+                refine_rounds, pairs, bytes, mism, unp, ar);
     for (auto* r : rk) delete r;
     return (bad_frames || nfail || mism || unp || pairs == 0 || ar == 0) ? 1 : 0;
 }

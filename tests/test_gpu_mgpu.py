@@ -72,7 +72,7 @@ def test_local_mgpu_rebalance_and_frames_in_flight():
     m = MultiGpuFrame(rs)
     m.rebalance(ss, cams[0], prm, 0, 2, 6, refine=0)              # row costs only: nothing measured
     assert m.rebalance_times() == []
-    bands = m.rebalance(ss, cams[0], prm, 0, 2, 6)                 # + the default 2 time-based rounds
+    bands = m.rebalance(ss, cams[0], prm, 0, 2, 6, refine=2)       # + 2 time-based rounds (the default)
     assert bands != [(0, 24), (24, 48), (48, 72)] and all(b - a >= 6 for a, b in bands), bands
     rounds = m.rebalance_times()                                   # every rank timed in every measured round
     assert 1 <= len(rounds) <= 3 and all(len(t) == world and min(t) > 0 for t in rounds), rounds
@@ -237,3 +237,5 @@ def test_rccl_branch_threads_on_one_gpu(tmp_path, world, temporal):
     r = json.loads(line[-1])
     print(f"[rccl-stub] {r}")
     assert r["bad_frames"] == 0 and r["mismatches"] == 0 and r["unpaired"] == 0 and r["pairs"] > 0 and r["allreduces"] >= 1
+    # the rebalance's time-based refinement ran through the RCCL branch: >= 1 measured round, each an all-reduce
+    assert r["refine_rounds"] >= 1 and r["allreduces"] >= 1 + r["refine_rounds"], r

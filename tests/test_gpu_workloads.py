@@ -179,10 +179,10 @@ def test_c5_1080p():
     """C5 at the shape BASELINE names: the C2 scene at 1920x1080 with the lights moving every frame, the camera
     orbiting, temporal (cap 20) + spatial reuse, ALL 240 frames of the sequence against the oracle rendering each
     moved scene.  A pixel outside 1e-4 is a reservoir-selection flip (ocml vs glibc last-ulp) that the temporal
-    history carries for a few frames.  Per frame: >= 99.5 % of pixels within 1e-4 and the frame's relative radiance
-    error (sum of per-pixel L2 differences / sum of per-pixel L2 radiance) <= 1e-4; the per-pixel mean is printed
-    and recorded but not bounded here -- a flip on a pixel darker than the 1e-3 floor weighs 100x in it
-    (DESIGN.md §5).  Every frame's figures go to gpurun_out/c5_240_stats.txt (profiles/r05_parity_stats.txt)."""
+    history carries for a few frames.  Per frame: >= 99.5 % of pixels within 1e-4, per-pixel mean <= 1e-4, and the
+    frame's relative radiance error (sum of per-pixel L2 differences / sum of per-pixel L2 radiance) <= 1e-4.
+    Every frame's figures go to gpurun_out/c5_240_stats.txt (profiles/r05_c5_240_stats.txt); the fraction settles
+    at ~99.93 % after frame 64 instead of drifting."""
     import os
     sc = scenes.cornell_many_lights(1024)
     W, H = 1920, 1080
@@ -219,7 +219,7 @@ def test_c5_1080p():
     worst = min(fr)
     print(f"[parity] C5 1080p {n} frames: worst frame {100 * worst:.4f} % (frame {int(np.argmin(fr))}), "
           f"mean of the last 16 {100 * float(np.mean(fr[-16:])):.4f} %, worst energy rel {max(r[4] for r in rows):.3g}")
-    bad = [r for r in rows if not (r[1] >= PIX_FRAC and r[4] <= MEAN_TOL)]
+    bad = [r for r in rows if not (r[1] >= PIX_FRAC and r[2] <= MEAN_TOL and r[4] <= MEAN_TOL)]
     assert not bad, bad[:5]
     assert float(np.mean(fr[-16:])) >= 0.998
 
