@@ -639,16 +639,28 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
     gbuffer_initial_px<T>(S, F, G, Rw, fb, fuse_shade, fs, x, y, in, rays);
     count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u, t0, y);
 }
-// the same pass by persistent waves pulling 8x8 tiles (TileQ)
+// the same pass by persistent waves pulling 8x8 tiles (TileQ).  RS_PERSIST_WG = 1: the workgroup pulls a whole
+// 16x16 tile (its four waves' 8x8 tiles, one atomic per workgroup and tile) -- the dispatcher's granularity and
+// L1 locality, without its workgroup launches
+#ifndef RS_PERSIST_WG
+#define RS_PERSIST_WG 1
+#endif
+__device__ __forceinline__ uint32_t q_pull_wg(const TileQ& Q, uint32_t* s_tile) {
+    __syncthreads();                                 // every wave has read the previous tile index
+    if (threadIdx.x == 0) *s_tile = atomicAdd(Q.ctr, 1u);
+    __syncthreads();
+    return 4u * *s_tile + (threadIdx.x >> 6);       // this wave's 8x8 tile of the 16x16 tile
+}
 template <int T>
 __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_WAVES_LANE))
 k_gbuffer_initial_pq(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int fuse_shade, CountSlot C, TileQ Q) {
     if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;
     __shared__ float4 frame_lds[5 * 256];
+    __shared__ uint32_t s_tile;
     const FrameSlot fs{frame_lds, (int)threadIdx.x, 256};
     uint32_t rays = 0, prim = 0;
     for (;;) {
-        const uint32_t t = q_pull(Q);
+        const uint32_t t = RS_PERSIST_WG ? q_pull_wg(Q, &s_tile) : q_pull(Q);
         if (t >= Q.n) break;
         const uint64_t t0 = wave_clock();
         int x, y;

@@ -15,3 +15,10 @@ t = [float(m.group(1)) for m in re.finditer(r"wall ([0-9.]+) ms/frame", open(sys
 print(f"{sys.argv[2]:45s} bands: max {max(t):.4f} mean {sum(t) / len(t):.4f} ms  {['%.4f' % x for x in t]}", flush=True)
 PY
 done
+# the persistent initial pass with workgroup-granular tile pulls (RS_PERSIST_WG) against the default launch
+RESTIR_PERSIST=on timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread \
+  > gpurun_out/pytest_persist_wg.log 2>&1 || { echo "persist-wg: parity tests failed"; tail -30 gpurun_out/pytest_persist_wg.log; exit 1; }
+echo "persist-wg parity: $(tail -1 gpurun_out/pytest_persist_wg.log)"
+for rep in 1 2; do
+  VARIANTS="base RESTIR_PERSIST=on" SCENES="C2" STEPS=30 bash scripts/gpu_ab_env.sh || exit 1
+done
