@@ -1817,6 +1817,12 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
     const DevScene S = c->scene->dev();
     int dst = (c->rcur == c->ra) ? c->rb : c->ra;
     int fuse = (pass_index == c->P.spatial_passes - 1) ? 1 : 0;
+    // the canonical reservoir's sample was visibility-tested from this very pixel (same origin, target, tnear and
+    // tfar: the same ray) when it was selected -- by the initial pass, the temporal pass (p-hat at the current
+    // surface) or the previous spatial pass -- except after a visibility pass, which keeps occluded samples with
+    // W = 0 (pg/ReSTIRIntegrator.cpp:302-312); the temporal pass passes such a reservoir through on a failed
+    // reprojection, so with the visibility pass only passes >= 1 know it
+    c->F.canon_vis = (!c->P.do_visibility_pass || pass_index > 0) ? 1 : 0;
     const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
     if (want_spatial_split(c, &c->P, c->F.y0, c->F.y1)) {
         const dim3 gs = grid_split(c->W, c->F.y0, c->F.y1);

@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(kPlocBlock) k_ploc_nearest(const int* C, int k
     const int i = base + threadIdx.x;
     if (i >= k) return;
     const float4 a = slo[threadIdx.x + kRadius], b = shi[threadIdx.x + kRadius];
-    float best = INFINITY;
+    double best = INFINITY;
     int bj = -1;
     for (int o = -kRadius; o <= kRadius; ++o) {
         int j = i + o;
@@ -366,7 +366,11 @@ __global__ void __launch_bounds__(kPlocBlock) k_ploc_nearest(const int* C, int k
         float ex = fmaxf(b.x, d.x) - fminf(a.x, c.x);
         float ey = fmaxf(b.y, d.y) - fminf(a.y, c.y);
         float ez = fmaxf(b.z, d.z) - fminf(a.z, c.z);
-        float area = ex * ey + ey * ez + ez * ex;
+        const float af = ex * ey + ey * ez + ez * ex;
+        // a float area that overflows (coordinates beyond ~1e19) is re-formed in double, so the nearest
+        // neighbour stays defined and PLOC keeps merging; finite areas compare exactly as before
+        const double area = af < INFINITY ? (double)af
+                                          : (double)ex * ey + (double)ey * ez + (double)ez * ex;
         if (area < best) { best = area; bj = j; }      // j ascending: ties keep the smaller index
     }
     N[i] = bj;

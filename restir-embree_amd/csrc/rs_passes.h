@@ -77,6 +77,8 @@ struct FrameConst {
     const int* row_order; // full-frame launches: grid row -> 16-px tile row, costliest first (or null)
     int n_order;          // entries of row_order (== the grid's rows when it applies)
     int debug_reproj;     // debugReprojection: k_temporal records, k_debug_reproj paints (full frames)
+    int canon_vis;        // spatial pass: the canonical (own) reservoir's sample is known unoccluded from the pixel
+                          //   (restir_capi.hip rs_tile_spatial; §3.2) -- its visibility ray is not traced again
     uint8_t* dbg;         // 2 x W*H bytes: [p] the pixel's own rejection (1..3), [W*H + p] forward-check hit
 };
 
@@ -1454,6 +1456,7 @@ k_spatial(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, 
                     const int i = i0 + k;
                     rr[k] = Rr.load(list_q(i));
                     pre[k] = evaluate_f_pre(F, smp_of(rr[k]), th.pos, false, sf, true, alive && i < cnt);
+                    pre[k].need = pre[k].need && !(i == 0 && F.canon_vis);   // known unoccluded: f = L as traced
                     act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
                     rays += act[k] ? 1u : 0u;
                 }
@@ -1631,7 +1634,7 @@ k_spatial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pas
         for (int i = 0; i < kk; ++i) {
             const Res rr = Rr.load(list_q(i));
             const FPre pre = evaluate_f_pre(F, smp_of(rr), th.pos, false, sf, true, alive && i < cnt);
-            if (pre.need) {
+            if (pre.need && !(i == 0 && F.canon_vis)) {       // the canonical sample: known unoccluded, not traced
                 const uint32_t b = point_bucket(S, rr.p, pre.dir);
                 L.slot[i * 64 + lane] = (uint16_t)atomicAdd(&L.cur[b], 1u);
                 bkt[i / 3] |= b << (10 * (i % 3));
@@ -1772,7 +1775,7 @@ k_spatial_split(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass
                 const int i = i0 + k * kSpatialSplit;
                 const Res rr = Rr.load(list_px(F, rng, acc, i < kk ? i : 0, x, y, p));
                 pre[k] = evaluate_f_pre(F, smp_of(rr), th.pos, false, sf, true, alive && i < cnt);
-                act[k] = pre[k].need; dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
+                act[k] = pre[k].need && !(i == 0 && F.canon_vis); dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
                 rays += act[k] ? 1u : 0u;
             }
             trace_any_multi<T, 2>(S, act, th.pos, dir, FLT_MIN + F.tnear_off, tf, occ);
