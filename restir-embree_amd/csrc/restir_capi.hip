@@ -1776,6 +1776,7 @@ extern "C" int rs_tile_temporal(rs_context* c) {
         // held without one), this launch walks both binary trees (same hits, rs_scene.h)
         if (!S.wnodes || !Sp.wnodes) c->twide = false;
         if (c->F.debug_reproj) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 2 * npx, c->fs));
+        c->F.canon_vis = c->P.do_visibility_pass ? 0 : 1;   // the current reservoir's sample: tested from this pixel
         // the wave-sorted shadow rays (TEMPORAL_SORT) unless RESTIR_SORT_TEMPORAL=off: C3 (per-lane) temporal
         // 1.54 -> 1.36 ms, C5 (lockstep) 0.210 -> 0.191 ms
         const bool tsort = c->sort_temporal != RS_SPLIT_OFF;

@@ -1244,8 +1244,11 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
                                           true, ok);
             ts.put(12 + k, e.ok ? length(e.L) : 0.0f);
             ts.put(16 + k, e.ok ? length(e.L * 0.0f) : 0.0f);
-            nd |= e.need ? 1u << k : 0u;
-            rays += e.need ? 1u : 0u;
+            // the current sample at the current surface (k = 0) is the initial pass's selection, found unoccluded
+            // from this pixel by the same ray (§3.2): not traced again (F.canon_vis: no visibility pass)
+            const bool need = e.need && !(k == 0 && F.canon_vis);
+            nd |= need ? 1u << k : 0u;
+            rays += need ? 1u : 0u;
         }
         ts.put3(0, cur.pos); ts.put3(3, prev.pos); ts.put3(6, cs.p); ts.put3(9, ps.p);
         if constexpr (kSort) {
