@@ -247,7 +247,8 @@ struct rs_context {
     int q_A[kLanes] = {}, q_B[kLanes] = {};
     int cus = 256;
     int sort_mode = RS_SPLIT_AUTO;         // wave-sorted initial pass (RESTIR_SORT=on|off; AUTO: per-lane walks)
-    int spatial_split = RS_SPLIT_AUTO;     // candidate-split spatial pass for small launches (RESTIR_SPATIAL_SPLIT)
+    int spatial_split = RS_SPLIT_OFF;      // candidate-split spatial pass for small launches (RESTIR_SPATIAL_SPLIT=
+                                           // auto|on; measured slower at C2's 1/8 bands: max 0.2304 vs 0.2198 ms)
     int sort_spatial = RS_SPLIT_AUTO;      // wave-sorted spatial pass, CONSTANT MIS, k <= 8 (RESTIR_SORT_SPATIAL=on|off;
                                            // AUTO: per-lane walks -- C3 2.21 -> 1.87 ms; lockstep C5 0.228 -> 0.250)
     int sort_temporal = RS_SPLIT_AUTO;     // wave-sorted temporal rays (RESTIR_SORT_TEMPORAL=off: per-ray walks)
@@ -426,9 +427,10 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->sort_temporal = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->sort_temporal = RS_SPLIT_OFF;
     }
-    if (const char* t = std::getenv("RESTIR_SPATIAL_SPLIT")) { // auto (default) | on | off
+    if (const char* t = std::getenv("RESTIR_SPATIAL_SPLIT")) { // off (default) | auto | on
         if (!std::strcmp(t, "on")) c->spatial_split = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->spatial_split = RS_SPLIT_OFF;
+        else if (!std::strcmp(t, "auto")) c->spatial_split = RS_SPLIT_AUTO;
     }
     if (const char* t = std::getenv("RESTIR_SORT_SPATIAL")) {  // auto (default) | on | off: wave-sorted spatial pass
         if (!std::strcmp(t, "on")) c->sort_spatial = RS_SPLIT_ON;

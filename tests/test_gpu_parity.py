@@ -244,7 +244,8 @@ def test_spatial_split_bit_identical(which, monkeypatch):
     """The candidate-split spatial pass (rs_passes.h k_spatial_split: an 8x8 tile's k + 1 visibility rays over three
     waves, occlusion bits through LDS, the stream in wave 0) renders frames and ray counts bit-identical to the
     one-thread-per-pixel pass, for both traversal kinds: the metric point (k = 4), k = 8 with the normal / depth
-    rejection on, and C3-like temporal + spatial frames; AUTO (small image, lockstep) uses it too."""
+    rejection on, and C3-like temporal + spatial frames; AUTO (small image, lockstep) uses it too.  (Off by
+    default: measured slower at C2's 1/8 bands)"""
     W, H = 72, 56
     cam = lambda f: sc.camera
     if which == "c2":
