@@ -247,6 +247,7 @@ struct rs_context {
     int q_A[kLanes] = {}, q_B[kLanes] = {};
     int cus = 256;
     int sort_mode = RS_SPLIT_AUTO;         // wave-sorted initial pass (RESTIR_SORT=on|off; AUTO: per-lane walks)
+    bool sep_margin = true;                // a band's G-buffer margin rows in their own launch (RESTIR_MARGIN_SPLIT=off)
     int spatial_split = RS_SPLIT_OFF;      // candidate-split spatial pass for small launches (RESTIR_SPATIAL_SPLIT=
                                            // auto|on; measured slower at C2's 1/8 bands: max 0.2304 vs 0.2198 ms)
     int sort_spatial = RS_SPLIT_AUTO;      // wave-sorted spatial pass, CONSTANT MIS, k <= 8 (RESTIR_SORT_SPATIAL=on|off;
@@ -427,6 +428,8 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->sort_temporal = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->sort_temporal = RS_SPLIT_OFF;
     }
+    if (const char* t = std::getenv("RESTIR_MARGIN_SPLIT"))    // on (default) | off
+        c->sep_margin = std::strcmp(t, "off") != 0;
     if (const char* t = std::getenv("RESTIR_SPATIAL_SPLIT")) { // off (default) | auto | on
         if (!std::strcmp(t, "on")) c->spatial_split = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->spatial_split = RS_SPLIT_OFF;
@@ -1564,11 +1567,12 @@ static bool want_spatial_split(const rs_context* c, const rs_frame_params* P, in
     if (c->spatial_split == RS_SPLIT_ON) return true;
     return c->trav == TRAV_LOCKSTEP && grid_waves(grid_rows(c->W, y0, y1)) < (size_t)c->wave_slots;
 }
-static bool reserve_count_slots(rs_context* c, int k, const rs_frame_params* P, int gy0, int gy1, int y0, int y1) {
+static bool reserve_count_slots(rs_context* c, int k, const rs_frame_params* P, int gy0, int gy1, int y0, int y1,
+                                size_t extra = 0) {
     const size_t spatial = want_spatial_split(c, P, y0, y1) ? grid_waves(grid_split(c->W, y0, y1), kSpatialSplit)
                                                            : grid_waves(grid_rows(c->W, y0, y1));
     size_t need = (c->split ? grid_waves(grid_split(c->W, gy0, gy1), kSplit) : grid_waves(grid_rows(c->W, gy0, gy1))) +
-                  grid_waves(grid_rows(c->W, y0, y1)) * 4 + spatial * (size_t)std::max(0, P->spatial_passes);
+                  grid_waves(grid_rows(c->W, y0, y1)) * 4 + spatial * (size_t)std::max(0, P->spatial_passes) + extra;
     if (c->queue)
         need += grid_waves(grid_q_trace(c, grid_waves(grid_rows(c->W, gy0, gy1)))) + grid_waves(grid_rows(c->W, y0, y1));
     return use_parts(c, k, need);
@@ -1662,13 +1666,23 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     c->shade_fused = !P->do_visibility_pass && !temporal && !spatial;
     c->temporal_ran = c->spatial_ran = c->ev_temporal = false;
     const DevScene S = s->dev();
-    c->split = want_split(c, P, F.gy0, F.gy1);
     c->queue = want_queue(c, P, F.gy0, F.gy1);
+    // A band's G-buffer margin (the rows of the spatial halo beyond it) needs the G-buffer only.  Its rows get their
+    // own small launch, so the initial pass's 8-row tiles start at the band's first row: otherwise the top and
+    // bottom tile rows mix margin rows -- whose lanes idle through the whole candidate loop -- with band rows
+    // (C2's 1/8 band: 145 G rows in 19 tile rows for 135 RIS rows, 11 % of the pass's waves idle).  Full frames
+    // have no margin.
+    const bool margins = c->sep_margin && !c->queue && (F.gy0 < F.y0 || F.gy1 > F.y1);
+    FrameConst Fi = F;                          // the rows of the initial pass's launch
+    if (margins) { Fi.gy0 = F.y0; Fi.gy1 = F.y1; }
+    const size_t margin_waves = margins ? grid_waves(grid_rows(c->W, F.gy0, F.y0)) + grid_waves(grid_rows(c->W, F.y1, F.gy1)) : 0;
+    c->split = want_split(c, P, Fi.gy0, Fi.gy1);
     if (c->queue) {
         const size_t nw = grid_waves(grid_rows(c->W, F.gy0, F.gy1));
         if (int rc = ensure_queue(c, c->li, nw, (size_t)(F.gy1 - F.gy0) * c->W, P->m_area, P->m_brdf)) return rc;
     }
-    if (!reserve_count_slots(c, c->li, P, F.gy0, F.gy1, F.y0, F.y1)) return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
+    if (!reserve_count_slots(c, c->li, P, Fi.gy0, Fi.gy1, F.y0, F.y1, margin_waves))
+        return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
     if (c->fs != c->stream && c->lane_wait[c->li]) {   // this lane's previous frame ran on the context's stream
         HIPCHK(c, hipStreamWaitEvent(c->fs, c->lane_wait[c->li], 0));
     }
@@ -1688,11 +1702,22 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     for (int i = 0; i < EV_COUNT; ++i) c->ev[i] = c->evr[c->slot][i];
     HIPCHK(c, hipEventRecord(c->ev[EV_BEGIN], c->fs));
     c->prev_begin = c->ev[EV_BEGIN];
-    const dim3 gg = grid_rows(c->W, F.gy0, F.gy1), gb = grid_rows(c->W, F.y0, F.y1);
+    if (margins) {                              // the margin rows' G-buffer (no RIS rows: the candidate loops exit)
+        const int rr[2][2] = {{F.gy0, F.y0}, {F.y1, F.gy1}};
+        for (const auto& r : rr) {
+            if (r[0] >= r[1]) continue;
+            FrameConst Fm = F;
+            Fm.gy0 = r[0]; Fm.gy1 = r[1];
+            const dim3 gm = grid_rows(c->W, r[0], r[1]);
+            LAUNCH_TRAV(c, k_gbuffer_initial, gm, S, Fm, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, 0, count_slot(c, gm));
+            HIPCHK(c, hipGetLastError());
+        }
+    }
+    const dim3 gg = grid_rows(c->W, Fi.gy0, Fi.gy1), gb = grid_rows(c->W, F.y0, F.y1);
     if (c->split) {
-        const dim3 gs = grid_split(c->W, F.gy0, F.gy1);
+        const dim3 gs = grid_split(c->W, Fi.gy0, Fi.gy1);
         LAUNCH_TRAV_BS_SH(c, k_gbuffer_initial_split, gs, 64 * kSplit, split_lds_bytes(P->m_area + P->m_brdf, P->m_brdf),
-                          S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
+                          S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
                     c->shade_fused ? 1 : 0, count_slot(c, gs, kSplit));
     } else if (c->queue) {
         const QBuf& Q = c->qb[c->li];
@@ -1705,17 +1730,17 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
         k_q_resolve<<<gb, 256, 0, c->fs>>>(S, F, c->G[gnew], Q, ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                                            count_slot(c, gb));
     } else if (want_sorted(c, P, s)) {
-        LAUNCH_TRAV(c, k_gbuffer_initial_sorted, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
+        LAUNCH_TRAV(c, k_gbuffer_initial_sorted, gg, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                     count_slot(c, gg));
     } else if (want_persist(c, gg)) {
         // persistent waves pulling 8x8 tiles (rs_passes.h k_gbuffer_initial_pq): about one device's worth of
         // resident workgroups, never more than the tiles need
         const uint32_t nt = gg.x * gg.y * 4u;
         const dim3 gp((unsigned)std::min<size_t>((nt + 3) / 4, (size_t)c->cus * (size_t)persist_wgs(c)));
-        LAUNCH_TRAV(c, k_gbuffer_initial_pq, gp, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
+        LAUNCH_TRAV(c, k_gbuffer_initial_pq, gp, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                     count_slot(c, gp), TileQ{c->qctr[c->li], nt});
     } else {
-        LAUNCH_TRAV(c, k_gbuffer_initial, gg, S, F, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
+        LAUNCH_TRAV(c, k_gbuffer_initial, gg, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                     count_slot(c, gg));
     }
     HIPCHK(c, hipGetLastError());
