@@ -31,7 +31,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -440,6 +442,216 @@ __global__ void __launch_bounds__(256, BHalf<NT>::on ? BHalf<NT>::waves : 1) k_c
     }
 }
 
+// ---------------------------------------------------------------- the pipelined convolution (k_conv3p)
+// One workgroup of 8 waves per CU, persistent over 16 x 32-pixel output tiles (a wave: 8 x 8 pixels, the
+// fragments and epilogue of k_conv3), for layers with 4 n-tiles (49..64 output channels).  A stage = one
+// (tile, channel chunk): its halo image and its B fragments go global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4: no staging registers, no ds_write pass) into one of two stage buffers, and the
+// next stage's DMA is in flight across the barriers while the MFMAs run on this one -- across tile
+// boundaries too, so no tile waits for its first chunk.  Per stage: issue stage s + 1; counted
+// `s_waitcnt vmcnt` (this wave's part of stage s has landed; stage s + 1's loads stay in flight); raw
+// s_barrier (every wave's part has); MFMAs; raw s_barrier (the buffer may be refilled).  Never
+// __syncthreads(): its fence would drain the DMA in flight.
+// LDS-DMA writes 64 lanes x 16 B contiguously per instruction, so the halo image is slot-linear: 16-B slot q
+// of a stage holds halo pixel (hr, hc), 16-B part s chosen by q's byte offset in a pitched image --
+// 64-B pixels at a 2208-B row pitch (32-channel chunks), 32-B pixels at 1152 B (16-channel chunks), pitches
+// at which every fragment read is bank-conflict free (scripts/dn_lds_layout.py); the pad slots load zeros.
+constexpr int kPTH = 16, kPTW = 32;                     // output tile rows x columns
+constexpr int kPHH = kPTH + 2, kPHW = kPTW + 2;         // halo 18 x 34
+constexpr int kPPitch32 = 2208, kPPitch16 = 1152;
+constexpr int kPHalo32 = (kPHH - 1) * kPPitch32 + kPHW * 64;   // 39712 B
+constexpr int kPHalo16 = (kPHH - 1) * kPPitch16 + kPHW * 32;   // 20672 B
+constexpr int kPNT = 4;
+constexpr int kPBuf = kPHalo32 + 9 * kPNT * 1024;              // 76576 B per stage buffer
+constexpr int kPThreads = 512;
+static_assert(2 * kPBuf <= 163840, "two stage buffers fit the CU's LDS");
+static_assert(kPTH * kPTW * (kPNT * 16 + 8) * 2 <= kPBuf, "the epilogue's image fits a stage buffer");
+// s_waitcnt vmcnt count that retires stage s while stage s + 1 (of width w) stays in flight: the fewest
+// LDS-DMA instructions any wave issues for a stage of width w (halo: 2482 / 1292 slots, B: 2304 / 1280 slots,
+// 512 per round; waves whose slots run out issue one fewer)
+constexpr int kPWait32 = 8, kPWait16 = 4;
+
+__device__ __forceinline__ void glds16(const void* g, uint8_t* l) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+struct PTile { int tx0, ty0; };
+__device__ __forceinline__ PTile ptile(const ConvArgs& a, int t) {
+    const int tw = (a.w_ + kPTW - 1) / kPTW;
+    const int ty = t / tw;
+    return PTile{(t - ty * tw) * kPTW, ty * kPTH};
+}
+
+// LDS-DMA of stage (tile t, chunk c) into buffer `buf`
+__device__ __forceinline__ void pstage_issue(const ConvArgs& a, int t, int c, uint8_t* buf) {
+    const PTile T = ptile(a, t);
+    const int tid = (int)threadIdx.x, wv = tid >> 6;
+    const int s = a.ch_src[c];
+    const bool w32 = a.ch_w[c] == 32;
+    const _Float16* src = a.src[s];
+    const int cs = a.cs[s], sh = a.sh[s], sw = a.sw[s], up = a.up[s], base = a.ch_base[c];
+    const int nh = (w32 ? kPHalo32 : kPHalo16) / 16;
+#pragma unroll
+    for (int r = 0; r < (kPHalo32 / 16 + kPThreads - 1) / kPThreads; ++r) {
+        int q = r * kPThreads + tid;
+        asm volatile("" : "+v"(q));                    // recomputed per stage: hoisted, the slot maps spill
+        if (r * kPThreads + wv * 64 < nh) {                // the wave has slots in this round
+            const int o = q * 16;
+            int hr, hc, sl;
+            if (w32) { hr = o / kPPitch32; const int rem = o - hr * kPPitch32; hc = rem >> 6; sl = (rem >> 4) & 3; }
+            else { hr = o / kPPitch16; const int rem = o - hr * kPPitch16; hc = rem >> 5; sl = (rem >> 4) & 1; }
+            int y = T.ty0 - 1 + hr, x = T.tx0 - 1 + hc;
+            if (up) { y >>= 1; x >>= 1; }              // arithmetic: -1 stays -1 (the border)
+            size_t px = 0;                             // pixel 0 = the zero border
+            if (hc < kPHW && y <= sh && x <= sw) px = (size_t)(y + 1) * (size_t)(sw + 2) + (size_t)(x + 1);
+            if (q < nh)                                // lanes past the image would write the B fragments
+                glds16(src + px * cs + base + 8 * sl, buf + r * (kPThreads * 16) + wv * 1024);
+        }
+    }
+    const int nst = w32 ? 9 : 5, nb = nst * kPNT * 64;
+    const uint4* w = (const uint4*)a.w + (size_t)a.ch_step[c] * kPNT * 64;
+    uint8_t* bb = buf + kPHalo32;
+#pragma unroll
+    for (int r = 0; r < (9 * kPNT * 64 + kPThreads - 1) / kPThreads; ++r) {
+        int q = r * kPThreads + tid;
+        asm volatile("" : "+v"(q));
+        if (r * kPThreads + wv * 64 < nb) glds16(w + (q < nb ? q : 0), bb + r * (kPThreads * 16) + wv * 1024);
+    }
+}
+
+// MFMAs of one stage: chunk c's k-steps over the halo image and B fragments in `buf`
+__device__ __forceinline__ void pstage_compute(const ConvArgs& a, int c, const uint8_t* buf, f32x4 (&acc)[4][kPNT],
+                                               int lane, int X, int Yb) {
+    const int h = lane >> 4;
+    const half8* bp = (const half8*)(buf + kPHalo32) + lane;
+    if (a.ch_w[c] == 32) {
+        const uint8_t* ab = buf + Yb * kPPitch32 + X * 64 + h * 16;
+        for (int st = 0; st < 9; ++st) {
+            const int ky = st / 3, kx = st - 3 * ky;
+            half8 b[kPNT];
+#pragma unroll
+            for (int n = 0; n < kPNT; ++n) b[n] = bp[(st * kPNT + n) * 64];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const half8 av = *(const half8*)(ab + (2 * g + ky) * kPPitch32 + kx * 64);
+#pragma unroll
+                for (int n = 0; n < kPNT; ++n) acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[n], acc[g][n], 0, 0, 0);
+            }
+        }
+    } else {
+        const uint8_t* ab = buf + Yb * kPPitch16 + X * 32 + (h & 1) * 16;
+        for (int st = 0; st < 5; ++st) {
+            int tap = 2 * st + (h >> 1);
+            tap = tap > 8 ? 8 : tap;                   // tap 9: zero weights
+            const int ky = tap / 3, kx = tap - 3 * ky;
+            half8 b[kPNT];
+#pragma unroll
+            for (int n = 0; n < kPNT; ++n) b[n] = bp[(st * kPNT + n) * 64];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const half8 av = *(const half8*)(ab + (2 * g + ky) * kPPitch16 + kx * 32);
+#pragma unroll
+                for (int n = 0; n < kPNT; ++n) acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[n], acc[g][n], 0, 0, 0);
+            }
+        }
+    }
+}
+
+// a workgroup barrier that is not a fence (no vmcnt(0): the DMA in flight stays in flight); the empty asm
+// keeps the compiler from moving LDS accesses across it
+__device__ __forceinline__ void raw_barrier() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+}
+
+template <bool RELU>
+__global__ void __launch_bounds__(kPThreads) k_conv3p(ConvArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kPBuf];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wy = wv >> 2, wx = wv & 3;
+    const int i = lane & 15, h = lane >> 4;
+    const int X = 8 * wx + 2 * (i >> 2) + (i & 1);
+    const int Yb = 8 * wy + ((i >> 1) & 1);
+    const int ntiles = ((a.w_ + kPTW - 1) / kPTW) * ((a.h + kPTH - 1) / kPTH);
+    int t = blockIdx.x, c = 0, b = 0;
+    if (t >= ntiles) return;
+    float bv[kPNT];
+#pragma unroll
+    for (int n = 0; n < kPNT; ++n) {
+        bv[n] = a.bias[16 * n + i];
+        asm volatile("" : "+v"(bv[n]));                // loaded before the first DMA is issued
+    }
+    f32x4 acc[4][kPNT];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int n = 0; n < kPNT; ++n) acc[g][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    pstage_issue(a, t, 0, lds);
+    for (;;) {
+        int tn = t, cn = c + 1;
+        if (cn == a.nchunk) { cn = 0; tn = t + (int)gridDim.x; }
+        const bool more = tn < ntiles;
+        if (more) {
+            pstage_issue(a, tn, cn, lds + (b ^ 1) * kPBuf);
+            if (a.ch_w[cn] == 32) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPWait32) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPWait16) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        raw_barrier();                                 // every wave's part of stage (t, c) has landed
+        uint8_t* buf = lds + b * kPBuf;
+        pstage_compute(a, c, buf, acc, lane, X, Yb);
+        if (cn == 0 || !more) {                        // tile t done: bias, ReLU, f16 through LDS, 16-B stores
+            const PTile T = ptile(a, t);
+            constexpr int CP = kPNT * 16 + 8;
+            _Float16* o = (_Float16*)buf;
+            lds_barrier();                             // every wave's MFMAs have read the stage
+#pragma unroll
+            for (int n = 0; n < kPNT; ++n)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float v = acc[g][n][r] + bv[n];
+                        if (RELU) v = v > 0.0f ? v : 0.0f;
+                        const int px = (8 * wy + 2 * g + (r >> 1)) * kPTW + 8 * wx + 2 * h + (r & 1);
+                        o[px * CP + 16 * n + i] = (_Float16)v;
+                        acc[g][n][r] = 0.0f;
+                    }
+            lds_barrier();
+            // the image's LDS reads in asm: before a compiler-visible ds_read the compiler waits vmcnt(0) --
+            // for the next stage's DMA and for every store issued before it
+            constexpr int PPP = kPNT * 16 / 8, NK = kPTH * kPTW * PPP / kPThreads;
+            uint4 ov[NK];
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const int q = (int)threadIdx.x + k * kPThreads;
+                const int px = q / PPP, pc = q - px * PPP;
+                const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(o + px * CP + 8 * pc);
+                asm volatile("ds_read_b128 %0, %1" : "=v"(ov[k]) : "v"(la) : "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const int q = (int)threadIdx.x + k * kPThreads;
+                const int px = q / PPP, pc = q - px * PPP;
+                const int gy = T.ty0 + px / kPTW, gx = T.tx0 + px % kPTW;
+                if (gy < a.h && gx < a.w_)
+                    *(uint4*)(a.dst + ((size_t)(gy + 1) * (size_t)(a.w_ + 2) + (size_t)(gx + 1)) * a.dcs + 8 * pc) = ov[k];
+            }
+        }
+        if (!more) break;
+        lds_barrier();                                 // the buffer may be refilled
+        t = tn; c = cn; b ^= 1;
+    }
+}
+
 // ---------------------------------------------------------------- input transform + auto-exposure
 struct InArgs {
     const float* color; const float* albedo; const float* normal;
@@ -740,6 +952,8 @@ struct rs_denoiser {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t evl[17] = {};                    // timed: after the input transform, after each convolution
     bool timed = false;
+    bool pipe = true;                           // k_conv3p for the 4-n-tile layers (RESTIR_DN_PIPE=0: k_conv3)
+    int cus = 256;                              // its workgroups (RESTIR_DN_PIPE_GRID caps them: tests)
 };
 
 namespace {
@@ -806,6 +1020,9 @@ int create_impl(rs_context* ctx, const void* tza, size_t bytes, rs_denoiser** ou
     rs_denoiser* d = new rs_denoiser();
     d->ctx = ctx;
     d->device = rs::ctx_device(ctx);
+    if (const char* e = std::getenv("RESTIR_DN_PIPE")) d->pipe = std::strcmp(e, "0") != 0;
+    if (hipDeviceGetAttribute(&d->cus, hipDeviceAttributeMultiprocessorCount, d->device) != hipSuccess || d->cus < 1) d->cus = 256;
+    if (const char* e = std::getenv("RESTIR_DN_PIPE_GRID")) d->cus = std::max(1, std::atoi(e));
     if (!check_net(T, d->net, err)) { delete d; return rs::ctx_fail(ctx, RS_E_INVALID, "rs_denoiser_create: " + err); }
     (void)hipGetLastError();
     if (hipSetDevice(rs::ctx_device(ctx)) != hipSuccess) { delete d; return rs::ctx_fail(ctx, RS_E_HIP, "rs_denoiser_create: hipSetDevice"); }
@@ -887,6 +1104,17 @@ int denoise_run(rs_denoiser* d, hipStream_t st, const float* color, int cst, con
         else {
             a.out = out; a.ostride = ost; a.H = H; a.W = W; a.scale = d->d_scale;
             a.inv_norm = pu_forward(HDR_Y_MAX);
+        }
+        a.nt_total = L.nt;
+        if (d->pipe && ld.post == POST_STORE && L.nt == kPNT) {
+            // one persistent workgroup per CU over 16 x 32 tiles (or one per tile when there are fewer)
+            const size_t nt = (size_t)((a.w_ + kPTW - 1) / kPTW) * (size_t)((a.h + kPTH - 1) / kPTH);
+            const unsigned g = (unsigned)std::min<size_t>(nt, (size_t)d->cus);
+            if (ld.relu) k_conv3p<true><<<g, kPThreads, 0, st>>>(a);
+            else k_conv3p<false><<<g, kPThreads, 0, st>>>(a);
+            DCHK(d, hipGetLastError());
+            if (d->timed) DCHK(d, hipEventRecord(d->evl[l + 1], st));
+            continue;
         }
         // n-tiles per workgroup: all of them, unless the layer's tiles cannot fill the chip (the coarse
         // levels): then the output channels split over blockIdx.z (each split re-stages the input halo)

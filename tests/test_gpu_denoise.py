@@ -112,6 +112,32 @@ def test_every_layer_matches_float64(ctx, H, W):
         assert off.mean() <= 0.02, (name, float(off.mean()))
 
 
+@pytest.mark.parametrize("H,W,grid", [(48, 64, "2"), (37, 83, "3"), (540, 960, None), (1080, 1920, None)])
+def test_pipelined_conv_bit_identical(monkeypatch, H, W, grid):
+    """k_conv3p (the persistent LDS-DMA pipeline, csrc/rs_denoise.hip) against k_conv3 on the layers it runs
+    (dec_conv2a / 2b / 1a): the same k-steps in the same order on the same MFMA, so every tensor is bit-identical.
+    A capped grid makes each workgroup walk several tiles (the stage pipeline across tile boundaries)."""
+    r = Renderer(64, 48)
+    w = tza.random_unet_weights(seed=11)
+    color, albedo, normal = _images(H, W, seed=5 + H)
+    outs = {}
+    try:
+        for pipe in ("0", "1"):
+            monkeypatch.setenv("RESTIR_DN_PIPE", pipe)
+            if grid is not None:
+                monkeypatch.setenv("RESTIR_DN_PIPE_GRID", grid)
+            d = Denoiser(r, w)
+            out = _run(d, color, albedo, normal, scale=0.8)
+            outs[pipe] = (out, [d.dump(i)[0] for i in range(16)])
+            d.close()
+    finally:
+        r.close()
+    (o0, t0), (o1, t1) = outs["0"], outs["1"]
+    for i in range(16):
+        assert np.array_equal(t0[i].view(np.uint16), t1[i].view(np.uint16)), f"tensor {i}"
+    assert np.array_equal(o0, o1)
+
+
 def test_autoexposure_matches_reference(ctx):
     r, d, w = ctx
     for (H, W), seed in (((48, 64), 1), ((37, 91), 2), ((1080 // 4, 1920 // 4), 3)):
