@@ -461,15 +461,20 @@ constexpr int kPHH = kPTH + 2, kPHW = kPTW + 2;         // halo 18 x 34
 constexpr int kPPitch32 = 2208, kPPitch16 = 1152;
 constexpr int kPHalo32 = (kPHH - 1) * kPPitch32 + kPHW * 64;   // 39712 B
 constexpr int kPHalo16 = (kPHH - 1) * kPPitch16 + kPHW * 32;   // 20672 B
-constexpr int kPNT = 4;
-constexpr int kPBuf = kPHalo32 + 9 * kPNT * 1024;              // 76576 B per stage buffer
 constexpr int kPThreads = 512;
-static_assert(2 * kPBuf <= 163840, "two stage buffers fit the CU's LDS");
-static_assert(kPTH * kPTW * (kPNT * 16 + 8) * 2 <= kPBuf, "the epilogue's image fits a stage buffer");
-// s_waitcnt vmcnt count that retires stage s while stage s + 1 (of width w) stays in flight: the fewest
-// LDS-DMA instructions any wave issues for a stage of width w (halo: 2482 / 1292 slots, B: 2304 / 1280 slots,
-// 512 per round; waves whose slots run out issue one fewer)
-constexpr int kPWait32 = 8, kPWait16 = 4;
+// stage buffer: the 32-channel halo image, then the chunk's B fragments (k-step-major, NT KB per k-step)
+template <int NT> struct PCfg {
+    static constexpr int kBuf = kPHalo32 + 9 * NT * 1024;
+    // LDS-DMA instructions wave 7 (the wave with the fewest) issues for n slots: it skips the last round when
+    // that round's slots run out before its lanes
+    static constexpr int cnt7(int n) { return n > 448 ? (n - 448 + kPThreads - 1) / kPThreads : 0; }
+    // s_waitcnt vmcnt count that retires stage s while stage s + 1 (32- or 16-channel) stays in flight
+    static constexpr int kWait32 = cnt7(kPHalo32 / 16) + cnt7(9 * NT * 64);
+    static constexpr int kWait16 = cnt7(kPHalo16 / 16) + cnt7(5 * NT * 64);
+    static_assert(2 * kBuf <= 163840, "two stage buffers fit the CU's LDS");
+    static_assert(kPTH * kPTW * (NT * 16 + 8) * 2 <= kBuf, "the epilogue's image fits a stage buffer");
+};
+static_assert(PCfg<4>::kWait32 == 8 && PCfg<4>::kWait16 == 4, "vmcnt counts");
 
 __device__ __forceinline__ void glds16(const void* g, uint8_t* l) {
     __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
@@ -484,6 +489,7 @@ __device__ __forceinline__ PTile ptile(const ConvArgs& a, int t) {
 }
 
 // LDS-DMA of stage (tile t, chunk c) into buffer `buf`
+template <int NT>
 __device__ __forceinline__ void pstage_issue(const ConvArgs& a, int t, int c, uint8_t* buf) {
     const PTile T = ptile(a, t);
     const int tid = (int)threadIdx.x, wv = tid >> 6;
@@ -509,11 +515,11 @@ __device__ __forceinline__ void pstage_issue(const ConvArgs& a, int t, int c, ui
                 glds16(src + px * cs + base + 8 * sl, buf + r * (kPThreads * 16) + wv * 1024);
         }
     }
-    const int nst = w32 ? 9 : 5, nb = nst * kPNT * 64;
-    const uint4* w = (const uint4*)a.w + (size_t)a.ch_step[c] * kPNT * 64;
+    const int nst = w32 ? 9 : 5, nb = nst * NT * 64;
+    const uint4* w = (const uint4*)a.w + (size_t)a.ch_step[c] * NT * 64;
     uint8_t* bb = buf + kPHalo32;
 #pragma unroll
-    for (int r = 0; r < (9 * kPNT * 64 + kPThreads - 1) / kPThreads; ++r) {
+    for (int r = 0; r < (9 * NT * 64 + kPThreads - 1) / kPThreads; ++r) {
         int q = r * kPThreads + tid;
         asm volatile("" : "+v"(q));
         if (r * kPThreads + wv * 64 < nb) glds16(w + (q < nb ? q : 0), bb + r * (kPThreads * 16) + wv * 1024);
@@ -521,7 +527,8 @@ __device__ __forceinline__ void pstage_issue(const ConvArgs& a, int t, int c, ui
 }
 
 // MFMAs of one stage: chunk c's k-steps over the halo image and B fragments in `buf`
-__device__ __forceinline__ void pstage_compute(const ConvArgs& a, int c, const uint8_t* buf, f32x4 (&acc)[4][kPNT],
+template <int NT>
+__device__ __forceinline__ void pstage_compute(const ConvArgs& a, int c, const uint8_t* buf, f32x4 (&acc)[4][NT],
                                                int lane, int X, int Yb) {
     const int h = lane >> 4;
     const half8* bp = (const half8*)(buf + kPHalo32) + lane;
@@ -529,14 +536,14 @@ __device__ __forceinline__ void pstage_compute(const ConvArgs& a, int c, const u
         const uint8_t* ab = buf + Yb * kPPitch32 + X * 64 + h * 16;
         for (int st = 0; st < 9; ++st) {
             const int ky = st / 3, kx = st - 3 * ky;
-            half8 b[kPNT];
+            half8 b[NT];
 #pragma unroll
-            for (int n = 0; n < kPNT; ++n) b[n] = bp[(st * kPNT + n) * 64];
+            for (int n = 0; n < NT; ++n) b[n] = bp[(st * NT + n) * 64];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const half8 av = *(const half8*)(ab + (2 * g + ky) * kPPitch32 + kx * 64);
 #pragma unroll
-                for (int n = 0; n < kPNT; ++n) acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[n], acc[g][n], 0, 0, 0);
+                for (int n = 0; n < NT; ++n) acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[n], acc[g][n], 0, 0, 0);
             }
         }
     } else {
@@ -545,14 +552,14 @@ __device__ __forceinline__ void pstage_compute(const ConvArgs& a, int c, const u
             int tap = 2 * st + (h >> 1);
             tap = tap > 8 ? 8 : tap;                   // tap 9: zero weights
             const int ky = tap / 3, kx = tap - 3 * ky;
-            half8 b[kPNT];
+            half8 b[NT];
 #pragma unroll
-            for (int n = 0; n < kPNT; ++n) b[n] = bp[(st * kPNT + n) * 64];
+            for (int n = 0; n < NT; ++n) b[n] = bp[(st * NT + n) * 64];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const half8 av = *(const half8*)(ab + (2 * g + ky) * kPPitch16 + kx * 32);
 #pragma unroll
-                for (int n = 0; n < kPNT; ++n) acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[n], acc[g][n], 0, 0, 0);
+                for (int n = 0; n < NT; ++n) acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[n], acc[g][n], 0, 0, 0);
             }
         }
     }
@@ -569,9 +576,10 @@ __device__ __forceinline__ void lds_barrier() {
     raw_barrier();
 }
 
-template <bool RELU>
+template <int NT, int POST, bool RELU>
 __global__ void __launch_bounds__(kPThreads) k_conv3p(ConvArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kPBuf];
+    using C = PCfg<NT>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * C::kBuf];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int wy = wv >> 2, wx = wv & 3;
     const int i = lane & 15, h = lane >> 4;
@@ -580,60 +588,71 @@ __global__ void __launch_bounds__(kPThreads) k_conv3p(ConvArgs a) {
     const int ntiles = ((a.w_ + kPTW - 1) / kPTW) * ((a.h + kPTH - 1) / kPTH);
     int t = blockIdx.x, c = 0, b = 0;
     if (t >= ntiles) return;
-    float bv[kPNT];
+    float bv[NT];
 #pragma unroll
-    for (int n = 0; n < kPNT; ++n) {
+    for (int n = 0; n < NT; ++n) {
         bv[n] = a.bias[16 * n + i];
         asm volatile("" : "+v"(bv[n]));                // loaded before the first DMA is issued
     }
-    f32x4 acc[4][kPNT];
+    f32x4 acc[4][NT];
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int n = 0; n < kPNT; ++n) acc[g][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    pstage_issue(a, t, 0, lds);
+        for (int n = 0; n < NT; ++n) acc[g][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    pstage_issue<NT>(a, t, 0, lds);
     for (;;) {
         int tn = t, cn = c + 1;
         if (cn == a.nchunk) { cn = 0; tn = t + (int)gridDim.x; }
         const bool more = tn < ntiles;
         if (more) {
-            pstage_issue(a, tn, cn, lds + (b ^ 1) * kPBuf);
-            if (a.ch_w[cn] == 32) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPWait32) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPWait16) : "memory");
+            pstage_issue<NT>(a, tn, cn, lds + (b ^ 1) * C::kBuf);
+            if (a.ch_w[cn] == 32) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::kWait32) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::kWait16) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         raw_barrier();                                 // every wave's part of stage (t, c) has landed
-        uint8_t* buf = lds + b * kPBuf;
-        pstage_compute(a, c, buf, acc, lane, X, Yb);
-        if (cn == 0 || !more) {                        // tile t done: bias, ReLU, f16 through LDS, 16-B stores
+        uint8_t* buf = lds + b * C::kBuf;
+        pstage_compute<NT>(a, c, buf, acc, lane, X, Yb);
+        if (cn == 0 || !more) {                        // tile t done: bias, ReLU (, pool), f16 through LDS, 16-B stores
             const PTile T = ptile(a, t);
-            constexpr int CP = kPNT * 16 + 8;
+            constexpr int CP = NT * 16 + 8;            // LDS image pixel pitch (halves): k_conv3's epilogue
+            constexpr bool pool = POST == POST_POOL;
+            constexpr int OW = pool ? kPTW / 2 : kPTW, NPX = pool ? kPTH * kPTW / 4 : kPTH * kPTW;
             _Float16* o = (_Float16*)buf;
             lds_barrier();                             // every wave's MFMAs have read the stage
 #pragma unroll
-            for (int n = 0; n < kPNT; ++n)
+            for (int n = 0; n < NT; ++n)
 #pragma unroll
-                for (int g = 0; g < 4; ++g)
+                for (int g = 0; g < 4; ++g) {
+                    if constexpr (pool) {
+                        const f32x4 v4 = acc[g][n];
+                        float m = fmaxf(fmaxf(v4[0], v4[1]), fmaxf(v4[2], v4[3])) + bv[n];
+                        if (RELU) m = m > 0.0f ? m : 0.0f;
+                        o[((4 * wy + g) * OW + 4 * wx + h) * CP + 16 * n + i] = (_Float16)m;
+                    } else {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float v = acc[g][n][r] + bv[n];
-                        if (RELU) v = v > 0.0f ? v : 0.0f;
-                        const int px = (8 * wy + 2 * g + (r >> 1)) * kPTW + 8 * wx + 2 * h + (r & 1);
-                        o[px * CP + 16 * n + i] = (_Float16)v;
-                        acc[g][n][r] = 0.0f;
+                        for (int r = 0; r < 4; ++r) {
+                            float v = acc[g][n][r] + bv[n];
+                            if (RELU) v = v > 0.0f ? v : 0.0f;
+                            o[((8 * wy + 2 * g + (r >> 1)) * OW + 8 * wx + 2 * h + (r & 1)) * CP + 16 * n + i] = (_Float16)v;
+                        }
                     }
+                    acc[g][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                }
             lds_barrier();
             // the image's LDS reads in asm: before a compiler-visible ds_read the compiler waits vmcnt(0) --
             // for the next stage's DMA and for every store issued before it
-            constexpr int PPP = kPNT * 16 / 8, NK = kPTH * kPTW * PPP / kPThreads;
+            constexpr int PPP = NT * 2, NQ = NPX * PPP, NK = (NQ + kPThreads - 1) / kPThreads;
+            const int oh = pool ? a.h >> 1 : a.h, ow = pool ? a.w_ >> 1 : a.w_;
+            const int oy0 = pool ? T.ty0 >> 1 : T.ty0, ox0 = pool ? T.tx0 >> 1 : T.tx0;
             uint4 ov[NK];
 #pragma unroll
             for (int k = 0; k < NK; ++k) {
                 const int q = (int)threadIdx.x + k * kPThreads;
                 const int px = q / PPP, pc = q - px * PPP;
                 const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(o + px * CP + 8 * pc);
-                asm volatile("ds_read_b128 %0, %1" : "=v"(ov[k]) : "v"(la) : "memory");
+                if (NQ % kPThreads == 0 || q < NQ) asm volatile("ds_read_b128 %0, %1" : "=v"(ov[k]) : "v"(la) : "memory");
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
@@ -641,9 +660,9 @@ __global__ void __launch_bounds__(kPThreads) k_conv3p(ConvArgs a) {
             for (int k = 0; k < NK; ++k) {
                 const int q = (int)threadIdx.x + k * kPThreads;
                 const int px = q / PPP, pc = q - px * PPP;
-                const int gy = T.ty0 + px / kPTW, gx = T.tx0 + px % kPTW;
-                if (gy < a.h && gx < a.w_)
-                    *(uint4*)(a.dst + ((size_t)(gy + 1) * (size_t)(a.w_ + 2) + (size_t)(gx + 1)) * a.dcs + 8 * pc) = ov[k];
+                const int gy = oy0 + px / OW, gx = ox0 + px % OW;
+                if ((NQ % kPThreads == 0 || q < NQ) && gy < oh && gx < ow)
+                    *(uint4*)(a.dst + ((size_t)(gy + 1) * (size_t)(ow + 2) + (size_t)(gx + 1)) * a.dcs + 8 * pc) = ov[k];
             }
         }
         if (!more) break;
@@ -952,7 +971,8 @@ struct rs_denoiser {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t evl[17] = {};                    // timed: after the input transform, after each convolution
     bool timed = false;
-    bool pipe = true;                           // k_conv3p for the 4-n-tile layers (RESTIR_DN_PIPE=0: k_conv3)
+    uint32_t pipe = 0xffffu;                    // layers (bit l) on k_conv3p where it applies (2..4 n-tiles);
+                                                // RESTIR_DN_PIPE=<mask>, 0 = k_conv3 everywhere
     int cus = 256;                              // its workgroups (RESTIR_DN_PIPE_GRID caps them: tests)
 };
 
@@ -1011,6 +1031,21 @@ bool dispatch(int nt, int post, bool relu, const ConvArgs& a, dim3 g, hipStream_
 #undef RS_DN_CASE
 }
 
+bool dispatch_pipe(int nt, int post, bool relu, const ConvArgs& a, dim3 g, hipStream_t st) {
+#define RS_DNP_CASE(N)                                                                          \
+    case N:                                                                                     \
+        if (post == POST_POOL) k_conv3p<N, POST_POOL, true><<<g, kPThreads, 0, st>>>(a);        \
+        else if (relu) k_conv3p<N, POST_STORE, true><<<g, kPThreads, 0, st>>>(a);              \
+        else k_conv3p<N, POST_STORE, false><<<g, kPThreads, 0, st>>>(a);                       \
+        return true;
+    if (post == POST_POOL && !relu) return false;
+    switch (nt) {
+        RS_DNP_CASE(2) RS_DNP_CASE(3) RS_DNP_CASE(4)
+        default: return false;
+    }
+#undef RS_DNP_CASE
+}
+
 int create_impl(rs_context* ctx, const void* tza, size_t bytes, rs_denoiser** out) {
     if (!ctx || !tza || !out) return rs::ctx_fail(ctx, RS_E_INVALID, "rs_denoiser_create: null argument");
     *out = nullptr;
@@ -1020,7 +1055,7 @@ int create_impl(rs_context* ctx, const void* tza, size_t bytes, rs_denoiser** ou
     rs_denoiser* d = new rs_denoiser();
     d->ctx = ctx;
     d->device = rs::ctx_device(ctx);
-    if (const char* e = std::getenv("RESTIR_DN_PIPE")) d->pipe = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RESTIR_DN_PIPE")) d->pipe = std::strcmp(e, "1") == 0 ? 0xffffu : (uint32_t)std::strtoul(e, nullptr, 0);
     if (hipDeviceGetAttribute(&d->cus, hipDeviceAttributeMultiprocessorCount, d->device) != hipSuccess || d->cus < 1) d->cus = 256;
     if (const char* e = std::getenv("RESTIR_DN_PIPE_GRID")) d->cus = std::max(1, std::atoi(e));
     if (!check_net(T, d->net, err)) { delete d; return rs::ctx_fail(ctx, RS_E_INVALID, "rs_denoiser_create: " + err); }
@@ -1106,12 +1141,11 @@ int denoise_run(rs_denoiser* d, hipStream_t st, const float* color, int cst, con
             a.inv_norm = pu_forward(HDR_Y_MAX);
         }
         a.nt_total = L.nt;
-        if (d->pipe && ld.post == POST_STORE && L.nt == kPNT) {
+        if (((d->pipe >> l) & 1u) && ld.post != POST_FINAL && L.nt >= 2 && L.nt <= 4) {
             // one persistent workgroup per CU over 16 x 32 tiles (or one per tile when there are fewer)
             const size_t nt = (size_t)((a.w_ + kPTW - 1) / kPTW) * (size_t)((a.h + kPTH - 1) / kPTH);
-            const unsigned g = (unsigned)std::min<size_t>(nt, (size_t)d->cus);
-            if (ld.relu) k_conv3p<true><<<g, kPThreads, 0, st>>>(a);
-            else k_conv3p<false><<<g, kPThreads, 0, st>>>(a);
+            const dim3 g((unsigned)std::min<size_t>(nt, (size_t)d->cus));
+            if (!dispatch_pipe(L.nt, ld.post, ld.relu != 0, a, g, st)) return dfail(d, RS_E_UNSUPPORTED, "rs_denoise: unsupported layer");
             DCHK(d, hipGetLastError());
             if (d->timed) DCHK(d, hipEventRecord(d->evl[l + 1], st));
             continue;
