@@ -488,9 +488,14 @@ __device__ __forceinline__ PTile ptile(const ConvArgs& a, int t) {
     return PTile{(t - ty * tw) * kPTW, ty * kPTH};
 }
 
+// timing ablations of k_conv3p (wrong results; analysis builds only): bit 0 skips the B fragments' DMA after the
+// first stage, bit 1 the halo's
+#ifndef RS_DNP_ABLATE
+#define RS_DNP_ABLATE 0
+#endif
 // LDS-DMA of stage (tile t, chunk c) into buffer `buf`
 template <int NT>
-__device__ __forceinline__ void pstage_issue(const ConvArgs& a, int t, int c, uint8_t* buf) {
+__device__ __forceinline__ void pstage_issue(const ConvArgs& a, int t, int c, uint8_t* buf, bool first = true) {
     const PTile T = ptile(a, t);
     const int tid = (int)threadIdx.x, wv = tid >> 6;
     const int s = a.ch_src[c];
@@ -500,6 +505,7 @@ __device__ __forceinline__ void pstage_issue(const ConvArgs& a, int t, int c, ui
     const int nh = (w32 ? kPHalo32 : kPHalo16) / 16;
 #pragma unroll
     for (int r = 0; r < (kPHalo32 / 16 + kPThreads - 1) / kPThreads; ++r) {
+        if ((RS_DNP_ABLATE & 2) && !first) break;
         int q = r * kPThreads + tid;
         asm volatile("" : "+v"(q));                    // recomputed per stage: hoisted, the slot maps spill
         if (r * kPThreads + wv * 64 < nh) {                // the wave has slots in this round
@@ -520,6 +526,7 @@ __device__ __forceinline__ void pstage_issue(const ConvArgs& a, int t, int c, ui
     uint8_t* bb = buf + kPHalo32;
 #pragma unroll
     for (int r = 0; r < (9 * NT * 64 + kPThreads - 1) / kPThreads; ++r) {
+        if ((RS_DNP_ABLATE & 1) && !first) break;
         int q = r * kPThreads + tid;
         asm volatile("" : "+v"(q));
         if (r * kPThreads + wv * 64 < nb) glds16(w + (q < nb ? q : 0), bb + r * (kPThreads * 16) + wv * 1024);
@@ -605,8 +612,9 @@ __global__ void __launch_bounds__(kPThreads) k_conv3p(ConvArgs a) {
         if (cn == a.nchunk) { cn = 0; tn = t + (int)gridDim.x; }
         const bool more = tn < ntiles;
         if (more) {
-            pstage_issue<NT>(a, tn, cn, lds + (b ^ 1) * C::kBuf);
-            if (a.ch_w[cn] == 32) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::kWait32) : "memory");
+            pstage_issue<NT>(a, tn, cn, lds + (b ^ 1) * C::kBuf, RS_DNP_ABLATE == 0);
+            if (RS_DNP_ABLATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else if (a.ch_w[cn] == 32) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::kWait32) : "memory");
             else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::kWait16) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B builds of librestir_amd.so with changed compile-time switches (analysis tooling):
 #   scripts/build_variant.sh NAME "-DRS_X=1 -DRS_Y=2"   -> restir-embree_amd/_ab/lib_NAME.so
+# (REBUILD="rs_denoise ..." names the objects recompiled with the flags; default restir_capi rs_mgpu)
 # A -DNAME=v given here replaces the Makefile's own -DNAME=...; run with RESTIR_LIB=restir-embree_amd/_ab/lib_NAME.so.
 set -e
 cd "$(dirname "$0")/../restir-embree_amd"
@@ -16,6 +17,6 @@ PY
 )
 mkdir -p _ab "_build_$name"
 cp -p _build/*.o "_build_$name/"
-rm -f "_build_$name/restir_capi.o" "_build_$name/rs_mgpu.o"
+for o in ${REBUILD:-restir_capi rs_mgpu}; do rm -f "_build_$name/$o.o"; done
 make -s OBJ="_build_$name" LIB="_ab/lib_$name.so" HIPFLAGS="$flags" "_ab/lib_$name.so"
 echo "built _ab/lib_$name.so: $flags"
