@@ -341,10 +341,20 @@ __global__ void k_ploc_leaves(const uint64_t* keys, uint32_t n, const float4* lo
     C[j] = (int)j;
 }
 
-__global__ void __launch_bounds__(kPlocBlock) k_ploc_nearest(const int* C, int k, const float4* nlo, const float4* nhi,
-                                                             int* N) {
+// The iterations run in batches without a host round trip (kPlocBatch per synchronisation): the cluster count
+// and the next node id live in a device state that each iteration reads from slot p and writes to slot p ^ 1
+// (PlocState); grids are sized by the count at the last synchronisation, and an iteration that finds one
+// cluster left (or a failed one) passes the state and the cluster array through unchanged.
+struct PlocState { int k, base, err, pad; };
+constexpr int kPlocBatch = 4;
+
+__global__ void __launch_bounds__(kPlocBlock) k_ploc_nearest(const int* C, const PlocState* S, const float4* nlo,
+                                                             const float4* nhi, int* N) {
+    const int k = S->k;
+    if (k <= 1 || S->err) return;
     __shared__ float4 slo[kPlocBlock + 2 * kRadius], shi[kPlocBlock + 2 * kRadius];
     const int base = blockIdx.x * kPlocBlock;
+    if (base >= k) return;
     for (int t = threadIdx.x; t < kPlocBlock + 2 * kRadius; t += kPlocBlock) {
         int g = base - kRadius + t;
         if (g >= 0 && g < k) {
@@ -376,21 +386,34 @@ __global__ void __launch_bounds__(kPlocBlock) k_ploc_nearest(const int* C, int k
     N[i] = bj;
 }
 
-__global__ void k_ploc_flags(const int* N, int k, int* valid, int* merged) {
+// flags of the k live clusters; zeros over [k, kmax) so the scans may run over the host's bound kmax
+__global__ void k_ploc_flags(const int* N, const PlocState* S, int kmax, int* valid, int* merged) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= k) return;
+    const int k = S->k;
+    if (i >= kmax || k <= 1 || S->err) return;
+    if (i >= k) { valid[i] = 0; merged[i] = 0; return; }
     int j = N[i];
     bool mutual = j >= 0 && N[j] == i;
     valid[i] = (mutual && j < i) ? 0 : 1;   // the right partner of a merge disappears
     merged[i] = (mutual && i < j) ? 1 : 0;
 }
 
-__global__ void k_ploc_merge(const int* C, int k, const int* N, const int* valid, const int* merged, const int* pos,
-                             const int* mid, int base, float4* nlo, float4* nhi, int* parent, int* cnt, int* Cout) {
+__global__ void k_ploc_merge(const int* C, const PlocState* S, PlocState* Snext, const int* N, const int* valid,
+                             const int* merged, const int* pos, const int* mid, float4* nlo, float4* nhi, int* parent,
+                             int* cnt, int* Cout) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= k) return;
+    const PlocState s = *S;
+    if (s.k <= 1 || s.err) {                   // done (or failed): pass everything through
+        if (i == 0) { *Snext = s; Cout[0] = C[0]; }
+        return;
+    }
+    if (i >= s.k) return;
+    if (i == s.k - 1) {                        // the last cluster knows the totals of the scans
+        const int merges = mid[i] + merged[i];
+        *Snext = PlocState{pos[i] + valid[i], s.base + merges, merges <= 0 ? 1 : 0, 0};
+    }
     if (merged[i]) {
-        int id = base + mid[i];
+        int id = s.base + mid[i];
         int L = C[i], R = C[N[i]];
         float4 al = nlo[L], ah = nhi[L], bl = nlo[R], bh = nhi[R];
         nlo[id] = make_float4(fminf(al.x, bl.x), fminf(al.y, bl.y), fminf(al.z, bl.z), __int_as_float(L));
@@ -489,7 +512,7 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
     size_t tmp_bytes = 0, tmp2_bytes = 0;
     int init_cb[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
     int k = (int)n, base = (int)n, root = 0, max_depth = 0, kept_root = 1;
-    int h2[4];
+    PlocState* pst = nullptr;                  // two slots (the iteration's parity)
 
     PLOC_CHECK(hipMalloc(&lo, n * sizeof(float4)));
     PLOC_CHECK(hipMalloc(&hi, n * sizeof(float4)));
@@ -512,6 +535,7 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
     PLOC_CHECK(hipMalloc(&pos, n * sizeof(int)));
     PLOC_CHECK(hipMalloc(&mid, n * sizeof(int)));
     PLOC_CHECK(hipMalloc(&dmax, sizeof(int)));
+    PLOC_CHECK(hipMalloc(&pst, 2 * sizeof(PlocState)));
     PLOC_CHECK(hipMemcpyAsync(cb, init_cb, sizeof init_cb, hipMemcpyHostToDevice, st));
     PLOC_CHECK(hipMemsetAsync(dmax, 0, sizeof(int), st));
     PLOC_CHECK(hipMemsetAsync(parent, 0xff, (size_t)total * sizeof(int), st));   // -1
@@ -527,25 +551,29 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
     k_ploc_leaves<<<(n + B - 1) / B, B, 0, st>>>(keys_sorted, n, lo, hi, nlo, nhi, cnt, C0);
     PLOC_CHECK(hipGetLastError());
 
-    while (k > 1) {
-        int g = (k + B - 1) / B;
-        k_ploc_nearest<<<(k + kPlocBlock - 1) / kPlocBlock, kPlocBlock, 0, st>>>(C0, k, nlo, nhi, N);
-        k_ploc_flags<<<g, B, 0, st>>>(N, k, valid, merged);
-        PLOC_CHECK(hipGetLastError());
-        PLOC_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp2, tmp2_bytes, valid, pos, k, st));
-        PLOC_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp2, tmp2_bytes, merged, mid, k, st));
-        k_ploc_merge<<<g, B, 0, st>>>(C0, k, N, valid, merged, pos, mid, base, nlo, nhi, parent, cnt, C1);
-        PLOC_CHECK(hipGetLastError());
-        PLOC_CHECK(hipMemcpyAsync(&h2[0], pos + (k - 1), sizeof(int), hipMemcpyDeviceToHost, st));
-        PLOC_CHECK(hipMemcpyAsync(&h2[1], valid + (k - 1), sizeof(int), hipMemcpyDeviceToHost, st));
-        PLOC_CHECK(hipMemcpyAsync(&h2[2], mid + (k - 1), sizeof(int), hipMemcpyDeviceToHost, st));
-        PLOC_CHECK(hipMemcpyAsync(&h2[3], merged + (k - 1), sizeof(int), hipMemcpyDeviceToHost, st));
+    {
+        PlocState h0{k, base, 0, 0};
+        PLOC_CHECK(hipMemcpyAsync(&pst[0], &h0, sizeof h0, hipMemcpyHostToDevice, st));
+    }
+    for (int par = 0; k > 1;) {                  // batches of kPlocBatch iterations, one round trip each
+        const int kmax = k, g = (kmax + B - 1) / B;
+        for (int it = 0; it < kPlocBatch; ++it, par ^= 1) {
+            k_ploc_nearest<<<(kmax + kPlocBlock - 1) / kPlocBlock, kPlocBlock, 0, st>>>(C0, pst + par, nlo, nhi, N);
+            k_ploc_flags<<<g, B, 0, st>>>(N, pst + par, kmax, valid, merged);
+            PLOC_CHECK(hipGetLastError());
+            PLOC_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp2, tmp2_bytes, valid, pos, kmax, st));
+            PLOC_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp2, tmp2_bytes, merged, mid, kmax, st));
+            k_ploc_merge<<<g, B, 0, st>>>(C0, pst + par, pst + (par ^ 1), N, valid, merged, pos, mid, nlo, nhi, parent,
+                                          cnt, C1);
+            PLOC_CHECK(hipGetLastError());
+            std::swap(C0, C1);
+        }
+        PlocState hs{};
+        PLOC_CHECK(hipMemcpyAsync(&hs, pst + par, sizeof hs, hipMemcpyDeviceToHost, st));
         PLOC_CHECK(hipStreamSynchronize(st));
-        int merges = h2[2] + h2[3];
-        if (merges <= 0) { err = "PLOC made no progress"; goto fail; }
-        base += merges;
-        k = h2[0] + h2[1];
-        std::swap(C0, C1);
+        if (hs.err) { err = "PLOC made no progress"; goto fail; }
+        k = hs.k;
+        base = hs.base;
     }
     PLOC_CHECK(hipMemcpyAsync(&root, C0, sizeof(int), hipMemcpyDeviceToHost, st));
     PLOC_CHECK(hipStreamSynchronize(st));
@@ -574,7 +602,7 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
     nodes = nullptr; tris = nullptr;
 fail: {
         void* ptrs[] = {lo, hi, nlo, nhi, nodes, tris, cb, cnt, parent, C0, C1, N, valid, merged, pos, mid, depth,
-                        dmax, kept, collapsed, cost, keys, keys_sorted, tmp, tmp2};
+                        dmax, kept, collapsed, cost, keys, keys_sorted, tmp, tmp2, pst};
         for (void* p : ptrs) if (p) hipFree(p);
     }
     return *d_nodes || n == 0 ? 0 : -1;

@@ -979,8 +979,8 @@ struct rs_denoiser {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t evl[17] = {};                    // timed: after the input transform, after each convolution
     bool timed = false;
-    uint32_t pipe = 0xffffu;                    // layers (bit l) on k_conv3p where it applies (2..4 n-tiles);
-                                                // RESTIR_DN_PIPE=<mask>, 0 = k_conv3 everywhere
+    uint32_t pipe = 0u;                         // layers (bit l) on k_conv3p where it applies (2..4 n-tiles):
+                                                // RESTIR_DN_PIPE=<mask> or 1 (all); measured slower, off
     int cus = 256;                              // its workgroups (RESTIR_DN_PIPE_GRID caps them: tests)
 };
 

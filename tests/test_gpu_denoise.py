@@ -122,7 +122,7 @@ def test_pipelined_conv_bit_identical(monkeypatch, H, W, grid):
     color, albedo, normal = _images(H, W, seed=5 + H)
     outs = {}
     try:
-        for pipe in ("0", "1"):
+        for pipe in ("0", "1"):                # 1: every layer k_conv3p applies to
             monkeypatch.setenv("RESTIR_DN_PIPE", pipe)
             if grid is not None:
                 monkeypatch.setenv("RESTIR_DN_PIPE_GRID", grid)
