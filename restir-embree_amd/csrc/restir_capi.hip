@@ -24,6 +24,7 @@
 namespace rs {
 int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes, float4** d_tris,
               WideBvh* wide, std::string& err);
+void preload_code_objects();
 int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int** d_order, int** d_lvl_off,
                    std::vector<int>& lvl_off, std::string& err);
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
@@ -402,6 +403,7 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (hipEventCreate(&e) != hipSuccess) return bail("hipEventCreate failed");
     for (int i = 0; i < EV_COUNT; ++i) c->ev[i] = c->evr[0][i];
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail("context init failed");
+    rs::preload_code_objects();
     if (const char* t = std::getenv("RESTIR_TRAVERSAL")) {     // auto (default) | lockstep | lane
         if (!std::strcmp(t, "lockstep")) c->trav_mode = RS_TRAVERSAL_LOCKSTEP;
         else if (!std::strcmp(t, "lane")) c->trav_mode = RS_TRAVERSAL_LANE;

@@ -668,6 +668,14 @@ int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_
 // not apply (non-finite positions, no plan within the walk's depth) or its build fails, the scene keeps the
 // binary tree and the walks take the skip pointers (RESTIR_WIDE=off: never built).
 int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::string& err);
+void preload_wide_build();
+// HIP loads a source file's code object at the first launch (or attribute query) of one of its kernels: at
+// context creation, so that a scene build is not charged the one-time load of the builders (~10 ms at C3)
+void preload_code_objects() {
+    hipFuncAttributes fa;
+    (void)hipFuncGetAttributes(&fa, (const void*)k_ploc_nearest);
+    preload_wide_build();
+}
 void wide_free(WideBvh& w) {
     void* p[] = {w.nodes, w.tris, w.box};
     for (void* q : p) if (q) hipFree(q);

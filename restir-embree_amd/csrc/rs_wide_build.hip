@@ -365,6 +365,114 @@ __global__ void k_seg_link(const Seg* __restrict__ segs, int ns, const int2* __r
 
 // ---------------------------------------------------------------- 3 small segments: one workgroup each
 struct SmallSeg { int first, count, id, depth; };
+// Jobs (nodes) of more than kWaveJob triangles are split by the whole workgroup (bitonic sorts and scans in
+// LDS, barriers); smaller ones -- most of a segment's nodes -- go to a list that the four waves drain in
+// parallel, each splitting its subtree depth-first in registers (wave_subtree: shuffles, no barriers).  Both
+// make the host's decision (build_sah_host: sort by (centroid, triangle id), full-sweep SAH in double, first
+// minimum, earlier axes win ties).  Node ids are drawn from one counter in the segment's reserved range; the
+// order in which subtrees draw them does not change the wide tree (every later choice is a function of a
+// node's triangle set).
+constexpr int kWaveJob = 64;
+
+__device__ __forceinline__ bool key_after(int x, float cx, int tx, int y, float cy, int ty) {   // x after y?
+    if (x < 0) return y >= 0;                  // padding after everything
+    if (y < 0) return false;
+    return cy < cx || (cy == cx && ty < tx);
+}
+
+__device__ void wave_subtree(int4 J0, int lane, const int* s_tri, float (*s_lo)[kSmall], float (*s_hi)[kSmall],
+                             float (*s_cen)[kSmall], int* s_ord, int* s_next, int* s_maxd, int n, float4* nlo,
+                             float4* nhi, int* depth) {
+    int4 stk = make_int4(0, 0, 0, 0);          // lane i holds stack entry i (depth-first: <= 63 entries)
+    if (lane == 0) stk = J0;
+    int sp = 1;
+    while (sp > 0) {
+        int4 J;
+        J.x = __shfl(stk.x, sp - 1); J.y = __shfl(stk.y, sp - 1); J.z = __shfl(stk.z, sp - 1); J.w = __shfl(stk.w, sp - 1);
+        --sp;
+        const int f = J.x, c = J.y;
+        const bool in = lane < c;
+        const int e0 = in ? s_ord[f + lane] : -1;
+        double best = 1e300;
+        int bax = 0, bs = c / 2;
+        int srt[3];
+        float pl[3], ph[3];                    // the last axis' prefix box (the node box at lane c - 1)
+        for (int a = 0; a < 3; ++a) {
+            int x = e0;
+            float cx = x >= 0 ? s_cen[a][x] : 0.0f;
+            int tx = x >= 0 ? s_tri[x] : 0;
+            for (int k = 2; k <= 64; k <<= 1)
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    const int y = __shfl_xor(x, j);
+                    const float cy = __shfl_xor(cx, j);
+                    const int ty = __shfl_xor(tx, j);
+                    const bool up = (lane & k) == 0, lower = (lane & j) == 0;
+                    const bool mine_after = key_after(x, cx, tx, y, cy, ty);
+                    // the lower lane of an ascending pair keeps the smaller element
+                    const bool take = (lower == up) ? mine_after : key_after(y, cy, ty, x, cx, tx);
+                    if (take) { x = y; cx = cy; tx = ty; }
+                }
+            srt[a] = x;
+            float ql[3], qh[3];
+            for (int k = 0; k < 3; ++k) {
+                pl[k] = in ? s_lo[k][x] : 0.0f; ph[k] = in ? s_hi[k][x] : 0.0f;
+                ql[k] = pl[k]; qh[k] = ph[k];
+            }
+            // inclusive prefix (elements 0..lane) and suffix (lane..c-1) box scans
+            for (int o = 1; o < c; o <<= 1) {
+                for (int k = 0; k < 3; ++k) {
+                    const float ul = __shfl_up(pl[k], o), uh = __shfl_up(ph[k], o);
+                    const float dl = __shfl_down(ql[k], o), dh = __shfl_down(qh[k], o);
+                    if (in && lane >= o) { pl[k] = w_min(ul, pl[k]); ph[k] = w_max(uh, ph[k]); }
+                    if (in && lane + o < c) { ql[k] = w_min(ql[k], dl); qh[k] = w_max(qh[k], dh); }
+                }
+            }
+            // split at i = lane + 1 (left = sorted 0..lane): boxes grown from the empty box
+            double cost = 1e300;
+            const int i = lane + 1;
+            float rl[3], rh[3];
+            for (int k = 0; k < 3; ++k) { rl[k] = __shfl_down(ql[k], 1); rh[k] = __shfl_down(qh[k], 1); }
+            if (i < c) {
+                float ll[3], lh[3], Rl[3], Rh[3];
+                for (int k = 0; k < 3; ++k) {
+                    ll[k] = w_min(kEmpty, pl[k]); lh[k] = w_max(-kEmpty, ph[k]);
+                    Rl[k] = w_min(kEmpty, rl[k]); Rh[k] = w_max(-kEmpty, rh[k]);
+                }
+                cost = half_area_d(ll, lh) * i + half_area_d(Rl, Rh) * (c - i);
+            }
+            int bi = i;
+            for (int o = 32; o > 0; o >>= 1) {  // first minimum in position order
+                const double oc = __shfl_xor(cost, o);
+                const int ob = __shfl_xor(bi, o);
+                if (oc < cost || (oc == cost && ob < bi)) { cost = oc; bi = ob; }
+            }
+            if (cost < best) { best = cost; bax = a; bs = bi; }   // earlier axes win ties
+        }
+        const int xs = bax == 0 ? srt[0] : bax == 1 ? srt[1] : srt[2];
+        if (in) s_ord[f + lane] = xs;
+        float l[3], h[3];
+        for (int k = 0; k < 3; ++k) {
+            l[k] = w_min(kEmpty, __shfl(pl[k], c - 1));
+            h[k] = w_max(-kEmpty, __shfl(ph[k], c - 1));
+        }
+        const int cf[2] = {f, f + bs}, cc[2] = {bs, c - bs};
+        int cid[2];
+        for (int q = 0; q < 2; ++q) {
+            if (cc[q] == 1) { cid[q] = s_tri[__shfl(xs, cf[q] - f)]; continue; }
+            int id = 0;
+            if (lane == 0) { id = atomicAdd(s_next, 1); atomicMax(s_maxd, J.w + 1); }
+            cid[q] = __shfl(id, 0);
+            if (lane == sp) stk = make_int4(cf[q], cc[q], cid[q], J.w + 1);
+            ++sp;
+        }
+        if (lane == 0) {
+            nlo[J.z] = make_float4(l[0], l[1], l[2], __int_as_float(cid[0]));
+            nhi[J.z] = make_float4(h[0], h[1], h[2], __int_as_float(cid[1]));
+            depth[J.z - n] = J.w;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kB) k_small(const SmallSeg* __restrict__ segs, const int* __restrict__ idx,
                                              const float4* __restrict__ tlo, const float4* __restrict__ thi,
                                              const float4* __restrict__ tcen, int n, float4* nlo, float4* nhi,
@@ -377,8 +485,9 @@ __global__ void __launch_bounds__(kB) k_small(const SmallSeg* __restrict__ segs,
     __shared__ float s_plo[3][kSmall], s_phi[3][kSmall], s_qlo[3][kSmall], s_qhi[3][kSmall];
     __shared__ double s_bc[kB / 64];
     __shared__ int s_bi[kB / 64];
-    __shared__ int4 s_job[kSmall];
-    __shared__ int s_sp, s_next, s_maxd;
+    __shared__ int4 s_job[kSmall / kWaveJob + 8];
+    __shared__ int4 s_wjob[kSmall / 2];
+    __shared__ int s_sp, s_next, s_maxd, s_nw, s_take;
     __shared__ double s_best;
     __shared__ int s_bax, s_bs;
     if (tid < G.count) {
@@ -390,9 +499,14 @@ __global__ void __launch_bounds__(kB) k_small(const SmallSeg* __restrict__ segs,
         s_cen[0][tid] = c.x; s_cen[1][tid] = c.y; s_cen[2][tid] = c.z;
         s_ord[tid] = tid;
     }
-    if (tid == 0) { s_job[0] = make_int4(0, G.count, G.id, G.depth); s_sp = 1; s_next = G.id + 1; s_maxd = G.depth; }
+    if (tid == 0) {
+        s_sp = 0; s_nw = 0; s_take = 0;
+        if (G.count > kWaveJob) s_job[s_sp++] = make_int4(0, G.count, G.id, G.depth);
+        else s_wjob[s_nw++] = make_int4(0, G.count, G.id, G.depth);
+        s_next = G.id + 1; s_maxd = G.depth;
+    }
     __syncthreads();
-    while (true) {
+    while (true) {                             // the workgroup: jobs of more than kWaveJob triangles
         if (s_sp == 0) break;
         const int4 J = s_job[s_sp - 1];
         const int f = J.x, c = J.y;
@@ -488,7 +602,8 @@ __global__ void __launch_bounds__(kB) k_small(const SmallSeg* __restrict__ segs,
             for (int q = 0; q < 2; ++q) {
                 if (cc[q] == 1) { cid[q] = s_tri[s_ord[cf[q]]]; continue; }
                 cid[q] = s_next++;
-                s_job[s_sp++] = make_int4(cf[q], cc[q], cid[q], J.w + 1);
+                if (cc[q] > kWaveJob) s_job[s_sp++] = make_int4(cf[q], cc[q], cid[q], J.w + 1);
+                else s_wjob[s_nw++] = make_int4(cf[q], cc[q], cid[q], J.w + 1);
                 s_maxd = max(s_maxd, J.w + 1);
             }
             nlo[J.z] = make_float4(l[0], l[1], l[2], __int_as_float(cid[0]));
@@ -497,6 +612,16 @@ __global__ void __launch_bounds__(kB) k_small(const SmallSeg* __restrict__ segs,
         }
         __syncthreads();
     }
+    // the waves: subtrees of at most kWaveJob triangles, one list entry at a time
+    const int lane = tid & 63;
+    for (;;) {
+        int j = 0;
+        if (lane == 0) j = atomicAdd(&s_take, 1);
+        j = __shfl(j, 0);
+        if (j >= s_nw) break;
+        wave_subtree(s_wjob[j], lane, s_tri, s_lo, s_hi, s_cen, s_ord, &s_next, &s_maxd, n, nlo, nhi, depth);
+    }
+    __syncthreads();
     if (tid == 0) atomicMax(max_depth, s_maxd);
 }
 
@@ -538,53 +663,73 @@ __global__ void k_depth_fill_flat(const int* __restrict__ depth, int m, int* fil
     if (i < m) order[atomicAdd(&fill[depth[i]], 1)] = i;
 }
 // S(x, k, g) for the internal nodes of one depth level (SahCollapse::plan's loops, same float operations):
-// tables per internal node x - n, [g + 1][k - 1]
+// tables per internal node x - n, [g + 1][k - 1].  16 lanes per node, lane g + 1 computes row g: its D(k) from
+// the children's rows g (two coalesced 32-B rows), the node term N from D(8) of row g - 1 (the lane below,
+// by shuffle).  One lane per node walking all ten rows serially took 25-130 us per level launch (23 launches
+// at C3), latency on the children's tables.
+constexpr int kDpLanes = 16;
 __global__ void k_dp_level(const int* __restrict__ order, int b, int e, int n, const float4* __restrict__ nlo,
                            const float4* __restrict__ nhi, float* S, uint8_t* open, uint8_t* split) {
-    const int q = b + blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= e) return;
-    const int xi = order[q], x = n + xi;
-    const float4 xl = nlo[x], xh = nhi[x];
-    const int l = __float_as_int(xl.w), r = __float_as_int(xh.w);
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int q = b + t / kDpLanes, gi = t % kDpLanes, g = gi - 1;
+    const bool node = q < e, act = node && gi < kG;
     const float inf = 3.0e38f;
-    const float al = l < n ? area_f(nlo[l], nhi[l]) * kCtri : 0.0f, ar = r < n ? area_f(nlo[r], nhi[r]) * kCtri : 0.0f;
-    const float* Sl = l < n ? nullptr : S + (size_t)(l - n) * kG * 8;
-    const float* Sr = r < n ? nullptr : S + (size_t)(r - n) * kG * 8;
-    float* Sx = S + (size_t)xi * kG * 8;
-    uint8_t* Ox = open + (size_t)xi * kG * 8;
-    uint8_t* Px = split + (size_t)xi * kG * 8;
-    const float ax = area_f(xl, xh);
-    float Dprev[8] = {};
-    for (int g = -1; g <= kGmax; ++g) {
-        float D[8];
-        D[0] = 0.0f;
+    float D[8];
+    D[0] = 0.0f;
+    int xi = 0;
+    float ax = 0.0f;
+    if (act) {
+        xi = order[q];
+        const int x = n + xi;
+        const float4 xl = nlo[x], xh = nhi[x];
+        const int l = __float_as_int(xl.w), r = __float_as_int(xh.w);
+        ax = area_f(xl, xh);
+        float rl[8], rr[8];
+        if (l < n) { const float al = area_f(nlo[l], nhi[l]) * kCtri; for (int k = 0; k < 8; ++k) rl[k] = al; }
+        else {
+            const float4* p = (const float4*)(S + (size_t)(l - n) * kG * 8 + gi * 8);
+            const float4 u = p[0], v = p[1];
+            rl[0] = u.x; rl[1] = u.y; rl[2] = u.z; rl[3] = u.w; rl[4] = v.x; rl[5] = v.y; rl[6] = v.z; rl[7] = v.w;
+        }
+        if (r < n) { const float ar = area_f(nlo[r], nhi[r]) * kCtri; for (int k = 0; k < 8; ++k) rr[k] = ar; }
+        else {
+            const float4* p = (const float4*)(S + (size_t)(r - n) * kG * 8 + gi * 8);
+            const float4 u = p[0], v = p[1];
+            rr[0] = u.x; rr[1] = u.y; rr[2] = u.z; rr[3] = u.w; rr[4] = v.x; rr[5] = v.y; rr[6] = v.z; rr[7] = v.w;
+        }
+        uint8_t* Px = split + (size_t)xi * kG * 8 + gi * 8;
+#pragma unroll
         for (int k = 2; k <= 8; ++k) {
             float best = inf;
             int ba = 1;
+#pragma unroll
             for (int a = 1; a < k; ++a) {
-                const float sl = Sl ? Sl[(g + 1) * 8 + (a - 1)] : al;
-                const float sr = Sr ? Sr[(g + 1) * 8 + (k - a - 1)] : ar;
-                const float v = sl + sr;
+                const float v = rl[a - 1] + rr[k - a - 1];
                 if (v < best) { best = v; ba = a; }
             }
             D[k - 1] = best;
-            Px[(g + 1) * 8 + (k - 1)] = (uint8_t)ba;
+            Px[k - 1] = (uint8_t)ba;
         }
-        float Nx = inf;
-        if (g >= 0) {
-            const float d8 = Dprev[7];
-            Nx = d8 < inf ? ax * kCnode + d8 : inf;
-        }
-        Sx[(g + 1) * 8 + 0] = Nx;
-        Px[(g + 1) * 8 + 0] = 0;
-        Ox[(g + 1) * 8 + 0] = 0;
-        for (int k = 2; k <= 8; ++k) {
-            const float prev = Sx[(g + 1) * 8 + (k - 2)];
-            const bool o = D[k - 1] < prev;
-            Sx[(g + 1) * 8 + (k - 1)] = o ? D[k - 1] : prev;
-            Ox[(g + 1) * 8 + (k - 1)] = o ? 1 : 0;
-        }
-        for (int k = 0; k < 8; ++k) Dprev[k] = D[k];
+        Px[0] = 0;
+    } else {
+#pragma unroll
+        for (int k = 1; k < 8; ++k) D[k] = 0.0f;
+    }
+    const float d8 = __shfl_up(D[7], 1, kDpLanes);     // D(8) of row g - 1 (Dprev; zeros before row -1)
+    if (!act) return;
+    float Nx = inf;
+    if (g >= 0) Nx = d8 < inf ? ax * kCnode + d8 : inf;
+    float* Sx = S + (size_t)xi * kG * 8 + gi * 8;
+    uint8_t* Ox = open + (size_t)xi * kG * 8 + gi * 8;
+    float prev = Nx;
+    Sx[0] = Nx;
+    Ox[0] = 0;
+#pragma unroll
+    for (int k = 2; k <= 8; ++k) {
+        const bool o = D[k - 1] < prev;
+        prev = o ? D[k - 1] : prev;
+        Sx[k - 1] = prev;
+        Ox[k - 1] = o ? 1 : 0;
     }
 }
 
@@ -690,6 +835,13 @@ struct Scratch {
 // Builds the 8-wide tree of the n triangles at d_pos (device, 9 floats each) on `st`.  Returns 0 with *w filled
 // (device allocations owned by the caller), 1 when no tree applies (non-finite positions, or no plan within the
 // walk's depth: the walks then take the skip pointers; *w stays empty), -1 on a HIP error (err set).
+// the code object of this file loaded now (HIP loads a file's kernels at its first launch or query; see
+// rs::preload_code_objects)
+void preload_wide_build() {
+    hipFuncAttributes fa;
+    (void)hipFuncGetAttributes(&fa, (const void*)wb::k_small);
+}
+
 int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::string& err) {
     using namespace wb;
     *w = WideBvh{};
@@ -810,7 +962,7 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
         else k_depth_fill_flat<<<(m + kB - 1) / kB, kB, 0, st>>>(depth, m, cnt, order);
         for (int d = nd - 1; d >= 0; --d) {
             const int b = off[d], e = off[d + 1];
-            if (e > b) k_dp_level<<<(e - b + 127) / 128, 128, 0, st>>>(order, b, e, n, nlo, nhi, S, open, split);
+            if (e > b) k_dp_level<<<(unsigned)(((size_t)(e - b) * kDpLanes + 127) / 128), 128, 0, st>>>(order, b, e, n, nlo, nhi, S, open, split);
         }
         WB_HIP(hipGetLastError());
         float s_root = 0.0f;

@@ -23,7 +23,9 @@ from restir_amd import Renderer, scenes  # noqa: E402
 
 torch.cuda.set_device(0)
 sc = scenes.by_name(a.scene)
+t0 = time.perf_counter()
 r = Renderer(64, 48)
+print(f"context create wall {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
 for i in range(a.repeat):
     t0 = time.perf_counter()
     gs = r.load_scene(sc)

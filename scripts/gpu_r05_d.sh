@@ -16,3 +16,6 @@ print(f"{sys.argv[2]:45s} bands: max {max(t):.4f} mean {sum(t) / len(t):.4f} ms 
 PY
 done
 VARIANTS="base" SCENES="C2 C3 C5" STEPS=30 bash scripts/gpu_ab_env.sh || exit 1
+timeout -k 10 300 python scripts/initial_breakdown.py --scene C2 --frames 6 > gpurun_out/breakdown_C2.txt 2>&1 || exit 1
+timeout -k 10 400 python scripts/initial_breakdown.py --scene C3 --frames 4 > gpurun_out/breakdown_C3.txt 2>&1 || exit 1
+grep -h "initial_ms" gpurun_out/breakdown_C2.txt gpurun_out/breakdown_C3.txt
