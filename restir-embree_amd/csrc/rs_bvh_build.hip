@@ -514,28 +514,28 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
     int k = (int)n, base = (int)n, root = 0, max_depth = 0, kept_root = 1;
     PlocState* pst = nullptr;                  // two slots (the iteration's parity)
 
-    PLOC_CHECK(hipMalloc(&lo, n * sizeof(float4)));
-    PLOC_CHECK(hipMalloc(&hi, n * sizeof(float4)));
-    PLOC_CHECK(hipMalloc(&cb, 6 * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&keys, n * sizeof(uint64_t)));
-    PLOC_CHECK(hipMalloc(&keys_sorted, n * sizeof(uint64_t)));
-    PLOC_CHECK(hipMalloc(&nlo, (size_t)total * sizeof(float4)));
-    PLOC_CHECK(hipMalloc(&nhi, (size_t)total * sizeof(float4)));
-    PLOC_CHECK(hipMalloc(&cnt, (size_t)total * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&parent, (size_t)total * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&depth, (size_t)total * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&kept, (size_t)total * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&collapsed, (size_t)total * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&cost, (size_t)total * sizeof(float)));
-    PLOC_CHECK(hipMalloc(&C0, n * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&C1, n * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&N, n * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&valid, n * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&merged, n * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&pos, n * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&mid, n * sizeof(int)));
-    PLOC_CHECK(hipMalloc(&dmax, sizeof(int)));
-    PLOC_CHECK(hipMalloc(&pst, 2 * sizeof(PlocState)));
+    PLOC_CHECK(hipMallocAsync((void**)&lo, n * sizeof(float4), st));
+    PLOC_CHECK(hipMallocAsync((void**)&hi, n * sizeof(float4), st));
+    PLOC_CHECK(hipMallocAsync((void**)&cb, 6 * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&keys, n * sizeof(uint64_t), st));
+    PLOC_CHECK(hipMallocAsync((void**)&keys_sorted, n * sizeof(uint64_t), st));
+    PLOC_CHECK(hipMallocAsync((void**)&nlo, (size_t)total * sizeof(float4), st));
+    PLOC_CHECK(hipMallocAsync((void**)&nhi, (size_t)total * sizeof(float4), st));
+    PLOC_CHECK(hipMallocAsync((void**)&cnt, (size_t)total * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&parent, (size_t)total * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&depth, (size_t)total * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&kept, (size_t)total * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&collapsed, (size_t)total * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&cost, (size_t)total * sizeof(float), st));
+    PLOC_CHECK(hipMallocAsync((void**)&C0, n * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&C1, n * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&N, n * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&valid, n * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&merged, n * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&pos, n * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&mid, n * sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&dmax, sizeof(int), st));
+    PLOC_CHECK(hipMallocAsync((void**)&pst, 2 * sizeof(PlocState), st));
     PLOC_CHECK(hipMemcpyAsync(cb, init_cb, sizeof init_cb, hipMemcpyHostToDevice, st));
     PLOC_CHECK(hipMemsetAsync(dmax, 0, sizeof(int), st));
     PLOC_CHECK(hipMemsetAsync(parent, 0xff, (size_t)total * sizeof(int), st));   // -1
@@ -544,10 +544,10 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
     k_morton<<<(n + B - 1) / B, B, 0, st>>>(lo, hi, n, cb, keys);
     PLOC_CHECK(hipGetLastError());
     PLOC_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, keys_sorted, (int)n, 0, 62, st));
-    PLOC_CHECK(hipMalloc(&tmp, tmp_bytes));
+    PLOC_CHECK(hipMallocAsync(&tmp, tmp_bytes, st));
     PLOC_CHECK(hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, keys_sorted, (int)n, 0, 62, st));
     PLOC_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2_bytes, valid, pos, (int)n, st));
-    PLOC_CHECK(hipMalloc(&tmp2, tmp2_bytes));
+    PLOC_CHECK(hipMallocAsync(&tmp2, tmp2_bytes, st));
     k_ploc_leaves<<<(n + B - 1) / B, B, 0, st>>>(keys_sorted, n, lo, hi, nlo, nhi, cnt, C0);
     PLOC_CHECK(hipGetLastError());
 
@@ -601,9 +601,13 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_no
     *d_nodes = nodes; *d_tris = tris; *n_nodes = (uint32_t)kept_root;
     nodes = nullptr; tris = nullptr;
 fail: {
-        void* ptrs[] = {lo, hi, nlo, nhi, nodes, tris, cb, cnt, parent, C0, C1, N, valid, merged, pos, mid, depth,
+        // scratch: stream-ordered frees into the device pool (no synchronisation; the next build's or the wide
+        // build's allocations reuse it, see build_pool_setup); the outputs are ordinary allocations
+        void* ptrs[] = {lo, hi, nlo, nhi, cb, cnt, parent, C0, C1, N, valid, merged, pos, mid, depth,
                         dmax, kept, collapsed, cost, keys, keys_sorted, tmp, tmp2, pst};
-        for (void* p : ptrs) if (p) hipFree(p);
+        for (void* p : ptrs) if (p) (void)hipFreeAsync(p, st);
+        if (nodes) hipFree(nodes);
+        if (tris) hipFree(tris);
     }
     return *d_nodes || n == 0 ? 0 : -1;
 }
@@ -675,6 +679,15 @@ void preload_code_objects() {
     hipFuncAttributes fa;
     (void)hipFuncGetAttributes(&fa, (const void*)k_ploc_nearest);
     preload_wide_build();
+    // the builders' scratch comes from the device's default pool (hipMallocAsync): keep up to 2 GiB of it
+    // cached between builds instead of returning it to the driver at every synchronisation
+    int dev = 0;
+    hipMemPool_t pool;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t keep = 2ull << 30;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    (void)hipGetLastError();
 }
 void wide_free(WideBvh& w) {
     void* p[] = {w.nodes, w.tris, w.box};

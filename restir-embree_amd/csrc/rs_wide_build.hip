@@ -391,6 +391,8 @@ __device__ void wave_subtree(int4 J0, int lane, const int* s_tri, float (*s_lo)[
         J.x = __shfl(stk.x, sp - 1); J.y = __shfl(stk.y, sp - 1); J.z = __shfl(stk.z, sp - 1); J.w = __shfl(stk.w, sp - 1);
         --sp;
         const int f = J.x, c = J.y;
+        int P = 2;                             // sort width: c rounded up to a power of two (lanes >= P idle)
+        while (P < c) P <<= 1;
         const bool in = lane < c;
         const int e0 = in ? s_ord[f + lane] : -1;
         double best = 1e300;
@@ -401,7 +403,7 @@ __device__ void wave_subtree(int4 J0, int lane, const int* s_tri, float (*s_lo)[
             int x = e0;
             float cx = x >= 0 ? s_cen[a][x] : 0.0f;
             int tx = x >= 0 ? s_tri[x] : 0;
-            for (int k = 2; k <= 64; k <<= 1)
+            for (int k = 2; k <= P; k <<= 1)
                 for (int j = k >> 1; j > 0; j >>= 1) {
                     const int y = __shfl_xor(x, j);
                     const float cy = __shfl_xor(cx, j);
@@ -801,6 +803,11 @@ __global__ void k_wide_emit(WideQ* wq, int q0, int q1, int tri_off, const int* _
 }
 
 // ---------------------------------------------------------------- 6 wide-leaf triangles
+// a wide level's totals for the host: next-level nodes (scan + last count), leaf triangles, the failure flag
+__global__ void k_level_totals(const int* si, const int* ni, const int* sl, const int* nl, int cnt, const int* bad,
+                               int* out) {
+    if (threadIdx.x == 0) { out[0] = si[cnt - 1]; out[1] = ni[cnt - 1]; out[2] = sl[cnt - 1]; out[3] = nl[cnt - 1]; out[4] = *bad; }
+}
 __global__ void k_wide_gather(const float* __restrict__ pos, const int* __restrict__ prims, uint32_t m, float4* tris) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= m) return;
@@ -813,15 +820,18 @@ __global__ void k_wide_gather(const float* __restrict__ pos, const int* __restri
 }
 
 // device scratch freed on every exit
+// stream-ordered scratch from the device pool (rs_bvh_build.hip preload_code_objects keeps it cached)
 struct Scratch {
+    hipStream_t st;
     std::vector<void*> p;
+    explicit Scratch(hipStream_t s) : st(s) {}
     template <class T> bool get(T** out, size_t count) {
         *out = nullptr;
-        if (hipMalloc((void**)out, std::max<size_t>(1, count) * sizeof(T)) != hipSuccess) return false;
+        if (hipMallocAsync((void**)out, std::max<size_t>(1, count) * sizeof(T), st) != hipSuccess) return false;
         p.push_back((void*)*out);
         return true;
     }
-    ~Scratch() { for (void* q : p) hipFree(q); }
+    ~Scratch() { for (void* q : p) (void)hipFreeAsync(q, st); }
 };
 
 }  // namespace wb
@@ -847,7 +857,7 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
     *w = WideBvh{};
     if (n <= 0) { w->status = RS_WIDE_EMPTY; return 1; }
     if (n >= (1 << 24)) { w->status = RS_WIDE_TOO_MANY; return 1; }   // the node word's 24-bit child index
-    Scratch X;
+    Scratch X(st);
     const int total = 2 * n - 1, m = n - 1;          // binary nodes, internal nodes
     float4 *tlo, *thi, *tcen, *nlo, *nhi;
     int *idx, *tmp, *depth, *bad, *dmax;
@@ -975,8 +985,9 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
     WideQ* wq = nullptr;
     int *kidv = nullptr, *ni = nullptr, *nl = nullptr, *si = nullptr, *sl = nullptr, *prims = nullptr;
     const int maxw = std::max(1, m);                 // every wide node is an internal binary node (or the lone triangle)
+    int* tot5 = nullptr;
     WB_CHECK(X.get(&wq, maxw) && X.get(&kidv, (size_t)8 * maxw) && X.get(&ni, maxw) && X.get(&nl, maxw) &&
-             X.get(&si, maxw) && X.get(&sl, maxw) && X.get(&prims, n), "scratch allocation failed");
+             X.get(&si, maxw) && X.get(&sl, maxw) && X.get(&prims, n) && X.get(&tot5, 5), "scratch allocation failed");
     size_t scan_bytes = 0;
     WB_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, ni, si, maxw, st));
     void* scan_tmp = nullptr;
@@ -1002,11 +1013,8 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
                                                           prims, bad);
         WB_HIP(hipGetLastError());
         int h[5];
-        WB_HIP(hipMemcpyAsync(&h[0], si + cnt - 1, sizeof(int), hipMemcpyDeviceToHost, st));
-        WB_HIP(hipMemcpyAsync(&h[1], ni + cnt - 1, sizeof(int), hipMemcpyDeviceToHost, st));
-        WB_HIP(hipMemcpyAsync(&h[2], sl + cnt - 1, sizeof(int), hipMemcpyDeviceToHost, st));
-        WB_HIP(hipMemcpyAsync(&h[3], nl + cnt - 1, sizeof(int), hipMemcpyDeviceToHost, st));
-        WB_HIP(hipMemcpyAsync(&h[4], bad, sizeof(int), hipMemcpyDeviceToHost, st));
+        k_level_totals<<<1, 64, 0, st>>>(si, ni, sl, nl, cnt, bad, tot5);   // one read-back per level
+        WB_HIP(hipMemcpyAsync(h, tot5, sizeof h, hipMemcpyDeviceToHost, st));
         WB_HIP(hipStreamSynchronize(st));
         if (h[4]) { err = h[4] & 4 ? "wide BVH: no conservative quantisation" : "wide BVH: slot expansion failed"; return -1; }
         const int nq = h[0] + h[1];
