@@ -101,17 +101,20 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 }
 // constant-rate (100 MHz) clock at a wave's start, for the optional per-row cost record
 __device__ __forceinline__ uint64_t wave_clock() { return __builtin_amdgcn_s_memrealtime(); }
+// load-balancing record (rs_mgpu_rebalance, TiledRenderer.rebalance): the wave's lifetime spread evenly over the 8
+// rows of its 8x8 tile from its top row (lanes 0..7 one row each), so band boundaries balance to the row rather than
+// to the tile row.  Row-spread atomics, only while tracking is on (calibration frames).
+__device__ __forceinline__ void row_cost_add(CountSlot C, uint64_t t0, int y) {
+    if (!C.row_cost) return;
+    const int yt = __builtin_amdgcn_readfirstlane(y) + (int)(threadIdx.x & 63);
+    const float w = (float)(wave_clock() - t0) * 0.125f;
+    if ((threadIdx.x & 63) < 8 && yt >= C.y0 && yt < C.y1) atomicAdd(C.row_cost + yt, w);
+}
 __device__ __forceinline__ void count_rays(CountSlot C, uint32_t rays, uint32_t primary, uint64_t t0, int y) {
     uint32_t r = wave_sum(rays), p = wave_sum(primary);
     if ((threadIdx.x & 63) == 0)
         C.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)] = make_uint2(r, p);
-    // load-balancing record (TiledRenderer.rebalance): the wave's lifetime, charged to its top row.
-    // Row-spread same-address atomics, only while tracking is on (calibration frames).
-    if (C.row_cost) {
-        const int yt = __builtin_amdgcn_readfirstlane(y);
-        if ((threadIdx.x & 63) == 0 && yt >= C.y0 && yt < C.y1)
-            atomicAdd(C.row_cost + yt, (float)(wave_clock() - t0));
-    }
+    row_cost_add(C, t0, y);
 }
 
 // sum n slot pairs into the frame totals (and the context's running totals): kReduceBlocks
@@ -601,11 +604,7 @@ __device__ __forceinline__ void count_store(CountSlot C, uint32_t rays, uint32_t
     if ((threadIdx.x & 63) == 0)
         C.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)] = make_uint2(r, p);
 }
-__device__ __forceinline__ void row_cost_add(CountSlot C, uint64_t t0, int y) {
-    if (!C.row_cost) return;
-    const int yt = __builtin_amdgcn_readfirstlane(y);
-    if ((threadIdx.x & 63) == 0 && yt >= C.y0 && yt < C.y1) atomicAdd(C.row_cost + yt, (float)(wave_clock() - t0));
-}
+
 #ifndef RS_PERSIST
 #define RS_PERSIST 0           // 1: full-frame initial passes launch persistent waves (restir_capi.hip want_persist)
 #endif
