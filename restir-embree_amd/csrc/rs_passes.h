@@ -104,11 +104,15 @@ __device__ __forceinline__ uint64_t wave_clock() { return __builtin_amdgcn_s_mem
 // load-balancing record (rs_mgpu_rebalance, TiledRenderer.rebalance): the wave's lifetime spread evenly over the 8
 // rows of its 8x8 tile from its top row (lanes 0..7 one row each), so band boundaries balance to the row rather than
 // to the tile row.  Row-spread atomics, only while tracking is on (calibration frames).
+#ifndef RS_ROWCOST_SPREAD
+#define RS_ROWCOST_SPREAD 1    // 0: the whole wave's time on its top row (round 4)
+#endif
 __device__ __forceinline__ void row_cost_add(CountSlot C, uint64_t t0, int y) {
     if (!C.row_cost) return;
+    constexpr int kRows = RS_ROWCOST_SPREAD ? 8 : 1;
     const int yt = __builtin_amdgcn_readfirstlane(y) + (int)(threadIdx.x & 63);
-    const float w = (float)(wave_clock() - t0) * 0.125f;
-    if ((threadIdx.x & 63) < 8 && yt >= C.y0 && yt < C.y1) atomicAdd(C.row_cost + yt, w);
+    const float w = (float)(wave_clock() - t0) * (1.0f / kRows);
+    if ((threadIdx.x & 63) < kRows && yt >= C.y0 && yt < C.y1) atomicAdd(C.row_cost + yt, w);
 }
 __device__ __forceinline__ void count_rays(CountSlot C, uint32_t rays, uint32_t primary, uint64_t t0, int y) {
     uint32_t r = wave_sum(rays), p = wave_sum(primary);
