@@ -441,6 +441,8 @@ static int measure_bands(rs_mgpu* m, const rs_scene* const* scenes, const rs_cam
     return m->allreduce(t.data(), m->world, 0);
 }
 
+constexpr int kBandGrain = 8;                // band boundaries on whole 8-row wave tiles (balanced_bounds_grain)
+
 extern "C" int rs_mgpu_rebalance(rs_mgpu* m, const rs_scene* const* scenes, const rs_camera* cam,
                                  const rs_frame_params* P, uint32_t first_frame, int n_frames, int min_rows) {
     if (!m || !cam || !P || n_frames < 1) return RS_E_INVALID;
@@ -465,7 +467,7 @@ extern "C" int rs_mgpu_rebalance(rs_mgpu* m, const rs_scene* const* scenes, cons
     const int halo = mgpu::halo_rows(P->spatial_radius, P->do_spatial && P->spatial_passes > 0);
     std::vector<int> b;
     const int rows = std::max(std::max(1, min_rows), halo);
-    if (!mgpu::balanced_bounds(cost, m->world, rows, b))
+    if (!mgpu::balanced_bounds_grain(cost, m->world, rows, kBandGrain, b))
         return m->error(RS_E_INVALID, "rs_mgpu_rebalance: bands of min_rows do not fit");
     m->bounds = b;
     // Time-based refinement: row costs predict a band's time only to about +-7 % (the per-row
@@ -492,7 +494,7 @@ extern "C" int rs_mgpu_rebalance(rs_mgpu* m, const rs_scene* const* scenes, cons
                 for (int y = m->bounds[r]; y < m->bounds[r + 1]; ++y) cost[y] *= t[r] / c;
         }
         std::vector<int> nb;
-        if (!mgpu::balanced_bounds(cost, m->world, rows, nb)) break;
+        if (!mgpu::balanced_bounds_grain(cost, m->world, rows, kBandGrain, nb)) break;
         if (nb == m->bounds) break;              // converged: nothing left to measure
         m->bounds = nb;
     }

@@ -154,12 +154,23 @@ def _torch_stream(st):
     return torch.cuda.stream(st)
 
 
-def balanced_bands(costs, world: int, min_rows: int = 1):
+def balanced_bands(costs, world: int, min_rows: int = 1, grain: int = 1):
     """Contiguous row bands [(y0, y1)] * world with (as nearly as rows allow) equal summed cost.
     Deterministic (every rank computes the same split from the same all-reduced costs); every band
-    keeps >= min_rows rows (the spatial halo must fit inside a neighbour's band)."""
+    keeps >= min_rows rows (the spatial halo must fit inside a neighbour's band).  grain > 1: boundaries on
+    multiples of grain rows (csrc/rs_mgpu_core.h balanced_bounds_grain: whole 8-row wave tiles), falling back
+    to single rows when H is not a multiple of grain or the bands of min_rows do not fit in whole units."""
     c = np.asarray(costs, np.float64)
     H = c.shape[0]
+    if grain > 1:
+        G, mg = -(-H // grain), -(-min_rows // grain)
+        if H % grain == 0 and world * mg <= G:
+            cc = np.where(np.isfinite(c) & (c > 0), c, 0.0)
+            cg = np.zeros(G)
+            np.add.at(cg, np.arange(H) // grain, cc)
+            b = balanced_bands(cg, world, mg)
+            ys = [0] + [min(e * grain, H) for _, e in b[:-1]] + [H]
+            return [(ys[r], ys[r + 1]) for r in range(world)]
     if world * min_rows > H:
         raise ValueError(f"{world} bands of >= {min_rows} rows do not fit in {H} rows")
     c = np.where(np.isfinite(c) & (c > 0), c, 0.0)
@@ -176,6 +187,7 @@ def balanced_bands(costs, world: int, min_rows: int = 1):
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
 
+BAND_GRAIN = 8      # band boundaries on whole 8-row wave tiles (rs_mgpu.hip kBandGrain)
 DEFAULT_LANES = 3   # lanes of a backend that does not say (the library's default run-ahead depth 2, + 1)
 
 
@@ -271,7 +283,7 @@ class TiledRenderer:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         total = t.cpu().numpy()
         h = max(1, min_rows if min_rows is not None else 8)
-        self.set_bands(balanced_bands(total, self.world, h))
+        self.set_bands(balanced_bands(total, self.world, h, grain=BAND_GRAIN))
         self.reset_history()
         return self.bands
 

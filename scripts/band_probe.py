@@ -33,7 +33,7 @@ def main():
     import torch
     from restir_amd import Renderer, scenes
     from restir_amd.params import metric_params, c3_params
-    from restir_amd.distributed import band_rows, halo_rows, balanced_bands
+    from restir_amd.distributed import band_rows, halo_rows, balanced_bands, BAND_GRAIN
 
     sc = scenes.sponza_like() if a.scene == "C3" else scenes.cornell_many_lights(1024)
     prm = metric_params() if a.scene == "C2" else c3_params()
@@ -64,7 +64,7 @@ def main():
         cases = [(a.all_ranks, k) for k in range(a.all_ranks)]
     bands_of = {}
     for N in {n for n, _ in cases}:
-        bands_of[N] = balanced_bands(costs, N, 8) if costs is not None else [band_rows(H, k, N) for k in range(N)]
+        bands_of[N] = balanced_bands(costs, N, 8, grain=BAND_GRAIN) if costs is not None else [band_rows(H, k, N) for k in range(N)]
 
     def probe(N, rank, y0, y1, tag=""):
         halo = halo_rows(prm) if N > 1 else 0
@@ -115,7 +115,7 @@ def main():
                 ck = c[y0:y1].sum()
                 if ck > 0:
                     c[y0:y1] *= tk / ck
-            bands = balanced_bands(c, N, 8)
+            bands = balanced_bands(c, N, 8, grain=BAND_GRAIN)
         return
     for N, rank in cases:
         y0, y1 = bands_of[N][rank]

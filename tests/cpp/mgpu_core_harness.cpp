@@ -137,6 +137,14 @@ int harness_balanced(const double* costs, int H, int world, int min_rows, int32_
     for (int i = 0; i <= world; ++i) out[i] = b[i];
     return 0;
 }
+// rs::mgpu::balanced_bounds_grain (rs_mgpu_rebalance's split: boundaries on whole `grain`-row wave tiles)
+int harness_balanced_grain(const double* costs, int H, int world, int min_rows, int grain, int32_t* out) {
+    std::vector<double> c(costs, costs + H);
+    std::vector<int> b;
+    if (!rs::mgpu::balanced_bounds_grain(c, world, min_rows, grain, b)) return -1;
+    for (int i = 0; i <= world; ++i) out[i] = b[i];
+    return 0;
+}
 int harness_halo(float radius) { return rs::mgpu::halo_rows(radius, true); }
 
 // Every rank of a `world`-rank frame issues its halo and gather plans through issue_plan (the code the

@@ -34,6 +34,8 @@ def _harness():
                                 ctypes.POINTER(ctypes.c_int)]
     L.harness_balanced.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_int32)]
+    L.harness_balanced_grain.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]
     L.harness_halo.argtypes = [ctypes.c_float]
     L.harness_plan_check.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
@@ -109,6 +111,27 @@ def test_native_band_balancing_matches_python():
             assert [(int(out[i]), int(out[i + 1])) for i in range(world)] == py, (H, world, mr)
     for r in (30.0, 24.999998, 24.9, 25.0, 0.5, 0.0):
         assert L.harness_halo(r) == halo_rows(P.metric_params(spatial_radius=r))
+
+
+def test_band_balancing_on_wave_tiles():
+    """rs_mgpu_rebalance's split on whole 8-row wave tiles (rs_mgpu_core.h balanced_bounds_grain) equals the
+    Python restatement (distributed.balanced_bands(grain=8)); boundaries are multiples of 8 with >= min_rows rows,
+    and heights that are not a multiple of 8 (or too few units) fall back to the row-exact split."""
+    from restir_amd.distributed import balanced_bands
+    L = _harness()
+    rng = np.random.default_rng(5)
+    for H, world, mr in [(1080, 8, 5), (2160, 8, 5), (1080, 2, 8), (48, 4, 5), (100, 4, 1), (37, 2, 5), (64, 8, 5)]:
+        for costs in (rng.uniform(0, 1, H), np.r_[np.zeros(H // 2), np.ones(H - H // 2)], np.zeros(H),
+                      np.linspace(1, 9, H) ** 2):
+            out = np.zeros(world + 1, np.int32)
+            c = np.ascontiguousarray(costs, np.float64)
+            assert L.harness_balanced_grain(c.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), H, world, mr, 8,
+                                            out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))) == 0
+            py = balanced_bands(costs, world, mr, grain=8)
+            assert [(int(out[i]), int(out[i + 1])) for i in range(world)] == py, (H, world, mr)
+            assert all(y1 - y0 >= mr for y0, y1 in py)
+            if H % 8 == 0 and world * -(-mr // 8) <= H // 8:
+                assert all(y0 % 8 == 0 for y0, _ in py), py
 
 
 @pytest.mark.parametrize("world", [2, 3, 4, 5, 6, 7, 8])
