@@ -269,11 +269,7 @@ struct ConvLds {
     static constexpr int kBytes = kIn > kOut ? kIn : kOut;
 };
 
-// ALLC > 0 (coarse levels, NT = 1): every channel chunk's halo and B fragments are loaded into registers at once
-// (up to ALLC chunks), then staged through LDS one chunk at a time -- one global round trip per workgroup
-// instead of one per chunk.  A 1/8- or 1/16-resolution layer has one round of workgroups or less, so a
-// workgroup's chain of dependent chunk loads (~3.5 us each) was the layer's time.
-template <int NT, int POST, bool RELU, int ALLC = 0>
+template <int NT, int POST, bool RELU>
 __global__ void __launch_bounds__(256, BHalf<NT>::on ? BHalf<NT>::waves : 1) k_conv3(ConvArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[ConvLds<NT, POST>::kBytes];
     uint8_t* const bbuf = lds + kChunkBytes;
@@ -293,27 +289,7 @@ __global__ void __launch_bounds__(256, BHalf<NT>::on ? BHalf<NT>::waves : 1) k_c
         for (int n = 0; n < NT; ++n) acc[g][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
     uint4 st[kStageRegs];
-    if constexpr (ALLC > 0) {
-        static_assert(BStage<NT>::lds, "ALLC: B staged whole-chunk");
-        uint4 sa[ALLC][kStageRegs], ba[ALLC][BStage<NT>::kRegs];
-#pragma unroll
-        for (int c = 0; c < ALLC; ++c) {       // unconditional loads (chunk 0 again past the last one): no
-            const int cc = c < a.nchunk ? c : 0;   // branch and no wait between them
-            stage_load(a, cc, tx0, ty0, sa[c]);
-            bstage_load<NT>(a, cc, n0, ba[c]);
-        }
-#pragma unroll
-        for (int c = 0; c < ALLC; ++c) {
-            if (c < a.nchunk) {                // wave-uniform
-                if (c > 0) __syncthreads();    // the previous chunk's MFMAs have read the buffers
-                stage_store(lds, a.ch_w[c] >> 3, sa[c]);
-                bstage_store<NT>(bbuf, a.ch_w[c] == 32 ? 9 : 5, ba[c]);
-                __syncthreads();
-                compute_chunk<NT>(a, c, lds, bbuf, acc, lane, X, Yb, n0);
-            }
-        }
-        __syncthreads();
-    } else if constexpr (BStage<NT>::lds) {    // single halo + B buffers, two barriers per chunk
+    if constexpr (BStage<NT>::lds) {           // single halo + B buffers, two barriers per chunk
         uint4 bs[BStage<NT>::kRegs];
         stage_load(a, 0, tx0, ty0, st);
         bstage_load<NT>(a, 0, n0, bs);
@@ -1006,8 +982,6 @@ struct rs_denoiser {
     uint32_t pipe = 0u;                         // layers (bit l) on k_conv3p where it applies (2..4 n-tiles):
                                                 // RESTIR_DN_PIPE=<mask> or 1 (all); measured slower, off
     int cus = 256;                              // its workgroups (RESTIR_DN_PIPE_GRID caps them: tests)
-    uint32_t allc = 0u;                         // layers (bit l) on k_conv3's all-chunks-loaded form where it
-                                                // applies (NT = 1, <= 5 chunks): RESTIR_DN_ALLC=<mask> | 1
 };
 
 namespace {
@@ -1045,15 +1019,6 @@ int ensure_bufs(rs_denoiser* d, int H, int W, hipStream_t st) {
 
 template <int NT, int POST, bool RELU>
 void launch(const ConvArgs& a, dim3 g, hipStream_t st) { k_conv3<NT, POST, RELU><<<g, 256, 0, st>>>(a); }
-
-constexpr int kAllc = 5;                      // k_conv3's ALLC form: layers of <= 5 chunks at NT = 1
-bool dispatch_allc(int post, bool relu, const ConvArgs& a, dim3 g, hipStream_t st) {
-    if (a.nchunk > kAllc || !relu) return false;
-    if (post == POST_POOL) k_conv3<1, POST_POOL, true, kAllc><<<g, 256, 0, st>>>(a);
-    else if (post == POST_STORE) k_conv3<1, POST_STORE, true, kAllc><<<g, 256, 0, st>>>(a);
-    else return false;
-    return true;
-}
 
 bool dispatch(int nt, int post, bool relu, const ConvArgs& a, dim3 g, hipStream_t st) {
 #define RS_DN_CASE(N)                                                       \
@@ -1101,7 +1066,6 @@ int create_impl(rs_context* ctx, const void* tza, size_t bytes, rs_denoiser** ou
     if (const char* e = std::getenv("RESTIR_DN_PIPE")) d->pipe = std::strcmp(e, "1") == 0 ? 0xffffu : (uint32_t)std::strtoul(e, nullptr, 0);
     if (hipDeviceGetAttribute(&d->cus, hipDeviceAttributeMultiprocessorCount, d->device) != hipSuccess || d->cus < 1) d->cus = 256;
     if (const char* e = std::getenv("RESTIR_DN_PIPE_GRID")) d->cus = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("RESTIR_DN_ALLC")) d->allc = std::strcmp(e, "1") == 0 ? 0xffffu : (uint32_t)std::strtoul(e, nullptr, 0);
     if (!check_net(T, d->net, err)) { delete d; return rs::ctx_fail(ctx, RS_E_INVALID, "rs_denoiser_create: " + err); }
     (void)hipGetLastError();
     if (hipSetDevice(rs::ctx_device(ctx)) != hipSuccess) { delete d; return rs::ctx_fail(ctx, RS_E_HIP, "rs_denoiser_create: hipSetDevice"); }
@@ -1203,9 +1167,7 @@ int denoise_run(rs_denoiser* d, hipStream_t st, const float* color, int cst, con
             for (int k = L.nt < kMaxNtw ? L.nt : kMaxNtw; k >= 1; --k)
                 if (L.nt % k == 0) { ntw = k; if ((size_t)gx * gy * (L.nt / k) >= kFillWorkgroups) break; }
         const dim3 g(gx, gy, (unsigned)(L.nt / ntw));
-        const bool allc = ((d->allc >> l) & 1u) && ntw == 1 && dispatch_allc(ld.post, ld.relu != 0, a, g, st);
-        if (!allc && !dispatch(ntw, ld.post, ld.relu != 0, a, g, st))
-            return dfail(d, RS_E_UNSUPPORTED, "rs_denoise: unsupported layer width");
+        if (!dispatch(ntw, ld.post, ld.relu != 0, a, g, st)) return dfail(d, RS_E_UNSUPPORTED, "rs_denoise: unsupported layer width");
         DCHK(d, hipGetLastError());
         if (d->timed) DCHK(d, hipEventRecord(d->evl[l + 1], st));
     }

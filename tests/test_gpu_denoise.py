@@ -112,29 +112,6 @@ def test_every_layer_matches_float64(ctx, H, W):
         assert off.mean() <= 0.02, (name, float(off.mean()))
 
 
-@pytest.mark.parametrize("H,W", [(48, 64), (37, 83), (1080, 1920)])
-def test_all_chunks_conv_bit_identical(monkeypatch, H, W):
-    """k_conv3's all-chunks-loaded form (RESTIR_DN_ALLC: the coarse layers at NT = 1 load every chunk's halo and
-    B fragments at once) against the chunk-by-chunk form: same k-steps, same order, same MFMA -- bit-identical."""
-    r = Renderer(64, 48)
-    w = tza.random_unet_weights(seed=13)
-    color, albedo, normal = _images(H, W, seed=9 + H)
-    outs = {}
-    try:
-        for allc in ("0", "1"):
-            monkeypatch.setenv("RESTIR_DN_ALLC", allc)
-            d = Denoiser(r, w)
-            out = _run(d, color, albedo, normal, scale=0.8)
-            outs[allc] = (out, [d.dump(i)[0] for i in range(16)])
-            d.close()
-    finally:
-        r.close()
-    (o0, t0), (o1, t1) = outs["0"], outs["1"]
-    for i in range(16):
-        assert np.array_equal(t0[i].view(np.uint16), t1[i].view(np.uint16)), f"tensor {i}"
-    assert np.array_equal(o0, o1)
-
-
 @pytest.mark.parametrize("H,W,grid", [(48, 64, "2"), (37, 83, "3"), (540, 960, None), (1080, 1920, None)])
 def test_pipelined_conv_bit_identical(monkeypatch, H, W, grid):
     """k_conv3p (the persistent LDS-DMA pipeline, csrc/rs_denoise.hip) against k_conv3 on the layers it runs
