@@ -161,6 +161,8 @@ struct rs_context {
     uint32_t* qctr[kLanes] = {};           // persistent-wave tile queues (rs_passes.h TileQ): 4 words per lane
     int persist_mode = RS_PERSIST ? RS_SPLIT_AUTO : RS_SPLIT_OFF;
     int persist_wgs[4] = {};               // resident workgroups per CU of the persistent initial kernel, per kind
+    int persist_sorted = RS_SPLIT_OFF;     // RESTIR_PERSIST_SORTED: the sorted pass by persistent waves
+    int persist_sorted_wgs[4] = {};
     // pass timing without a per-frame host sync: every frame records into its own slot of an event
     // ring; slots are folded into the running totals lazily (when reused, or on rs_get_timing_totals)
     static constexpr int kEvRing = 64;
@@ -416,6 +418,11 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->queue_mode = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->queue_mode = RS_SPLIT_OFF;
         else if (!std::strcmp(t, "auto")) c->queue_mode = RS_SPLIT_AUTO;
+    }
+    if (const char* t = std::getenv("RESTIR_PERSIST_SORTED")) {   // persistent-wave sorted pass: auto | on | off
+        if (!std::strcmp(t, "on")) c->persist_sorted = RS_SPLIT_ON;
+        else if (!std::strcmp(t, "off")) c->persist_sorted = RS_SPLIT_OFF;
+        else if (!std::strcmp(t, "auto")) c->persist_sorted = RS_SPLIT_AUTO;
     }
     if (const char* t = std::getenv("RESTIR_PERSIST")) {       // persistent-wave initial pass: auto | on | off
         if (!std::strcmp(t, "on")) c->persist_mode = RS_SPLIT_ON;
@@ -1562,6 +1569,27 @@ static bool want_persist(rs_context* c, dim3 grid) {
     if (c->persist_mode == RS_SPLIT_ON) return true;
     return grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_wgs(c);
 }
+// the sorted initial pass by persistent waves (RESTIR_PERSIST_SORTED): AUTO = launches of more than one round
+static int persist_sorted_wgs(rs_context* c) {
+    const int kind = c->trav | (c->twide ? TRAV_WIDE : 0);
+    int& n = c->persist_sorted_wgs[kind];
+    if (!n) {
+        hipError_t e = hipSuccess;
+        switch (kind) {
+            case TRAV_LANE | TRAV_WIDE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_sorted_pq<TRAV_LANE | TRAV_WIDE>, 256, 0); break;
+            case TRAV_LANE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_sorted_pq<TRAV_LANE>, 256, 0); break;
+            case TRAV_WIDE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_sorted_pq<TRAV_WIDE>, 256, 0); break;
+            default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_sorted_pq<TRAV_LOCKSTEP>, 256, 0); break;
+        }
+        if (e != hipSuccess || n <= 0) n = RS_INITIAL_WAVES_SORT;
+    }
+    return n;
+}
+static bool want_persist_sorted(rs_context* c, dim3 grid) {
+    if (c->persist_sorted == RS_SPLIT_OFF) return false;
+    if (c->persist_sorted == RS_SPLIT_ON) return true;
+    return grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_sorted_wgs(c);
+}
 // the candidate-split spatial pass (rs_passes.h k_spatial_split): CONSTANT MIS, k <= 8, and (AUTO) a lockstep launch
 // of less than one round of the device's resident waves -- a rank's band (per-lane walks keep the sorted pass)
 static bool want_spatial_split(const rs_context* c, const rs_frame_params* P, int y0, int y1) {
@@ -1732,8 +1760,16 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
         k_q_resolve<<<gb, 256, 0, c->fs>>>(S, F, c->G[gnew], Q, ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                                            count_slot(c, gb));
     } else if (want_sorted(c, P, s)) {
-        LAUNCH_TRAV(c, k_gbuffer_initial_sorted, gg, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
-                    count_slot(c, gg));
+        if (want_persist_sorted(c, gg)) {
+            // persistent waves, each pulling 8x8 tiles (rs_passes.h k_gbuffer_initial_sorted_pq)
+            const uint32_t nt = gg.x * gg.y * 4u;
+            const dim3 gp((unsigned)std::min<size_t>((nt + 3) / 4, (size_t)c->cus * (size_t)persist_sorted_wgs(c)));
+            LAUNCH_TRAV(c, k_gbuffer_initial_sorted_pq, gp, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
+                        c->shade_fused ? 1 : 0, count_slot(c, gp), TileQ{c->qctr[c->li], nt});
+        } else {
+            LAUNCH_TRAV(c, k_gbuffer_initial_sorted, gg, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
+                        count_slot(c, gg));
+        }
     } else if (want_persist(c, gg)) {
         // persistent waves pulling 8x8 tiles (rs_passes.h k_gbuffer_initial_pq): about one device's worth of
         // resident workgroups, never more than the tiles need

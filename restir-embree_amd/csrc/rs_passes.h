@@ -602,6 +602,16 @@ __device__ __forceinline__ bool pixel_of_q(const FrameConst& F, int ya, int yb, 
     y = y < yb ? y : yb - 1;
     return in;
 }
+// the unclamped origin of 8x8 tile t (pixel_of_q's layout)
+__device__ __forceinline__ void tile_origin_q(const FrameConst& F, int ya, int yb, uint32_t t, int& tx0, int& ty0) {
+    const int gx = (F.W + 15) / 16, gy = (yb - ya + 15) / 16;
+    const int q = (int)(t >> 2), w = (int)(t & 3u);
+    const int bx = q % gx;
+    int by = q / gx;
+    if (F.row_order && ya == 0 && yb == F.H && F.n_order == gy) by = order_row(F.row_order, (uint32_t)by);
+    tx0 = bx * 16 + (w & 1) * 8;
+    ty0 = ya + by * 16 + (w >> 1) * 8;
+}
 // count_rays for a persistent wave: the slot of this wave once at the end; the per-row cost per tile
 __device__ __forceinline__ void count_store(CountSlot C, uint32_t rays, uint32_t primary) {
     const uint32_t r = wave_sum(rays), p = wave_sum(primary);
@@ -783,17 +793,12 @@ __device__ __forceinline__ void brdf_unpark(const uint32_t* sl, int lane, Res& r
     r.p = mk(v[0], v[1], v[2]); r.n = mk(v[3], v[4], v[5]); r.li = mk(v[6], v[7], v[8]); r.wsum = v[9];
     bp = v[10]; fs = mk(v[11], v[12], v[13]);
 }
+// one wave's 8x8 tile of the sorted pass: lane = pixel (x, y) (clamped; `in` whether it exists), the tile's
+// unclamped origin (tx0, ty0) for the pixel index of a ray's source lane, the wave's LDS region L
 template <int T>
-__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES_SORT_LOCKSTEP, RS_INITIAL_WAVES_SORT))
-k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int fuse_shade, CountSlot C) {
-    const uint64_t t0 = wave_clock();
-    if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
-    __shared__ SortLds lds[4];
-    SortLds& L = lds[threadIdx.x >> 6];
-    const int lane = threadIdx.x & 63;
-    int x, y;
-    uint32_t rays = 0;
-    const bool in = pixel_of(F, F.gy0, F.gy1, x, y);
+__device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst& F, const GBuf& G, const ResBuf& Rw,
+                                            float* fb, int fuse_shade, SortLds& L, int lane, int x, int y, bool in,
+                                            int tx0, int ty0, uint32_t& rays) {
     const size_t p = (size_t)y * F.W + x;
     {
         const GElem g = gbuffer_fill<T>(S, F, x, y, in);
@@ -860,7 +865,8 @@ k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb,
                     const uint32_t pick = L.slot[sl] & 0x1fffffu, k = sl >> 6, src = sl & 63u;
                     const vec3 o = mk(L.px[src], L.py[src], L.pz[src]);
                     Rng q;
-                    q.init(F.seed, F.frame, PASS_INITIAL, tile_pixel(F, F.gy0, F.gy1, (int)src));
+                    q.init(F.seed, F.frame, PASS_INITIAL,
+                           (uint32_t)(ty0 + (int)(src >> 3)) * (uint32_t)F.W + (uint32_t)(tx0 + (int)(src & 7u)));
                     q.n = cand_slot(c0 + (int)k) + 1u;
                     const float r1 = q.range(0, 1), r2 = q.range(0, 1);    // area_sample_at's draws
                     const float4* E = S.emis + 8 * (size_t)pick;
@@ -939,7 +945,50 @@ k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb,
         Rw.store(p, r);
         if (fuse_shade) store_rgb(fb, p, shade_px(r, f_sel, G.load(p).le));
     }
+}
+template <int T>
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES_SORT_LOCKSTEP, RS_INITIAL_WAVES_SORT))
+k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int fuse_shade, CountSlot C) {
+    const uint64_t t0 = wave_clock();
+    if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;   // this frame's counter (rs_tile_begin)
+    __shared__ SortLds lds[4];
+    int x, y, bx, by;
+    uint32_t rays = 0;
+    const bool in = pixel_of(F, F.gy0, F.gy1, x, y);
+    tile_of(F, F.gy0, F.gy1, bx, by);
+    const int wave = threadIdx.x >> 6;
+    sorted_tile<T>(S, F, G, Rw, fb, fuse_shade, lds[wave], threadIdx.x & 63, x, y, in, bx * 16 + (wave & 1) * 8,
+                   F.gy0 + by * 16 + (wave >> 1) * 8, rays);
     count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u, t0, y);
+}
+// the same pass by persistent waves (RESTIR_PERSIST_SORTED): about one device's worth of resident workgroups,
+// every WAVE pulling 8x8 tiles from a per-launch counter in the grid's dispatch order (costliest tile rows first
+// on full frames).  The waves of the sorted pass are independent (each its own LDS region), so a wave that
+// finishes its tile takes the next at once instead of holding its workgroup's slot until the slowest of the
+// four finishes -- per-lane walks vary from tile to tile.
+template <int T>
+__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES_SORT_LOCKSTEP, RS_INITIAL_WAVES_SORT))
+k_gbuffer_initial_sorted_pq(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int fuse_shade, CountSlot C,
+                            TileQ Q) {
+    if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;
+    __shared__ SortLds lds[4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t rays = 0, prim = 0;
+    for (;;) {
+        const uint32_t t = q_pull(Q);
+        if (t >= Q.n) break;
+        const uint64_t t0 = wave_clock();
+        int x, y;
+        const bool in = pixel_of_q(F, F.gy0, F.gy1, t, x, y);
+        int tx0, ty0;
+        tile_origin_q(F, F.gy0, F.gy1, t, tx0, ty0);
+        sorted_tile<T>(S, F, G, Rw, fb, fuse_shade, lds[wave], lane, x, y, in, tx0, ty0, rays);
+        rays += in ? 1u : 0u;
+        prim += in ? 1u : 0u;
+        row_cost_add(C, t0, y);
+    }
+    count_store(C, rays, prim);
+    q_exit(Q);
 }
 
 // ---------------------------------------------------------------- candidate-split initial pass

@@ -712,6 +712,30 @@ def test_wide_tree_live_on_c3():
         assert fetches.mean() < 100.0       # a broken tree (e.g. boxes opened for every ray) walks far more
 
 
+@pytest.mark.parametrize("W,H", [(64, 40), (1920, 1080)])
+def test_persistent_sorted_pass_bit_identical(W, H, monkeypatch):
+    """The sorted initial pass by persistent waves (rs_passes.h k_gbuffer_initial_sorted_pq, RESTIR_PERSIST_SORTED:
+    every wave pulls 8x8 tiles from a per-launch counter) renders the one-launch kernel's frames bit for bit --
+    at 1080p each resident wave walks several tiles; the ray totals agree too (per-wave counts stored once)."""
+    sc = scenes.sponza_like(target_tris=30_000, n_lamps=128)
+    prm = P.c3_params(m_area=32)
+    cam = lambda f: scenes.orbit_camera(sc.camera, f, 240, 0.3)   # noqa: E731
+    out = {}
+    for mode in ("on", "off"):
+        monkeypatch.setenv("RESTIR_PERSIST_SORTED", mode)
+        g = Renderer(W, H)
+        g.set_traversal("lane")
+        gs = g.load_scene(sc)
+        fr = [g.produce_restir(gs, cam(f), prm, f, timed=True).copy() for f in range(3)]
+        out[mode] = (fr, int(g.last_times.rays), g.reservoirs().copy())
+        gs.close()
+        g.close()
+    for f, (a, b) in enumerate(zip(out["on"][0], out["off"][0])):
+        assert np.array_equal(a, b), f"frame {f}: persistent sorted pass != one-launch"
+    assert out["on"][1] == out["off"][1]
+    assert np.array_equal(out["on"][2], out["off"][2])
+
+
 @pytest.mark.parametrize("which", ["c3", "c3_a37", "c2_lane", "c2_lockstep"])
 def test_sorted_initial_pass_bit_identical(which, monkeypatch):
     """The wave-sorted initial, temporal and spatial passes (rs_passes.h k_gbuffer_initial_sorted, k_temporal<T |
