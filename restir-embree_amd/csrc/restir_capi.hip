@@ -1582,6 +1582,7 @@ static int persist_sorted_wgs(rs_context* c) {
             default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_sorted_pq<TRAV_LOCKSTEP>, 256, 0); break;
         }
         if (e != hipSuccess || n <= 0) n = RS_INITIAL_WAVES_SORT;
+        if (const char* t = std::getenv("RESTIR_PERSIST_SORTED_WGS")) n = std::max(1, std::min(n, std::atoi(t)));
     }
     return n;
 }
