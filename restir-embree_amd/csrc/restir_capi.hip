@@ -161,7 +161,7 @@ struct rs_context {
     uint32_t* qctr[kLanes] = {};           // persistent-wave tile queues (rs_passes.h TileQ): 4 words per lane
     int persist_mode = RS_PERSIST ? RS_SPLIT_AUTO : RS_SPLIT_OFF;
     int persist_wgs[4] = {};               // resident workgroups per CU of the persistent initial kernel, per kind
-    int persist_sorted = RS_SPLIT_OFF;     // RESTIR_PERSIST_SORTED: the sorted pass by persistent waves
+    int persist_sorted = RS_SPLIT_AUTO;    // RESTIR_PERSIST_SORTED: the sorted pass by persistent waves
     int persist_sorted_wgs[4] = {};
     // pass timing without a per-frame host sync: every frame records into its own slot of an event
     // ring; slots are folded into the running totals lazily (when reused, or on rs_get_timing_totals)
@@ -1569,7 +1569,13 @@ static bool want_persist(rs_context* c, dim3 grid) {
     if (c->persist_mode == RS_SPLIT_ON) return true;
     return grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_wgs(c);
 }
-// the sorted initial pass by persistent waves (RESTIR_PERSIST_SORTED): AUTO = launches of more than one round
+// the sorted initial pass by persistent waves (RESTIR_PERSIST_SORTED).  AUTO (default): with frames in flight
+// (run-ahead > 0) and more than one round of the one-launch kernel's waves, kPersistSortedWgs resident workgroups
+// per CU -- fewer than the kernel's occupancy, so the other frames' temporal and spatial passes run beside it.
+// The pass alone is slower that way (C3 16.7-16.9 vs 14.9-15.0 ms), the frame throughput higher (C3 60.8-61.6 vs
+// 60.0-60.1 frames/s over three sessions; 2 workgroups per CU: 58.3-58.5); one frame in flight keeps
+// the one-launch kernel.
+constexpr int kPersistSortedWgs = 3;
 static int persist_sorted_wgs(rs_context* c) {
     const int kind = c->trav | (c->twide ? TRAV_WIDE : 0);
     int& n = c->persist_sorted_wgs[kind];
@@ -1582,14 +1588,18 @@ static int persist_sorted_wgs(rs_context* c) {
             default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_sorted_pq<TRAV_LOCKSTEP>, 256, 0); break;
         }
         if (e != hipSuccess || n <= 0) n = RS_INITIAL_WAVES_SORT;
-        if (const char* t = std::getenv("RESTIR_PERSIST_SORTED_WGS")) n = std::max(1, std::min(n, std::atoi(t)));
     }
+    return n;
+}
+static int persist_sorted_grid_wgs(rs_context* c) {     // resident workgroups per CU of the persistent launch
+    int n = std::min(persist_sorted_wgs(c), kPersistSortedWgs);
+    if (const char* t = std::getenv("RESTIR_PERSIST_SORTED_WGS")) n = std::max(1, std::min(persist_sorted_wgs(c), std::atoi(t)));
     return n;
 }
 static bool want_persist_sorted(rs_context* c, dim3 grid) {
     if (c->persist_sorted == RS_SPLIT_OFF) return false;
     if (c->persist_sorted == RS_SPLIT_ON) return true;
-    return grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_sorted_wgs(c);
+    return c->ahead > 0 && grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_sorted_wgs(c);
 }
 // the candidate-split spatial pass (rs_passes.h k_spatial_split): CONSTANT MIS, k <= 8, and (AUTO) a lockstep launch
 // of less than one round of the device's resident waves -- a rank's band (per-lane walks keep the sorted pass)
@@ -1764,7 +1774,7 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
         if (want_persist_sorted(c, gg)) {
             // persistent waves, each pulling 8x8 tiles (rs_passes.h k_gbuffer_initial_sorted_pq)
             const uint32_t nt = gg.x * gg.y * 4u;
-            const dim3 gp((unsigned)std::min<size_t>((nt + 3) / 4, (size_t)c->cus * (size_t)persist_sorted_wgs(c)));
+            const dim3 gp((unsigned)std::min<size_t>((nt + 3) / 4, (size_t)c->cus * (size_t)persist_sorted_grid_wgs(c)));
             LAUNCH_TRAV(c, k_gbuffer_initial_sorted_pq, gp, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
                         c->shade_fused ? 1 : 0, count_slot(c, gp), TileQ{c->qctr[c->li], nt});
         } else {
