@@ -1599,7 +1599,12 @@ static int persist_sorted_grid_wgs(rs_context* c) {     // resident workgroups p
 static bool want_persist_sorted(rs_context* c, dim3 grid) {
     if (c->persist_sorted == RS_SPLIT_OFF) return false;
     if (c->persist_sorted == RS_SPLIT_ON) return true;
-    return c->ahead > 0 && grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_sorted_wgs(c);
+    // full frames only, and not while row costs are being recorded: a throttled persistent launch charges its
+    // early (costly, contended) tiles more and its late ones less than the one-launch kernel a band runs, so
+    // bounds balanced on its row costs come out uneven (C4's eight 4K bands: max 9.59 vs 8.96 ms)
+    const bool full = c->tile.y0 == 0 && c->tile.y1 == c->H;
+    return c->ahead > 0 && full && !c->track_rows && !c->tune_rows &&
+           grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_sorted_wgs(c);
 }
 // the candidate-split spatial pass (rs_passes.h k_spatial_split): CONSTANT MIS, k <= 8, and (AUTO) a lockstep launch
 // of less than one round of the device's resident waves -- a rank's band (per-lane walks keep the sorted pass)
