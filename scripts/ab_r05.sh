@@ -18,6 +18,8 @@ for so in restir-embree_amd/_ab/*.so; do
   python - "$n" gpurun_out/ab_$n.log <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-print(f"{sys.argv[1]:>14s} fps={d['value']:8.2f} " + " ".join(f"{k}={v:.3f}" for k, v in d['pass_ms_one_frame_in_flight'].items() if v > 0.01), flush=True)
+kr = d.get('kernel_roofline', {})
+print(f"{sys.argv[1]:>14s} fps={d['value']:8.2f} {kr.get('kernel', '')}_ms={kr.get('kernel_ms', 0):.3f} " +
+      " ".join(f"{k}={v:.3f}" for k, v in d.get('pass_ms_one_frame_in_flight', {}).items() if v > 0.01), flush=True)
 PY
 done; done
