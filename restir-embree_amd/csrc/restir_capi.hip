@@ -159,6 +159,7 @@ struct rs_context {
     ulonglong2* d_red = nullptr;           // k_reduce_counts partials + ticket (= reds[li])
     ulonglong2* reds[kLanes] = {};
     uint32_t* qctr[kLanes] = {};           // persistent-wave tile queues (rs_passes.h TileQ): 4 words per lane
+    float* candw[kLanes] = {};             // the sorted initial pass's candidate weights (FrameConst::cand_w), per lane
     int persist_mode = RS_PERSIST ? RS_SPLIT_AUTO : RS_SPLIT_OFF;
     int persist_wgs[4] = {};               // resident workgroups per CU of the persistent initial kernel, per kind
     int persist_sorted = RS_SPLIT_AUTO;    // RESTIR_PERSIST_SORTED: the sorted pass by persistent waves
@@ -556,6 +557,7 @@ extern "C" void rs_context_destroy(rs_context* c) {
     for (auto* p : c->cnts) if (p) hipFree(p);
     for (auto* p : c->reds) if (p) hipFree(p);
     for (auto* p : c->qctr) if (p) hipFree(p);
+    for (auto* p : c->candw) if (p) hipFree(p);
     if (c->d_tot) hipFree(c->d_tot);
     void* post[] = {c->acc, c->display, c->post_part, c->post_out};
     for (void* p : post) if (p) hipFree(p);
@@ -1776,6 +1778,9 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
         k_q_resolve<<<gb, 256, 0, c->fs>>>(S, F, c->G[gnew], Q, ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                                            count_slot(c, gb));
     } else if (want_sorted(c, P, s)) {
+        if (RS_SORT_STORE_W && !c->candw[c->li])      // first sorted frame on this lane: the full frame's tiles
+            HIPCHK(c, hipMalloc(&c->candw[c->li], sort_scratch_floats(c->W, c->H) * sizeof(float)));
+        Fi.cand_w = c->candw[c->li];
         if (want_persist_sorted(c, gg)) {
             // persistent waves, each pulling 8x8 tiles (rs_passes.h k_gbuffer_initial_sorted_pq)
             const uint32_t nt = gg.x * gg.y * 4u;

@@ -80,6 +80,7 @@ struct FrameConst {
     int canon_vis;        // spatial pass: the canonical (own) reservoir's sample is known unoccluded from the pixel
                           //   (restir_capi.hip rs_tile_spatial; §3.2) -- its visibility ray is not traced again
     uint8_t* dbg;         // 2 x W*H bytes: [p] the pixel's own rejection (1..3), [W*H + p] forward-check hit
+    float* cand_w;        // the sorted initial pass's phase-A candidate weights (RS_SORT_STORE_W), per 8x8 tile
 };
 
 struct Counters { unsigned long long rays, primary, reproj_outside; };   // per-frame totals
@@ -720,6 +721,17 @@ k_gbuffer_initial_pq(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int
 #define RS_INITIAL_WAVES_SORT_LOCKSTEP 5
 #endif
 constexpr int kSortChunk = RS_SORT_CHUNK;   // area candidates per sort round
+// Phase A's unoccluded candidate weights kept for phase C in global memory (one coalesced 256-B store and load
+// per candidate and wave, per 8x8 tile: FrameConst::cand_w) instead of phase C drawing every candidate again (its
+// light pick, the emitter record gathers, the sample, both Phong powf)
+#ifndef RS_SORT_STORE_W
+#define RS_SORT_STORE_W 1
+#endif
+static_assert(!RS_SORT_STORE_W || kSortChunk <= 16, "ok and NaN bits of a chunk share one word");
+// floats of FrameConst::cand_w for a W x rows launch (its 8x8 tiles x kSortChunk x 64)
+__host__ __device__ inline size_t sort_scratch_floats(int W, int rows) {
+    return (size_t)(2 * ((W + 15) / 16)) * (size_t)(2 * ((rows + 15) / 16)) * (size_t)(kSortChunk * 64);
+}
 static_assert(kSortChunk >= 1 && kSortChunk <= 32, "one occlusion word per pixel; 11-bit ranks");
 struct SortLds {                            // one wave's region (7.3 KB at 16 candidates)
     uint32_t slot[kSortChunk * 64];         // slot k * 64 + lane: light | rank in its bucket << 21
@@ -826,11 +838,20 @@ __device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst&
                 wave_lds_sync();
                 uint32_t needm = 0u;
                 uint32_t bkt[(kSortChunk + 3) / 4] = {};                // the needed rays' buckets, 8 bits each
+#if RS_SORT_STORE_W
+                uint32_t flg = 0u;                                      // bit k: ok; bit 16 + k: its occluded weight is NaN
+                float* const wst = F.cand_w + ((size_t)((ty0 - F.gy0) >> 3) * (size_t)(2 * ((F.W + 15) >> 4)) +
+                                               (size_t)(tx0 >> 3)) * (size_t)(kSortChunk * 64) + lane;
+#endif
                 {
                     const GElem g = G.load(p);
                     const ShadeFrame sf = make_frame(g, cam);
                     for (int k = 0; k < nk; ++k) {
                         const AreaCand a = area_cand(S, F, g.pos, sf, rng, c0 + k, tv, alive, inv_ma);
+#if RS_SORT_STORE_W
+                        wst[k * 64] = a.wu;
+                        flg |= (a.ok ? 1u << k : 0u) | (a.wo_nan ? 1u << (16 + k) : 0u);
+#endif
                         if (a.need) {
                             const uint32_t rank = atomicAdd(&L.cur[a.bucket], 1u);
                             L.slot[k * 64 + lane] = a.pick | (rank << 21);
@@ -883,8 +904,17 @@ __device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst&
                     if (act && occ) atomicOr(&L.occ[src], 1u << k);
                 }
                 wave_lds_sync();
-                // ---- C: re-drawn weights, the reservoir stream in candidate order (lane = pixel)
+                // ---- C: phase A's weights, the reservoir stream in candidate order (lane = pixel)
                 const uint32_t occm = L.occ[lane];
+#if RS_SORT_STORE_W
+                for (int k = 0; k < nk; ++k) {
+                    const int c = c0 + k;
+                    const bool use_u = ((flg >> k) & 1u) && !(((needm & occm) >> k) & 1u);
+                    const float w = use_u ? wst[k * 64] : (((flg >> (16 + k)) & 1u) ? __int_as_float(0x7fc00000) : 0.0f);
+                    rng.n = cand_slot(c) + 3u;
+                    if (alive && res_add_w(r, w, 0, rng)) sel = c;
+                }
+#else
                 const GElem g = G.load(p);
                 const ShadeFrame sf = make_frame(g, cam);
                 for (int k = 0; k < nk; ++k) {
@@ -895,6 +925,7 @@ __device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst&
                     rng.n = cand_slot(c) + 3u;
                     if (alive && res_add_w(r, w, 0, rng)) sel = c;
                 }
+#endif
             }
             if (sel >= 0) {
                 const GElem g = G.load(p);
