@@ -160,6 +160,7 @@ struct rs_context {
     ulonglong2* reds[kLanes] = {};
     uint32_t* qctr[kLanes] = {};           // persistent-wave tile queues (rs_passes.h TileQ): 4 words per lane
     float* candw[kLanes] = {};             // the sorted initial pass's candidate weights (FrameConst::cand_w), per lane
+    float4* candr[kLanes] = {};            // ... and its shadow rays (FrameConst::cand_ray), per lane
     int persist_mode = RS_PERSIST ? RS_SPLIT_AUTO : RS_SPLIT_OFF;
     int persist_wgs[4] = {};               // resident workgroups per CU of the persistent initial kernel, per kind
     int persist_sorted = RS_SPLIT_AUTO;    // RESTIR_PERSIST_SORTED: the sorted pass by persistent waves
@@ -558,6 +559,7 @@ extern "C" void rs_context_destroy(rs_context* c) {
     for (auto* p : c->reds) if (p) hipFree(p);
     for (auto* p : c->qctr) if (p) hipFree(p);
     for (auto* p : c->candw) if (p) hipFree(p);
+    for (auto* p : c->candr) if (p) hipFree(p);
     if (c->d_tot) hipFree(c->d_tot);
     void* post[] = {c->acc, c->display, c->post_part, c->post_out};
     for (void* p : post) if (p) hipFree(p);
@@ -1781,6 +1783,9 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
         if (RS_SORT_STORE_W && !c->candw[c->li])      // first sorted frame on this lane: the full frame's tiles
             HIPCHK(c, hipMalloc(&c->candw[c->li], sort_scratch_floats(c->W, c->H) * sizeof(float)));
         Fi.cand_w = c->candw[c->li];
+        if (RS_SORT_STORE_RAY && !c->candr[c->li])
+            HIPCHK(c, hipMalloc(&c->candr[c->li], sort_scratch_floats(c->W, c->H) * sizeof(float4)));
+        Fi.cand_ray = c->candr[c->li];
         if (want_persist_sorted(c, gg)) {
             // persistent waves, each pulling 8x8 tiles (rs_passes.h k_gbuffer_initial_sorted_pq)
             const uint32_t nt = gg.x * gg.y * 4u;

@@ -81,6 +81,7 @@ struct FrameConst {
                           //   (restir_capi.hip rs_tile_spatial; §3.2) -- its visibility ray is not traced again
     uint8_t* dbg;         // 2 x W*H bytes: [p] the pixel's own rejection (1..3), [W*H + p] forward-check hit
     float* cand_w;        // the sorted initial pass's phase-A candidate weights (RS_SORT_STORE_W), per 8x8 tile
+    float4* cand_ray;     // ... and its needed shadow rays' (direction, tfar) (RS_SORT_STORE_RAY), per 8x8 tile
 };
 
 struct Counters { unsigned long long rays, primary, reproj_outside; };   // per-frame totals
@@ -728,6 +729,11 @@ constexpr int kSortChunk = RS_SORT_CHUNK;   // area candidates per sort round
 #define RS_SORT_STORE_W 1
 #endif
 static_assert(!RS_SORT_STORE_W || kSortChunk <= 16, "ok and NaN bits of a chunk share one word");
+// ... and the needed shadow rays' (direction, tfar) for phase B (one 16-B load per ray instead of re-forming it
+// from the candidate's RNG slots and the emitter's three vertices)
+#ifndef RS_SORT_STORE_RAY
+#define RS_SORT_STORE_RAY 1
+#endif
 // floats of FrameConst::cand_w for a W x rows launch (its 8x8 tiles x kSortChunk x 64)
 __host__ __device__ inline size_t sort_scratch_floats(int W, int rows) {
     return (size_t)(2 * ((W + 15) / 16)) * (size_t)(2 * ((rows + 15) / 16)) * (size_t)(kSortChunk * 64);
@@ -768,7 +774,7 @@ __device__ __forceinline__ uint32_t ray_bucket(const DevScene& S, uint32_t pick,
     return (oct << 3) | (eb >> 3);
 }
 // candidate c of a pixel: area_batch's sample and unoccluded evaluation (pick, weights, shadow ray need)
-struct AreaCand { uint32_t pick, bucket; float wu; bool ok, need, wo_nan; };
+struct AreaCand { uint32_t pick, bucket; float wu; bool ok, need, wo_nan; vec3 dir; float tfar; };
 __device__ __forceinline__ AreaCand area_cand(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
                                               Rng& rng, int c, bool tv, bool alive, float inv_ma) {
     AreaCand a;
@@ -784,6 +790,8 @@ __device__ __forceinline__ AreaCand area_cand(const DevScene& S, const FrameCons
     a.wo_nan = wo != wo;
     a.ok = pr.ok;
     a.need = pr.need;
+    a.dir = pr.dir;
+    a.tfar = pr.tfar;
     return a;
 }
 
@@ -838,10 +846,10 @@ __device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst&
                 wave_lds_sync();
                 uint32_t needm = 0u;
                 uint32_t bkt[(kSortChunk + 3) / 4] = {};                // the needed rays' buckets, 8 bits each
+                const size_t wtile = (size_t)((ty0 - F.gy0) >> 3) * (size_t)(2 * ((F.W + 15) >> 4)) + (size_t)(tx0 >> 3);
 #if RS_SORT_STORE_W
                 uint32_t flg = 0u;                                      // bit k: ok; bit 16 + k: its occluded weight is NaN
-                float* const wst = F.cand_w + ((size_t)((ty0 - F.gy0) >> 3) * (size_t)(2 * ((F.W + 15) >> 4)) +
-                                               (size_t)(tx0 >> 3)) * (size_t)(kSortChunk * 64) + lane;
+                float* const wst = F.cand_w + wtile * (size_t)(kSortChunk * 64) + lane;
 #endif
                 {
                     const GElem g = G.load(p);
@@ -853,6 +861,9 @@ __device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst&
                         flg |= (a.ok ? 1u << k : 0u) | (a.wo_nan ? 1u << (16 + k) : 0u);
 #endif
                         if (a.need) {
+#if RS_SORT_STORE_RAY
+                            F.cand_ray[wtile * (size_t)(kSortChunk * 64) + (size_t)(k * 64 + lane)] = f4(a.dir, a.tfar);
+#endif
                             const uint32_t rank = atomicAdd(&L.cur[a.bucket], 1u);
                             L.slot[k * 64 + lane] = a.pick | (rank << 21);
                             bkt[k >> 2] |= a.bucket << (8 * (k & 3));
@@ -885,6 +896,12 @@ __device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst&
                     const uint32_t sl = L.e[act ? j : 0u];
                     const uint32_t pick = L.slot[sl] & 0x1fffffu, k = sl >> 6, src = sl & 63u;
                     const vec3 o = mk(L.px[src], L.py[src], L.pz[src]);
+#if RS_SORT_STORE_RAY
+                    (void)pick;
+                    const float4 dt = F.cand_ray[wtile * (size_t)(kSortChunk * 64) + sl];   // phase A's evaluate_f_pre ray
+                    const vec3 ld = xyz(dt);
+                    const float tfar = dt.w;
+#else
                     Rng q;
                     q.init(F.seed, F.frame, PASS_INITIAL,
                            (uint32_t)(ty0 + (int)(src >> 3)) * (uint32_t)F.W + (uint32_t)(tx0 + (int)(src & 7u)));
@@ -899,6 +916,7 @@ __device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst&
                     const float r2s = dot(ld, ld);
                     ld = normalize(ld);
                     const float tfar = sqrtf(r2s) - F.tfar_off;
+#endif
                     const bool occ = trace_any<T>(S, act, o, ld, FLT_MIN + F.tnear_off, tfar);
                     rays += act ? 1u : 0u;
                     if (act && occ) atomicOr(&L.occ[src], 1u << k);
