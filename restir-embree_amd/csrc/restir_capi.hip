@@ -908,7 +908,7 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
 // TriangleCDF tables from the positions on the device (rs_scene_update_positions): the same float
 // operations in the same order as build_geometry's host loop -- sequential total and prefix sum in
 // one lane, everything else data-parallel -- so the tables are bit-identical to a fresh scene's.
-constexpr int kLightBlock = 1024, kLightChunk = 8192;
+constexpr int kLightBlock = kRefitBlock, kLightChunk = 8192;
 __device__ __forceinline__ void light_table(const float* __restrict__ pos, const float4* __restrict__ tri_nrm,
                                             const float4* __restrict__ mats, const int* __restrict__ emis_tri,
                                             uint32_t ne, float4* em, float* cdf, int* guide) {

@@ -42,8 +42,14 @@ struct WideBvh {
     int status = 0;              // why there is no tree (include/restir_c.h RS_WIDE_*): 0 live
 };
 
-constexpr int kRefitBlock = 1024;
-constexpr int kRefitSmall = 4 * kRefitBlock;     // levels up to this many nodes go to the 1-block batch
+// Workgroup size of the refits and of the per-update kernel (k_scene_update).  Updates run on the next frame's
+// lane beside earlier frames' passes, which hold every CU: a workgroup of 1024 threads needs 16 free wave slots
+// on one CU at once and waited for the passes' tails to be dispatched (C5: 0.68 ms per update under the profiler)
+#ifndef RS_REFIT_BLOCK
+#define RS_REFIT_BLOCK 256
+#endif
+constexpr int kRefitBlock = RS_REFIT_BLOCK;
+constexpr int kRefitSmall = 4096;                // levels up to this many nodes go to the 1-block batch
 
 __device__ __forceinline__ void refit_node(float4* nodes, float4* tris, const float* __restrict__ pos, int i) {
     const float4 a = nodes[2 * i], b = nodes[2 * i + 1];
