@@ -1005,8 +1005,9 @@ struct RefitArgs { float4* nodes; float4* tris; const float* pos; const int* ord
 __global__ void __launch_bounds__(kLightBlock) k_scene_update(const float* __restrict__ pos, const float4* __restrict__ tri_nrm,
                                                               const float4* __restrict__ mats, const int* __restrict__ emis_tri,
                                                               uint32_t ne, float4* em, float* cdf, int* guide, RefitArgs R,
-                                                              WideRefitArgs W) {
+                                                              WideRefitArgs W, int jobs) {
     static_assert(kLightBlock == kRefitBlock, "one workgroup size for every job");
+    if (!((jobs >> blockIdx.x) & 1)) return;   // RESTIR_UPDATE_SPLIT: one job per launch (a kernel trace times each)
     if (blockIdx.x == 0) {
         if (ne) light_table(pos, tri_nrm, mats, emis_tri, ne, em, cdf, guide);
     } else if (blockIdx.x == 1) {
@@ -1142,7 +1143,12 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
             k_wide_refit<<<wb[i].blocks, kRefitBlock, 0, st>>>(A);
         }
     }
-    k_scene_update<<<3, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, em, cdf, guide, R, W);
+    // the light tables, the binary refit's last levels and the wide refit's last levels, one workgroup each
+    // (RESTIR_UPDATE_SPLIT=1, diagnostic: three launches in stream order, one job each -- scripts/update_probe.py)
+    static const bool split = [] { const char* e = getenv("RESTIR_UPDATE_SPLIT"); return e && e[0] == '1'; }();
+    for (int j = split ? 1 : 7; j <= (split ? 4 : 7); j <<= 1)
+        k_scene_update<<<3, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, em, cdf, guide,
+                                                  R, W, j);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(s->update_ev, st));
     s->update_recorded = true;
