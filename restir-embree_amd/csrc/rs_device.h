@@ -54,8 +54,15 @@ __device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, 
 // ---------------------------------------------------------------- counter RNG
 // Replaces Utils::getRandomValue's shared mt19937 (pg/utils.cpp:175-176,199-202): one independent
 // stream per (seed, frame, pass, full-frame pixel), consumed in the reference's per-pixel order.
+#ifndef RS_DIAG_CHEAP_RNG
+#define RS_DIAG_CHEAP_RNG 0    // timing diagnostic only (scripts/gpu_r05_an.sh): a multiply-free hash; breaks parity
+#endif
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
+#if RS_DIAG_CHEAP_RNG
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5; x ^= x >> 16; return x;
+#else
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16; return x;
+#endif
 }
 struct Rng {
     uint32_t key, n;
