@@ -73,7 +73,10 @@ def test_local_mgpu_rebalance_and_frames_in_flight():
     m.rebalance(ss, cams[0], prm, 0, 2, 6, refine=0)              # row costs only: nothing measured
     assert m.rebalance_times() == []
     bands = m.rebalance(ss, cams[0], prm, 0, 2, 6, refine=2)       # + 2 time-based rounds (the default)
-    assert bands != [(0, 24), (24, 48), (48, 72)] and all(b - a >= 6 for a, b in bands), bands
+    # contiguous bands of >= 6 rows over the image.  (Bands are cut on 8-row wave tiles when the height allows, so
+    # at 72 rows the equal split 24/24/24 is a legitimate outcome of the measured rounds -- not asserted against.)
+    assert bands[0][0] == 0 and bands[-1][1] == H and all(bands[i][1] == bands[i + 1][0] for i in range(world - 1)), bands
+    assert all(b - a >= 6 for a, b in bands), bands
     rounds = m.rebalance_times()                                   # every rank timed in every measured round
     assert 1 <= len(rounds) <= 3 and all(len(t) == world and min(t) > 0 for t in rounds), rounds
     clones = []
