@@ -58,7 +58,13 @@ __device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, 
 #define RS_DIAG_CHEAP_RNG 0    // timing diagnostic only (scripts/gpu_r05_an.sh): a multiply-free hash; breaks parity
 #endif
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
-#if RS_DIAG_CHEAP_RNG
+#if RS_DIAG_CHEAP_RNG == 2
+    // two full-rate 24-bit multiplies (v_mul_u32_u24), the top bits folded down before each (scripts/rng_quality.py
+    // "hash24": avalanche bias as lowbias32's); timing study only -- the oracle keeps lowbias32
+    x ^= x >> 16; x = __umul24(x, 0x7feb35u) ^ (x >> 24);
+    x ^= x >> 15; x = __umul24(x, 0x846ca7u) ^ (x >> 24);
+    x ^= x >> 16; return x;
+#elif RS_DIAG_CHEAP_RNG
     x ^= x << 13; x ^= x >> 17; x ^= x << 5; x ^= x >> 16; return x;
 #else
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16; return x;
