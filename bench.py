@@ -525,15 +525,88 @@ def write_full(path, rec):
         print(f"warning: cannot write {path}: {ex}", file=sys.stderr)
 
 
+# ---------------------------------------------------------------- rank launcher (--gpus N without torchrun)
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(base: dict, rank: int, world: int, port: int) -> dict:
+    """The environment of rank `rank` of a `world`-rank job on this node (what torchrun would set)."""
+    env = dict(base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(port)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def check_world(gpus: int, env: dict):
+    """None when this process should run as a rank (WORLD_SIZE set and equal to --gpus, or --gpus 1 alone);
+    "launch" when it must start --gpus ranks itself; an error message on a --gpus / WORLD_SIZE mismatch."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else None
+    if int(ws) != gpus:
+        return f"--gpus {gpus} but WORLD_SIZE={ws}: the launcher and the flag disagree"
+    return None
+
+
+def launch_ranks(argv, world: int, env=None, cmd=None, poll_s: float = 0.2) -> int:
+    """Starts `world` child processes of this script (fresh interpreters: nothing here has touched the GPU),
+    one per rank with torchrun's environment, and waits.  Rank 0's stdout (the JSON line) passes through;
+    the first child to fail ends the others (their exact PIDs) and its exit code is returned."""
+    base = dict(os.environ if env is None else env)
+    port = free_port()
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)]
+    procs = []
+    for r in range(world):
+        procs.append(subprocess.Popen(cmd + list(argv), env=rank_env(base, r, world, port),
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc, kill_at = 0, None
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr)
+                    for q in live:
+                        q.terminate()
+                    kill_at = time.monotonic() + 30.0
+            if live and kill_at is not None and time.monotonic() > kill_at:
+                for q in live:
+                    q.kill()
+            if live:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     args = parse()
+    verdict = check_world(args.gpus, os.environ)
+    if verdict == "launch":
+        # --gpus N > 1 without a launcher: start N ranks here, before this process touches the GPU
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    if verdict is not None:
+        print(f"bench.py: {verdict}", file=sys.stderr)
+        sys.exit(2)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     W, H = args.width, args.height
     # RESTIR_FORCE_MULTI=1 runs the N>1 code path with one rank (a rehearsal of the multi-GPU flow on a
     # one-GPU box: RCCL refuses two ranks on one device)

@@ -286,6 +286,12 @@ int rs_max_run_ahead(void);
  * pg/simpleguidx11.h:152) or 2 -- consecutive frames alternate between two buffers, so a consumer
  * (the multi-GPU gather, an async copy) may still read frame f while frame f+1 renders. */
 int rs_context_set_frame_ring(rs_context* ctx, int n);
+/* Device bytes of the wave-sorted initial pass's hand-off buffers (phase A's candidate weights and shadow rays,
+ * 20 B per candidate slot), summed over the run-ahead lanes.  They are grown on demand before a frame is
+ * enqueued and sized by the launch: one region per resident wave of the persistent launch (C3 1080p: ~63 MB
+ * per lane), one per 8x8 tile of a one-launch grid (a band's rows only).  If the device cannot hold them
+ * the frame runs the one-thread-per-pixel initial pass instead (the same results). */
+int rs_context_handoff_bytes(const rs_context* ctx, uint64_t* bytes);
 /* Load-balancing record for tile sharding (no reference counterpart): while enabled, every pass
  * kernel's waves add their lifetime (100 MHz ticks) to the image row at the top of their tile, for rows
  * inside the context's band.  rs_get_row_costs copies the H per-row sums to `costs` (host, H floats;
@@ -456,6 +462,11 @@ int rs_mgpu_rebalance(rs_mgpu* m, const rs_scene* const* scenes, const rs_camera
  * the current bands (gathered, frames in flight), all-reduces every rank's own time per frame (its frames'
  * begin..shade span minus its halo exchanges, plus rank 0's gather), rescales each band's row costs to its
  * time and balances again; the measured bands with the lowest maximum are kept.  rounds = 0: row costs only.
+ * The setting persists on `m` until set again (the Python wrapper passes 2 whenever its caller gives none).
+ * Side effects: rs_mgpu_rebalance renders n_frames frames, plus per measured round 2 + max(n_frames, 6)
+ * gathered frames (frame indices first_frame, first_frame + 1, ...), which overwrite rank 0's framebuffer;
+ * the contexts' timing totals and the rs_mgpu stats keep counting those frames (read as deltas, never
+ * reset); the history is reset on return.
  * rs_mgpu_rebalance_times: the last rebalance's measured ms per rank (world values) of measured round r. */
 int rs_mgpu_set_rebalance_refine(rs_mgpu* m, int rounds);
 int rs_mgpu_rebalance_times(const rs_mgpu* m, int round, double* ms);

@@ -35,6 +35,9 @@
 #include <string.h>
 #include <float.h>
 #include <immintrin.h>
+/* the path's transcendental functions: one shared sequence of IEEE operations with the HIP kernels
+ * (restir-embree_amd/csrc/rs_libm.h), so frames match bit for bit; glibc's libm is not called on the path */
+#include "../restir-embree_amd/csrc/rs_libm.h"
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -211,17 +214,29 @@ static double betacf(double a, double b, double x) {
 }
 double or_ibeta(double x, double a, double b) {
     if (!(x > 0.0)) return 0.0;
-    double lbeta = lgamma(a) + lgamma(b) - lgamma(a + b);
-    if (x >= 1.0) return exp(lbeta);
-    double lbt = a * log(x) + b * log1p(-x);
+    double lbeta = rs_lgamma_d(a) + rs_lgamma_d(b) - rs_lgamma_d(a + b);
+    if (x >= 1.0) return rs_exp_d(lbeta);
+    double lbt = a * rs_log_d(x) + b * rs_log1p_d(-x);
     if (x < (a + 1.0) / (a + b + 2.0))
-        return exp(lbt) * betacf(a, b, x) / a;
-    return exp(lbeta) - exp(lbt) * betacf(b, a, 1.0 - x) / b;
+        return rs_exp_d(lbt) * betacf(a, b, x) / a;
+    return rs_exp_d(lbeta) - rs_exp_d(lbt) * betacf(b, a, 1.0 - x) / b;
+}
+/* rs_libm.h's functions over arrays (tests/test_oracle.py test_libm_correctly_rounded) */
+void or_libm_f1(int which, const float* x, float* o, int n) {
+    for (int i = 0; i < n; ++i)
+        o[i] = which == 0 ? rs_expf(x[i]) : which == 1 ? rs_lgammaf(x[i]) : which == 2 ? rs_sinf(x[i]) : rs_cosf(x[i]);
+}
+void or_libm_powf(const float* x, const float* y, float* o, int n) {
+    for (int i = 0; i < n; ++i) o[i] = rs_powf(x[i], y[i]);
+}
+void or_libm_d1(int which, const double* x, double* o, int n) {
+    for (int i = 0; i < n; ++i)
+        o[i] = which == 0 ? rs_log_d(x[i]) : which == 1 ? rs_exp_d(x[i]) : which == 2 ? rs_log1p_d(x[i]) : rs_lgamma_d(x[i]);
 }
 /* MaterialPhong::ibeta (pg/MaterialPhong.cpp:246-248): float in, Boost promotes to double, float out */
 static inline float ibeta_f(float x, float a, float b) { return (float)or_ibeta((double)x, (double)a, (double)b); }
 /* MaterialPhong::gamma_quot (pg/MaterialPhong.cpp:224-226) */
-static inline float gamma_quot(float a, float b) { return expf(lgammaf(a) - lgammaf(b)); }
+static inline float gamma_quot(float a, float b) { return rs_expf(rs_lgammaf(a) - rs_lgammaf(b)); }
 /* MaterialPhong::calc_I_M (pg/MaterialPhong.cpp:228-244) */
 float or_calc_I_M(float nDotV, float n) {
     float costerm = nDotV;
@@ -231,7 +246,7 @@ float or_calc_I_M(float nDotV, float n) {
     sinterm_sq = gmin(gmax(sinterm_sq, 0.0f), 1.0f);
     if (n >= 1e-18f) negterm *= halfn * ibeta_f(sinterm_sq, halfn, 0.5f);
     return (OR_TWO_PI * costerm + OR_ROOT_PI * gamma_quot(halfn + 0.5f, halfn + 1.0f) *
-            (powf(sinterm_sq, halfn) - negterm)) / (n + 2.0f);
+            (rs_powf(sinterm_sq, halfn) - negterm)) / (n + 2.0f);
 }
 
 /* ------------------------------------------------------------------ scene */
@@ -428,7 +443,7 @@ static float srgb_expand1(float u) {
     if (u <= 0.0f) return 0.0f;
     if (u >= 1.0f) return 1.0f;
     if (u <= 0.04045f) return u / 12.92f;
-    return powf((u + 0.055f) / 1.055f, 2.4f);
+    return rs_powf((u + 0.055f) / 1.055f, 2.4f);
 }
 /* Texture ctor (pg/Texture.cpp:9-57) + Texture::expand applied n_expand times (:141-160) */
 static int tex_load(or_tex* t, const or_texdesc* d, int n_expand) {
@@ -908,7 +923,7 @@ static hitinfo intersect(const fctx* F, v3 o, v3 d, float tnear, uint64_t* rays)
 static inline float cosine_pdf(v3 n, v3 wi) { return gmax(dot(n, wi), 0.0f) * OR_ONE_OVER_PI; }
 /* CosineLobeDistribution::getPdf (pg/Distribution.h:65-67) */
 static inline float lobe_pdf(v3 wi, v3 wr, float gamma) {
-    return (gamma + 1.0f) * OR_ONE_OVER_2PI * powf(gmax(0.0f, dot(wi, wr)), gamma);
+    return (gamma + 1.0f) * OR_ONE_OVER_2PI * rs_powf(gmax(0.0f, dot(wi, wr)), gamma);
 }
 /* pdf eval dispatch: always MaterialPhong::evalPdf (pg/ReSTIRIntegrator.h:54-59, pg/MaterialPhong.cpp:150-172) */
 static float phong_eval_pdf(const or_gbe* g, v3 cam, v3 wi) {
@@ -932,7 +947,7 @@ static v3 eval_brdf(const or_gbe* g, v3 cam, v3 wi, float im_cached, int use_cac
     if (use_cache) i_m = im_cached;
     else { float nDotV = dot(Vv, g->nrm); i_m = 1.0f / or_calc_I_M(nDotV, g->shin); }
     v3 wr = nrmz(reflect(neg(Vv), g->nrm));
-    float pw = powf(gmax(dot(wi, wr), 0.0f), g->shin);
+    float pw = rs_powf(gmax(dot(wi, wr), 0.0f), g->shin);
     f = add(f, scl(scl(g->ks, i_m), pw));
     return f;
 }
@@ -976,8 +991,8 @@ static v3 to_world(v3 smp, v3 n) {
 }
 static v3 cosine_sample_u(v3 n, float r1, float r2) {
     float ang = OR_PI * 2.0f * r1;
-    float x = cosf(ang) * sqrtf(1.0f - r2);
-    float y = sinf(ang) * sqrtf(1.0f - r2);
+    float x = rs_cosf(ang) * sqrtf(1.0f - r2);
+    float y = rs_sinf(ang) * sqrtf(1.0f - r2);
     float z = sqrtf(r2);
     return to_world(nrmz(V(x, y, z)), n);
 }
@@ -988,9 +1003,9 @@ static v3 cosine_sample(v3 n, rng_t* rng) {
 /* CosineLobeDistribution::sample (pg/Distribution.h:37-57) */
 static v3 lobe_sample_u(v3 wr, float gamma, float r1, float r2) {
     float ang = 2.0f * OR_PI * r1;
-    float x = cosf(ang) * sqrtf(1.0f - powf(r2, 2.0f / (gamma + 1.0f)));
-    float y = sinf(ang) * sqrtf(1.0f - powf(r2, 2.0f / (gamma + 1.0f)));
-    float z = powf(r2, 1.0f / (gamma + 1.0f));
+    float x = rs_cosf(ang) * sqrtf(1.0f - rs_powf(r2, 2.0f / (gamma + 1.0f)));
+    float y = rs_sinf(ang) * sqrtf(1.0f - rs_powf(r2, 2.0f / (gamma + 1.0f)));
+    float z = rs_powf(r2, 1.0f / (gamma + 1.0f));
     return to_world(nrmz(V(x, y, z)), wr);
 }
 static v3 lobe_sample(v3 wr, float gamma, rng_t* rng) {
@@ -1334,8 +1349,8 @@ static void pass_temporal(fctx* F, const or_res* Rr, const or_res* Rl, or_res* R
 static void disk_offset(float radius, rng_t* rng, int* ox, int* oy) {
     float theta = rnd(rng, 0, 2.0f) * OR_PI;
     float r = sqrtf(rnd(rng, 0, radius));
-    float x = r * cosf(theta);
-    float y = r * sinf(theta);
+    float x = r * rs_cosf(theta);
+    float y = r * rs_sinf(theta);
     *ox = (int)x; *oy = (int)y;
 }
 
@@ -1627,7 +1642,7 @@ static float mis_pdf_for(const mis_surf* h, v3 wi) {
 static v3 mis_brdf(const mis_surf* h, v3 wi) {
     v3 f = scl(h->kd, OR_ONE_OVER_PI);
     if (!h->phong) return f;
-    return add(f, scl(scl(h->ks, h->i_m), powf(gmax(dot(wi, h->wr), 0.0f), h->shin)));
+    return add(f, scl(scl(h->ks, h->i_m), rs_powf(gmax(dot(wi, h->wr), 0.0f), h->shin)));
 }
 /* evaluateLightingGI (pg/MaterialLambert.cpp:10-18, pg/MaterialPhong.cpp:18-67) */
 static v3 mis_sample(const mis_surf* h, rng_t* rng, v3* f_r, float* pdf) {
@@ -1644,7 +1659,7 @@ static v3 mis_sample(const mis_surf* h, rng_t* rng, v3* f_r, float* pdf) {
         *f_r = scl(h->kd, OR_ONE_OVER_PI);
     } else {
         wi = lobe_sample(h->wr, h->shin, rng);
-        *f_r = scl(scl(h->ks, h->i_m), powf(gmax(dot(wi, h->wr), 0.0f), h->shin));
+        *f_r = scl(scl(h->ks, h->i_m), rs_powf(gmax(dot(wi, h->wr), 0.0f), h->shin));
     }
     float pd = cosine_pdf(h->n, wi) * h->pf;
     float ps = lobe_pdf(wi, h->wr, h->shin) * (1.0f - h->pf);
@@ -1862,7 +1877,7 @@ static inline float post_compress(float u) {
     if (u <= 0.0f) return 0.0f;
     if (u >= 1.0f) return 1.0f;
     if ((double)u <= 0.0031308) return u * 12.92f;
-    return 1.055f * powf(u, 1.0f / 2.4f) - 0.055f;
+    return 1.055f * rs_powf(u, 1.0f / 2.4f) - 0.055f;
 }
 void or_post_apply(int W, int y0, int y1, const float* frame, float* acc, int acc_frames, int tonemap,
                    int gamma_correct, float* display_rgba, double* sum, double* sqr_sum) {

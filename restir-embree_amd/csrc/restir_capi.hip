@@ -5,7 +5,6 @@
 // (pg/Scene.cpp:8-16, pg/ModelLoader.cpp:218-321, pg/TriangleCDF.cpp:8-34), computes the camera
 // (pg/camera.cpp:12-84) and sequences the passes of produceRestir (pg/simpleguidx11.cpp:359-487).
 #include "rs_passes.h"
-#include "rs_queue.h"
 #include "rs_mis.h"
 #include "rs_post.h"
 #include "rs_refit.h"
@@ -161,8 +160,7 @@ struct rs_context {
     uint32_t* qctr[kLanes] = {};           // persistent-wave tile queues (rs_passes.h TileQ): 4 words per lane
     float* candw[kLanes] = {};             // the sorted initial pass's candidate weights (FrameConst::cand_w), per lane
     float4* candr[kLanes] = {};            // ... and its shadow rays (FrameConst::cand_ray), per lane
-    int persist_mode = RS_PERSIST ? RS_SPLIT_AUTO : RS_SPLIT_OFF;
-    int persist_wgs[4] = {};               // resident workgroups per CU of the persistent initial kernel, per kind
+    size_t cand_slots[kLanes] = {};        // wave slots candw / candr hold (ensure_handoff)
     int persist_sorted = RS_SPLIT_AUTO;    // RESTIR_PERSIST_SORTED: the sorted pass by persistent waves
     int persist_sorted_wgs[4] = {};
     // pass timing without a per-frame host sync: every frame records into its own slot of an event
@@ -242,19 +240,10 @@ struct rs_context {
     uint64_t rb_seq = 0;
     hipEvent_t fb_read[kLanes] = {};
     hipEvent_t join_ev = nullptr;          // rs::ctx_join
-    // queued initial pass (rs_queue.h): mode (RS_SPLIT_* values: AUTO = incoherent scenes), the last
-    // frame's choice, per-lane queue storage (sized for the largest launch so far)
     uint8_t* d_dbg = nullptr;              // debugReprojection marks (FrameConst::dbg), on first use
-    int queue_mode = RS_SPLIT_OFF;
-    bool queue = false;
-    QBuf qb[kLanes] = {};
-    size_t q_slots[kLanes] = {}, q_px[kLanes] = {}, q_waves[kLanes] = {};
-    int q_A[kLanes] = {}, q_B[kLanes] = {};
     int cus = 256;
     int sort_mode = RS_SPLIT_AUTO;         // wave-sorted initial pass (RESTIR_SORT=on|off; AUTO: per-lane walks)
     bool sep_margin = true;                // a band's G-buffer margin rows in their own launch (RESTIR_MARGIN_SPLIT=off)
-    int spatial_split = RS_SPLIT_OFF;      // candidate-split spatial pass for small launches (RESTIR_SPATIAL_SPLIT=
-                                           // auto|on; measured slower at C2's 1/8 bands: max 0.2304 vs 0.2198 ms)
     int sort_spatial = RS_SPLIT_AUTO;      // wave-sorted spatial pass, CONSTANT MIS, k <= 8 (RESTIR_SORT_SPATIAL=on|off;
                                            // AUTO: per-lane walks -- C3 2.21 -> 1.87 ms; lockstep C5 0.228 -> 0.250)
     int sort_temporal = RS_SPLIT_AUTO;     // wave-sorted temporal rays (RESTIR_SORT_TEMPORAL=off: per-ray walks)
@@ -416,20 +405,10 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
         if (!std::strcmp(t, "on")) c->split_mode = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->split_mode = RS_SPLIT_OFF;
     }
-    if (const char* t = std::getenv("RESTIR_QUEUE")) {         // off (default: measured slower) | on | auto
-        if (!std::strcmp(t, "on")) c->queue_mode = RS_SPLIT_ON;
-        else if (!std::strcmp(t, "off")) c->queue_mode = RS_SPLIT_OFF;
-        else if (!std::strcmp(t, "auto")) c->queue_mode = RS_SPLIT_AUTO;
-    }
     if (const char* t = std::getenv("RESTIR_PERSIST_SORTED")) {   // persistent-wave sorted pass: auto | on | off
         if (!std::strcmp(t, "on")) c->persist_sorted = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->persist_sorted = RS_SPLIT_OFF;
         else if (!std::strcmp(t, "auto")) c->persist_sorted = RS_SPLIT_AUTO;
-    }
-    if (const char* t = std::getenv("RESTIR_PERSIST")) {       // persistent-wave initial pass: auto | on | off
-        if (!std::strcmp(t, "on")) c->persist_mode = RS_SPLIT_ON;
-        else if (!std::strcmp(t, "off")) c->persist_mode = RS_SPLIT_OFF;
-        else if (!std::strcmp(t, "auto")) c->persist_mode = RS_SPLIT_AUTO;
     }
     if (const char* t = std::getenv("RESTIR_SORT")) {          // auto (default) | on | off: wave-sorted initial pass
         if (!std::strcmp(t, "on")) c->sort_mode = RS_SPLIT_ON;
@@ -441,11 +420,6 @@ extern "C" int rs_context_create(int hip_device, int width, int height, void* hi
     }
     if (const char* t = std::getenv("RESTIR_MARGIN_SPLIT"))    // on (default) | off
         c->sep_margin = std::strcmp(t, "off") != 0;
-    if (const char* t = std::getenv("RESTIR_SPATIAL_SPLIT")) { // off (default) | auto | on
-        if (!std::strcmp(t, "on")) c->spatial_split = RS_SPLIT_ON;
-        else if (!std::strcmp(t, "off")) c->spatial_split = RS_SPLIT_OFF;
-        else if (!std::strcmp(t, "auto")) c->spatial_split = RS_SPLIT_AUTO;
-    }
     if (const char* t = std::getenv("RESTIR_SORT_SPATIAL")) {  // auto (default) | on | off: wave-sorted spatial pass
         if (!std::strcmp(t, "on")) c->sort_spatial = RS_SPLIT_ON;
         else if (!std::strcmp(t, "off")) c->sort_spatial = RS_SPLIT_OFF;
@@ -491,6 +465,14 @@ extern "C" int rs_context_set_run_ahead(rs_context* c, int depth) {
     c->join_next = true;
     return RS_OK;
 }
+extern "C" int rs_context_handoff_bytes(const rs_context* c, uint64_t* bytes) {
+    if (!c || !bytes) return RS_E_INVALID;
+    uint64_t b = 0;
+    for (size_t s : c->cand_slots) b += (uint64_t)s * (uint64_t)(kSortChunk * 64) * (sizeof(float) + sizeof(float4));
+    *bytes = b;
+    return RS_OK;
+}
+
 extern "C" int rs_context_set_frame_ring(rs_context* c, int n) {
     if (!c) return fail(nullptr, RS_E_INVALID, "rs_context_set_frame_ring: null context");
     if (n != 1 && n != 2) return fail(c, RS_E_INVALID, "rs_context_set_frame_ring: n must be 1 or 2");
@@ -543,10 +525,6 @@ extern "C" void rs_context_destroy(rs_context* c) {
     for (auto st : c->lane) if (st) hipStreamSynchronize(st);
     for (rs_denoiser* d : c->denoisers) rs::denoiser_detach(d);   // their rs_denoiser_destroy frees the rest
     for (auto e : c->rb_ev) if (e) hipEventDestroy(e);
-    for (auto& q : c->qb) {
-        void* ptrs[] = {q.ray, q.rid, q.cnt, q.cw, q.occ, q.brdf, q.bw};
-        for (void* p : ptrs) if (p) hipFree(p);
-    }
     if (c->join_ev) hipEventDestroy(c->join_ev);
     for (auto& g : c->G) {
         float4* f[5] = {g.g0, g.g1, g.g2, g.g3, g.g4};
@@ -587,7 +565,7 @@ static float srgb_expand1(float u) {
     if (u <= 0.0f) return 0.0f;
     if (u >= 1.0f) return 1.0f;
     if (u <= 0.04045f) return u / 12.92f;
-    return powf((u + 0.055f) / 1.055f, 2.4f);
+    return rs_powf((u + 0.055f) / 1.055f, 2.4f);
 }
 
 // A texture in the layout the reference's Texture holds after FreeImage_ConvertToRawBits
@@ -1005,9 +983,8 @@ struct RefitArgs { float4* nodes; float4* tris; const float* pos; const int* ord
 __global__ void __launch_bounds__(kLightBlock) k_scene_update(const float* __restrict__ pos, const float4* __restrict__ tri_nrm,
                                                               const float4* __restrict__ mats, const int* __restrict__ emis_tri,
                                                               uint32_t ne, float4* em, float* cdf, int* guide, RefitArgs R,
-                                                              WideRefitArgs W, int jobs) {
+                                                              WideRefitArgs W) {
     static_assert(kLightBlock == kRefitBlock, "one workgroup size for every job");
-    if (!((jobs >> blockIdx.x) & 1)) return;   // RESTIR_UPDATE_SPLIT: one job per launch (a kernel trace times each)
     if (blockIdx.x == 0) {
         if (ne) light_table(pos, tri_nrm, mats, emis_tri, ne, em, cdf, guide);
     } else if (blockIdx.x == 1) {
@@ -1144,11 +1121,8 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
         }
     }
     // the light tables, the binary refit's last levels and the wide refit's last levels, one workgroup each
-    // (RESTIR_UPDATE_SPLIT=1, diagnostic: three launches in stream order, one job each -- scripts/update_probe.py)
-    static const bool split = [] { const char* e = getenv("RESTIR_UPDATE_SPLIT"); return e && e[0] == '1'; }();
-    for (int j = split ? 1 : 7; j <= (split ? 4 : 7); j <<= 1)
-        k_scene_update<<<3, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, em, cdf, guide,
-                                                  R, W, j);
+    k_scene_update<<<3, kLightBlock, 0, st>>>(s->d_pos, s->d_tri_nrm, s->d_mats, s->d_emis_tri, s->n_emis, em, cdf, guide,
+                                              R, W);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(s->update_ev, st));
     s->update_recorded = true;
@@ -1520,65 +1494,6 @@ static bool want_split(const rs_context* c, const rs_frame_params* P, int gy0, i
     const size_t rounds = c->ahead > 0 ? 1 : 3;
     return c->trav == TRAV_LOCKSTEP && grid_waves(grid_rows(c->W, gy0, gy1)) < rounds * c->wave_slots;
 }
-// the queued initial pass (rs_queue.h) for incoherent scenes: AUTO = the frame walks per lane (the
-// traversal kind AUTO picked for C3-like scenes; lockstep walks of coherent rays gain nothing from lane
-// refill and would pay the queue's memory traffic)
-static bool want_queue(const rs_context* c, const rs_frame_params* P, int gy0, int gy1) {
-    if (c->split || P->m_area <= 0 || P->m_area > 255 || (size_t)(gy1 - gy0) * c->W >= (1u << 24)) return false;
-    if (c->queue_mode == RS_SPLIT_ON) return true;
-    if (c->queue_mode == RS_SPLIT_OFF) return false;
-    return c->trav == TRAV_LANE;
-}
-static dim3 grid_q_trace(const rs_context* c, size_t n_seg) {
-    const size_t wgs = std::min((n_seg + 3) / 4, (size_t)c->cus * RS_Q_TRACE_WAVES);
-    return dim3((unsigned)std::max<size_t>(1, wgs));
-}
-// queue storage of lane k for a launch of n_waves generate waves over px local pixels
-static int ensure_queue(rs_context* c, int k, size_t n_waves, size_t px, int A, int B) {
-    QBuf& q = c->qb[k];
-    const size_t slots = n_waves * 64 * (size_t)A;
-    if (slots > c->q_slots[k] || px > c->q_px[k] || n_waves > c->q_waves[k] || A > c->q_A[k] || B > c->q_B[k]) {
-        sync_all(c);
-        void* ptrs[] = {q.ray, q.rid, q.cnt, q.cw, q.occ, q.brdf, q.bw};
-        for (void* p : ptrs) if (p) hipFree(p);
-        q = QBuf{};
-        c->q_slots[k] = c->q_px[k] = c->q_waves[k] = 0; c->q_A[k] = c->q_B[k] = 0;
-        const size_t pa = px * (size_t)std::max(1, A), pb = px * (size_t)std::max(1, B);
-        HIPCHK(c, hipMalloc(&q.ray, slots * sizeof(float4)));
-        HIPCHK(c, hipMalloc(&q.rid, slots * sizeof(uint32_t)));
-        HIPCHK(c, hipMalloc(&q.cnt, n_waves * sizeof(uint32_t)));
-        HIPCHK(c, hipMalloc(&q.cw, pa * sizeof(float2)));
-        HIPCHK(c, hipMalloc(&q.occ, pa));
-        HIPCHK(c, hipMalloc(&q.brdf, pb * 3 * sizeof(float4)));
-        HIPCHK(c, hipMalloc(&q.bw, pb * sizeof(float)));
-        c->q_slots[k] = slots; c->q_px[k] = px; c->q_waves[k] = n_waves; c->q_A[k] = A; c->q_B[k] = B;
-    }
-    q.P = (uint32_t)px;
-    q.A = A;
-    return RS_OK;
-}
-// the persistent-wave initial pass (RESTIR_PERSIST / RS_PERSIST): AUTO = launches of more than one round of the
-// device's resident waves (a smaller launch starts every tile at once either way)
-static int persist_wgs(rs_context* c) {
-    const int kind = c->trav | (c->twide ? TRAV_WIDE : 0);
-    int& n = c->persist_wgs[kind];
-    if (!n) {                                   // resident workgroups per CU of the kernel the frame would launch
-        hipError_t e = hipSuccess;
-        switch (kind) {
-            case TRAV_LANE | TRAV_WIDE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_pq<TRAV_LANE | TRAV_WIDE>, 256, 0); break;
-            case TRAV_LANE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_pq<TRAV_LANE>, 256, 0); break;
-            case TRAV_WIDE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_pq<TRAV_WIDE>, 256, 0); break;
-            default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gbuffer_initial_pq<TRAV_LOCKSTEP>, 256, 0); break;
-        }
-        if (e != hipSuccess || n <= 0) n = RS_INITIAL_WAVES;
-    }
-    return n;
-}
-static bool want_persist(rs_context* c, dim3 grid) {
-    if (c->persist_mode == RS_SPLIT_OFF) return false;
-    if (c->persist_mode == RS_SPLIT_ON) return true;
-    return grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_wgs(c);
-}
 // the sorted initial pass by persistent waves (RESTIR_PERSIST_SORTED).  AUTO (default): with frames in flight
 // (run-ahead > 0) and more than one round of the one-launch kernel's waves, kPersistSortedWgs resident workgroups
 // per CU -- fewer than the kernel's occupancy, so the other frames' temporal and spatial passes run beside it.
@@ -1616,21 +1531,31 @@ static bool want_persist_sorted(rs_context* c, dim3 grid) {
     return c->ahead > 0 && full && !c->track_rows && !c->tune_rows &&
            grid_waves(grid) > (size_t)c->cus * 4 * (size_t)persist_sorted_wgs(c);
 }
-// the candidate-split spatial pass (rs_passes.h k_spatial_split): CONSTANT MIS, k <= 8, and (AUTO) a lockstep launch
-// of less than one round of the device's resident waves -- a rank's band (per-lane walks keep the sorted pass)
-static bool want_spatial_split(const rs_context* c, const rs_frame_params* P, int y0, int y1) {
-    if (c->spatial_split == RS_SPLIT_OFF || P->spatial_mis != MIS_CONSTANT || P->spatial_neighbors + 1 > kSpatialSortMax) return false;
-    if (c->spatial_split == RS_SPLIT_ON) return true;
-    return c->trav == TRAV_LOCKSTEP && grid_waves(grid_rows(c->W, y0, y1)) < (size_t)c->wave_slots;
+// the sorted initial pass's hand-off buffers of lane k (FrameConst::cand_w, cand_ray: kSortChunk x 64 candidates per
+// wave slot, 20 B each) for `slots` wave slots, grown on demand; false (nothing allocated) when the device is out of
+// memory.  Sized by the launch, not the frame: the persistent launch's resident waves (C3 1080p: 3 workgroups x 4
+// waves x 256 CUs x 20 KB = 63 MB per lane), a one-launch band its own tiles.
+static bool ensure_handoff(rs_context* c, int k, size_t slots) {
+    if (slots <= c->cand_slots[k]) return true;
+    sync_all(c);                                   // frames in flight on the lane may still read the old buffers
+    if (c->candw[k]) hipFree(c->candw[k]);
+    if (c->candr[k]) hipFree(c->candr[k]);
+    c->candw[k] = nullptr; c->candr[k] = nullptr; c->cand_slots[k] = 0;
+    const size_t n = slots * (size_t)(kSortChunk * 64);
+    if (hipMalloc(&c->candw[k], n * sizeof(float)) != hipSuccess || hipMalloc(&c->candr[k], n * sizeof(float4)) != hipSuccess) {
+        (void)hipGetLastError();
+        if (c->candw[k]) hipFree(c->candw[k]);
+        c->candw[k] = nullptr; c->candr[k] = nullptr;
+        return false;
+    }
+    c->cand_slots[k] = slots;
+    return true;
 }
 static bool reserve_count_slots(rs_context* c, int k, const rs_frame_params* P, int gy0, int gy1, int y0, int y1,
                                 size_t extra = 0) {
-    const size_t spatial = want_spatial_split(c, P, y0, y1) ? grid_waves(grid_split(c->W, y0, y1), kSpatialSplit)
-                                                           : grid_waves(grid_rows(c->W, y0, y1));
+    const size_t spatial = grid_waves(grid_rows(c->W, y0, y1));
     size_t need = (c->split ? grid_waves(grid_split(c->W, gy0, gy1), kSplit) : grid_waves(grid_rows(c->W, gy0, gy1))) +
                   grid_waves(grid_rows(c->W, y0, y1)) * 4 + spatial * (size_t)std::max(0, P->spatial_passes) + extra;
-    if (c->queue)
-        need += grid_waves(grid_q_trace(c, grid_waves(grid_rows(c->W, gy0, gy1)))) + grid_waves(grid_rows(c->W, y0, y1));
     return use_parts(c, k, need);
 }
 
@@ -1722,20 +1647,28 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
     c->shade_fused = !P->do_visibility_pass && !temporal && !spatial;
     c->temporal_ran = c->spatial_ran = c->ev_temporal = false;
     const DevScene S = s->dev();
-    c->queue = want_queue(c, P, F.gy0, F.gy1);
     // A band's G-buffer margin (the rows of the spatial halo beyond it) needs the G-buffer only.  Its rows get their
     // own small launch, so the initial pass's 8-row tiles start at the band's first row: otherwise the top and
     // bottom tile rows mix margin rows -- whose lanes idle through the whole candidate loop -- with band rows
     // (C2's 1/8 band: 145 G rows in 19 tile rows for 135 RIS rows, 11 % of the pass's waves idle).  Full frames
     // have no margin.
-    const bool margins = c->sep_margin && !c->queue && (F.gy0 < F.y0 || F.gy1 > F.y1);
+    const bool margins = c->sep_margin && (F.gy0 < F.y0 || F.gy1 > F.y1);
     FrameConst Fi = F;                          // the rows of the initial pass's launch
     if (margins) { Fi.gy0 = F.y0; Fi.gy1 = F.y1; }
     const size_t margin_waves = margins ? grid_waves(grid_rows(c->W, F.gy0, F.y0)) + grid_waves(grid_rows(c->W, F.y1, F.gy1)) : 0;
     c->split = want_split(c, P, Fi.gy0, Fi.gy1);
-    if (c->queue) {
-        const size_t nw = grid_waves(grid_rows(c->W, F.gy0, F.gy1));
-        if (int rc = ensure_queue(c, c->li, nw, (size_t)(F.gy1 - F.gy0) * c->W, P->m_area, P->m_brdf)) return rc;
+    // the initial pass's kernel, chosen (and its hand-off buffers grown) before anything of the frame is enqueued:
+    // 0 one thread per pixel, 1 wave-sorted (one launch), 2 wave-sorted by persistent waves
+    const dim3 gg = grid_rows(c->W, Fi.gy0, Fi.gy1), gb = grid_rows(c->W, F.y0, F.y1);
+    int init_kind = 0;
+    dim3 gp(1);
+    if (!c->split && want_sorted(c, P, s)) {
+        init_kind = want_persist_sorted(c, gg) ? 2 : 1;
+        if (init_kind == 2)
+            gp = dim3((unsigned)std::min<size_t>((size_t)gg.x * gg.y, (size_t)c->cus * (size_t)persist_sorted_grid_wgs(c)));
+        // one slot per resident wave of the persistent launch (reused tile after tile), else per 8x8 tile of the launch
+        const size_t slots = init_kind == 2 ? (size_t)gp.x * 4 : (size_t)gg.x * gg.y * 4;
+        if (!ensure_handoff(c, c->li, slots)) init_kind = 0;   // out of memory: the one-thread-per-pixel pass (same bits)
     }
     if (!reserve_count_slots(c, c->li, P, Fi.gy0, Fi.gy1, F.y0, F.y1, margin_waves))
         return fail(c, RS_E_HIP, "hipMalloc(count slots) failed");
@@ -1769,46 +1702,26 @@ extern "C" int rs_tile_begin(rs_context* c, const rs_scene* s, const rs_camera* 
             HIPCHK(c, hipGetLastError());
         }
     }
-    const dim3 gg = grid_rows(c->W, Fi.gy0, Fi.gy1), gb = grid_rows(c->W, F.y0, F.y1);
     if (c->split) {
         const dim3 gs = grid_split(c->W, Fi.gy0, Fi.gy1);
         LAUNCH_TRAV_BS_SH(c, k_gbuffer_initial_split, gs, 64 * kSplit, split_lds_bytes(P->m_area + P->m_brdf, P->m_brdf),
                           S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
                     c->shade_fused ? 1 : 0, count_slot(c, gs, kSplit));
-    } else if (c->queue) {
-        const QBuf& Q = c->qb[c->li];
-        LAUNCH_TRAV(c, k_q_generate, gg, S, F, c->G[gnew], Q, count_slot(c, gg));
-        HIPCHK(c, hipGetLastError());
-        const size_t n_seg = grid_waves(gg);
-        const dim3 gt = grid_q_trace(c, n_seg);
-        k_q_trace<<<gt, 256, 0, c->fs>>>(S, F, c->G[gnew], Q, (uint32_t)n_seg, count_slot(c, gt));
-        HIPCHK(c, hipGetLastError());
-        k_q_resolve<<<gb, 256, 0, c->fs>>>(S, F, c->G[gnew], Q, ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
-                                           count_slot(c, gb));
-    } else if (want_sorted(c, P, s)) {
-        if (RS_SORT_STORE_W && !c->candw[c->li])      // first sorted frame on this lane: the full frame's tiles
-            HIPCHK(c, hipMalloc(&c->candw[c->li], sort_scratch_floats(c->W, c->H) * sizeof(float)));
+    } else if (init_kind > 0) {
         Fi.cand_w = c->candw[c->li];
-        if (RS_SORT_STORE_RAY && !c->candr[c->li])
-            HIPCHK(c, hipMalloc(&c->candr[c->li], sort_scratch_floats(c->W, c->H) * sizeof(float4)));
         Fi.cand_ray = c->candr[c->li];
-        if (want_persist_sorted(c, gg)) {
-            // persistent waves, each pulling 8x8 tiles (rs_passes.h k_gbuffer_initial_sorted_pq)
+        if (init_kind == 2) {
+            // persistent waves, each pulling 8x8 tiles (rs_passes.h k_gbuffer_initial_sorted_pq); the queue's counters
+            // from zero on the frame's stream (the last exiting wave also re-arms them, but an aborted launch would
+            // leave every later one pulling past the end)
             const uint32_t nt = gg.x * gg.y * 4u;
-            const dim3 gp((unsigned)std::min<size_t>((nt + 3) / 4, (size_t)c->cus * (size_t)persist_sorted_grid_wgs(c)));
+            HIPCHK(c, hipMemsetAsync(c->qctr[c->li], 0, 4 * sizeof(uint32_t), c->fs));
             LAUNCH_TRAV(c, k_gbuffer_initial_sorted_pq, gp, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb,
                         c->shade_fused ? 1 : 0, count_slot(c, gp), TileQ{c->qctr[c->li], nt});
         } else {
             LAUNCH_TRAV(c, k_gbuffer_initial_sorted, gg, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                         count_slot(c, gg));
         }
-    } else if (want_persist(c, gg)) {
-        // persistent waves pulling 8x8 tiles (rs_passes.h k_gbuffer_initial_pq): about one device's worth of
-        // resident workgroups, never more than the tiles need
-        const uint32_t nt = gg.x * gg.y * 4u;
-        const dim3 gp((unsigned)std::min<size_t>((nt + 3) / 4, (size_t)c->cus * (size_t)persist_wgs(c)));
-        LAUNCH_TRAV(c, k_gbuffer_initial_pq, gp, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
-                    count_slot(c, gp), TileQ{c->qctr[c->li], nt});
     } else {
         LAUNCH_TRAV(c, k_gbuffer_initial, gg, S, Fi, c->G[gnew], ResBuf{c->R[c->ra]}, c->fb, c->shade_fused ? 1 : 0,
                     count_slot(c, gg));
@@ -1922,17 +1835,7 @@ extern "C" int rs_tile_spatial(rs_context* c, int pass_index) {
     // reprojection, so with the visibility pass only passes >= 1 know it
     c->F.canon_vis = (!c->P.do_visibility_pass || pass_index > 0) ? 1 : 0;
     const dim3 gb = grid_rows(c->W, c->F.y0, c->F.y1);
-    if (want_spatial_split(c, &c->P, c->F.y0, c->F.y1)) {
-        const dim3 gs = grid_split(c->W, c->F.y0, c->F.y1);
-        const bool tev = c->tuning && c->tune_n + 2 <= (int)(sizeof(c->tune_ev) / sizeof(c->tune_ev[0]));
-        if (tev) HIPCHK(c, hipEventRecord(c->tune_ev[c->tune_n], c->fs));
-        LAUNCH_TRAV_BS(c, k_spatial_split, gs, 64 * kSpatialSplit, S, c->F, c->G[c->gcur], ResBuf{c->R[c->rcur]},
-                       ResBuf{c->R[dst]}, pass_index, fuse, c->fb, count_slot(c, gs, kSpatialSplit));
-        if (tev) {
-            HIPCHK(c, hipEventRecord(c->tune_ev[c->tune_n + 1], c->fs));
-            c->tune_n += 2;
-        }
-    } else {
+    {
         const CountSlot cs = count_slot(c, gb);
         const GBuf& G = c->G[c->gcur];
         const ResBuf Rr{c->R[c->rcur]}, Rw{c->R[dst]};
@@ -2402,21 +2305,11 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
     const bool act = i0 < n;
     const uint32_t i = act ? i0 : n - 1;
     vec3 O = mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), D = mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    if (any >= 6 && any <= 12 && S.n_wnodes == 0u) {   // the 8-wide modes need the scene's wide tree
+    if (any >= 6 && any <= 10 && S.n_wnodes == 0u) {   // the 8-wide modes need the scene's wide tree
         if (act) { prim_out[i] = -1; t_out[i] = -1.0f; }
         return;
     }
-    if (any == 11 || any == 12) {   // the wave-coherent walks over the 8-wide tree (rs_scene.h RS_WLOCK): 11 closest, 12 any
-        if (any == 11) {
-            const Hit h = closest_wlock(S, act, O, D, tn[i], tf[i]);
-            if (act) { prim_out[i] = h.prim; t_out[i] = h.prim >= 0 ? h.t : -1.0f; }
-        } else {
-            bool oc;
-            const float tni = tn[i], tfi = tf[i];
-            occluded_wlock_multi<1>(S, &act, O, &D, tni, &tfi, &oc);
-            if (act) { prim_out[i] = oc ? 1 : 0; t_out[i] = 0.0f; }
-        }
-    } else if (any >= 8 && any <= 10) {  // timing probes of the 8-wide walk: 8 closest walk with the ray's tfar,
+    if (any >= 8 && any <= 10) {  // timing probes of the 8-wide walk: 8 closest walk with the ray's tfar,
         const vec3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);   // 9 any-hit without triangle tests,
         Hit h; h.t = tf[i]; h.u = h.v = 0.0f; h.prim = -1;        // 10 any-hit with statistics off
         uint32_t occ = 0u, lost = 0u;

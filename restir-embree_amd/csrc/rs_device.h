@@ -2,13 +2,14 @@
 //
 // Every function states the reference code it follows (pg/ = template/src/pg/pg1_embree/).  The
 // arithmetic keeps glm 0.9.9's operation order (the reference's maths library) and the file is
-// compiled with -ffp-contract=off so results match the CPU restatement to the last bit wherever the
-// math library is not involved (sqrt and division are correctly rounded on both sides;
-// sin/cos/pow/exp/lgamma differ by <= 2 ulp between glibc and ROCm's ocml).
+// compiled with -ffp-contract=off so results match the CPU restatement to the last bit (sqrt and division are
+// correctly rounded on both sides; sin/cos/pow/exp/lgamma and the double log/exp/log1p/lgamma of the incomplete
+// beta are rs_libm.h's fixed operation sequences, shared with the oracle, instead of ocml / glibc).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <float.h>
+#include "rs_libm.h"
 
 namespace rs {
 
@@ -54,21 +55,8 @@ __device__ __forceinline__ float4 f4(vec3 v, float w) { return make_float4(v.x, 
 // ---------------------------------------------------------------- counter RNG
 // Replaces Utils::getRandomValue's shared mt19937 (pg/utils.cpp:175-176,199-202): one independent
 // stream per (seed, frame, pass, full-frame pixel), consumed in the reference's per-pixel order.
-#ifndef RS_DIAG_CHEAP_RNG
-#define RS_DIAG_CHEAP_RNG 0    // timing diagnostic only (scripts/gpu_r05_an.sh): a multiply-free hash; breaks parity
-#endif
-__device__ __forceinline__ uint32_t hash32(uint32_t x) {
-#if RS_DIAG_CHEAP_RNG == 2
-    // two full-rate 24-bit multiplies (v_mul_u32_u24), the top bits folded down before each (scripts/rng_quality.py
-    // "hash24": avalanche bias as lowbias32's); timing study only -- the oracle keeps lowbias32
-    x ^= x >> 16; x = __umul24(x, 0x7feb35u) ^ (x >> 24);
-    x ^= x >> 15; x = __umul24(x, 0x846ca7u) ^ (x >> 24);
-    x ^= x >> 16; return x;
-#elif RS_DIAG_CHEAP_RNG
-    x ^= x << 13; x ^= x >> 17; x ^= x << 5; x ^= x >> 16; return x;
-#else
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {   // lowbias32
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16; return x;
-#endif
 }
 struct Rng {
     uint32_t key, n;
@@ -115,11 +103,11 @@ __device__ inline double betacf(double a, double b, double x) {
 }
 __device__ inline double ibeta_d(double x, double a, double b) {
     if (!(x > 0.0)) return 0.0;
-    double lbeta = lgamma(a) + lgamma(b) - lgamma(a + b);
-    if (x >= 1.0) return exp(lbeta);
-    double lbt = a * log(x) + b * log1p(-x);
-    if (x < (a + 1.0) / (a + b + 2.0)) return exp(lbt) * betacf(a, b, x) / a;
-    return exp(lbeta) - exp(lbt) * betacf(b, a, 1.0 - x) / b;
+    double lbeta = rs_lgamma_d(a) + rs_lgamma_d(b) - rs_lgamma_d(a + b);
+    if (x >= 1.0) return rs_exp_d(lbeta);
+    double lbt = a * rs_log_d(x) + b * rs_log1p_d(-x);
+    if (x < (a + 1.0) / (a + b + 2.0)) return rs_exp_d(lbt) * betacf(a, b, x) / a;
+    return rs_exp_d(lbeta) - rs_exp_d(lbt) * betacf(b, a, 1.0 - x) / b;
 }
 // MaterialPhong::calc_I_M (pg/MaterialPhong.cpp:224-244); gamma_quot in float as in the reference.
 __device__ inline float calc_I_M(float nDotV, float n) {
@@ -129,8 +117,8 @@ __device__ inline float calc_I_M(float nDotV, float n) {
     float negterm = costerm;
     sinterm_sq = gmin(gmax(sinterm_sq, 0.0f), 1.0f);
     if (n >= 1e-18f) negterm *= halfn * (float)ibeta_d((double)sinterm_sq, (double)halfn, 0.5);
-    float gq = expf(lgammaf(halfn + 0.5f) - lgammaf(halfn + 1.0f));
-    return (kTwoPi * costerm + kRootPi * gq * (powf(sinterm_sq, halfn) - negterm)) / (n + 2.0f);
+    float gq = rs_expf(rs_lgammaf(halfn + 0.5f) - rs_lgammaf(halfn + 1.0f));
+    return (kTwoPi * costerm + kRootPi * gq * (rs_powf(sinterm_sq, halfn) - negterm)) / (n + 2.0f);
 }
 
 // ---------------------------------------------------------------- G-buffer element
@@ -242,7 +230,7 @@ __device__ __forceinline__ bool is_phong(int type) { return type == MT_PHONG || 
 // [0, 1]), so the powf is skipped for them -- the MIS pdf of every area candidate on a diffuse wall
 __device__ __forceinline__ float phong_pdf(const ShadeFrame& s, vec3 wi) {
     float pdf = gmax(dot(s.nrm, wi), 0.0f) * kOneOverPi * s.pf;
-    pdf += (s.omp != 0.0f || !isfinite(s.a)) ? s.a * powf(gmax(0.0f, dot(wi, s.wr)), s.shin) * s.omp : 0.0f;
+    pdf += (s.omp != 0.0f || !isfinite(s.a)) ? s.a * rs_powf(gmax(0.0f, dot(wi, s.wr)), s.shin) * s.omp : 0.0f;
     return pdf;
 }
 // BRDF eval dispatch (pg/ReSTIRIntegrator.h:32-41): Phong for PHONG/DIELECTRIC
@@ -250,7 +238,7 @@ __device__ __forceinline__ float phong_pdf(const ShadeFrame& s, vec3 wi) {
 __device__ __forceinline__ vec3 eval_brdf(const ShadeFrame& s, vec3 wi) {
     vec3 f = s.kd_pi;
     if (!is_phong(s.type)) return f;
-    float pw = powf(gmax(dot(wi, s.wr), 0.0f), s.shin);
+    float pw = rs_powf(gmax(dot(wi, s.wr), 0.0f), s.shin);
     return f + s.ks_im * pw;
 }
 __device__ __forceinline__ float phong_pdf(const GElem& g, vec3 cam, vec3 wi) { return phong_pdf(make_frame(g, cam), wi); }
@@ -270,16 +258,20 @@ __device__ __forceinline__ vec3 cosine_sample(vec3 n, Rng& rng) {
     float r1 = rng.range(0, 1), r2 = rng.range(0, 1);
     float ang = kPi * 2.0f * r1;
     float sq = sqrtf(1.0f - r2);
-    float x = cosf(ang) * sq, y = sinf(ang) * sq, z = sqrtf(r2);
+    float sn, cs;
+    rs_sincosf(ang, &sn, &cs);
+    float x = cs * sq, y = sn * sq, z = sqrtf(r2);
     return to_world(normalize(mk(x, y, z)), n);
 }
 // CosineLobeDistribution::sample (pg/Distribution.h:37-57)
 __device__ __forceinline__ vec3 lobe_sample(vec3 wr, float gamma, Rng& rng) {
     float r1 = rng.range(0, 1), r2 = rng.range(0, 1);
     float ang = 2.0f * kPi * r1;
-    float sq = sqrtf(1.0f - powf(r2, 2.0f / (gamma + 1.0f)));
-    float x = cosf(ang) * sq, y = sinf(ang) * sq;
-    float z = powf(r2, 1.0f / (gamma + 1.0f));
+    float sq = sqrtf(1.0f - rs_powf(r2, 2.0f / (gamma + 1.0f)));
+    float sn, cs;
+    rs_sincosf(ang, &sn, &cs);
+    float x = cs * sq, y = sn * sq;
+    float z = rs_powf(r2, 1.0f / (gamma + 1.0f));
     return to_world(normalize(mk(x, y, z)), wr);
 }
 // BRDF sampling dispatch (pg/ReSTIRIntegrator.h:43-52): Lambert (pg/MaterialLambert.cpp:43-53) or
@@ -293,7 +285,7 @@ __device__ __forceinline__ vec3 sample_brdf(const ShadeFrame& s, Rng& rng, float
     float r0 = rng.range(0.0f, s.maxD + s.maxS);
     vec3 wi = (r0 < s.maxD) ? cosine_sample(s.nrm, rng) : lobe_sample(s.wr, s.shin, rng);
     float pd = gmax(dot(s.nrm, wi), 0.0f) * kOneOverPi * s.pf;
-    float ps = s.a * powf(gmax(0.0f, dot(wi, s.wr)), s.shin) * s.omp;
+    float ps = s.a * rs_powf(gmax(0.0f, dot(wi, s.wr)), s.shin) * s.omp;
     pdf = pd + ps;
     return wi;
 }

@@ -99,32 +99,52 @@ struct rs_mgpu {
     }
 
     // ---- transfer statistics (rs_mgpu_get_stats): per frame, HIP events around each halo exchange and
-    // the gather on rank 0's (local: local rank 0's) frame stream, folded when the ring slot is reused
-    static constexpr int kStatRing = 8, kTimedPasses = 4;
-    hipEvent_t sev[kStatRing][2 * kTimedPasses + 2] = {};
+    // the gather on every local rank's frame stream, folded when the ring slot is reused.  stats.halo_ms /
+    // gather_ms are local rank 0's (the ABI's figures); halo_ms_rank / gather_ms_rank hold every local
+    // rank's, so measure_bands can take each rank's own exchange time out of its band time.
+    static constexpr int kStatRing = 8, kTimedPasses = 4, kEvPerRank = 2 * kTimedPasses + 2;
+    std::vector<hipEvent_t> sev[kStatRing];     // [local rank * kEvPerRank + event]
     int s_nx[kStatRing] = {};                   // exchanges recorded in the slot
     bool s_gather[kStatRing] = {}, s_pending[kStatRing] = {};
     int s_slot = 0;
     size_t halo_bytes = 0;                      // per halo slot of the frame in progress
     rs_mgpu_stats stats{};
+    std::vector<double> halo_ms_rank, gather_ms_rank;
+    hipEvent_t& ev(int slot, size_t i, int e) { return sev[slot][i * kEvPerRank + e]; }
+    static double span(hipEvent_t a, hipEvent_t b) {
+        float ms = 0.0f;
+        if (hipEventSynchronize(b) == hipSuccess && hipEventElapsedTime(&ms, a, b) == hipSuccess) return ms;
+        return 0.0;
+    }
     void fold(int k) {
         if (!s_pending[k]) return;
         s_pending[k] = false;
-        float ms = 0.0f;
-        for (int x = 0; x < s_nx[k]; ++x)
-            if (hipEventSynchronize(sev[k][2 * x + 1]) == hipSuccess && hipEventElapsedTime(&ms, sev[k][2 * x], sev[k][2 * x + 1]) == hipSuccess)
-                stats.halo_ms += ms;
-        if (s_gather[k] && hipEventSynchronize(sev[k][2 * kTimedPasses + 1]) == hipSuccess &&
-            hipEventElapsedTime(&ms, sev[k][2 * kTimedPasses], sev[k][2 * kTimedPasses + 1]) == hipSuccess)
-            stats.gather_ms += ms;
+        for (size_t i = 0; i < ranks.size(); ++i) {
+            double h = 0.0, g = 0.0;
+            for (int x = 0; x < s_nx[k]; ++x) h += span(ev(k, i, 2 * x), ev(k, i, 2 * x + 1));
+            if (s_gather[k]) g = span(ev(k, i, 2 * kTimedPasses), ev(k, i, 2 * kTimedPasses + 1));
+            halo_ms_rank[i] += h; gather_ms_rank[i] += g;
+            if (i == 0) { stats.halo_ms += h; stats.gather_ms += g; }
+        }
     }
     int begin_frame_stats() {
         s_slot = (s_slot + 1) % kStatRing;
         fold(s_slot);
-        if (!sev[s_slot][0])
-            for (auto& e : sev[s_slot]) HIPCHK_M(this, hipEventCreate(&e));
+        if (halo_ms_rank.size() != ranks.size()) { halo_ms_rank.assign(ranks.size(), 0.0); gather_ms_rank.assign(ranks.size(), 0.0); }
+        if (sev[s_slot].empty()) {
+            sev[s_slot].assign(ranks.size() * kEvPerRank, nullptr);
+            for (size_t i = 0; i < ranks.size(); ++i) {     // each rank's events on its context's device
+                HIPCHK_M(this, hipSetDevice(ctx_device(ranks[i].ctx)));
+                for (int e = 0; e < kEvPerRank; ++e) HIPCHK_M(this, hipEventCreate(&ev(s_slot, i, e)));
+            }
+            HIPCHK_M(this, hipSetDevice(ctx_device(ranks[0].ctx)));
+        }
         s_nx[s_slot] = 0; s_gather[s_slot] = false; s_pending[s_slot] = true;
         stats.frames++;
+        return 0;
+    }
+    int record_all(std::vector<GpuRank*>& rk, int e) {
+        for (size_t i = 0; i < rk.size(); ++i) HIPCHK_M(this, hipEventRecord(ev(s_slot, i, e), rk[i]->st));
         return 0;
     }
 
@@ -174,7 +194,8 @@ struct rs_mgpu {
     int exchange_halo(std::vector<GpuRank*>& rk, int pass) {
         if (world == 1) return 0;
         const bool timed = pass < kTimedPasses;
-        if (timed) HIPCHK_M(this, hipEventRecord(sev[s_slot][2 * pass], rk[0]->st));
+        if (timed)
+            if (int rc = record_all(rk, 2 * pass)) return rc;
         std::vector<std::vector<mgpu::Xfer>> plans;
         for (size_t i = 0; i < rk.size(); ++i) {
             plans.push_back(mgpu::halo_plan(rank_ids[i], world, halo_bytes));
@@ -191,7 +212,7 @@ struct rs_mgpu {
             return rc;
         }
         if (timed) {
-            HIPCHK_M(this, hipEventRecord(sev[s_slot][2 * pass + 1], rk[0]->st));
+            if (int rc = record_all(rk, 2 * pass + 1)) return rc;
             s_nx[s_slot] = pass + 1;
         }
         return 0;
@@ -203,7 +224,7 @@ struct rs_mgpu {
     // transfer that reads (senders) or writes (rank 0) this lane's framebuffer.
     int gather(std::vector<GpuRank*>& rk) {
         if (world == 1) return 0;
-        HIPCHK_M(this, hipEventRecord(sev[s_slot][2 * kTimedPasses], rk[0]->st));
+        if (int rc = record_all(rk, 2 * kTimedPasses)) return rc;
         const size_t row = (size_t)W * 3 * sizeof(float);
         std::vector<std::vector<mgpu::Xfer>> plans;
         for (size_t i = 0; i < rk.size(); ++i) {
@@ -219,7 +240,7 @@ struct rs_mgpu {
         } else if (int rc = local_exchange(rk, plans)) {
             return rc;
         }
-        HIPCHK_M(this, hipEventRecord(sev[s_slot][2 * kTimedPasses + 1], rk[0]->st));
+        if (int rc = record_all(rk, 2 * kTimedPasses + 1)) return rc;
         s_gather[s_slot] = true;
         for (auto* g : rk)
             if (int rc = ctx_join(g->ctx, g->st)) return rc;
@@ -412,31 +433,37 @@ extern "C" int rs_mgpu_set_rebalance_refine(rs_mgpu* m, int rounds) {
 // Each rank's own time per frame with `bounds`: `warm` unmeasured frames (the history after a boundary move,
 // lazily grown buffers), then `n` frames with the gather.  A rank's time is its frames' begin..shade span
 // (rs_pass_times.total_ms, event ring, frames in flight as in production) minus the halo exchanges on its
-// stream (which include waiting for slower neighbours), plus -- on rank 0 -- the gather it receives.
+// own stream (which include waiting for slower neighbours), plus -- on global rank 0 -- the gather it
+// receives.  Every local rank has its own exchange spans (rs_mgpu::halo_ms_rank), so no local rank looks
+// cheaper than another.  The caller's timing totals and transfer statistics are read as deltas, not reset.
 // All-reduced, so every rank sees the same vector and makes the same choice.
 static int measure_bands(rs_mgpu* m, const rs_scene* const* scenes, const rs_camera* cam, const rs_frame_params* P,
                          uint32_t& frame, int warm, int n, std::vector<double>& t) {
     if (int rc = rs_mgpu_reset_history(m)) return rc;   // the previous G-buffer rows of a moved band
     for (int f = 0; f < warm; ++f)
         if (int rc = rs_mgpu_render_frame(m, scenes, cam, P, frame++, 1, nullptr, nullptr)) return rc;
-    rs_pass_times sum{};
-    uint32_t nf = 0;
+    const size_t nl = m->ranks.size();
+    std::vector<double> ms0(nl), halo0, gather0;
+    std::vector<uint32_t> nf0(nl);
     rs_mgpu_stats st{};
-    for (auto& g : m->ranks)
-        if (int rc = rs_get_timing_totals(g.ctx, &sum, &nf, 1)) return rc;
-    if (int rc = rs_mgpu_get_stats(m, &st, 1)) return rc;
+    if (int rc = rs_mgpu_get_stats(m, &st, 0)) return rc;   // folds every finished frame's spans
+    halo0 = m->halo_ms_rank; gather0 = m->gather_ms_rank;
+    for (size_t i = 0; i < nl; ++i) {
+        rs_pass_times sum{};
+        if (int rc = rs_get_timing_totals(m->ranks[i].ctx, &sum, &nf0[i], 0)) return rc;
+        ms0[i] = sum.total_ms;
+    }
     for (int f = 0; f < n; ++f)
         if (int rc = rs_mgpu_render_frame(m, scenes, cam, P, frame++, 1, nullptr, nullptr)) return rc;
-    if (int rc = rs_mgpu_get_stats(m, &st, 1)) return rc;
+    if (int rc = rs_mgpu_get_stats(m, &st, 0)) return rc;
     t.assign(m->world, 0.0);
-    for (size_t i = 0; i < m->ranks.size(); ++i) {
-        if (int rc = rs_get_timing_totals(m->ranks[i].ctx, &sum, &nf, 1)) return rc;
-        double v = sum.total_ms;
-        if (i == 0) {                           // the transfer spans are recorded on the first local rank's stream
-            v -= st.halo_ms;
-            if (m->rank_ids[0] == 0) v += st.gather_ms;
-        }
-        t[m->rank_ids[i]] = std::max(0.0, v) / std::max<uint32_t>(1, nf);
+    for (size_t i = 0; i < nl; ++i) {
+        rs_pass_times sum{};
+        uint32_t nf = 0;
+        if (int rc = rs_get_timing_totals(m->ranks[i].ctx, &sum, &nf, 0)) return rc;
+        double v = (sum.total_ms - ms0[i]) - (m->halo_ms_rank[i] - halo0[i]);
+        if (m->rank_ids[i] == 0) v += m->gather_ms_rank[i] - gather0[i];
+        t[m->rank_ids[i]] = std::max(0.0, v) / std::max<uint32_t>(1, nf - nf0[i]);
     }
     return m->allreduce(t.data(), m->world, 0);
 }

@@ -29,7 +29,7 @@ __device__ __forceinline__ float mis_power(float pdf, float other) {
 __device__ __forceinline__ vec3 dvs(vec3 v, float s) { return mk(v.x / s, v.y / s, v.z / s); }   // glm vec3 / scalar
 __device__ __forceinline__ float cos_pdf(vec3 n, vec3 wi) { return gmax(dot(n, wi), 0.0f) * kOneOverPi; }
 __device__ __forceinline__ float lobe_pdf(vec3 wi, vec3 wr, float g) {      // pg/Distribution.h:65-67
-    return (g + 1.0f) * kOneOver2Pi * powf(gmax(0.0f, dot(wi, wr)), g);
+    return (g + 1.0f) * kOneOver2Pi * rs_powf(gmax(0.0f, dot(wi, wr)), g);
 }
 // getPdfForSample (pg/MaterialLambert.cpp:20-23, pg/MaterialPhong.cpp:94-119)
 __device__ __forceinline__ float mis_pdf_for(const MisSurf& h, vec3 wi) {
@@ -42,7 +42,7 @@ __device__ __forceinline__ float mis_pdf_for(const MisSurf& h, vec3 wi) {
 __device__ __forceinline__ vec3 mis_brdf(const MisSurf& h, vec3 wi) {
     vec3 f = h.kd * kOneOverPi;
     if (!h.phong) return f;
-    return f + (h.ks * h.i_m) * powf(gmax(dot(wi, h.wr), 0.0f), h.shin);
+    return f + (h.ks * h.i_m) * rs_powf(gmax(dot(wi, h.wr), 0.0f), h.shin);
 }
 // evaluateLightingGI (pg/MaterialLambert.cpp:10-18, pg/MaterialPhong.cpp:18-67)
 __device__ __forceinline__ vec3 mis_sample(const MisSurf& h, Rng& rng, vec3& f_r, float& pdf) {
@@ -59,7 +59,7 @@ __device__ __forceinline__ vec3 mis_sample(const MisSurf& h, Rng& rng, vec3& f_r
         f_r = h.kd * kOneOverPi;
     } else {
         wi = lobe_sample(h.wr, h.shin, rng);
-        f_r = (h.ks * h.i_m) * powf(gmax(dot(wi, h.wr), 0.0f), h.shin);
+        f_r = (h.ks * h.i_m) * rs_powf(gmax(dot(wi, h.wr), 0.0f), h.shin);
     }
     float pd = cos_pdf(h.n, wi) * h.pf;
     float ps = lobe_pdf(wi, h.wr, h.shin) * (1.0f - h.pf);

@@ -16,6 +16,7 @@
 // Triangles keep file order.
 #include "../../include/restir_c.h"
 #include "rs_image.h"
+#include "rs_libm.h"
 
 #include <cmath>
 #include <cstdio>
@@ -34,7 +35,7 @@ static float srgb_expand(float u) {
     if (u <= 0.0f) return 0.0f;
     if (u >= 1.0f) return 1.0f;
     if (u <= 0.04045f) return u / 12.92f;
-    return powf((u + 0.055f) / 1.055f, 2.4f);
+    return rs_powf((u + 0.055f) / 1.055f, 2.4f);
 }
 
 struct MtlTex { std::string dir; std::map<std::string, int> ids; std::vector<std::string> files; };

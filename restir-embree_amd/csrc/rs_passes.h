@@ -621,10 +621,6 @@ __device__ __forceinline__ void count_store(CountSlot C, uint32_t rays, uint32_t
         C.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)] = make_uint2(r, p);
 }
 
-#ifndef RS_PERSIST
-#define RS_PERSIST 0           // 1: full-frame initial passes launch persistent waves (restir_capi.hip want_persist)
-#endif
-
 // G-buffer + initialRenderPass of one pixel (the body of k_gbuffer_initial)
 template <int T>
 __device__ __forceinline__ void gbuffer_initial_px(const DevScene& S, const FrameConst& F, const GBuf& G, const ResBuf& Rw,
@@ -655,40 +651,6 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_
     const FrameSlot fs{frame_lds, (int)threadIdx.x, 256};
     gbuffer_initial_px<T>(S, F, G, Rw, fb, fuse_shade, fs, x, y, in, rays);
     count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u, t0, y);
-}
-// the same pass by persistent waves pulling 8x8 tiles (TileQ).  RS_PERSIST_WG = 1: the workgroup pulls a whole
-// 16x16 tile (its four waves' 8x8 tiles, one atomic per workgroup and tile) -- the dispatcher's granularity and
-// L1 locality, without its workgroup launches
-#ifndef RS_PERSIST_WG
-#define RS_PERSIST_WG 1
-#endif
-__device__ __forceinline__ uint32_t q_pull_wg(const TileQ& Q, uint32_t* s_tile) {
-    __syncthreads();                                 // every wave has read the previous tile index
-    if (threadIdx.x == 0) *s_tile = atomicAdd(Q.ctr, 1u);
-    __syncthreads();
-    return 4u * *s_tile + (threadIdx.x >> 6);       // this wave's 8x8 tile of the 16x16 tile
-}
-template <int T>
-__global__ void __launch_bounds__(256, RS_WAVES(T, RS_INITIAL_WAVES, RS_INITIAL_WAVES_LANE))
-k_gbuffer_initial_pq(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int fuse_shade, CountSlot C, TileQ Q) {
-    if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) *C.outside = 0ull;
-    __shared__ float4 frame_lds[5 * 256];
-    __shared__ uint32_t s_tile;
-    const FrameSlot fs{frame_lds, (int)threadIdx.x, 256};
-    uint32_t rays = 0, prim = 0;
-    for (;;) {
-        const uint32_t t = RS_PERSIST_WG ? q_pull_wg(Q, &s_tile) : q_pull(Q);
-        if (t >= Q.n) break;
-        const uint64_t t0 = wave_clock();
-        int x, y;
-        const bool in = pixel_of_q(F, F.gy0, F.gy1, t, x, y);
-        gbuffer_initial_px<T>(S, F, G, Rw, fb, fuse_shade, fs, x, y, in, rays);
-        rays += in ? 1u : 0u;
-        prim += in ? 1u : 0u;
-        row_cost_add(C, t0, y);
-    }
-    count_store(C, rays, prim);
-    q_exit(Q);
 }
 // ---------------------------------------------------------------- wave-sorted initial pass (per-lane wide walks)
 // The per-lane walks of incoherent scenes (C3) are bound by the vector-memory data path returning a wave's
@@ -723,8 +685,10 @@ k_gbuffer_initial_pq(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb, int
 #endif
 constexpr int kSortChunk = RS_SORT_CHUNK;   // area candidates per sort round
 // Phase A's unoccluded candidate weights kept for phase C in global memory (one coalesced 256-B store and load
-// per candidate and wave, per 8x8 tile: FrameConst::cand_w) instead of phase C drawing every candidate again (its
-// light pick, the emitter record gathers, the sample, both Phong powf)
+// per candidate and wave: FrameConst::cand_w) instead of phase C drawing every candidate again (its light pick, the
+// emitter record gathers, the sample, both Phong powf).  The region is the wave's hand-off slot: its resident wave
+// slot in the persistent launch (reused tile after tile, so the few MB stay in the caches), its 8x8 tile in a
+// one-launch grid (restir_capi.hip ensure_handoff sizes both by the launch)
 #ifndef RS_SORT_STORE_W
 #define RS_SORT_STORE_W 1
 #endif
@@ -734,10 +698,6 @@ static_assert(!RS_SORT_STORE_W || kSortChunk <= 16, "ok and NaN bits of a chunk 
 #ifndef RS_SORT_STORE_RAY
 #define RS_SORT_STORE_RAY 1
 #endif
-// floats of FrameConst::cand_w for a W x rows launch (its 8x8 tiles x kSortChunk x 64)
-__host__ __device__ inline size_t sort_scratch_floats(int W, int rows) {
-    return (size_t)(2 * ((W + 15) / 16)) * (size_t)(2 * ((rows + 15) / 16)) * (size_t)(kSortChunk * 64);
-}
 static_assert(kSortChunk >= 1 && kSortChunk <= 32, "one occlusion word per pixel; 11-bit ranks");
 struct SortLds {                            // one wave's region (7.3 KB at 16 candidates)
     uint32_t slot[kSortChunk * 64];         // slot k * 64 + lane: light | rank in its bucket << 21
@@ -814,11 +774,11 @@ __device__ __forceinline__ void brdf_unpark(const uint32_t* sl, int lane, Res& r
     bp = v[10]; fs = mk(v[11], v[12], v[13]);
 }
 // one wave's 8x8 tile of the sorted pass: lane = pixel (x, y) (clamped; `in` whether it exists), the tile's
-// unclamped origin (tx0, ty0) for the pixel index of a ray's source lane, the wave's LDS region L
+// unclamped origin (tx0, ty0) for the pixel index of a ray's source lane, the wave's LDS region L, its hand-off slot
 template <int T>
 __device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst& F, const GBuf& G, const ResBuf& Rw,
                                             float* fb, int fuse_shade, SortLds& L, int lane, int x, int y, bool in,
-                                            int tx0, int ty0, uint32_t& rays) {
+                                            int tx0, int ty0, size_t hslot, uint32_t& rays) {
     const size_t p = (size_t)y * F.W + x;
     {
         const GElem g = gbuffer_fill<T>(S, F, x, y, in);
@@ -846,7 +806,7 @@ __device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst&
                 wave_lds_sync();
                 uint32_t needm = 0u;
                 uint32_t bkt[(kSortChunk + 3) / 4] = {};                // the needed rays' buckets, 8 bits each
-                const size_t wtile = (size_t)((ty0 - F.gy0) >> 3) * (size_t)(2 * ((F.W + 15) >> 4)) + (size_t)(tx0 >> 3);
+                const size_t wtile = hslot;
 #if RS_SORT_STORE_W
                 uint32_t flg = 0u;                                      // bit k: ok; bit 16 + k: its occluded weight is NaN
                 float* const wst = F.cand_w + wtile * (size_t)(kSortChunk * 64) + lane;
@@ -1006,8 +966,9 @@ k_gbuffer_initial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* fb,
     const bool in = pixel_of(F, F.gy0, F.gy1, x, y);
     tile_of(F, F.gy0, F.gy1, bx, by);
     const int wave = threadIdx.x >> 6;
-    sorted_tile<T>(S, F, G, Rw, fb, fuse_shade, lds[wave], threadIdx.x & 63, x, y, in, bx * 16 + (wave & 1) * 8,
-                   F.gy0 + by * 16 + (wave >> 1) * 8, rays);
+    const int tx0 = bx * 16 + (wave & 1) * 8, ty0 = F.gy0 + by * 16 + (wave >> 1) * 8;
+    const size_t hslot = (size_t)((ty0 - F.gy0) >> 3) * (size_t)(2 * ((F.W + 15) >> 4)) + (size_t)(tx0 >> 3);   // the launch's 8x8 tile
+    sorted_tile<T>(S, F, G, Rw, fb, fuse_shade, lds[wave], threadIdx.x & 63, x, y, in, tx0, ty0, hslot, rays);
     count_rays(C, rays + (in ? 1u : 0u), in ? 1u : 0u, t0, y);
 }
 // the same pass by persistent waves (RESTIR_PERSIST_SORTED): about one device's worth of resident workgroups,
@@ -1031,7 +992,8 @@ k_gbuffer_initial_sorted_pq(DevScene S, FrameConst F, GBuf G, ResBuf Rw, float* 
         const bool in = pixel_of_q(F, F.gy0, F.gy1, t, x, y);
         int tx0, ty0;
         tile_origin_q(F, F.gy0, F.gy1, t, tx0, ty0);
-        sorted_tile<T>(S, F, G, Rw, fb, fuse_shade, lds[wave], lane, x, y, in, tx0, ty0, rays);
+        sorted_tile<T>(S, F, G, Rw, fb, fuse_shade, lds[wave], lane, x, y, in, tx0, ty0,
+                       (size_t)blockIdx.x * 4 + (size_t)wave, rays);   // the resident wave's slot
         rays += in ? 1u : 0u;
         prim += in ? 1u : 0u;
         row_cost_add(C, t0, y);
@@ -1458,7 +1420,9 @@ __device__ __forceinline__ size_t neighbor_px(const FrameConst& F, const Rng& rn
     float u0 = rng.at(2u * i), u1 = rng.at(2u * i + 1u);
     float theta = (0.0f + (2.0f - 0.0f) * u0) * kPi;
     float r = sqrtf(0.0f + (F.radius - 0.0f) * u1);
-    float ox = r * cosf(theta), oy = r * sinf(theta);
+    float sn, cs;
+    rs_sincosf(theta, &sn, &cs);
+    float ox = r * cs, oy = r * sn;
     int nx = x + (int)ox, ny = y + (int)oy;
     nx = nx < 0 ? 0 : (nx > F.W - 1 ? F.W - 1 : nx);
     ny = ny < 0 ? 0 : (ny > F.H - 1 ? F.H - 1 : ny);
@@ -1805,114 +1769,6 @@ k_spatial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pas
             Rw.store(p, res);
             if (fuse_shade) store_rgb(fb, p, shade_px(res, f_sel, th.le));
         }
-    }
-    count_rays(C, rays, 0, t0, y);
-}
-
-// ---------------------------------------------------------------- candidate-split spatial pass (small launches)
-// A rank's band of a multi-GPU frame gives the spatial pass less than one round of waves (C2 1/8 band: 0.9), so the
-// launch takes as long as its slowest wave.  Here a workgroup is ONE 8x8 tile with kSpatialSplit waves: every wave
-// makes the pixel's neighbour selection itself (stateless RNG slots; the same list in every wave), traces the
-// visibility rays of its share of the list positions (i = g, g + kSpatialSplit, ...; a pixel's rays share one walk
-// two at a time, as k_spatial's) and sets the pixel's occlusion bits in LDS; wave 0 then runs k_spatial_sorted's
-// phase C -- every candidate re-evaluated with its bit, the reservoir stream in list order.  CONSTANT MIS, k <= 8.
-// The rays and the stream are k_spatial's: frames are bit-identical (tests/test_gpu_parity.py).
-#ifndef RS_SPATIAL_SPLIT
-#define RS_SPATIAL_SPLIT 3
-#endif
-constexpr int kSpatialSplit = RS_SPATIAL_SPLIT;
-template <int T>
-__global__ void __launch_bounds__(64 * kSpatialSplit, RS_WAVES(T, RS_SPATIAL_WAVES_SMALL, RS_SPATIAL_WAVES_LANE))
-k_spatial_split(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pass_idx, int fuse_shade, float* fb, CountSlot C) {
-    __shared__ uint32_t occ_lds[64];
-    const uint64_t t0 = wave_clock();
-    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-    int x = blockIdx.x * 8 + (lane & 7), y = F.y0 + blockIdx.y * 8 + (lane >> 3);
-    const bool in = x < F.W && y < F.y1;
-    x = x < F.W ? x : F.W - 1;
-    y = y < F.y1 ? y : F.y1 - 1;
-    const size_t p = (size_t)y * F.W + x;
-    uint32_t rays = 0;
-    const vec3 cam = F.cam.pos;
-    GElem th = G.load(p);
-    const bool emissive = any_pos(th.le);
-    const bool alive = in && !emissive;
-    if (g == 0) {
-        occ_lds[lane] = 0u;
-        if (in && emissive) {                              // :319-324
-            Res r = Rr.load(p);
-            Rw.store(p, r);
-            if (fuse_shade) store_rgb(fb, p, shade_px(r, mk(0, 0, 0), th.le));
-        }
-    }
-    __syncthreads();
-    Rng rng; rng.init(F.seed, F.frame, PASS_SPATIAL0 + (uint32_t)pass_idx, (uint32_t)p);
-    uint64_t acc = 0;                                      // neighbour selection (:334-374), as k_spatial
-    int M = 1;
-    if (__ballot(alive) != 0) {
-        for (int i = 0; i < F.k; ++i) {
-            size_t q = neighbor_px(F, rng, i, x, y);
-            if (any_pos(G.le(q))) continue;
-            if (F.reject) {
-                float4 nq = G.g1[q];
-                float ns = dot(xyz(nq), th.nrm);
-                if (ns < F.min_normal_sim) continue;
-                float nd = G.g0[q].w;
-                float dr = 0;
-                if (nd > 0) dr = th.depth / nd;
-                float hd = F.max_depth_diff * 0.5f;
-                if (dr < 1.0f - hd || dr > 1.0f + hd) continue;
-            }
-            acc |= 1ull << i;
-            M += 1;
-        }
-        const int cnt = M, kk = F.k + 1;
-        const ShadeFrame sf = make_frame(th, cam);
-        // this wave's list positions, two rays per walk
-        for (int i0 = g; i0 < kk; i0 += 2 * kSpatialSplit) {
-            FPre pre[2];
-            bool act[2], occ[2];
-            vec3 dir[2];
-            float tf[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int i = i0 + k * kSpatialSplit;
-                const Res rr = Rr.load(list_px(F, rng, acc, i < kk ? i : 0, x, y, p));
-                pre[k] = evaluate_f_pre(F, smp_of(rr), th.pos, false, sf, true, alive && i < cnt);
-                act[k] = pre[k].need && !(i == 0 && F.canon_vis); dir[k] = pre[k].dir; tf[k] = pre[k].tfar; occ[k] = false;
-                rays += act[k] ? 1u : 0u;
-            }
-            trace_any_multi<T, 2>(S, act, th.pos, dir, FLT_MIN + F.tnear_off, tf, occ);
-#pragma unroll
-            for (int k = 0; k < 2; ++k)
-                if (act[k] && occ[k]) atomicOr(&occ_lds[lane], 1u << (i0 + k * kSpatialSplit));
-        }
-    }
-    __syncthreads();
-    if (g != 0 || __ballot(alive) == 0) { count_rays(C, rays, 0, t0, y); return; }
-    // ---- wave 0: the reservoir stream in list order (k_spatial_sorted's phase C)
-    asm volatile("" ::: "memory");
-    th = G.load(p);
-    const ShadeFrame sf = make_frame(th, cam);
-    rng.n = 2u * (uint32_t)F.k;
-    const uint32_t occm = occ_lds[lane];
-    const int cnt = M, kk = F.k + 1;
-    const float rcpM = M > 0 ? 1.0f / (float)M : 0.0f;
-    Res res = res_empty();
-    vec3 f_sel = mk(0, 0, 0);
-    for (int i = 0; i < kk; ++i) {
-        const Res rr = Rr.load(list_px(F, rng, acc, i, x, y, p));
-        const FPre pre = evaluate_f_pre(F, smp_of(rr), th.pos, false, sf, true, alive && i < cnt);
-        const vec3 f = evaluate_f_post(pre, ((occm >> i) & 1u) != 0u);
-        const float rw = rcpM * length(f) * rr.W;
-        if (alive && i < cnt && res_add(res, smp_of(rr), rw, rr.conf, rng)) f_sel = f;
-    }
-    const float fph = smp_valid(smp_of(res)) ? length(f_sel) : 0.0f;  // :481
-    res.W = fph > 0.0f ? res.wsum / fph : 0.0f;
-    res_cap(res, F.cap);
-    if (alive) {
-        Rw.store(p, res);
-        if (fuse_shade) store_rgb(fb, p, shade_px(res, f_sel, th.le));
     }
     count_rays(C, rays, 0, t0, y);
 }

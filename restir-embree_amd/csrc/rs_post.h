@@ -28,7 +28,7 @@ __device__ __forceinline__ float post_compress(float u) {
     if (u <= 0.0f) return 0.0f;
     if (u >= 1.0f) return 1.0f;
     if ((double)u <= 0.0031308) return u * 12.92f;
-    return 1.055f * powf(u, 1.0f / 2.4f) - 0.055f;
+    return 1.055f * rs_powf(u, 1.0f / 2.4f) - 0.055f;
 }
 
 __global__ void __launch_bounds__(256) k_post(const float* __restrict__ frame, float* __restrict__ acc,

@@ -558,183 +558,12 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
     return h;
 }
 
-// ---------------------------------------------------------------- wave-coherent walks over the 8-wide tree
-// The lockstep idea of the skip-pointer walks above, on the 8-wide tree: the WAVE walks one
-// group stack -- wave-uniform (base, slot mask) pairs in SGPRs -- and every step fetches ONE wide node with
-// scalar loads (80 B, no per-lane gather); each lane tests the node's 8 child boxes against each of its rays
-// (wide_hits, the per-lane walk's conservative test), and the wave visits the union of the children any live
-// ray of any lane hit (an OR reduction across the wave).  Leaf slots of that union are tested as wave-uniform
-// triangles (scalar loads) by the rays that hit the slot.  The wave's steps are the union of its lanes' wide
-// paths: about half the binary lockstep union's dependent steps (CPU lab, C2, per candidate: 12.9 vs 27.3),
-// each with 8 child tests per ray instead of one box test.  A ray keeps no per-level entry record: it tests
-// every node the wave visits (a ray that missed a node's box misses its children's exact boxes too; only
-// their outward-rounded planes can admit it), which is conservative, so the hits are every walk's hits.
-// The group stack holds one group per level, so the build's depth bound (<= kWideStack) never overflows it.
-#ifndef RS_WLOCK
-#define RS_WLOCK 0          // bit 0: any-hit (shadow) lockstep walks on the wide tree; bit 1: closest-hit walks
-#endif
-__device__ __forceinline__ uint4 sload4u(const uint4* p, uint32_t i) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    typedef const uint32_t __attribute__((address_space(4)))* cu_ptr;
-    cu_ptr q = (cu_ptr)(const uint32_t*)(p + i);
-    return make_uint4(q[0], q[1], q[2], q[3]);
-#else
-    return p[i];
-#endif
-}
-// OR over all 64 lanes (EXEC must be all ones), wave-uniform result
-__device__ __forceinline__ uint32_t wave_or_full(uint32_t v) {
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);   // row_half_mirror
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);   // row_mirror
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-__device__ __forceinline__ uint32_t wave_or_partial(uint32_t v) {
-    uint32_t m = 0u;
-    uint64_t act = __ballot(1);
-    while (act) {
-        const int lane = __builtin_ctzll(act);
-        act &= act - 1;
-        m |= (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
-    }
-    return m;
-}
-__device__ __forceinline__ uint32_t wave_or(bool full, uint32_t v) { return full ? wave_or_full(v) : wave_or_partial(v); }
-// the wave's group stack: uniform values only (SGPRs), s[0] = top
-struct WaveStack {
-    uint32_t s[kWideStack];
-    int n;
-    __device__ __forceinline__ void init() {
-#pragma unroll
-        for (int k = 0; k < kWideStack; ++k) s[k] = 0u;
-        n = 0;
-    }
-    __device__ __forceinline__ void push(uint32_t v) {
-#pragma unroll
-        for (int k = kWideStack - 1; k > 0; --k) s[k] = s[k - 1];
-        s[0] = v;
-        n = n < kWideStack ? n + 1 : n;
-    }
-    __device__ __forceinline__ uint32_t pop() {
-        const uint32_t top = s[0];
-#pragma unroll
-        for (int k = 0; k < kWideStack - 1; ++k) s[k] = s[k + 1];
-        --n;
-        return top;
-    }
-};
-// K any-hit rays per lane from one origin (occluded_wave_multi's contract), one wave-coherent wide walk
-template <int K>
-__device__ __forceinline__ void occluded_wlock_multi(const DevScene& S, const bool* active, vec3 o, const vec3* d,
-                                                     float tnear, const float* tfar, bool* occ) {
-    const bool full = __ballot(1) == ~0ull;
-    vec3 inv[K];
-    uint32_t live = 0u;                     // bit k: ray k still walking (active, not occluded)
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        inv[k] = mk(1.0f / d[k].x, 1.0f / d[k].y, 1.0f / d[k].z);
-        live |= active[k] ? (1u << k) : 0u;
-    }
-    uint32_t occb = 0u;
-    WaveStack st;
-    st.init();
-    uint32_t gb = 0u, gm = __ballot(live != 0u) != 0 ? 1u : 0u;   // root group: node 0, slot 0
-    while (gm != 0u) {                                            // wave-uniform
-        const uint32_t slot = (uint32_t)__builtin_ctz(gm);
-        const uint32_t rest = gm & (gm - 1u);
-        if (rest != 0u) st.push((gb << 8) | rest);
-        const uint32_t node = gb + slot;
-        const uint4 w0 = sload4u(S.wnodes, 5 * node), w1 = sload4u(S.wnodes, 5 * node + 1),
-                    w2 = sload4u(S.wnodes, 5 * node + 2), w3 = sload4u(S.wnodes, 5 * node + 3),
-                    w4 = sload4u(S.wnodes, 5 * node + 4);
-        uint32_t hk[K], any = 0u;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t h = wide_hits(w0, w1, w2, w3, w4, o, inv[k], tnear, tfar[k]);
-            hk[k] = ((live >> k) & 1u) ? h : 0u;
-            any |= hk[k];
-        }
-        const uint32_t u = wave_or(full, any);                   // the children some live ray hit
-        const uint32_t ni = (w0.w >> 24) & 0xfu, tb = w1.y;
-        uint32_t tm = u >> ni;                                    // leaf slots -> triangles tb + (slot - ni)
-        while (tm != 0u) {                                        // wave-uniform
-            const uint32_t j = (uint32_t)__builtin_ctz(tm);
-            tm &= tm - 1u;
-            const uint32_t tri = 3u * (tb + j);
-            const float4 T0 = sload(S.wtris, tri), T1 = sload(S.wtris, tri + 1), T2 = sload(S.wtris, tri + 2);
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const bool want = ((hk[k] >> (ni + j)) & (live >> k) & 1u) != 0u;
-                if (__ballot(want) != 0) {                        // wave-uniform
-                    float t, uu, vv;
-                    const bool hit = tri_test_nb(T0, T1, T2, o, d[k], tnear, tfar[k], t, uu, vv);
-                    const bool oc = want && hit;
-                    occb |= oc ? (1u << k) : 0u;
-                    live &= oc ? ~(1u << k) : ~0u;
-                }
-            }
-        }
-        if (__ballot(live != 0u) == 0) break;                     // every ray of the wave is occluded
-        const uint32_t ngm = u & ((1u << ni) - 1u);
-        if (ngm != 0u) { gb = w1.x; gm = ngm; }
-        else if (st.n > 0) { const uint32_t top = st.pop(); gb = top >> 8; gm = top & 0xffu; }
-        else gm = 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) occ[k] = (occb >> k) & 1u;
-}
-// one closest-hit ray per lane (rtcIntersect1 semantics: ties to the smaller t, then the smaller prim)
-__device__ __forceinline__ Hit closest_wlock(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-    const bool full = __ballot(1) == ~0ull;
-    const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
-    WaveStack st;
-    st.init();
-    uint32_t gb = 0u, gm = __ballot(active) != 0 ? 1u : 0u;
-    while (gm != 0u) {
-        const uint32_t slot = (uint32_t)__builtin_ctz(gm);
-        const uint32_t rest = gm & (gm - 1u);
-        if (rest != 0u) st.push((gb << 8) | rest);
-        const uint32_t node = gb + slot;
-        const uint4 w0 = sload4u(S.wnodes, 5 * node), w1 = sload4u(S.wnodes, 5 * node + 1),
-                    w2 = sload4u(S.wnodes, 5 * node + 2), w3 = sload4u(S.wnodes, 5 * node + 3),
-                    w4 = sload4u(S.wnodes, 5 * node + 4);
-        const uint32_t hits = active ? wide_hits(w0, w1, w2, w3, w4, o, inv, tnear, h.t) : 0u;
-        const uint32_t u = wave_or(full, hits);
-        const uint32_t ni = (w0.w >> 24) & 0xfu, tb = w1.y;
-        uint32_t tm = u >> ni;
-        while (tm != 0u) {
-            const uint32_t j = (uint32_t)__builtin_ctz(tm);
-            tm &= tm - 1u;
-            const uint32_t tri = 3u * (tb + j);
-            const float4 T0 = sload(S.wtris, tri);
-            const bool want = ((hits >> (ni + j)) & 1u) != 0u;
-            float t, uu, vv;
-            const bool hh = want & tri_test_nb(T0, sload(S.wtris, tri + 1), sload(S.wtris, tri + 2), o, d, tnear, h.t, t, uu, vv);
-            const int prim = __float_as_int(T0.w);
-            const bool better = hh & (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim));
-            h.t = better ? t : h.t; h.u = better ? uu : h.u; h.v = better ? vv : h.v;
-            h.prim = better ? prim : h.prim;
-        }
-        const uint32_t ngm = u & ((1u << ni) - 1u);
-        if (ngm != 0u) { gb = w1.x; gm = ngm; }
-        else if (st.n > 0) { const uint32_t top = st.pop(); gb = top >> 8; gm = top & 0xffu; }
-        else gm = 0u;
-    }
-    return h;
-}
-
 // ---------------------------------------------------------------- dispatch
 // Every lane of the wave must make the call (convergent call sites); `active` selects the lanes with a ray.
 template <int T, int K>
 __device__ __forceinline__ void trace_any_multi(const DevScene& S, const bool* active, vec3 o, const vec3* d,
                                                 float tnear, const float* tfar, bool* occ) {
-    if (!trav_lane(T) && trav_wide(T) && (RS_WLOCK & 1)) {
-        occluded_wlock_multi<K>(S, active, o, d, tnear, tfar, occ);
-    } else if (!trav_lane(T)) {
+    if (!trav_lane(T)) {
         occluded_wave_multi<K>(S, active, o, d, tnear, tfar, occ);
     } else {   // one walk after the other (measured faster than interleaving the K walks, and than one
                // loop running a lane's walks back to back: that spilled the hot loop, 2.5x slower on C3)
@@ -744,17 +573,11 @@ __device__ __forceinline__ void trace_any_multi(const DevScene& S, const bool* a
 }
 template <int T>
 __device__ __forceinline__ bool trace_any(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-    if (!trav_lane(T) && trav_wide(T) && (RS_WLOCK & 1)) {
-        bool oc;
-        occluded_wlock_multi<1>(S, &active, o, &d, tnear, &tfar, &oc);
-        return oc;
-    }
     if (!trav_lane(T)) return occluded_wave(S, active, o, d, tnear, tfar);
     return occluded_lane<trav_wide(T)>(S, active, o, d, tnear, tfar);
 }
 template <int T>
 __device__ __forceinline__ Hit trace_closest(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
-    if (!trav_lane(T) && trav_wide(T) && (RS_WLOCK & 2)) return closest_wlock(S, active, o, d, tnear, tfar);
     if (!trav_lane(T)) return closest_wave(S, active, o, d, tnear, tfar);
     return closest_lane<trav_wide(T)>(S, active, o, d, tnear, tfar);
 }

@@ -18,6 +18,7 @@ import numpy as np
 from .renderer import CameraDesc, PassTimes, RestirError, camera_desc, load_library
 
 ID_BYTES = 128
+DEFAULT_REFINE = 2        # rs_mgpu_rebalance's time-based refinement rounds unless the caller says otherwise
 
 
 class MgpuStats(ctypes.Structure):
@@ -86,9 +87,10 @@ class MultiGpuFrame:
     def rebalance(self, scenes, camera, params, first_frame: int = 0, n_frames: int = 2, min_rows: int = 8,
                   refine: int | None = None):
         """Cost-balanced bands (rs_mgpu_rebalance): row costs, then `refine` rounds of time-based refinement
-        (None: the library's default, 2; 0: row costs only).  rebalance_times() has the measured rounds."""
-        if refine is not None:
-            self._check(self.lib.rs_mgpu_set_rebalance_refine(self.h, int(refine)))
+        (None: the library's default, DEFAULT_REFINE = 2, whatever an earlier call set; 0: row costs only).
+        rebalance_times() has the measured rounds."""
+        rounds = DEFAULT_REFINE if refine is None else int(refine)
+        self._check(self.lib.rs_mgpu_set_rebalance_refine(self.h, rounds))
         cam = camera_desc(camera)
         self._check(self.lib.rs_mgpu_rebalance(self.h, self._scenes(scenes), ctypes.byref(cam), ctypes.byref(params),
                                                int(first_frame), int(n_frames), int(min_rows)))

@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = [
     "rs_context_get_traversal", "rs_get_timing_totals", "rs_scene_update_positions", "rs_post_frame",
     "rs_post_reset", "rs_scene_rebuild", "rs_render_direct_mis", "rs_scene_create_textured", "rs_scene_set_sky",
     "rs_scene_load_sky", "rs_image_decode", "rs_context_set_initial_split", "rs_context_get_initial_split",
-    "rs_context_set_frame_ring", "rs_context_set_run_ahead", "rs_max_run_ahead", "rs_tile_stream", "rs_export_png",
+    "rs_context_set_frame_ring", "rs_context_handoff_bytes", "rs_context_set_run_ahead", "rs_max_run_ahead", "rs_tile_stream", "rs_export_png",
     "rs_image_encode_png", "rs_context_track_row_costs", "rs_get_row_costs", "rs_frame_readback", "rs_frame_wait",
     "rs_host_alloc", "rs_host_free", "rs_mgpu_unique_id", "rs_mgpu_create", "rs_mgpu_create_local",
     "rs_mgpu_destroy", "rs_mgpu_set_bands", "rs_mgpu_get_bands", "rs_mgpu_rebalance", "rs_mgpu_render_frame",
@@ -180,6 +180,7 @@ def load_library(path: str = LIB_PATH):
     L.rs_context_set_initial_split.argtypes = [vp, i32]
     L.rs_context_get_initial_split.argtypes = [vp, ip, ip]
     L.rs_context_set_frame_ring.argtypes = [vp, i32]
+    L.rs_context_handoff_bytes.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.rs_context_set_run_ahead.argtypes = [vp, i32]
     L.rs_max_run_ahead.argtypes = []
     L.rs_max_run_ahead.restype = i32
@@ -542,6 +543,12 @@ class Renderer:
         """1 (default) or 2 framebuffers alternating per frame (a reader may lag one frame)."""
         self._check(self.lib.rs_context_set_frame_ring(self.h, int(n)))
 
+    def handoff_bytes(self) -> int:
+        """rs_context_handoff_bytes: device bytes of the sorted initial pass's hand-off buffers (all lanes)."""
+        v = ctypes.c_uint64()
+        self._check(self.lib.rs_context_handoff_bytes(self.h, ctypes.byref(v)))
+        return int(v.value)
+
     def track_row_costs(self, enable: bool = True):
         """Record per-row wave time in every pass (load balancing of tile-sharded frames)."""
         self._check(self.lib.rs_context_track_row_costs(self.h, 1 if enable else 0))
@@ -595,13 +602,10 @@ class Renderer:
         return self.frame_data if copy_out else None
 
     def debug_trace(self, scene: Scene, o, d, tnear, tfar, any_hit: bool, lockstep: bool = True,
-                    stats: bool = False, wide_stats: bool = False, wave_wide: bool = False):
+                    stats: bool = False, wide_stats: bool = False):
         """Raw BVH queries.  stats=True: per-lane skip-pointer walk statistics instead -- returns
         (visits, triangle_tests) int arrays per ray; wide_stats=True: the 8-wide walk's (node fetches,
-        triangle tests, stack overflow flags); wave_wide=True: the wave-coherent walk over the 8-wide tree
-        (rs_scene.h occluded_wlock_multi / closest_wlock; -1 results when the scene has no wide tree)."""
-        if wave_wide:
-            return self._debug_trace(scene, o, d, tnear, tfar, 12 if any_hit else 11)
+        triangle tests, stack overflow flags)."""
         if wide_stats:
             t, prim = self._debug_trace(scene, o, d, tnear, tfar, 7 if any_hit else 6)
             p = prim.view(np.uint32)

@@ -30,8 +30,8 @@ def _ptr(a, t=_f32p):
 
 
 def build():
-    src = os.path.join(ROOT, "oracle", "restir_oracle.c")
-    if (not os.path.exists(LIB_PATH)) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(ROOT, "oracle", "restir_oracle.c"), os.path.join(ROOT, "restir-embree_amd", "csrc", "rs_libm.h")]
+    if (not os.path.exists(LIB_PATH)) or os.path.getmtime(LIB_PATH) < max(os.path.getmtime(p) for p in srcs):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
     return LIB_PATH
 
@@ -97,8 +97,36 @@ def lib():
         L.or_ctx_rebuilt.restype = ctypes.c_uint64
         L.or_ctx_rebuilt.argtypes = [ctypes.c_void_p]
         L.or_kat_mis.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float, _f32p]
+        L.or_libm_f1.argtypes = [ctypes.c_int, _f32p, _f32p, ctypes.c_int]
+        L.or_libm_powf.argtypes = [_f32p, _f32p, _f32p, ctypes.c_int]
+        L.or_libm_d1.argtypes = [ctypes.c_int, _f64p, _f64p, ctypes.c_int]
         _lib = L
     return _lib
+
+
+def libm_f1(name, x):
+    """rs_libm.h (shared by the oracle and the kernels): expf / lgammaf / sinf / cosf over a float32 array"""
+    x = np.ascontiguousarray(x, np.float32)
+    o = np.empty_like(x)
+    lib().or_libm_f1(["expf", "lgammaf", "sinf", "cosf"].index(name), _ptr(x), _ptr(o), x.size)
+    return o
+
+
+def libm_f2(name, x, y):
+    assert name == "powf"
+    x, y = np.ascontiguousarray(x, np.float32), np.ascontiguousarray(y, np.float32)
+    o = np.empty_like(x)
+    lib().or_libm_powf(_ptr(x), _ptr(y), _ptr(o), x.size)
+    return o
+
+
+def libm_d1(name, x):
+    """rs_libm.h's double log / exp / log1p / lgamma (the incomplete beta's)"""
+    x = np.ascontiguousarray(x, np.float64)
+    o = np.empty_like(x)
+    p = ctypes.POINTER(ctypes.c_double)
+    lib().or_libm_d1(["log", "exp", "log1p", "lgamma"].index(name), _ptr(x, p), _ptr(o, p), x.size)
+    return o
 
 
 class OraclePost:
