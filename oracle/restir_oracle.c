@@ -301,7 +301,20 @@ static float bb_area(const aabb* b) {
     return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
 }
 
-typedef struct { aabb* tb; float* cen; uint32_t* idx; or_node* nodes; int n_nodes; } bvh_build_t;
+typedef struct { aabb* tb; float* cen; uint32_t* idx; or_node* nodes; int n_nodes; float eps; } bvh_build_t;
+
+/* every node box is inflated by 2^-16 x the scene's largest |coordinate| (at least 1): restates rs_wide.h
+ * box_epsilon.  Moller-Trumbore accepts hits whose point o + t d lies a few ulps outside the triangle's box; without
+ * the margin a slab test can cull that box, and which box that is depends on the tree (this oracle's binary and
+ * 8-wide trees disagreed on 1 of 8.3 M C3 primary rays).  With it every tree returns the triangle test's answer. */
+static float or_box_epsilon(const float* pos, size_t nfloats) {
+    float m = 1.0f;
+    for (size_t i = 0; i < nfloats; ++i) {
+        const float a = fabsf(pos[i]);
+        if (a - a == 0.0f && a > m) m = a;
+    }
+    return m * (1.0f / 65536.0f);
+}
 
 static int bvh_build_rec(bvh_build_t* B, int first, int count) {
     int ni = B->n_nodes++;
@@ -312,7 +325,7 @@ static int bvh_build_rec(bvh_build_t* B, int first, int count) {
         bb_grow(&bb, &B->tb[t]);
         bb_grow_p(&cb, V(B->cen[3 * t], B->cen[3 * t + 1], B->cen[3 * t + 2]));
     }
-    memcpy(N->lo, bb.lo, sizeof bb.lo); memcpy(N->hi, bb.hi, sizeof bb.hi);
+    for (int a = 0; a < 3; ++a) { N->lo[a] = bb.lo[a] - B->eps; N->hi[a] = bb.hi[a] + B->eps; }
     if (count <= 4) { N->first = first; N->count = count; N->left = N->right = -1; return ni; }
     enum { NB = 16 };
     int best_axis = -1, best_split = -1; float best_cost = FLT_MAX;
@@ -421,6 +434,7 @@ or_scene* or_scene_create(uint32_t n_tris, const float* pos, const float* nrm, c
         for (int a = 0; a < 3; ++a) B.cen[3 * t + a] = 0.5f * (B.tb[t].lo[a] + B.tb[t].hi[a]);
         B.idx[t] = t;
     }
+    B.eps = or_box_epsilon(pos, 9 * (size_t)n_tris);
     if (n_tris) bvh_build_rec(&B, 0, (int)n_tris);
     s->nodes = B.nodes; s->n_nodes = B.n_nodes; s->tri_index = B.idx;
     free(B.tb); free(B.cen);
