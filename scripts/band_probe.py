@@ -2,7 +2,10 @@
 communication -- the compute + host-overhead floor of bench.py --gpus N.  For N in (1, 2, 4, 8) it renders
 the middle band of the frame (rank N//2, margin/halo as TiledRenderer sets them) K times through the
 tile ABI and reports wall ms/frame, GPU ms/frame (event ring) and host ms per render() call.
-Usage: python scripts/band_probe.py [--scene C2|C3|C5] [--steps K] [--balanced] [--all-ranks N [--refine R]]"""
+--gather: rank 0 also receives the other ranks' band framebuffers -- N-1 device-to-device copies of their rows into
+its frame on the frame's lane stream after its shade, as rs_mgpu issues the RCCL receives (the local stand-in for
+the xGMI gather; on 8 GPUs each band arrives over its own link in parallel).
+Usage: python scripts/band_probe.py [--scene C2|C3|C5] [--steps K] [--balanced] [--all-ranks N [--refine R]] [--gather]"""
 import argparse
 import os
 import sys
@@ -29,11 +32,12 @@ def main():
     ap.add_argument("--refine", type=int, default=0,
                     help="with --all-ranks: rounds of time-based rebalancing (each band's row costs rescaled to its "
                          "measured time, bands balanced again; the rs_mgpu_rebalance refinement)")
+    ap.add_argument("--gather", action="store_true", help="rank 0: + the N-1 band framebuffer copies into its frame")
     a = ap.parse_args()
     import torch
     from restir_amd import Renderer, scenes
     from restir_amd.params import metric_params, c3_params
-    from restir_amd.distributed import band_rows, halo_rows, balanced_bands, BAND_GRAIN
+    from restir_amd.distributed import band_rows, halo_rows, balanced_bands, BAND_GRAIN, _CudaBuf
 
     sc = scenes.sponza_like() if a.scene == "C3" else scenes.cornell_many_lights(1024)
     prm = metric_params() if a.scene == "C2" else c3_params()
@@ -66,8 +70,11 @@ def main():
     for N in {n for n, _ in cases}:
         bands_of[N] = balanced_bands(costs, N, 8, grain=BAND_GRAIN) if costs is not None else [band_rows(H, k, N) for k in range(N)]
 
-    def probe(N, rank, y0, y1, tag=""):
+    gather_src = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda") if a.gather else None
+
+    def probe(N, rank, y0, y1, tag="", bands=None):
         halo = halo_rows(prm) if N > 1 else 0
+        gather = a.gather and rank == 0 and N > 1 and bands is not None
         margin = halo          # rs_mgpu_render_frame's G-buffer margin (a temporal reprojection beyond it rebuilds)
 
         def frame(f):
@@ -77,7 +84,14 @@ def main():
             for p in range(prm.spatial_passes if prm.do_spatial else 0):
                 r.tile_halo_ptr(0)
                 r.tile_spatial(p)
-            r.tile_finish(False)
+            sp = r.tile_stream()[0] if gather else None
+            band = r.tile_finish(False)
+            if gather:      # the other ranks' rows into this frame, on its lane stream (rs_mgpu's receive order)
+                fb = torch.as_tensor(_CudaBuf(band - y0 * W * 12, W * H * 12, "<f4", 4), device="cuda")
+                with torch.cuda.stream(torch.cuda.ExternalStream(sp)):
+                    for k, (b0, b1) in enumerate(bands):
+                        if k != rank:
+                            fb[b0 * W * 3:b1 * W * 3].copy_(gather_src[b0 * W * 3:b1 * W * 3])
 
         for f in range(6):
             frame(f)
@@ -97,7 +111,7 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         tot, n = r.timing_totals()
-        print(f"{tag}{a.scene} ahead={a.ahead} inflight={a.inflight} split={a.split}:{int(r.initial_split()[1])} N={N} rank={rank} rows={y1 - y0} margin={margin}: wall {dt / a.steps * 1e3:.4f} ms/frame, "
+        print(f"{tag}{a.scene} ahead={a.ahead} inflight={a.inflight} split={a.split}:{int(r.initial_split()[1])} N={N} rank={rank} rows={y1 - y0} margin={margin}{' +gather' if gather else ''}: wall {dt / a.steps * 1e3:.4f} ms/frame, "
               f"gpu {tot.total_ms / n:.4f} ms (initial {tot.gbuffer_initial_ms / n:.4f}, spatial {tot.spatial_ms / n:.4f}, "
               f"temporal {tot.temporal_ms / n:.4f}), host {host / a.steps * 1e3:.4f} ms/call; "
               f"ideal (N=1 / N) -> efficiency bound", flush=True)
@@ -108,7 +122,7 @@ def main():
         c = np.asarray(costs, np.float64).copy()
         bands = bands_of[N]
         for it in range(a.refine + 1):
-            t = [probe(N, k, y0, y1, f"[round {it}] ") for k, (y0, y1) in enumerate(bands)]
+            t = [probe(N, k, y0, y1, f"[round {it}] ", bands) for k, (y0, y1) in enumerate(bands)]
             print(f"[round {it}] bands {[y1 - y0 for y0, y1 in bands]}: max {max(t):.4f} mean {np.mean(t):.4f} ms",
                   flush=True)
             for (y0, y1), tk in zip(bands, t):          # each band's rows rescaled to its measured time
@@ -119,7 +133,7 @@ def main():
         return
     for N, rank in cases:
         y0, y1 = bands_of[N][rank]
-        probe(N, rank, y0, y1)
+        probe(N, rank, y0, y1, bands=bands_of[N])
 
 
 if __name__ == "__main__":
