@@ -24,6 +24,7 @@ namespace rs {
 int build_bvh(const float* d_pos, uint32_t n, float eps, hipStream_t st, float4** d_nodes, uint32_t* n_nodes,
               float4** d_tris, WideBvh* wide, std::string& err);
 void preload_code_objects();
+void builder_pool_trim();
 int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int** d_order, int** d_lvl_off,
                    std::vector<int>& lvl_off, std::string& err);
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
@@ -877,7 +878,8 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     s->wide_on = rc == 0 && s->wide.n_nodes > 0 && s->wide.depth <= kWideStack;   // deeper: the skip pointers
     hipEventRecord(e1, st);
     if (rc == 0 && hipStreamSynchronize(st) == hipSuccess) hipEventElapsedTime(&s->build_ms, e0, e1);
-    else { err = "BVH build failed: " + berr; rc = -1; }
+    else { err = "BVH build failed: " + berr; rc = -1; (void)hipStreamSynchronize(st); }
+    builder_pool_trim();                          // the build's scratch back to the driver (stream drained above)
     hipEventDestroy(e0); hipEventDestroy(e1);
     if (rc == 0 && bvh_refit_plan(s->d_nodes, s->n_nodes, st, &s->d_refit_order, &s->d_refit_lvl, s->refit_lvl, berr) != 0) {
         err = berr; rc = -1;

@@ -24,6 +24,7 @@
 #include <utility>
 #include <cstring>
 #include <algorithm>
+#include <mutex>
 #include "rs_refit.h"
 #include "rs_wide.h"
 #include "../../include/restir_c.h"
@@ -493,6 +494,40 @@ __global__ void k_ploc_emit(const float4* nlo, const float4* nhi, const int* par
 }
 
 
+// The builders' scratch (stream-ordered allocations) comes from a private pool per device, never the device's
+// default pool that the host process (PyTorch, other libraries) shares: it caches its blocks across the launches
+// of one build (release threshold: unlimited) and is trimmed to empty after every build (builder_pool_trim).
+static hipMemPool_t g_builder_pool[64] = {};
+static std::mutex g_builder_pool_mu;
+hipMemPool_t builder_pool() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(g_builder_pool_mu);
+    if (!g_builder_pool[dev]) {
+        hipMemPoolProps pp = {};
+        pp.allocType = hipMemAllocationTypePinned;
+        pp.location.type = hipMemLocationTypeDevice;
+        pp.location.id = dev;
+        hipMemPool_t pl = nullptr;
+        if (hipMemPoolCreate(&pl, &pp) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+        uint64_t keep = ~0ull;
+        (void)hipMemPoolSetAttribute(pl, hipMemPoolAttrReleaseThreshold, &keep);
+        g_builder_pool[dev] = pl;
+    }
+    return g_builder_pool[dev];
+}
+hipError_t pool_malloc(void** p, size_t bytes, hipStream_t st) {
+    hipMemPool_t pl = builder_pool();
+    return pl ? hipMallocFromPoolAsync(p, bytes, pl, st) : hipMallocAsync(p, bytes, st);
+}
+// after a build has finished on the host's view (its stream synchronised): return the scratch to the driver
+void builder_pool_trim() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+    std::lock_guard<std::mutex> lk(g_builder_pool_mu);
+    if (g_builder_pool[dev]) (void)hipMemPoolTrimTo(g_builder_pool[dev], 0);
+}
+
 #define PLOC_CHECK(x)                                                                  \
     do {                                                                               \
         hipError_t e_ = (x);                                                           \
@@ -518,28 +553,28 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, float eps, hipStream_t st, fl
     int k = (int)n, base = (int)n, root = 0, max_depth = 0, kept_root = 1;
     PlocState* pst = nullptr;                  // two slots (the iteration's parity)
 
-    PLOC_CHECK(hipMallocAsync((void**)&lo, n * sizeof(float4), st));
-    PLOC_CHECK(hipMallocAsync((void**)&hi, n * sizeof(float4), st));
-    PLOC_CHECK(hipMallocAsync((void**)&cb, 6 * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&keys, n * sizeof(uint64_t), st));
-    PLOC_CHECK(hipMallocAsync((void**)&keys_sorted, n * sizeof(uint64_t), st));
-    PLOC_CHECK(hipMallocAsync((void**)&nlo, (size_t)total * sizeof(float4), st));
-    PLOC_CHECK(hipMallocAsync((void**)&nhi, (size_t)total * sizeof(float4), st));
-    PLOC_CHECK(hipMallocAsync((void**)&cnt, (size_t)total * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&parent, (size_t)total * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&depth, (size_t)total * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&kept, (size_t)total * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&collapsed, (size_t)total * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&cost, (size_t)total * sizeof(float), st));
-    PLOC_CHECK(hipMallocAsync((void**)&C0, n * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&C1, n * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&N, n * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&valid, n * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&merged, n * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&pos, n * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&mid, n * sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&dmax, sizeof(int), st));
-    PLOC_CHECK(hipMallocAsync((void**)&pst, 2 * sizeof(PlocState), st));
+    PLOC_CHECK(pool_malloc((void**)&lo, n * sizeof(float4), st));
+    PLOC_CHECK(pool_malloc((void**)&hi, n * sizeof(float4), st));
+    PLOC_CHECK(pool_malloc((void**)&cb, 6 * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&keys, n * sizeof(uint64_t), st));
+    PLOC_CHECK(pool_malloc((void**)&keys_sorted, n * sizeof(uint64_t), st));
+    PLOC_CHECK(pool_malloc((void**)&nlo, (size_t)total * sizeof(float4), st));
+    PLOC_CHECK(pool_malloc((void**)&nhi, (size_t)total * sizeof(float4), st));
+    PLOC_CHECK(pool_malloc((void**)&cnt, (size_t)total * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&parent, (size_t)total * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&depth, (size_t)total * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&kept, (size_t)total * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&collapsed, (size_t)total * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&cost, (size_t)total * sizeof(float), st));
+    PLOC_CHECK(pool_malloc((void**)&C0, n * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&C1, n * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&N, n * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&valid, n * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&merged, n * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&pos, n * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&mid, n * sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&dmax, sizeof(int), st));
+    PLOC_CHECK(pool_malloc((void**)&pst, 2 * sizeof(PlocState), st));
     PLOC_CHECK(hipMemcpyAsync(cb, init_cb, sizeof init_cb, hipMemcpyHostToDevice, st));
     PLOC_CHECK(hipMemsetAsync(dmax, 0, sizeof(int), st));
     PLOC_CHECK(hipMemsetAsync(parent, 0xff, (size_t)total * sizeof(int), st));   // -1
@@ -548,10 +583,10 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, float eps, hipStream_t st, fl
     k_morton<<<(n + B - 1) / B, B, 0, st>>>(lo, hi, n, cb, keys);
     PLOC_CHECK(hipGetLastError());
     PLOC_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, keys_sorted, (int)n, 0, 62, st));
-    PLOC_CHECK(hipMallocAsync(&tmp, tmp_bytes, st));
+    PLOC_CHECK(pool_malloc(&tmp, tmp_bytes, st));
     PLOC_CHECK(hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, keys_sorted, (int)n, 0, 62, st));
     PLOC_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2_bytes, valid, pos, (int)n, st));
-    PLOC_CHECK(hipMallocAsync(&tmp2, tmp2_bytes, st));
+    PLOC_CHECK(pool_malloc(&tmp2, tmp2_bytes, st));
     k_ploc_leaves<<<(n + B - 1) / B, B, 0, st>>>(keys_sorted, n, lo, hi, nlo, nhi, cnt, C0);
     PLOC_CHECK(hipGetLastError());
 
@@ -683,14 +718,7 @@ void preload_code_objects() {
     hipFuncAttributes fa;
     (void)hipFuncGetAttributes(&fa, (const void*)k_ploc_nearest);
     preload_wide_build();
-    // the builders' scratch comes from the device's default pool (hipMallocAsync): keep up to 2 GiB of it
-    // cached between builds instead of returning it to the driver at every synchronisation
-    int dev = 0;
-    hipMemPool_t pool;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t keep = 2ull << 30;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    }
+    (void)builder_pool();
     (void)hipGetLastError();
 }
 void wide_free(WideBvh& w) {

@@ -35,6 +35,8 @@
 #include "../../include/restir_c.h"
 #include "rs_wide.h"
 
+namespace rs { hipError_t pool_malloc(void** p, size_t bytes, hipStream_t st); }
+
 namespace rs {
 namespace wb {
 
@@ -828,7 +830,7 @@ struct Scratch {
     explicit Scratch(hipStream_t s) : st(s) {}
     template <class T> bool get(T** out, size_t count) {
         *out = nullptr;
-        if (hipMallocAsync((void**)out, std::max<size_t>(1, count) * sizeof(T), st) != hipSuccess) return false;
+        if (pool_malloc((void**)out, std::max<size_t>(1, count) * sizeof(T), st) != hipSuccess) return false;
         p.push_back((void*)*out);
         return true;
     }
