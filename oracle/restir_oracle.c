@@ -270,7 +270,8 @@ typedef struct {
     float total_area;
     /* BVH */
     or_node* nodes; int n_nodes; uint32_t* tri_index;
-    struct or_wnode* wn; int n_wn;   /* 8-wide tree over the same leaves (or_scene_set_wide), or NULL */
+    struct or_wnode* wn; int n_wn;
+    float box_eps;                   /* the closest-hit walks' box margin (or_box_epsilon) */   /* 8-wide tree over the same leaves (or_scene_set_wide), or NULL */
     /* textures: per-material map slots (0-based, -1 none: diffuse, specular,
        shininess, normal), per-triangle uv (6) / tangents (9), textures in FreeImage layout, sky */
     int32_t* maps; float* uv; float* tan;
@@ -301,12 +302,13 @@ static float bb_area(const aabb* b) {
     return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
 }
 
-typedef struct { aabb* tb; float* cen; uint32_t* idx; or_node* nodes; int n_nodes; float eps; } bvh_build_t;
+typedef struct { aabb* tb; float* cen; uint32_t* idx; or_node* nodes; int n_nodes; } bvh_build_t;
 
-/* every node box is inflated by 2^-16 x the scene's largest |coordinate| (at least 1): restates rs_wide.h
+/* the closest-hit walks' box margin: 2^-16 x the scene's largest |coordinate| (at least 1), restating rs_wide.h
  * box_epsilon.  Moller-Trumbore accepts hits whose point o + t d lies a few ulps outside the triangle's box; without
- * the margin a slab test can cull that box, and which box that is depends on the tree (this oracle's binary and
- * 8-wide trees disagreed on 1 of 8.3 M C3 primary rays).  With it every tree returns the triangle test's answer. */
+ * a margin a closest-hit walk can cull that box after finding a tied neighbour, and which box that is depends on the
+ * tree (this oracle's binary and 8-wide trees disagreed on 1 of 8.3 M C3 4K primary rays).  With it every tree
+ * returns the triangle test's answer.  The any-hit walks keep the exact boxes (as the kernels do). */
 static float or_box_epsilon(const float* pos, size_t nfloats) {
     float m = 1.0f;
     for (size_t i = 0; i < nfloats; ++i) {
@@ -325,7 +327,7 @@ static int bvh_build_rec(bvh_build_t* B, int first, int count) {
         bb_grow(&bb, &B->tb[t]);
         bb_grow_p(&cb, V(B->cen[3 * t], B->cen[3 * t + 1], B->cen[3 * t + 2]));
     }
-    for (int a = 0; a < 3; ++a) { N->lo[a] = bb.lo[a] - B->eps; N->hi[a] = bb.hi[a] + B->eps; }
+    memcpy(N->lo, bb.lo, sizeof bb.lo); memcpy(N->hi, bb.hi, sizeof bb.hi);
     if (count <= 4) { N->first = first; N->count = count; N->left = N->right = -1; return ni; }
     enum { NB = 16 };
     int best_axis = -1, best_split = -1; float best_cost = FLT_MAX;
@@ -434,7 +436,7 @@ or_scene* or_scene_create(uint32_t n_tris, const float* pos, const float* nrm, c
         for (int a = 0; a < 3; ++a) B.cen[3 * t + a] = 0.5f * (B.tb[t].lo[a] + B.tb[t].hi[a]);
         B.idx[t] = t;
     }
-    B.eps = or_box_epsilon(pos, 9 * (size_t)n_tris);
+    s->box_eps = or_box_epsilon(pos, 9 * (size_t)n_tris);
     if (n_tris) bvh_build_rec(&B, 0, (int)n_tris);
     s->nodes = B.nodes; s->n_nodes = B.n_nodes; s->tri_index = B.idx;
     free(B.tb); free(B.cen);
@@ -603,13 +605,14 @@ static inline int tri_hit(const or_scene* s, uint32_t t, v3 o, v3 d, float tnear
 
 /* conservative slab test: interval widened by (1 +- 4 eps) so it never culls a box whose
    contents the triangle test would accept */
-static inline int box_hit(const or_node* n, v3 o, v3 inv, float tnear, float tfar, float* tentry) {
+static inline int box_hit(const or_node* n, v3 o, v3 inv, float tnear, float tfar, float* tentry, const float* ew) {
     float oo[3] = {o.x, o.y, o.z}, ii[3] = {inv.x, inv.y, inv.z};
     float t0 = tnear, t1 = tfar;
     for (int a = 0; a < 3; ++a) {
         float ta = (n->lo[a] - oo[a]) * ii[a];
         float tb = (n->hi[a] - oo[a]) * ii[a];
         float mn = fminf(ta, tb), mx = fmaxf(ta, tb);
+        if (ew) { mn = mn - ew[a]; mx = mx + ew[a]; }   /* closest-hit margin (or_box_epsilon) */
         t0 = fmaxf(t0, mn); t1 = fminf(t1, mx);
     }
     *tentry = t0;
@@ -625,11 +628,12 @@ static or_hit closest_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar
     if (!s->n_nodes) return h;
     if (s->wn) return closest_hit_wide(s, o, d, tnear, tfar);
     v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float ew[3] = {s->box_eps * fabsf(inv.x), s->box_eps * fabsf(inv.y), s->box_eps * fabsf(inv.z)};
     int stack[128]; int sp = 0; stack[sp++] = 0;
     while (sp) {
         const or_node* n = &s->nodes[stack[--sp]];
         float te;
-        if (!box_hit(n, o, inv, tnear, h.t, &te)) continue;
+        if (!box_hit(n, o, inv, tnear, h.t, &te, ew)) continue;
         if (n->count) {
             for (int i = n->first; i < n->first + n->count; ++i) {
                 uint32_t t = s->tri_index[i]; float tt, uu, vv;
@@ -654,7 +658,7 @@ static int any_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
     while (sp) {
         const or_node* n = &s->nodes[stack[--sp]];
         float te;
-        if (!box_hit(n, o, inv, tnear, tfar, &te)) continue;
+        if (!box_hit(n, o, inv, tnear, tfar, &te, NULL)) continue;
         if (n->count) {
             for (int i = n->first; i < n->first + n->count; ++i) {
                 float tt, uu, vv;
@@ -717,15 +721,16 @@ int or_scene_set_wide(or_scene* s, int on) {
 
 /* box_hit for the 8 children: bit c = child c accepted; tentry[c] = its entry t */
 __attribute__((target("avx2"))) static inline uint32_t box8(const or_wnode* w, const __m256* O, const __m256* I,
-                                                              float tnear, float tfar, float* tentry) {
+                                                              float tnear, float tfar, float* tentry, const __m256* E) {
     __m256 t0 = _mm256_set1_ps(tnear), t1 = _mm256_set1_ps(tfar);
     for (int a = 0; a < 3; ++a) {
         const __m256 ta = _mm256_mul_ps(_mm256_sub_ps(_mm256_loadu_ps(w->lo[a]), O[a]), I[a]);
         const __m256 tb = _mm256_mul_ps(_mm256_sub_ps(_mm256_loadu_ps(w->hi[a]), O[a]), I[a]);
         const __m256 nb = _mm256_cmp_ps(tb, tb, _CMP_UNORD_Q);
         /* fminf / fmaxf(ta, tb): the non-NaN operand if one is NaN (min_ps/max_ps return tb then) */
-        const __m256 mn = _mm256_blendv_ps(_mm256_min_ps(ta, tb), ta, nb);
-        const __m256 mx = _mm256_blendv_ps(_mm256_max_ps(ta, tb), ta, nb);
+        __m256 mn = _mm256_blendv_ps(_mm256_min_ps(ta, tb), ta, nb);
+        __m256 mx = _mm256_blendv_ps(_mm256_max_ps(ta, tb), ta, nb);
+        if (E) { mn = _mm256_sub_ps(mn, E[a]); mx = _mm256_add_ps(mx, E[a]); }   /* closest-hit margin */
         t0 = _mm256_max_ps(mn, t0);   /* fmaxf(t0, mn): t0 when mn is NaN */
         t1 = _mm256_min_ps(mx, t1);
     }
@@ -743,7 +748,7 @@ __attribute__((target("avx2"))) static int any_hit_wide(const or_scene* s, v3 o,
     float te[8];
     while (sp) {
         const or_wnode* w = &s->wn[stack[--sp]];
-        uint32_t m = box8(w, O, I, tnear, tfar, te);
+        uint32_t m = box8(w, O, I, tnear, tfar, te, NULL);
         while (m) {
             const int c = __builtin_ctz(m); m &= m - 1;
             const int32_t k = w->kid[c];
@@ -765,11 +770,13 @@ __attribute__((target("avx2"))) static or_hit closest_hit_wide(const or_scene* s
     const v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const __m256 O[3] = {_mm256_set1_ps(o.x), _mm256_set1_ps(o.y), _mm256_set1_ps(o.z)};
     const __m256 I[3] = {_mm256_set1_ps(inv.x), _mm256_set1_ps(inv.y), _mm256_set1_ps(inv.z)};
+    const __m256 E[3] = {_mm256_set1_ps(s->box_eps * fabsf(inv.x)), _mm256_set1_ps(s->box_eps * fabsf(inv.y)),
+                         _mm256_set1_ps(s->box_eps * fabsf(inv.z))};
     int stack[OR_WSTACK]; int sp = 0; stack[sp++] = 0;
     float te[8];
     while (sp) {
         const or_wnode* w = &s->wn[stack[--sp]];
-        uint32_t m = box8(w, O, I, tnear, h.t, te);
+        uint32_t m = box8(w, O, I, tnear, h.t, te, E);
         int near[8]; int nn = 0;
         while (m) {
             const int c = __builtin_ctz(m); m &= m - 1;

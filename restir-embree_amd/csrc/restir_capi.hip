@@ -21,14 +21,14 @@
 #include <algorithm>
 
 namespace rs {
-int build_bvh(const float* d_pos, uint32_t n, float eps, hipStream_t st, float4** d_nodes, uint32_t* n_nodes,
-              float4** d_tris, WideBvh* wide, std::string& err);
+int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes, float4** d_tris,
+              WideBvh* wide, std::string& err);
 void preload_code_objects();
 void builder_pool_trim();
 int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int** d_order, int** d_lvl_off,
                    std::vector<int>& lvl_off, std::string& err);
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
-              const std::vector<int>& lvl_off, float eps, hipStream_t st, int* tail, std::string& err);
+              const std::vector<int>& lvl_off, hipStream_t st, int* tail, std::string& err);
 void wide_free(WideBvh& w);
 }
 
@@ -44,7 +44,7 @@ struct rs_scene {
     float* d_cdf = nullptr;
     int* d_cdf_guide = nullptr;
     float build_ms = 0.0f;
-    float box_eps = 0.0f;                 // BVH box inflation (rs_wide.h box_epsilon), fixed at the last full build
+    float box_eps = 0.0f;                 // closest-hit box margin (rs_wide.h box_epsilon), set at the last full build
     // host copies (rs_scene_rebuild re-derives the tables on the host)
     std::vector<float> h_nrm;
     std::vector<uint32_t> h_tri_mat;
@@ -98,6 +98,7 @@ struct rs_scene {
         S.wnodes = wide_on ? wide.nodes : nullptr; S.wtris = wide.tris; S.n_wnodes = wide_on ? wide.n_nodes : 0u;
         S.ebucket = d_ebucket;
         S.ecen = vec3{ecen[0], ecen[1], ecen[2]};
+        S.box_eps = box_eps;
         return S;
     }
     // the geometry of generation `g` if this scene still holds it (current, or the a_* copy of g == a_geo)
@@ -874,7 +875,7 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     hipEventRecord(e0, st);
     std::string berr;
     s->box_eps = box_epsilon(pos.data(), pos.size());
-    int rc = build_bvh(s->d_pos, n, s->box_eps, st, &s->d_nodes, &s->n_nodes, &s->d_tris, &s->wide, berr);
+    int rc = build_bvh(s->d_pos, n, st, &s->d_nodes, &s->n_nodes, &s->d_tris, &s->wide, berr);
     s->wide_on = rc == 0 && s->wide.n_nodes > 0 && s->wide.depth <= kWideStack;   // deeper: the skip pointers
     hipEventRecord(e1, st);
     if (rc == 0 && hipStreamSynchronize(st) == hipSuccess) hipEventElapsedTime(&s->build_ms, e0, e1);
@@ -983,7 +984,7 @@ __device__ __forceinline__ void light_table(const float* __restrict__ pos, const
 
 // one launch for the three independent single-workgroup jobs of an update: workgroup 0 the light
 // tables, workgroup 1 the last (small-level) batch of the binary refit, workgroup 2 that of the 8-wide refit
-struct RefitArgs { float4* nodes; float4* tris; const float* pos; const int* order; const int* lvl_off; int l0, l1; float eps; };
+struct RefitArgs { float4* nodes; float4* tris; const float* pos; const int* order; const int* lvl_off; int l0, l1; };
 __global__ void __launch_bounds__(kLightBlock) k_scene_update(const float* __restrict__ pos, const float4* __restrict__ tri_nrm,
                                                               const float4* __restrict__ mats, const int* __restrict__ emis_tri,
                                                               uint32_t ne, float4* em, float* cdf, int* guide, RefitArgs R,
@@ -992,7 +993,7 @@ __global__ void __launch_bounds__(kLightBlock) k_scene_update(const float* __res
     if (blockIdx.x == 0) {
         if (ne) light_table(pos, tri_nrm, mats, emis_tri, ne, em, cdf, guide);
     } else if (blockIdx.x == 1) {
-        refit_levels(R.nodes, R.tris, R.pos, R.order, R.lvl_off, R.l0, R.l1, 0, 1, R.eps);
+        refit_levels(R.nodes, R.tris, R.pos, R.order, R.lvl_off, R.l0, R.l1, 0, 1);
     } else if (W.l_deep >= W.l_top) {
         wide_refit_levels(W, 0, 1);
     }
@@ -1110,17 +1111,17 @@ extern "C" int rs_scene_update_positions(rs_scene* s, const float* positions, co
     HIPCHK(c, hipEventRecord(s->stage_ev[k], st));
     std::string err;
     int tail[2];
-    if (bvh_refit(nodes, tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, s->refit_lvl, s->box_eps, st, tail, err) != 0)
+    if (bvh_refit(nodes, tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, s->refit_lvl, st, tail, err) != 0)
         return fail(c, RS_E_HIP, "rs_scene_update_positions: " + err);
-    RefitArgs R{nodes, tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, tail[0], tail[1], s->box_eps};
+    RefitArgs R{nodes, tris, s->d_pos, s->d_refit_order, s->d_refit_lvl, tail[0], tail[1]};
     // the 8-wide tree keeps its topology and is refit too (rs_refit.h): large levels alone, the last run of
     // small levels up to the root in the fused launch's third workgroup
-    WideRefitArgs W = wide_refit_args(*wt, s->d_pos, -1, 0, s->box_eps);
+    WideRefitArgs W = wide_refit_args(*wt, s->d_pos, -1, 0);
     if (s->wide_on) {
         const std::vector<WideBatch> wb = wide_refit_batches(*wt);
         for (size_t i = 0; i < wb.size(); ++i) {
             if (i + 1 == wb.size() && wb[i].blocks == 1) { W.l_deep = wb[i].l_deep; W.l_top = wb[i].l_top; break; }
-            WideRefitArgs A = wide_refit_args(*wt, s->d_pos, wb[i].l_deep, wb[i].l_top, s->box_eps);
+            WideRefitArgs A = wide_refit_args(*wt, s->d_pos, wb[i].l_deep, wb[i].l_top);
             k_wide_refit<<<wb[i].blocks, kRefitBlock, 0, st>>>(A);
         }
     }
@@ -2353,7 +2354,7 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
                         }
                 }
             } else {
-                closest_visit<false>(S, a, b, k, O, D, inv, tn[i], cur, h);
+                closest_visit<false>(S, a, b, k, O, D, inv, box_margin(S, inv), tn[i], cur, h);
             }
         }
         if (act) { prim_out[i] = (int32_t)((visits << 16) | (tris & 0xffff)); t_out[i] = occ ? 1.0f : 0.0f; }

@@ -186,7 +186,7 @@ __device__ __forceinline__ bool is_emitted(const BuildNode* N, int n, int c) {
     return true;
 }
 
-__global__ void k_emit(const BuildNode* N, int n, float4* out, float eps) {
+__global__ void k_emit(const BuildNode* N, int n, float4* out) {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     int total = 2 * n - 1;
     if (c >= total || !is_emitted(N, n, c)) return;
@@ -199,10 +199,8 @@ __global__ void k_emit(const BuildNode* N, int n, float4* out, float eps) {
     bool leaf = (c >= n - 1) || is_collapsed(N, n, c);
     int skip = idx + (leaf ? 1 : X.kept);
     int info = leaf ? ((X.first << 3) | (X.last - X.first)) : -1;
-    float l[3] = {X.lo[0], X.lo[1], X.lo[2]}, h[3] = {X.hi[0], X.hi[1], X.hi[2]};
-    box_inflate(l, h, eps);                                   // rs_wide.h box_epsilon
-    out[2 * idx] = make_float4(l[0], l[1], l[2], __int_as_float(skip));
-    out[2 * idx + 1] = make_float4(h[0], h[1], h[2], __int_as_float(info));
+    out[2 * idx] = make_float4(X.lo[0], X.lo[1], X.lo[2], __int_as_float(skip));
+    out[2 * idx + 1] = make_float4(X.hi[0], X.hi[1], X.hi[2], __int_as_float(info));
 }
 
 __global__ void k_leaf_tris(const float* __restrict__ pos, const uint64_t* keys, uint32_t n, float4* tris) {
@@ -224,7 +222,7 @@ __global__ void k_leaf_tris(const float* __restrict__ pos, const uint64_t* keys,
 
 // Builds the BVH for n triangles at d_pos (n*9 floats, device).  On success *d_nodes (2*n_nodes
 // float4) and *d_tris (3*n float4) are new device allocations owned by the caller.
-int build_bvh_lbvh(const float* d_pos, uint32_t n, float eps, hipStream_t st, float4** d_nodes, uint32_t* n_nodes,
+int build_bvh_lbvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes,
                    float4** d_tris, std::string& err) {
     *d_nodes = nullptr; *d_tris = nullptr; *n_nodes = 0;
     if (n == 0) return 0;
@@ -276,9 +274,9 @@ int build_bvh_lbvh(const float* d_pos, uint32_t n, float eps, hipStream_t st, fl
     BVH_CHECK(hipMemsetAsync(nodes + 2 * (size_t)kept_root, 0, 2 * sizeof(float4), st));
     BVH_CHECK(hipMalloc(&tris, (size_t)n * 3 * sizeof(float4)));
     if (n > 1) {
-        k_emit<<<gt, B, 0, st>>>(N, (int)n, nodes, eps);
+        k_emit<<<gt, B, 0, st>>>(N, (int)n, nodes);
     } else {
-        k_emit<<<1, B, 0, st>>>(N, 1, nodes, eps);
+        k_emit<<<1, B, 0, st>>>(N, 1, nodes);
     }
     k_leaf_tris<<<gn, B, 0, st>>>(d_pos, keys_sorted, n, tris);
     BVH_CHECK(hipGetLastError());
@@ -463,8 +461,7 @@ __global__ void k_ploc_leaf_init(int n, float* cost, int* kept, int* collapsed) 
 // preorder index + triangle-slot offset by walking to the root; emits the skip-pointer nodes and,
 // for every primitive leaf, its triangle in leaf order
 __global__ void k_ploc_emit(const float4* nlo, const float4* nhi, const int* parent, const int* cnt, const int* kept,
-                            const int* collapsed, int n, const float* __restrict__ pos, float4* out, float4* tris,
-                            float eps) {
+                            const int* collapsed, int n, const float* __restrict__ pos, float4* out, float4* tris) {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= 2 * n - 1) return;
     bool emitted = true;
@@ -487,10 +484,9 @@ __global__ void k_ploc_emit(const float4* nlo, const float4* nhi, const int* par
     bool leaf = (c < n) || collapsed[c];
     int skip = idx + (leaf ? 1 : kept[c]);
     int info = leaf ? ((off << 3) | (cnt[c] - 1)) : -1;
-    float l[3] = {nlo[c].x, nlo[c].y, nlo[c].z}, h[3] = {nhi[c].x, nhi[c].y, nhi[c].z};
-    box_inflate(l, h, eps);                                   // rs_wide.h box_epsilon
-    out[2 * idx] = make_float4(l[0], l[1], l[2], __int_as_float(skip));
-    out[2 * idx + 1] = make_float4(h[0], h[1], h[2], __int_as_float(info));
+    float4 a = nlo[c], b = nhi[c];
+    out[2 * idx] = make_float4(a.x, a.y, a.z, __int_as_float(skip));
+    out[2 * idx + 1] = make_float4(b.x, b.y, b.z, __int_as_float(info));
 }
 
 
@@ -534,7 +530,7 @@ void builder_pool_trim() {
         if (e_ != hipSuccess) { err = std::string(#x ": ") + hipGetErrorString(e_); goto fail; } \
     } while (0)
 
-int build_bvh_ploc(const float* d_pos, uint32_t n, float eps, hipStream_t st, float4** d_nodes, uint32_t* n_nodes,
+int build_bvh_ploc(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes,
                    float4** d_tris, std::string& err) {
     *d_nodes = nullptr; *d_tris = nullptr; *n_nodes = 0;
     if (n == 0) return 0;
@@ -634,7 +630,7 @@ int build_bvh_ploc(const float* d_pos, uint32_t n, float eps, hipStream_t st, fl
     PLOC_CHECK(hipMalloc(&nodes, ((size_t)kept_root + 1) * 2 * sizeof(float4)));
     PLOC_CHECK(hipMemsetAsync(nodes + 2 * (size_t)kept_root, 0, 2 * sizeof(float4), st));
     PLOC_CHECK(hipMalloc(&tris, (size_t)n * 3 * sizeof(float4)));
-    k_ploc_emit<<<(total + B - 1) / B, B, 0, st>>>(nlo, nhi, parent, cnt, kept, collapsed, (int)n, d_pos, nodes, tris, eps);
+    k_ploc_emit<<<(total + B - 1) / B, B, 0, st>>>(nlo, nhi, parent, cnt, kept, collapsed, (int)n, d_pos, nodes, tris);
     PLOC_CHECK(hipGetLastError());
     PLOC_CHECK(hipStreamSynchronize(st));
     *d_nodes = nodes; *d_tris = tris; *n_nodes = (uint32_t)kept_root;
@@ -655,8 +651,8 @@ fail: {
 // multi-workgroup launches always get l1 == l0 + 1
 __global__ void __launch_bounds__(kRefitBlock) k_refit(float4* nodes, float4* tris, const float* __restrict__ pos,
                                                        const int* __restrict__ order, const int* __restrict__ lvl_off,
-                                                       int l0, int l1, float eps) {
-    refit_levels(nodes, tris, pos, order, lvl_off, l0, l1, blockIdx.x, gridDim.x, eps);
+                                                       int l0, int l1) {
+    refit_levels(nodes, tris, pos, order, lvl_off, l0, l1, blockIdx.x, gridDim.x);
 }
 
 // node ids grouped by depth, deepest level first (host, once per topology)
@@ -694,13 +690,13 @@ int bvh_refit_plan(const float4* d_nodes, uint32_t n_nodes, hipStream_t st, int*
 // stream-ordered refit; no host synchronisation.  With *tail != nullptr a final single-workgroup
 // batch is not launched but returned (levels [tail[0], tail[1])) for the caller to fuse.
 int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_order, const int* d_lvl_off,
-              const std::vector<int>& lvl_off, float eps, hipStream_t st, int* tail, std::string& err) {
+              const std::vector<int>& lvl_off, hipStream_t st, int* tail, std::string& err) {
     const std::vector<RefitBatch> bs = refit_batches(lvl_off);
     if (tail) tail[0] = tail[1] = 0;
     for (size_t i = 0; i < bs.size(); ++i) {
         const RefitBatch& r = bs[i];
         if (tail && i + 1 == bs.size() && r.blocks == 1) { tail[0] = r.l0; tail[1] = r.l1; break; }
-        k_refit<<<r.blocks, kRefitBlock, 0, st>>>(d_nodes, d_tris, d_pos, d_order, d_lvl_off, r.l0, r.l1, eps);
+        k_refit<<<r.blocks, kRefitBlock, 0, st>>>(d_nodes, d_tris, d_pos, d_order, d_lvl_off, r.l0, r.l1);
     }
     if (hipGetLastError() != hipSuccess) { err = "refit launch failed"; return -1; }
     return 0;
@@ -710,7 +706,7 @@ int bvh_refit(float4* d_nodes, float4* d_tris, const float* d_pos, const int* d_
 // 8-wide tree of the per-lane walks from the positions alone (rs_wide_build.hip); it is optional: when it does
 // not apply (non-finite positions, no plan within the walk's depth) or its build fails, the scene keeps the
 // binary tree and the walks take the skip pointers (RESTIR_WIDE=off: never built).
-int build_wide_gpu(const float* d_pos, int n, float eps, hipStream_t st, WideBvh* w, std::string& err);
+int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::string& err);
 void preload_wide_build();
 // HIP loads a source file's code object at the first launch (or attribute query) of one of its kernels: at
 // context creation, so that a scene build is not charged the one-time load of the builders (~10 ms at C3)
@@ -726,16 +722,16 @@ void wide_free(WideBvh& w) {
     for (void* q : p) if (q) hipFree(q);
     w = WideBvh{};
 }
-int build_bvh(const float* d_pos, uint32_t n, float eps, hipStream_t st, float4** d_nodes, uint32_t* n_nodes,
-              float4** d_tris, WideBvh* wide, std::string& err) {
+int build_bvh(const float* d_pos, uint32_t n, hipStream_t st, float4** d_nodes, uint32_t* n_nodes, float4** d_tris,
+              WideBvh* wide, std::string& err) {
     const char* e = getenv("RESTIR_BVH");
     const char* w = getenv("RESTIR_WIDE");
     if (w && std::string(w) == "off") { if (wide) { wide_free(*wide); wide->status = RS_WIDE_OFF; } wide = nullptr; }
-    const int rc = (e && std::string(e) == "lbvh") ? build_bvh_lbvh(d_pos, n, eps, st, d_nodes, n_nodes, d_tris, err)
-                                                   : build_bvh_ploc(d_pos, n, eps, st, d_nodes, n_nodes, d_tris, err);
+    const int rc = (e && std::string(e) == "lbvh") ? build_bvh_lbvh(d_pos, n, st, d_nodes, n_nodes, d_tris, err)
+                                                   : build_bvh_ploc(d_pos, n, st, d_nodes, n_nodes, d_tris, err);
     if (rc != 0 || !wide) return rc;
     std::string werr;
-    if (const int wr = build_wide_gpu(d_pos, (int)n, eps, st, wide, werr); wr != 0) {   // optional: binary walks
+    if (const int wr = build_wide_gpu(d_pos, (int)n, st, wide, werr); wr != 0) {   // optional: binary walks
         const int why = wr < 0 ? RS_WIDE_ERROR : (wide->status ? wide->status : RS_WIDE_ERROR);
         wide_free(*wide);
         wide->status = why;

@@ -51,7 +51,7 @@ struct WideBvh {
 constexpr int kRefitBlock = RS_REFIT_BLOCK;
 constexpr int kRefitSmall = 4096;                // levels up to this many nodes go to the 1-block batch
 
-__device__ __forceinline__ void refit_node(float4* nodes, float4* tris, const float* __restrict__ pos, int i, float eps) {
+__device__ __forceinline__ void refit_node(float4* nodes, float4* tris, const float* __restrict__ pos, int i) {
     const float4 a = nodes[2 * i], b = nodes[2 * i + 1];
     const int leaf = __float_as_int(b.w);
     float l[3], h[3];
@@ -71,7 +71,6 @@ __device__ __forceinline__ void refit_node(float4* nodes, float4* tris, const fl
             tris[3 * k + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
             tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
         }
-        for (int ax = 0; ax < 3; ++ax) { l[ax] = l[ax] - eps; h[ax] = h[ax] + eps; }   // rs_wide.h box_epsilon
     } else {
         const int L = i + 1, R = __float_as_int(nodes[2 * L].w);
         const float4 al = nodes[2 * L], ah = nodes[2 * L + 1], bl = nodes[2 * R], bh = nodes[2 * R + 1];
@@ -85,11 +84,11 @@ __device__ __forceinline__ void refit_node(float4* nodes, float4* tris, const fl
 // levels [l0, l1) of the plan (one workgroup walks them with barriers in between)
 __device__ __forceinline__ void refit_levels(float4* nodes, float4* tris, const float* __restrict__ pos,
                                              const int* __restrict__ order, const int* __restrict__ lvl_off,
-                                             int l0, int l1, int block, int nblocks, float eps) {
+                                             int l0, int l1, int block, int nblocks) {
     for (int lv = l0; lv < l1; ++lv) {
         const int b = lvl_off[lv], e = lvl_off[lv + 1];
         for (int q = b + block * kRefitBlock + threadIdx.x; q < e; q += nblocks * kRefitBlock)
-            refit_node(nodes, tris, pos, order[q], eps);
+            refit_node(nodes, tris, pos, order[q]);
         if (lv + 1 < l1) __syncthreads();
     }
 }
@@ -121,7 +120,6 @@ struct WideRefitArgs {
     uint4* nodes; float4* tris; float4* box; const float* pos;
     int lvl[kWideLevels + 1];
     int l_deep, l_top;           // levels l_deep down to l_top (inclusive), deepest first; l_deep < l_top: none
-    float eps;                   // leaf-box inflation (rs_wide.h box_epsilon)
 };
 __device__ __forceinline__ void wide_refit_node(const WideRefitArgs& A, uint32_t j) {
     const uint4 w0 = A.nodes[5 * (size_t)j], w1 = A.nodes[5 * (size_t)j + 1];
@@ -147,7 +145,6 @@ __device__ __forceinline__ void wide_refit_node(const WideRefitArgs& A, uint32_t
             // stays encodable and its planes stay a superset of the finite triangles below
             if (!fin)
                 for (int a = 0; a < 3; ++a) kb[i].lo[a] = kb[i].hi[a] = 0.0f;
-            box_inflate(kb[i].lo, kb[i].hi, A.eps);          // interior slots' boxes are inflated unions already
             const float v0x = p[0], v0y = p[1], v0z = p[2];
             A.tris[3 * t] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
             A.tris[3 * t + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
@@ -188,8 +185,8 @@ inline std::vector<WideBatch> wide_refit_batches(const WideBvh& w) {
     }
     return out;
 }
-inline WideRefitArgs wide_refit_args(const WideBvh& w, const float* pos, int l_deep, int l_top, float eps) {
-    WideRefitArgs A{w.nodes, w.tris, w.box, pos, {}, l_deep, l_top, eps};
+inline WideRefitArgs wide_refit_args(const WideBvh& w, const float* pos, int l_deep, int l_top) {
+    WideRefitArgs A{w.nodes, w.tris, w.box, pos, {}, l_deep, l_top};
     for (int i = 0; i <= kWideLevels; ++i) A.lvl[i] = w.lvl[i];
     return A;
 }

@@ -44,6 +44,7 @@ struct DevScene {
     // the wave-sorted initial pass groups its shadow rays by (rs_passes.h k_gbuffer_initial_sorted)
     const uint8_t* ebucket;
     vec3 ecen;                // centre of the emitters' centroid bounds (the sorted spatial pass's target cells)
+    float box_eps;            // the closest-hit walks' box margin in scene units (rs_wide.h box_epsilon)
 };
 constexpr int kCdfGuide = 1024;
 
@@ -103,6 +104,20 @@ __device__ __forceinline__ bool box_test(float4 a, float4 b, vec3 o, vec3 inv, f
     return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
 }
 
+// the closest-hit walks' test: the box widened by `ew` = box_epsilon x |1/d| per axis in t (the margin in space
+// along each axis, rs_wide.h box_epsilon), so a triangle the test accepts is never culled with its box
+__device__ __forceinline__ bool box_test_m(float4 a, float4 b, vec3 o, vec3 inv, float tnear, float tfar, vec3 ew) {
+    float tx0 = (a.x - o.x) * inv.x, tx1 = (b.x - o.x) * inv.x;
+    float ty0 = (a.y - o.y) * inv.y, ty1 = (b.y - o.y) * inv.y;
+    float tz0 = (a.z - o.z) * inv.z, tz1 = (b.z - o.z) * inv.z;
+    float t0 = fmaxf(fmaxf(fmaxf(tnear, fminf(tx0, tx1) - ew.x), fminf(ty0, ty1) - ew.y), fminf(tz0, tz1) - ew.z);
+    float t1 = fminf(fminf(fminf(tfar, fmaxf(tx0, tx1) + ew.x), fmaxf(ty0, ty1) + ew.y), fmaxf(tz0, tz1) + ew.z);
+    return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
+}
+__device__ __forceinline__ vec3 box_margin(const DevScene& S, vec3 inv) {
+    return mk(S.box_eps * fabsf(inv.x), S.box_eps * fabsf(inv.y), S.box_eps * fabsf(inv.z));
+}
+
 struct Hit { float t, u, v; int prim; };
 
 // uniform-index load through the constant address space -> s_load (scalar cache), no VGPR address
@@ -133,9 +148,9 @@ __device__ __forceinline__ float4 ld4(const float4* p, uint32_t i) {
 // result does not depend on the visit order.
 template <bool Uniform>
 __device__ __forceinline__ void closest_visit(const DevScene& S, float4 a, float4 b, uint32_t i, vec3 o, vec3 d,
-                                              vec3 inv, float tnear, uint32_t& cur, Hit& h) {
+                                              vec3 inv, vec3 ew, float tnear, uint32_t& cur, Hit& h) {
     const uint32_t skip = (uint32_t)__float_as_int(a.w);
-    if (!box_test(a, b, o, inv, tnear, h.t)) { cur = skip; return; }
+    if (!box_test_m(a, b, o, inv, tnear, h.t, ew)) { cur = skip; return; }
     const int leaf = __float_as_int(b.w);
     if (leaf < 0) { cur = i + 1; return; }
     const int first = leaf >> 3, cnt = (leaf & 7) + 1;
@@ -187,13 +202,14 @@ __device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i
 __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i, vec3 o, vec3 d, vec3 inv, float tnear,
                                                   Hit& h) {
     const uint32_t n = S.n_nodes;
+    const vec3 ew = box_margin(S, inv);
     while (__ballot(i < n) != 0) {
         const bool live = i < n;
         const uint32_t ii = live ? i : 0u;
         const float4 a = S.nodes[2 * ii], b = S.nodes[2 * ii + 1];
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
-        const bool hit = live & box_test(a, b, o, inv, tnear, h.t);
+        const bool hit = live & box_test_m(a, b, o, inv, tnear, h.t, ew);
         const bool in_leaf = hit & (leaf >= 0);
         const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
         for (int j = 0; j < 8; ++j) {
@@ -265,7 +281,7 @@ struct WideStack {
 __device__ __forceinline__ float ubyte_f(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xffu); }
 // the 8 child boxes of node (w0..w4) against the ray; bit c = slot c hit (valid slots only)
 __device__ __forceinline__ uint32_t wide_hits(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, vec3 o, vec3 inv,
-                                              float tnear, float tfar) {
+                                              float tnear, float tfar, vec3 ew = vec3{0.0f, 0.0f, 0.0f}) {
     const uint32_t eb = w0.w;
     const vec3 s = mk(__uint_as_float((eb & 0xffu) << 23), __uint_as_float(((eb >> 8) & 0xffu) << 23),
                       __uint_as_float(((eb >> 16) & 0xffu) << 23));
@@ -274,8 +290,9 @@ __device__ __forceinline__ uint32_t wide_hits(uint4 w0, uint4 w1, uint4 w2, uint
                       (__uint_as_float(w0.z) - o.z) * inv.z);
     // per axis the near (far) t lowered (raised) by 2^-22 |b|: the rounding of b and of b -+ that bound
     // (an axis the ray is almost parallel to has a huge |b| and widens only itself)
-    const float ex = 2.384185791015625e-07f * fabsf(b.x), ey = 2.384185791015625e-07f * fabsf(b.y),
-                ez = 2.384185791015625e-07f * fabsf(b.z);
+    // (+ ew: the closest-hit walks' box margin, rs_wide.h box_epsilon; 0 for the any-hit walks)
+    const float ex = 2.384185791015625e-07f * fabsf(b.x) + ew.x, ey = 2.384185791015625e-07f * fabsf(b.y) + ew.y,
+                ez = 2.384185791015625e-07f * fabsf(b.z) + ew.z;
     const vec3 bn = mk(b.x - ex, b.y - ey, b.z - ez), bf = mk(b.x + ex, b.y + ey, b.z + ez);
     // near / far planes per axis by the direction's sign (lo bytes near for a positive direction)
     const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
@@ -306,6 +323,7 @@ __device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o
                                           float tfar, Hit& h, uint32_t& occ, uint32_t& lost, uint32_t* stats = nullptr) {
     uint32_t gb = 0u, gm = active ? 1u : 0u;       // root group: node 0, slot 0
     uint32_t n_fetch = 0u, n_tri = 0u;
+    const vec3 ew = Any ? mk(0.0f, 0.0f, 0.0f) : box_margin(S, inv);
     WideStack st;
     st.init();
     while (__ballot(gm != 0u) != 0) {
@@ -318,7 +336,7 @@ __device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o
         const uint4* P = S.wnodes + 5 * (size_t)node;
         const uint4 w0 = P[0], w1 = P[1], w2 = P[2], w3 = P[3], w4 = P[4];
         const float tf = Any ? tfar : h.t;
-        uint32_t hits = live ? wide_hits(w0, w1, w2, w3, w4, o, inv, tnear, tf) : 0u;
+        uint32_t hits = live ? wide_hits(w0, w1, w2, w3, w4, o, inv, tnear, tf, ew) : 0u;
         const uint32_t ni = (w0.w >> 24) & 0xfu;
         uint32_t tm = NoTri ? 0u : hits >> ni;      // leaf slots ni.. -> triangles tri_base + (slot - ni)
         const uint32_t tb = w1.y;
@@ -522,6 +540,7 @@ __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, ve
 __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     const bool full = __ballot(1) == ~0ull;
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const vec3 ew = box_margin(S, inv);
     Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
     const uint32_t n = S.n_nodes;
     uint32_t i = active ? 0u : 0xffffffffu;
@@ -532,7 +551,7 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
         const bool at = i == m;
-        const bool hb = at && box_test(a, b, o, inv, tnear, h.t);
+        const bool hb = at && box_test_m(a, b, o, inv, tnear, h.t, ew);
         if (leaf >= 0) {                                      // wave-uniform
             if (__ballot(hb) != 0) {
                 const int first = leaf >> 3, cnt = (leaf & 7) + 1;

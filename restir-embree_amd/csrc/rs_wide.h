@@ -47,15 +47,16 @@ inline uint32_t h_f2u(float f) { uint32_t i; std::memcpy(&i, &f, 4); return i; }
 RS_HD inline bool w_finite(float x) { return x - x == 0.0f; }
 RS_HD inline float w_min(float a, float b) { return b < a ? b : a; }   // std::min / std::max
 RS_HD inline float w_max(float a, float b) { return a < b ? b : a; }
-// Box inflation of every emitted BVH box (binary and 8-wide, build and refit), in scene units: 2^-16 x the scene's
-// largest |coordinate| (at least 1).  Moller-Trumbore accepts a hit from its barycentrics, but the point o + t d of
-// its t can lie outside the triangle's box by a few ulps of the coordinates (a ray through the shared edge of two
-// triangles, C3: 2.5e-6 m at 10 m); along an axis the ray crosses slowly that is far beyond the slab test's 4-eps
-// t margin, so a box could be culled with the closest (or an occluding) triangle inside -- and which box that is
-// depends on the tree: two trees, two answers (the oracle's binary and 8-wide trees disagreed on 1 of 8.3 M primary
-// rays, the GPU's PLOC tree on others).  Inflated by ~100x that error, no box is culled whose triangle the test
-// accepts, so every tree and walk returns the triangle test's own answer (ties: smaller t, then smaller index).
-// oracle/restir_oracle.c or_box_epsilon restates it.
+// The closest-hit walks' box margin, in scene units: 2^-16 x the scene's largest |coordinate| (at least 1).
+// Moller-Trumbore accepts a hit from its barycentrics, but the point o + t d of its t can lie outside the
+// triangle's box by a few ulps of the coordinates (a ray through the shared edge of two triangles, C3: 2.5e-6 m at
+// 10 m); along an axis the ray crosses slowly that is far beyond the slab test's 4-eps t margin, so a closest-hit
+// walk could cull the box of the tie-winning triangle after finding its neighbour -- and which box that is depends
+// on the tree (the oracle's binary and 8-wide trees disagreed on 1 of 8.3 M C3 4K primary rays).  The closest-hit
+// slab tests widen every box by this margin (rs_scene.h box_test_m, wide_hits), so every tree returns the triangle
+// test's own answer (ties: smaller t, then smaller index).  The any-hit (shadow) walks keep the exact boxes: a
+// margin on them lets every ray from a flat layer's surface (walls, the C2 light layer) enter the layer's thin
+// boxes, which cost the lockstep walk up to 3.8x (2^-16) and 3 % (2^-22) on C2.  oracle/restir_oracle.c restates it.
 inline float box_epsilon(const float* pos, size_t nfloats) {
     float m = 1.0f;
     for (size_t i = 0; i < nfloats; ++i) {
@@ -63,9 +64,6 @@ inline float box_epsilon(const float* pos, size_t nfloats) {
         if (w_finite(a) && a > m) m = a;
     }
     return m * (1.0f / 65536.0f);
-}
-RS_HD inline void box_inflate(float* lo, float* hi, float eps) {
-    for (int a = 0; a < 3; ++a) { lo[a] = lo[a] - eps; hi[a] = hi[a] + eps; }
 }
 // quantisation frame of one axis: s = 2^e >= extent / 255 and >= the float spacing at the box, o = a float
 // multiple of s <= lo with o + 255 s >= hi; every child box [clo, chi] quantises OUTWARD to bytes ql, qh with
@@ -339,7 +337,7 @@ struct SahCollapse {
 inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, std::vector<uint32_t>& out,
                            std::vector<int>& tri_prims, int& depth, std::string& err, int collapse = 0,
                            float c_node = 1.0f, float c_tri = 0.3f, int max_depth = 8,
-                           std::vector<int>* slot_src = nullptr, float eps = 0.0f) {   // optional: 8 per node, the source node of each slot
+                           std::vector<int>* slot_src = nullptr) {   // optional: 8 per node, the source node of each slot
     out.clear(); tri_prims.clear(); depth = 0;
     if (slot_src) slot_src->clear();
     if (n <= 0) return 0;
@@ -391,7 +389,7 @@ inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, 
         }
         for (int i = ni; i < nv; ++i) tri_prims.push_back(h_f2i(nhi[4 * (size_t)kids[i] + 3]));
         WBox kb[8], u;
-        for (int i = 0; i < nv; ++i) { kb[i] = box(kids[i]); box_inflate(kb[i].lo, kb[i].hi, eps); }
+        for (int i = 0; i < nv; ++i) kb[i] = box(kids[i]);
         uint32_t w[20];
         if (!wide_encode(kb, nv, ni, child_base, tri_base, w, &u)) {
             bool fin = true;

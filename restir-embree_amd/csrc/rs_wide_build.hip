@@ -781,7 +781,7 @@ __global__ void k_wide_kids(const WideQ* __restrict__ wq, int q0, int q1, int n,
 __global__ void k_wide_emit(WideQ* wq, int q0, int q1, int tri_off, const int* __restrict__ kids,
                             const int* __restrict__ n_int, const int* __restrict__ n_leaf, const int* __restrict__ s_int,
                             const int* __restrict__ s_leaf, const float4* __restrict__ nlo, const float4* __restrict__ nhi,
-                            uint4* nodes, float4* box, int* prims, int* bad, float eps) {
+                            uint4* nodes, float4* box, int* prims, int* bad) {
     const int i = q0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= q1) return;
     const int ni = n_int[i - q0], nv = ni + n_leaf[i - q0];
@@ -793,7 +793,6 @@ __global__ void k_wide_emit(WideQ* wq, int q0, int q1, int tri_off, const int* _
         const int x = kids[8 * (size_t)i + j];
         const float4 l = nlo[x], h = nhi[x];
         kb[j] = WBox{{l.x, l.y, l.z}, {h.x, h.y, h.z}};
-        box_inflate(kb[j].lo, kb[j].hi, eps);                    // rs_wide.h box_epsilon
         if (j < ni) wq[cb + j] = WideQ{x, g - 1};
         else prims[tb + (j - ni)] = __float_as_int(h.w);
     }
@@ -855,7 +854,7 @@ void preload_wide_build() {
     (void)hipFuncGetAttributes(&fa, (const void*)wb::k_small);
 }
 
-int build_wide_gpu(const float* d_pos, int n, float eps, hipStream_t st, WideBvh* w, std::string& err) {
+int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::string& err) {
     using namespace wb;
     *w = WideBvh{};
     if (n <= 0) { w->status = RS_WIDE_EMPTY; return 1; }
@@ -1013,7 +1012,7 @@ int build_wide_gpu(const float* d_pos, int n, float eps, hipStream_t st, WideBvh
         WB_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ni, si, cnt, st));
         WB_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, nl, sl, cnt, st));
         k_wide_emit<<<(cnt + kB - 1) / kB, kB, 0, st>>>(wq, q0, q1, tri_off, kidv, ni, nl, si, sl, nlo, nhi, nodes_s, box_s,
-                                                          prims, bad, eps);
+                                                          prims, bad);
         WB_HIP(hipGetLastError());
         int h[5];
         k_level_totals<<<1, 64, 0, st>>>(si, ni, sl, nl, cnt, bad, tot5);   // one read-back per level

@@ -167,9 +167,7 @@ int wide_build_host(const float* pos, int n, uint32_t* words, int cap_nodes, int
     std::vector<int> P;
     int depth = 0;
     std::string err;
-    // the product inflates every emitted box by the scene's box_epsilon (rs_wide.h); so does this restatement
-    if (rs::build_wide_host(nlo.data(), nhi.data(), n, root, W, P, depth, err, 1, 1.0f, 0.3f, 8, nullptr,
-                            rs::box_epsilon(pos, 9 * (size_t)n)) != 0) return -1;
+    if (rs::build_wide_host(nlo.data(), nhi.data(), n, root, W, P, depth, err, 1) != 0) return -1;
     const int nn = (int)(W.size() / 20);
     if (nn > cap_nodes) return -3;
     std::memcpy(words, W.data(), W.size() * sizeof(uint32_t));
