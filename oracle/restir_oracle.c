@@ -270,7 +270,8 @@ typedef struct {
     float total_area;
     /* BVH */
     or_node* nodes; int n_nodes; uint32_t* tri_index;
-    struct or_wnode* wn; int n_wn;   /* 8-wide tree over the same leaves (or_scene_set_wide), or NULL */
+    struct or_wnode* wn; int n_wn;
+    float box_eps;                   /* the closest-hit walks' box margin (or_box_epsilon) */   /* 8-wide tree over the same leaves (or_scene_set_wide), or NULL */
     /* textures: per-material map slots (0-based, -1 none: diffuse, specular,
        shininess, normal), per-triangle uv (6) / tangents (9), textures in FreeImage layout, sky */
     int32_t* maps; float* uv; float* tan;
@@ -302,6 +303,20 @@ static float bb_area(const aabb* b) {
 }
 
 typedef struct { aabb* tb; float* cen; uint32_t* idx; or_node* nodes; int n_nodes; } bvh_build_t;
+
+/* the closest-hit walks' box margin: 2^-16 x the scene's largest |coordinate| (at least 1), restating rs_wide.h
+ * box_epsilon.  Moller-Trumbore accepts hits whose point o + t d lies a few ulps outside the triangle's box; without
+ * a margin a closest-hit walk can cull that box after finding a tied neighbour, and which box that is depends on the
+ * tree (this oracle's binary and 8-wide trees disagreed on 1 of 8.3 M C3 4K primary rays).  With it every tree
+ * returns the triangle test's answer.  The any-hit walks keep the exact boxes (as the kernels do). */
+static float or_box_epsilon(const float* pos, size_t nfloats) {
+    float m = 1.0f;
+    for (size_t i = 0; i < nfloats; ++i) {
+        const float a = fabsf(pos[i]);
+        if (a - a == 0.0f && a > m) m = a;
+    }
+    return m * (1.0f / 65536.0f);
+}
 
 static int bvh_build_rec(bvh_build_t* B, int first, int count) {
     int ni = B->n_nodes++;
@@ -421,6 +436,7 @@ or_scene* or_scene_create(uint32_t n_tris, const float* pos, const float* nrm, c
         for (int a = 0; a < 3; ++a) B.cen[3 * t + a] = 0.5f * (B.tb[t].lo[a] + B.tb[t].hi[a]);
         B.idx[t] = t;
     }
+    s->box_eps = or_box_epsilon(pos, 9 * (size_t)n_tris);
     if (n_tris) bvh_build_rec(&B, 0, (int)n_tris);
     s->nodes = B.nodes; s->n_nodes = B.n_nodes; s->tri_index = B.idx;
     free(B.tb); free(B.cen);
@@ -565,15 +581,9 @@ static void apply_maps(const or_scene* s, uint32_t prim, float u, float v, uint3
 }
 
 /* ------------------------------------------------------------------ ray queries */
-static inline int box_hit(const or_node* n, v3 o, v3 inv, float tnear, float tfar, float* tentry);
 /* Moller-Trumbore with fixed operation order; the HIP product uses the same arithmetic.
- * Replaces Embree's rtcIntersect1/rtcOccluded1 triangle test (pg/Intersection.h:43-83).
- * Box-consistency rule (restates rs_scene.h tri_box_ok): a hit at t counts only if the slab test of the
- * triangle's own box passes on [tnear, t] -- Moller-Trumbore can accept a hit whose point o + t d lies a few ulps
- * outside the triangle's box (an edge shared with a box face), which a slab test of some tree would cull; with the
- * rule no tree culls an accepted triangle (the slab test is monotone in the box and in tfar), so the oracle's
- * binary and 8-wide trees and the kernels' PLOC and 8-wide trees all return the same hits. */
-static inline int tri_hit(const or_scene* s, uint32_t t, v3 o, v3 d, v3 dinv, float tnear, float tfar,
+ * Replaces Embree's rtcIntersect1/rtcOccluded1 triangle test (pg/Intersection.h:43-83). */
+static inline int tri_hit(const or_scene* s, uint32_t t, v3 o, v3 d, float tnear, float tfar,
                           float* tt, float* uu, float* vv) {
     v3 v0 = s->p0[t];
     v3 e1 = sub(s->p1[t], v0), e2 = sub(s->p2[t], v0);
@@ -589,27 +599,20 @@ static inline int tri_hit(const or_scene* s, uint32_t t, v3 o, v3 d, v3 dinv, fl
     if (!(v >= 0.0f && u + v <= 1.0f)) return 0;
     float t_ = dot(e2, q) * inv;
     if (!(t_ >= tnear && t_ <= tfar)) return 0;
-    {
-        const v3 a = s->p0[t], b = s->p1[t], c = s->p2[t];
-        or_node tb;
-        tb.lo[0] = gmin(gmin(a.x, b.x), c.x); tb.lo[1] = gmin(gmin(a.y, b.y), c.y); tb.lo[2] = gmin(gmin(a.z, b.z), c.z);
-        tb.hi[0] = gmax(gmax(a.x, b.x), c.x); tb.hi[1] = gmax(gmax(a.y, b.y), c.y); tb.hi[2] = gmax(gmax(a.z, b.z), c.z);
-        float te;
-        if (!box_hit(&tb, o, dinv, tnear, t_, &te)) return 0;
-    }
     *tt = t_; *uu = u; *vv = v;
     return 1;
 }
 
 /* conservative slab test: interval widened by (1 +- 4 eps) so it never culls a box whose
    contents the triangle test would accept */
-static inline int box_hit(const or_node* n, v3 o, v3 inv, float tnear, float tfar, float* tentry) {
+static inline int box_hit(const or_node* n, v3 o, v3 inv, float tnear, float tfar, float* tentry, const float* ew) {
     float oo[3] = {o.x, o.y, o.z}, ii[3] = {inv.x, inv.y, inv.z};
     float t0 = tnear, t1 = tfar;
     for (int a = 0; a < 3; ++a) {
         float ta = (n->lo[a] - oo[a]) * ii[a];
         float tb = (n->hi[a] - oo[a]) * ii[a];
         float mn = fminf(ta, tb), mx = fmaxf(ta, tb);
+        if (ew) { mn = mn - ew[a]; mx = mx + ew[a]; }   /* closest-hit margin (or_box_epsilon) */
         t0 = fmaxf(t0, mn); t1 = fminf(t1, mx);
     }
     *tentry = t0;
@@ -625,15 +628,16 @@ static or_hit closest_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar
     if (!s->n_nodes) return h;
     if (s->wn) return closest_hit_wide(s, o, d, tnear, tfar);
     v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float ew[3] = {s->box_eps * fabsf(inv.x), s->box_eps * fabsf(inv.y), s->box_eps * fabsf(inv.z)};
     int stack[128]; int sp = 0; stack[sp++] = 0;
     while (sp) {
         const or_node* n = &s->nodes[stack[--sp]];
         float te;
-        if (!box_hit(n, o, inv, tnear, h.t, &te)) continue;
+        if (!box_hit(n, o, inv, tnear, h.t, &te, ew)) continue;
         if (n->count) {
             for (int i = n->first; i < n->first + n->count; ++i) {
                 uint32_t t = s->tri_index[i]; float tt, uu, vv;
-                if (tri_hit(s, t, o, d, inv, tnear, h.t, &tt, &uu, &vv)) {
+                if (tri_hit(s, t, o, d, tnear, h.t, &tt, &uu, &vv)) {
                     if (!h.hit || tt < h.t || (tt == h.t && t < h.prim)) {
                         h.hit = 1; h.t = tt; h.u = uu; h.v = vv; h.prim = t;
                     }
@@ -654,11 +658,11 @@ static int any_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
     while (sp) {
         const or_node* n = &s->nodes[stack[--sp]];
         float te;
-        if (!box_hit(n, o, inv, tnear, tfar, &te)) continue;
+        if (!box_hit(n, o, inv, tnear, tfar, &te, NULL)) continue;
         if (n->count) {
             for (int i = n->first; i < n->first + n->count; ++i) {
                 float tt, uu, vv;
-                if (tri_hit(s, s->tri_index[i], o, d, inv, tnear, tfar, &tt, &uu, &vv)) return 1;
+                if (tri_hit(s, s->tri_index[i], o, d, tnear, tfar, &tt, &uu, &vv)) return 1;
             }
         } else {
             stack[sp++] = n->right; stack[sp++] = n->left;
@@ -717,15 +721,16 @@ int or_scene_set_wide(or_scene* s, int on) {
 
 /* box_hit for the 8 children: bit c = child c accepted; tentry[c] = its entry t */
 __attribute__((target("avx2"))) static inline uint32_t box8(const or_wnode* w, const __m256* O, const __m256* I,
-                                                              float tnear, float tfar, float* tentry) {
+                                                              float tnear, float tfar, float* tentry, const __m256* E) {
     __m256 t0 = _mm256_set1_ps(tnear), t1 = _mm256_set1_ps(tfar);
     for (int a = 0; a < 3; ++a) {
         const __m256 ta = _mm256_mul_ps(_mm256_sub_ps(_mm256_loadu_ps(w->lo[a]), O[a]), I[a]);
         const __m256 tb = _mm256_mul_ps(_mm256_sub_ps(_mm256_loadu_ps(w->hi[a]), O[a]), I[a]);
         const __m256 nb = _mm256_cmp_ps(tb, tb, _CMP_UNORD_Q);
         /* fminf / fmaxf(ta, tb): the non-NaN operand if one is NaN (min_ps/max_ps return tb then) */
-        const __m256 mn = _mm256_blendv_ps(_mm256_min_ps(ta, tb), ta, nb);
-        const __m256 mx = _mm256_blendv_ps(_mm256_max_ps(ta, tb), ta, nb);
+        __m256 mn = _mm256_blendv_ps(_mm256_min_ps(ta, tb), ta, nb);
+        __m256 mx = _mm256_blendv_ps(_mm256_max_ps(ta, tb), ta, nb);
+        if (E) { mn = _mm256_sub_ps(mn, E[a]); mx = _mm256_add_ps(mx, E[a]); }   /* closest-hit margin */
         t0 = _mm256_max_ps(mn, t0);   /* fmaxf(t0, mn): t0 when mn is NaN */
         t1 = _mm256_min_ps(mx, t1);
     }
@@ -743,7 +748,7 @@ __attribute__((target("avx2"))) static int any_hit_wide(const or_scene* s, v3 o,
     float te[8];
     while (sp) {
         const or_wnode* w = &s->wn[stack[--sp]];
-        uint32_t m = box8(w, O, I, tnear, tfar, te);
+        uint32_t m = box8(w, O, I, tnear, tfar, te, NULL);
         while (m) {
             const int c = __builtin_ctz(m); m &= m - 1;
             const int32_t k = w->kid[c];
@@ -751,7 +756,7 @@ __attribute__((target("avx2"))) static int any_hit_wide(const or_scene* s, v3 o,
             const or_node* n = &s->nodes[~k];
             for (int i = n->first; i < n->first + n->count; ++i) {
                 float tt, uu, vv;
-                if (tri_hit(s, s->tri_index[i], o, d, inv, tnear, tfar, &tt, &uu, &vv)) return 1;
+                if (tri_hit(s, s->tri_index[i], o, d, tnear, tfar, &tt, &uu, &vv)) return 1;
             }
         }
     }
@@ -765,11 +770,13 @@ __attribute__((target("avx2"))) static or_hit closest_hit_wide(const or_scene* s
     const v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const __m256 O[3] = {_mm256_set1_ps(o.x), _mm256_set1_ps(o.y), _mm256_set1_ps(o.z)};
     const __m256 I[3] = {_mm256_set1_ps(inv.x), _mm256_set1_ps(inv.y), _mm256_set1_ps(inv.z)};
+    const __m256 E[3] = {_mm256_set1_ps(s->box_eps * fabsf(inv.x)), _mm256_set1_ps(s->box_eps * fabsf(inv.y)),
+                         _mm256_set1_ps(s->box_eps * fabsf(inv.z))};
     int stack[OR_WSTACK]; int sp = 0; stack[sp++] = 0;
     float te[8];
     while (sp) {
         const or_wnode* w = &s->wn[stack[--sp]];
-        uint32_t m = box8(w, O, I, tnear, h.t, te);
+        uint32_t m = box8(w, O, I, tnear, h.t, te, E);
         int near[8]; int nn = 0;
         while (m) {
             const int c = __builtin_ctz(m); m &= m - 1;
@@ -783,7 +790,7 @@ __attribute__((target("avx2"))) static or_hit closest_hit_wide(const or_scene* s
             const or_node* n = &s->nodes[~k];
             for (int i = n->first; i < n->first + n->count; ++i) {
                 uint32_t t = s->tri_index[i]; float tt, uu, vv;
-                if (tri_hit(s, t, o, d, inv, tnear, h.t, &tt, &uu, &vv)) {
+                if (tri_hit(s, t, o, d, tnear, h.t, &tt, &uu, &vv)) {
                     if (!h.hit || tt < h.t || (tt == h.t && t < h.prim)) {
                         h.hit = 1; h.t = tt; h.u = uu; h.v = vv; h.prim = t;
                     }
@@ -903,28 +910,6 @@ typedef struct {
     int gy0, gy1;             /* G-buffer rows available (tile band + margin) */
 } fctx;
 
-/* diagnostic (scripts/parity_probe.py): record every occlusion ray whose origin is one of up to 16 given points --
- * origin, direction, tnear, tfar, result (9 floats) -- into a caller buffer */
-static struct { int n_pts; float pts[16][3]; float* buf; int cap; int count; } g_rec;
-void or_record_rays(int n_pts, const float* pts, float* buf, int cap) {
-    g_rec.n_pts = n_pts < 16 ? n_pts : 16;
-    for (int i = 0; i < g_rec.n_pts; ++i) for (int a = 0; a < 3; ++a) g_rec.pts[i][a] = pts[3 * i + a];
-    g_rec.buf = buf; g_rec.cap = cap; g_rec.count = 0;
-}
-int or_recorded_rays(void) { return g_rec.count; }
-static void record_ray(v3 o, v3 d, float tnear, float tfar, int res) {
-    for (int i = 0; i < g_rec.n_pts; ++i)
-        if (o.x == g_rec.pts[i][0] && o.y == g_rec.pts[i][1] && o.z == g_rec.pts[i][2]) {
-            const int k = __atomic_fetch_add(&g_rec.count, 1, __ATOMIC_RELAXED);
-            if (k < g_rec.cap) {
-                float* r = g_rec.buf + 9 * (size_t)k;
-                r[0] = o.x; r[1] = o.y; r[2] = o.z; r[3] = d.x; r[4] = d.y; r[5] = d.z; r[6] = tnear; r[7] = tfar;
-                r[8] = (float)res;
-            }
-            return;
-        }
-}
-
 /* Intersection::testOcclusion (pg/Intersection.h:43-60) */
 static int occluded(const fctx* F, v3 from, v3 to, uint64_t* rays) {
     float dist = len(sub(to, from));
@@ -932,9 +917,7 @@ static int occluded(const fctx* F, v3 from, v3 to, uint64_t* rays) {
     float tnear = FLT_MIN + F->P->tnear_offset;
     float tfar = dist - F->P->tfar_offset;
     (*rays)++;
-    const int res = any_hit(F->s, from, dir, tnear, tfar);
-    if (g_rec.n_pts) record_ray(from, dir, tnear, tfar, res);
-    return res;
+    return any_hit(F->s, from, dir, tnear, tfar);
 }
 
 /* Intersection::intersectEmbree + getGeometryAttributes (pg/Intersection.h:8-41,85-113) */

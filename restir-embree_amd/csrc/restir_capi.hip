@@ -44,6 +44,7 @@ struct rs_scene {
     float* d_cdf = nullptr;
     int* d_cdf_guide = nullptr;
     float build_ms = 0.0f;
+    float box_eps = 0.0f;                 // closest-hit box margin (rs_wide.h box_epsilon), set at the last full build
     // host copies (rs_scene_rebuild re-derives the tables on the host)
     std::vector<float> h_nrm;
     std::vector<uint32_t> h_tri_mat;
@@ -97,6 +98,7 @@ struct rs_scene {
         S.wnodes = wide_on ? wide.nodes : nullptr; S.wtris = wide.tris; S.n_wnodes = wide_on ? wide.n_nodes : 0u;
         S.ebucket = d_ebucket;
         S.ecen = vec3{ecen[0], ecen[1], ecen[2]};
+        S.box_eps = box_eps;
         return S;
     }
     // the geometry of generation `g` if this scene still holds it (current, or the a_* copy of g == a_geo)
@@ -872,6 +874,7 @@ static int build_geometry(rs_context* c, rs_scene* s, const std::vector<float>& 
     hipEventCreate(&e0); hipEventCreate(&e1);
     hipEventRecord(e0, st);
     std::string berr;
+    s->box_eps = box_epsilon(pos.data(), pos.size());
     int rc = build_bvh(s->d_pos, n, st, &s->d_nodes, &s->n_nodes, &s->d_tris, &s->wide, berr);
     s->wide_on = rc == 0 && s->wide.n_nodes > 0 && s->wide.depth <= kWideStack;   // deeper: the skip pointers
     hipEventRecord(e1, st);
@@ -2347,11 +2350,11 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
                             const float4* T = S.tris + 3 * ((leaf >> 3) + j);
                             float t, u, v;
                             ++tris;
-                            occ = tri_test(T[0], T[1], T[2], O, D, inv, tn[i], tf[i], t, u, v);
+                            occ = tri_test(T[0], T[1], T[2], O, D, tn[i], tf[i], t, u, v);
                         }
                 }
             } else {
-                closest_visit<false>(S, a, b, k, O, D, inv, tn[i], cur, h);
+                closest_visit<false>(S, a, b, k, O, D, inv, box_margin(S, inv), tn[i], cur, h);
             }
         }
         if (act) { prim_out[i] = (int32_t)((visits << 16) | (tris & 0xffff)); t_out[i] = occ ? 1.0f : 0.0f; }

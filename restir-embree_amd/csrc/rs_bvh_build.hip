@@ -12,7 +12,7 @@
 //   7 k_emit          collapse subtrees of <= kLeafMax triangles into leaves, preorder index by
 //                     walking up (idx = idx(parent) + 1 + [right child] * kept(left sibling)),
 //                     write the 32-B skip-pointer nodes
-//   8 k_leaf_tris     triangles in leaf order as (p0, prim), (p1), (p2): the exact vertices (rs_scene.h tri_test)
+//   8 k_leaf_tris     triangles in leaf order as (v0, prim), (e1), (e2)
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -210,8 +210,8 @@ __global__ void k_leaf_tris(const float* __restrict__ pos, const uint64_t* keys,
     const float* p = pos + 9 * (size_t)prim;
     float v0x = p[0], v0y = p[1], v0z = p[2];
     tris[3 * k] = make_float4(v0x, v0y, v0z, __int_as_float((int)prim));
-    tris[3 * k + 1] = make_float4(p[3], p[4], p[5], 0.0f);
-    tris[3 * k + 2] = make_float4(p[6], p[7], p[8], 0.0f);
+    tris[3 * k + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
+    tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
 }
 
 #define BVH_CHECK(x)                                                                   \
@@ -477,8 +477,8 @@ __global__ void k_ploc_emit(const float4* nlo, const float4* nhi, const int* par
         const float* p = pos + 9 * (size_t)prim;
         float v0x = p[0], v0y = p[1], v0z = p[2];
         tris[3 * off] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
-        tris[3 * off + 1] = make_float4(p[3], p[4], p[5], 0.0f);
-        tris[3 * off + 2] = make_float4(p[6], p[7], p[8], 0.0f);
+        tris[3 * off + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
+        tris[3 * off + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
     }
     if (!emitted) return;
     bool leaf = (c < n) || collapsed[c];

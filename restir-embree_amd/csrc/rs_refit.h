@@ -68,8 +68,8 @@ __device__ __forceinline__ void refit_node(float4* nodes, float4* tris, const fl
             }
             const float v0x = p[0], v0y = p[1], v0z = p[2];
             tris[3 * k] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
-            tris[3 * k + 1] = make_float4(p[3], p[4], p[5], 0.0f);
-            tris[3 * k + 2] = make_float4(p[6], p[7], p[8], 0.0f);
+            tris[3 * k + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
+            tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
         }
     } else {
         const int L = i + 1, R = __float_as_int(nodes[2 * L].w);
@@ -147,8 +147,8 @@ __device__ __forceinline__ void wide_refit_node(const WideRefitArgs& A, uint32_t
                 for (int a = 0; a < 3; ++a) kb[i].lo[a] = kb[i].hi[a] = 0.0f;
             const float v0x = p[0], v0y = p[1], v0z = p[2];
             A.tris[3 * t] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
-            A.tris[3 * t + 1] = make_float4(p[3], p[4], p[5], 0.0f);
-            A.tris[3 * t + 2] = make_float4(p[6], p[7], p[8], 0.0f);
+            A.tris[3 * t + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
+            A.tris[3 * t + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
         }
     }
     uint32_t w[20];

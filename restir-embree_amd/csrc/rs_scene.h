@@ -38,12 +38,13 @@ struct DevScene {
     int sky;                  // texture index of the equirect sky, -1 none
     // 8-wide tree of the per-lane walks (rs_bvh_build.hip build_wide); n_wnodes = 0: skip-pointer walks
     const uint4* wnodes;      // 5 per node
-    const float4* wtris;      // 3 per wide-leaf triangle: (p0, prim) (p1) (p2) -- the exact vertices (tri_test)
+    const float4* wtris;      // 3 per wide-leaf triangle: (v0, prim) (e1) (e2)
     uint32_t n_wnodes;
     // per emissive triangle: its bucket (0..63) in the Morton order of the emitters' centroids -- the key
     // the wave-sorted initial pass groups its shadow rays by (rs_passes.h k_gbuffer_initial_sorted)
     const uint8_t* ebucket;
     vec3 ecen;                // centre of the emitters' centroid bounds (the sorted spatial pass's target cells)
+    float box_eps;            // the closest-hit walks' box margin in scene units (rs_wide.h box_epsilon)
 };
 constexpr int kCdfGuide = 1024;
 
@@ -55,36 +56,10 @@ enum Trav : int { TRAV_LOCKSTEP = 0, TRAV_LANE = 1, TRAV_WIDE = 2 };
 constexpr bool trav_lane(int T) { return (T & TRAV_LANE) != 0; }
 constexpr bool trav_wide(int T) { return (T & TRAV_WIDE) != 0; }
 
-// conservative slab test (interval widened by 4 ulp-ish so no box the triangle test accepts is culled)
-__device__ __forceinline__ bool box_test(float4 a, float4 b, vec3 o, vec3 inv, float tnear, float tfar) {
-    float tx0 = (a.x - o.x) * inv.x, tx1 = (b.x - o.x) * inv.x;
-    float ty0 = (a.y - o.y) * inv.y, ty1 = (b.y - o.y) * inv.y;
-    float tz0 = (a.z - o.z) * inv.z, tz1 = (b.z - o.z) * inv.z;
-    float t0 = fmaxf(fmaxf(fmaxf(tnear, fminf(tx0, tx1)), fminf(ty0, ty1)), fminf(tz0, tz1));
-    float t1 = fminf(fminf(fminf(tfar, fmaxf(tx0, tx1)), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-    return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
-}
-
-// The triangle record (leaf order): A = (p0, prim bits), B = (p1, 0), C = (p2, 0) -- the exact vertices, so the
-// triangle's own box min/max(p0, p1, p2) is exactly the box every tree's leaf and ancestors contain.
-//
-// Moller-Trumbore, fixed op order (identical to oracle/restir_oracle.c tri_hit), plus a box-consistency rule: a
-// hit at t counts only if the slab test of the triangle's own box passes on [tnear, t].  Moller-Trumbore decides
-// from its barycentrics, but the point o + t d can lie a few ulps outside the triangle's box (a ray through an
-// edge shared with a box face, C3 4K: the hit point on a flat lamp's box edge seen by a ray with |d.x| = 0.004),
-// where a slab test culls it -- and which box culls it depends on the tree (PLOC vs SAH, binary vs 8-wide): two
-// trees, two answers (1 ray in ~1e8-1e9).  The slab test is monotone in the box and in tfar, so every ancestor box
-// of an accepted triangle passes it too: every tree and walk kind reaches every accepted triangle, and any-hit and
-// closest-hit results (ties: smaller t, then smaller index) no longer depend on the tree.  The rule only rejects
-// such edge hits (no hit the slab test of the triangle's box already rejects could be found by a walk anyway).
-__device__ __forceinline__ bool tri_box_ok(float4 A, float4 B, float4 C, vec3 o, vec3 inv, float tnear, float t) {
-    const float4 lo = make_float4(gmin(gmin(A.x, B.x), C.x), gmin(gmin(A.y, B.y), C.y), gmin(gmin(A.z, B.z), C.z), 0.0f);
-    const float4 hi = make_float4(gmax(gmax(A.x, B.x), C.x), gmax(gmax(A.y, B.y), C.y), gmax(gmax(A.z, B.z), C.z), 0.0f);
-    return box_test(lo, hi, o, inv, tnear, t);
-}
-__device__ __forceinline__ bool tri_test(float4 A, float4 B, float4 C, vec3 o, vec3 d, vec3 dinv, float tnear,
+// Moller-Trumbore, fixed op order (identical to oracle/restir_oracle.c tri_hit)
+__device__ __forceinline__ bool tri_test(float4 A, float4 B, float4 C, vec3 o, vec3 d, float tnear,
                                          float tfar, float& t_out, float& u_out, float& v_out) {
-    vec3 v0 = xyz(A), e1 = xyz(B) - v0, e2 = xyz(C) - v0;
+    vec3 v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
     vec3 p = cross(d, e2);
     float det = dot(e1, p);
     if (det == 0.0f) return false;
@@ -97,18 +72,16 @@ __device__ __forceinline__ bool tri_test(float4 A, float4 B, float4 C, vec3 o, v
     if (!(v >= 0.0f && u + v <= 1.0f)) return false;
     float t = dot(e2, q) * inv;
     if (!(t >= tnear && t <= tfar)) return false;
-    if (!tri_box_ok(A, B, C, o, dinv, tnear, t)) return false;
     t_out = t; u_out = u; v_out = v;
     return true;
 }
 
 // The same test without early returns (identical arithmetic and acceptance; with det == 0 the
 // quotients are inf/NaN and the explicit det check rejects).  Used by the lockstep walks, where the
-// triangle is shared by the wave: straight-line VALU instead of three nested exec-mask regions.  Every lane of
-// the wave must make the call (the box rule runs only when some lane's Moller-Trumbore accepted).
-__device__ __forceinline__ bool tri_test_nb(float4 A, float4 B, float4 C, vec3 o, vec3 d, vec3 dinv, float tnear,
-                                            float tfar, float& t, float& u, float& v) {
-    vec3 v0 = xyz(A), e1 = xyz(B) - v0, e2 = xyz(C) - v0;
+// triangle is shared by the wave: straight-line VALU instead of three nested exec-mask regions.
+__device__ __forceinline__ bool tri_test_nb(float4 A, float4 B, float4 C, vec3 o, vec3 d, float tnear, float tfar,
+                                            float& t, float& u, float& v) {
+    vec3 v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
     vec3 p = cross(d, e2);
     float det = dot(e1, p);
     float inv = 1.0f / det;
@@ -118,9 +91,31 @@ __device__ __forceinline__ bool tri_test_nb(float4 A, float4 B, float4 C, vec3 o
     v = dot(d, q) * inv;
     t = dot(e2, q) * inv;
     const bool ok_u = u >= 0.0f && u <= 1.0f, ok_v = v >= 0.0f && u + v <= 1.0f, ok_t = t >= tnear && t <= tfar;
-    bool hit = (det != 0.0f) & ok_u & ok_v & ok_t;
-    if (__ballot(hit) != 0) hit = hit && tri_box_ok(A, B, C, o, dinv, tnear, t);
-    return hit;
+    return (det != 0.0f) & ok_u & ok_v & ok_t;
+}
+
+// conservative slab test (interval widened by 4 ulp-ish so no box the triangle test accepts is culled)
+__device__ __forceinline__ bool box_test(float4 a, float4 b, vec3 o, vec3 inv, float tnear, float tfar) {
+    float tx0 = (a.x - o.x) * inv.x, tx1 = (b.x - o.x) * inv.x;
+    float ty0 = (a.y - o.y) * inv.y, ty1 = (b.y - o.y) * inv.y;
+    float tz0 = (a.z - o.z) * inv.z, tz1 = (b.z - o.z) * inv.z;
+    float t0 = fmaxf(fmaxf(fmaxf(tnear, fminf(tx0, tx1)), fminf(ty0, ty1)), fminf(tz0, tz1));
+    float t1 = fminf(fminf(fminf(tfar, fmaxf(tx0, tx1)), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
+}
+
+// the closest-hit walks' test: the box widened by `ew` = box_epsilon x |1/d| per axis in t (the margin in space
+// along each axis, rs_wide.h box_epsilon), so a triangle the test accepts is never culled with its box
+__device__ __forceinline__ bool box_test_m(float4 a, float4 b, vec3 o, vec3 inv, float tnear, float tfar, vec3 ew) {
+    float tx0 = (a.x - o.x) * inv.x, tx1 = (b.x - o.x) * inv.x;
+    float ty0 = (a.y - o.y) * inv.y, ty1 = (b.y - o.y) * inv.y;
+    float tz0 = (a.z - o.z) * inv.z, tz1 = (b.z - o.z) * inv.z;
+    float t0 = fmaxf(fmaxf(fmaxf(tnear, fminf(tx0, tx1) - ew.x), fminf(ty0, ty1) - ew.y), fminf(tz0, tz1) - ew.z);
+    float t1 = fminf(fminf(fminf(tfar, fmaxf(tx0, tx1) + ew.x), fmaxf(ty0, ty1) + ew.y), fmaxf(tz0, tz1) + ew.z);
+    return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
+}
+__device__ __forceinline__ vec3 box_margin(const DevScene& S, vec3 inv) {
+    return mk(S.box_eps * fabsf(inv.x), S.box_eps * fabsf(inv.y), S.box_eps * fabsf(inv.z));
 }
 
 struct Hit { float t, u, v; int prim; };
@@ -153,9 +148,9 @@ __device__ __forceinline__ float4 ld4(const float4* p, uint32_t i) {
 // result does not depend on the visit order.
 template <bool Uniform>
 __device__ __forceinline__ void closest_visit(const DevScene& S, float4 a, float4 b, uint32_t i, vec3 o, vec3 d,
-                                              vec3 inv, float tnear, uint32_t& cur, Hit& h) {
+                                              vec3 inv, vec3 ew, float tnear, uint32_t& cur, Hit& h) {
     const uint32_t skip = (uint32_t)__float_as_int(a.w);
-    if (!box_test(a, b, o, inv, tnear, h.t)) { cur = skip; return; }
+    if (!box_test_m(a, b, o, inv, tnear, h.t, ew)) { cur = skip; return; }
     const int leaf = __float_as_int(b.w);
     if (leaf < 0) { cur = i + 1; return; }
     const int first = leaf >> 3, cnt = (leaf & 7) + 1;
@@ -163,7 +158,7 @@ __device__ __forceinline__ void closest_visit(const DevScene& S, float4 a, float
         const uint32_t tri = 3u * (uint32_t)(first + j);
         const float4 T0 = ld4<Uniform>(S.tris, tri);
         float t, u, v;
-        if (tri_test(T0, ld4<Uniform>(S.tris, tri + 1), ld4<Uniform>(S.tris, tri + 2), o, d, inv, tnear, h.t, t, u, v)) {
+        if (tri_test(T0, ld4<Uniform>(S.tris, tri + 1), ld4<Uniform>(S.tris, tri + 2), o, d, tnear, h.t, t, u, v)) {
             const int prim = __float_as_int(T0.w);
             if (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim)) { h.t = t; h.u = u; h.v = v; h.prim = prim; }
         }
@@ -196,7 +191,7 @@ __device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i
             if (__ballot(want) == 0) break;
             const float4* T = S.tris + 3 * (want ? first + j : 0);
             float t, u, v;
-            const bool h = tri_test_nb(T[0], T[1], T[2], o, d, inv, tnear, tfar, t, u, v);
+            const bool h = tri_test_nb(T[0], T[1], T[2], o, d, tnear, tfar, t, u, v);
             occ = (want & h) ? 1u : occ;
         }
         i = !live ? i : (occ ? 0xffffffffu : ((hit & (leaf < 0)) ? i + 1 : skip));
@@ -207,13 +202,14 @@ __device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i
 __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i, vec3 o, vec3 d, vec3 inv, float tnear,
                                                   Hit& h) {
     const uint32_t n = S.n_nodes;
+    const vec3 ew = box_margin(S, inv);
     while (__ballot(i < n) != 0) {
         const bool live = i < n;
         const uint32_t ii = live ? i : 0u;
         const float4 a = S.nodes[2 * ii], b = S.nodes[2 * ii + 1];
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
-        const bool hit = live & box_test(a, b, o, inv, tnear, h.t);
+        const bool hit = live & box_test_m(a, b, o, inv, tnear, h.t, ew);
         const bool in_leaf = hit & (leaf >= 0);
         const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
         for (int j = 0; j < 8; ++j) {
@@ -222,7 +218,7 @@ __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i,
             const float4* T = S.tris + 3 * (want ? first + j : 0);
             const float4 T0 = T[0];
             float t, u, v;
-            const bool hh = want & tri_test_nb(T0, T[1], T[2], o, d, inv, tnear, h.t, t, u, v);
+            const bool hh = want & tri_test_nb(T0, T[1], T[2], o, d, tnear, h.t, t, u, v);
             const int prim = __float_as_int(T0.w);
             const bool better = hh & (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim));
             h.t = better ? t : h.t; h.u = better ? u : h.u; h.v = better ? v : h.v;
@@ -285,7 +281,7 @@ struct WideStack {
 __device__ __forceinline__ float ubyte_f(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xffu); }
 // the 8 child boxes of node (w0..w4) against the ray; bit c = slot c hit (valid slots only)
 __device__ __forceinline__ uint32_t wide_hits(uint4 w0, uint4 w1, uint4 w2, uint4 w3, uint4 w4, vec3 o, vec3 inv,
-                                              float tnear, float tfar) {
+                                              float tnear, float tfar, vec3 ew = vec3{0.0f, 0.0f, 0.0f}) {
     const uint32_t eb = w0.w;
     const vec3 s = mk(__uint_as_float((eb & 0xffu) << 23), __uint_as_float(((eb >> 8) & 0xffu) << 23),
                       __uint_as_float(((eb >> 16) & 0xffu) << 23));
@@ -294,8 +290,9 @@ __device__ __forceinline__ uint32_t wide_hits(uint4 w0, uint4 w1, uint4 w2, uint
                       (__uint_as_float(w0.z) - o.z) * inv.z);
     // per axis the near (far) t lowered (raised) by 2^-22 |b|: the rounding of b and of b -+ that bound
     // (an axis the ray is almost parallel to has a huge |b| and widens only itself)
-    const float ex = 2.384185791015625e-07f * fabsf(b.x), ey = 2.384185791015625e-07f * fabsf(b.y),
-                ez = 2.384185791015625e-07f * fabsf(b.z);
+    // (+ ew: the closest-hit walks' box margin, rs_wide.h box_epsilon; 0 for the any-hit walks)
+    const float ex = 2.384185791015625e-07f * fabsf(b.x) + ew.x, ey = 2.384185791015625e-07f * fabsf(b.y) + ew.y,
+                ez = 2.384185791015625e-07f * fabsf(b.z) + ew.z;
     const vec3 bn = mk(b.x - ex, b.y - ey, b.z - ez), bf = mk(b.x + ex, b.y + ey, b.z + ez);
     // near / far planes per axis by the direction's sign (lo bytes near for a positive direction)
     const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
@@ -326,6 +323,7 @@ __device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o
                                           float tfar, Hit& h, uint32_t& occ, uint32_t& lost, uint32_t* stats = nullptr) {
     uint32_t gb = 0u, gm = active ? 1u : 0u;       // root group: node 0, slot 0
     uint32_t n_fetch = 0u, n_tri = 0u;
+    const vec3 ew = Any ? mk(0.0f, 0.0f, 0.0f) : box_margin(S, inv);
     WideStack st;
     st.init();
     while (__ballot(gm != 0u) != 0) {
@@ -338,7 +336,7 @@ __device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o
         const uint4* P = S.wnodes + 5 * (size_t)node;
         const uint4 w0 = P[0], w1 = P[1], w2 = P[2], w3 = P[3], w4 = P[4];
         const float tf = Any ? tfar : h.t;
-        uint32_t hits = live ? wide_hits(w0, w1, w2, w3, w4, o, inv, tnear, tf) : 0u;
+        uint32_t hits = live ? wide_hits(w0, w1, w2, w3, w4, o, inv, tnear, tf, ew) : 0u;
         const uint32_t ni = (w0.w >> 24) & 0xfu;
         uint32_t tm = NoTri ? 0u : hits >> ni;      // leaf slots ni.. -> triangles tri_base + (slot - ni)
         const uint32_t tb = w1.y;
@@ -350,7 +348,7 @@ __device__ __forceinline__ void wide_walk(const DevScene& S, bool active, vec3 o
             const float4* T = S.wtris + 3 * (size_t)(want ? tb + j : 0u);
             const float4 T0 = T[0];
             float t, u, v;
-            const bool hh = want & tri_test_nb(T0, T[1], T[2], o, d, inv, tnear, Any ? tfar : h.t, t, u, v);
+            const bool hh = want & tri_test_nb(T0, T[1], T[2], o, d, tnear, Any ? tfar : h.t, t, u, v);
             if (Any) {
                 occ = hh ? 1u : occ;
             } else {
@@ -486,7 +484,7 @@ __device__ __forceinline__ void occluded_wave_multi(const DevScene& S, const boo
                 for (int k = 0; k < K; ++k) {
                     if (__ballot((want >> k) & 1u) != 0) {        // wave-uniform
                         float t, u, v;
-                        const bool hit = tri_test_nb(T0, T1, T2, o, d[k], inv[k], tnear, tfar[k], t, u, v);
+                        const bool hit = tri_test_nb(T0, T1, T2, o, d[k], tnear, tfar[k], t, u, v);
                         occb |= (((want >> k) & 1u) && hit) ? (1u << k) : 0u;
                     }
                 }
@@ -527,7 +525,7 @@ __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, ve
                 const uint32_t tri = 3u * (uint32_t)(first + k);
                 float t, u, v;
                 const bool hit = tri_test_nb(sload(S.tris, tri), sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d,
-                                             inv, tnear, tfar, t, u, v);
+                                             tnear, tfar, t, u, v);
                 occ = (want && hit) ? 1u : occ;
             }
             i = at ? ((hb && occ) ? 0xffffffffu : skip) : i;
@@ -542,6 +540,7 @@ __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, ve
 __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     const bool full = __ballot(1) == ~0ull;
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const vec3 ew = box_margin(S, inv);
     Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
     const uint32_t n = S.n_nodes;
     uint32_t i = active ? 0u : 0xffffffffu;
@@ -552,7 +551,7 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
         const bool at = i == m;
-        const bool hb = at && box_test(a, b, o, inv, tnear, h.t);
+        const bool hb = at && box_test_m(a, b, o, inv, tnear, h.t, ew);
         if (leaf >= 0) {                                      // wave-uniform
             if (__ballot(hb) != 0) {
                 const int first = leaf >> 3, cnt = (leaf & 7) + 1;
@@ -560,8 +559,8 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
                     const uint32_t tri = 3u * (uint32_t)(first + k);
                     const float4 T0 = sload(S.tris, tri);
                     float t, u, v;
-                    const bool hit = hb & tri_test_nb(T0, sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d, inv,
-                                                       tnear, h.t, t, u, v);
+                    const bool hit = hb & tri_test_nb(T0, sload(S.tris, tri + 1), sload(S.tris, tri + 2), o, d, tnear,
+                                                       h.t, t, u, v);
                     const int prim = __float_as_int(T0.w);
                     const bool better = hit && (h.prim < 0 || t < h.t || (t == h.t && prim < h.prim));
                     h.t = better ? t : h.t; h.u = better ? u : h.u; h.v = better ? v : h.v;

@@ -47,6 +47,24 @@ inline uint32_t h_f2u(float f) { uint32_t i; std::memcpy(&i, &f, 4); return i; }
 RS_HD inline bool w_finite(float x) { return x - x == 0.0f; }
 RS_HD inline float w_min(float a, float b) { return b < a ? b : a; }   // std::min / std::max
 RS_HD inline float w_max(float a, float b) { return a < b ? b : a; }
+// The closest-hit walks' box margin, in scene units: 2^-16 x the scene's largest |coordinate| (at least 1).
+// Moller-Trumbore accepts a hit from its barycentrics, but the point o + t d of its t can lie outside the
+// triangle's box by a few ulps of the coordinates (a ray through the shared edge of two triangles, C3: 2.5e-6 m at
+// 10 m); along an axis the ray crosses slowly that is far beyond the slab test's 4-eps t margin, so a closest-hit
+// walk could cull the box of the tie-winning triangle after finding its neighbour -- and which box that is depends
+// on the tree (the oracle's binary and 8-wide trees disagreed on 1 of 8.3 M C3 4K primary rays).  The closest-hit
+// slab tests widen every box by this margin (rs_scene.h box_test_m, wide_hits), so every tree returns the triangle
+// test's own answer (ties: smaller t, then smaller index).  The any-hit (shadow) walks keep the exact boxes: a
+// margin on them lets every ray from a flat layer's surface (walls, the C2 light layer) enter the layer's thin
+// boxes, which cost the lockstep walk up to 3.8x (2^-16) and 3 % (2^-22) on C2.  oracle/restir_oracle.c restates it.
+inline float box_epsilon(const float* pos, size_t nfloats) {
+    float m = 1.0f;
+    for (size_t i = 0; i < nfloats; ++i) {
+        const float a = pos[i] < 0.0f ? -pos[i] : pos[i];
+        if (w_finite(a) && a > m) m = a;
+    }
+    return m * (1.0f / 65536.0f);
+}
 // quantisation frame of one axis: s = 2^e >= extent / 255 and >= the float spacing at the box, o = a float
 // multiple of s <= lo with o + 255 s >= hi; every child box [clo, chi] quantises OUTWARD to bytes ql, qh with
 // o + ql s <= clo and o + qh s >= chi, all checked in double, where o, s and q are exact (the first k that

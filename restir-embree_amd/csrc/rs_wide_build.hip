@@ -22,7 +22,7 @@
 //   5 k_wide_kids / k_wide_emit   the wide nodes breadth-first, one launch pair per wide level (<= 9): each
 //                     node expands its slots from the tables, exclusive scans place its interior children and
 //                     leaf triangles, and rs_wide.h wide_encode quantises its child boxes (outward, exact)
-//   6 k_wide_gather   the wide-leaf triangles (p0, prim) (p1) (p2)
+//   6 k_wide_gather   the wide-leaf triangles (v0, prim) (e1) (e2)
 // Every choice is a function of a node's triangle set, so the arrays' order inside a level never matters.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -817,8 +817,8 @@ __global__ void k_wide_gather(const float* __restrict__ pos, const int* __restri
     const float* p = pos + 9 * (size_t)prim;
     const float v0x = p[0], v0y = p[1], v0z = p[2];
     tris[3 * k] = make_float4(v0x, v0y, v0z, __int_as_float(prim));
-    tris[3 * k + 1] = make_float4(p[3], p[4], p[5], 0.0f);
-    tris[3 * k + 2] = make_float4(p[6], p[7], p[8], 0.0f);
+    tris[3 * k + 1] = make_float4(p[3] - v0x, p[4] - v0y, p[5] - v0z, 0.0f);
+    tris[3 * k + 2] = make_float4(p[6] - v0x, p[7] - v0y, p[8] - v0z, 0.0f);
 }
 
 // device scratch freed on every exit

@@ -512,10 +512,9 @@ def test_direct_mis_and_restir_converge_to_the_same_image(which):
 def test_edge_hit_is_tree_independent():
     """A primary ray of C3 at 3840x2160 (pixel (1211, 1458), orbit frame 0) crosses the shared edge z = 0.158333 of
     triangles 65325 and 65388 at the same t.  Moller-Trumbore accepts both, but the point o + t d lies 2.5e-6 above
-    65325's box; the oracle's 8-wide walk culled that box after finding 65388 while the binary walk found 65325 first:
-    two trees, two hits.  With the box-consistency rule (rs_scene.h tri_box_ok, oracle tri_hit) a hit counts only if
-    the slab test of the triangle's own box passes on [tnear, t], so 65325 is rejected by every tree and both return
-    65388."""
+    65325's box, so before the box inflation (rs_wide.h box_epsilon, restated as or_box_epsilon) the 8-wide walk culled
+    that box after finding 65388 while the binary walk found 65325 first: two trees, two hits.  Now both trees return
+    the tie rule's answer (smaller t, then smaller index)."""
     sc = scenes.sponza_like()
     cam = scenes.orbit_camera(sc.camera, 0, 240, 0.3)
     out = np.zeros(36, np.float32)
@@ -524,4 +523,4 @@ def test_edge_hit_is_tree_independent():
     d = out[33:36][None].copy()
     tnear = np.float32(np.finfo(np.float32).tiny) + np.float32(0.01)
     hits = [O.OracleScene(sc, wide=w).trace_closest(o, d, tnear, 3.0e38) for w in (True, False)]
-    assert hits[0][1][0] == hits[1][1][0] == 65388 and hits[0][0][0] == hits[1][0][0]
+    assert hits[0][1][0] == hits[1][1][0] == 65325 and hits[0][0][0] == hits[1][0][0]
