@@ -910,6 +910,28 @@ typedef struct {
     int gy0, gy1;             /* G-buffer rows available (tile band + margin) */
 } fctx;
 
+/* diagnostic (scripts/anyhit_probe.py): record every occlusion ray whose origin is one of up to 16 given points --
+ * origin, direction, tnear, tfar, result (9 floats) -- into a caller buffer */
+static struct { int n_pts; float pts[16][3]; float* buf; int cap; int count; } g_rec;
+void or_record_rays(int n_pts, const float* pts, float* buf, int cap) {
+    g_rec.n_pts = n_pts < 16 ? n_pts : 16;
+    for (int i = 0; i < g_rec.n_pts; ++i) for (int a = 0; a < 3; ++a) g_rec.pts[i][a] = pts[3 * i + a];
+    g_rec.buf = buf; g_rec.cap = cap; g_rec.count = 0;
+}
+int or_recorded_rays(void) { return g_rec.count; }
+static void record_ray(v3 o, v3 d, float tnear, float tfar, int res) {
+    for (int i = 0; i < g_rec.n_pts; ++i)
+        if (o.x == g_rec.pts[i][0] && o.y == g_rec.pts[i][1] && o.z == g_rec.pts[i][2]) {
+            const int k = __atomic_fetch_add(&g_rec.count, 1, __ATOMIC_RELAXED);
+            if (k < g_rec.cap) {
+                float* r = g_rec.buf + 9 * (size_t)k;
+                r[0] = o.x; r[1] = o.y; r[2] = o.z; r[3] = d.x; r[4] = d.y; r[5] = d.z; r[6] = tnear; r[7] = tfar;
+                r[8] = (float)res;
+            }
+            return;
+        }
+}
+
 /* Intersection::testOcclusion (pg/Intersection.h:43-60) */
 static int occluded(const fctx* F, v3 from, v3 to, uint64_t* rays) {
     float dist = len(sub(to, from));
@@ -917,7 +939,9 @@ static int occluded(const fctx* F, v3 from, v3 to, uint64_t* rays) {
     float tnear = FLT_MIN + F->P->tnear_offset;
     float tfar = dist - F->P->tfar_offset;
     (*rays)++;
-    return any_hit(F->s, from, dir, tnear, tfar);
+    const int res = any_hit(F->s, from, dir, tnear, tfar);
+    if (g_rec.n_pts) record_ray(from, dir, tnear, tfar, res);
+    return res;
 }
 
 /* Intersection::intersectEmbree + getGeometryAttributes (pg/Intersection.h:8-41,85-113) */
