@@ -605,14 +605,16 @@ static inline int tri_hit(const or_scene* s, uint32_t t, v3 o, v3 d, float tnear
 
 /* conservative slab test: interval widened by (1 +- 4 eps) so it never culls a box whose
    contents the triangle test would accept */
-static inline int box_hit(const or_node* n, v3 o, v3 inv, float tnear, float tfar, float* tentry, const float* ew) {
+/* closest-hit margin (or_box_epsilon): olo = o + e, ohi = o - e, the origins the lo / hi planes are taken from,
+   i.e. the box widened by e on every side (NULL: no margin; rs_scene.h box_test_m) */
+static inline int box_hit(const or_node* n, v3 o, v3 inv, float tnear, float tfar, float* tentry, const float* olo,
+                          const float* ohi) {
     float oo[3] = {o.x, o.y, o.z}, ii[3] = {inv.x, inv.y, inv.z};
     float t0 = tnear, t1 = tfar;
     for (int a = 0; a < 3; ++a) {
-        float ta = (n->lo[a] - oo[a]) * ii[a];
-        float tb = (n->hi[a] - oo[a]) * ii[a];
+        float ta = (n->lo[a] - (olo ? olo[a] : oo[a])) * ii[a];
+        float tb = (n->hi[a] - (ohi ? ohi[a] : oo[a])) * ii[a];
         float mn = fminf(ta, tb), mx = fmaxf(ta, tb);
-        if (ew) { mn = mn - ew[a]; mx = mx + ew[a]; }   /* closest-hit margin (or_box_epsilon) */
         t0 = fmaxf(t0, mn); t1 = fminf(t1, mx);
     }
     *tentry = t0;
@@ -628,12 +630,13 @@ static or_hit closest_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar
     if (!s->n_nodes) return h;
     if (s->wn) return closest_hit_wide(s, o, d, tnear, tfar);
     v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const float ew[3] = {s->box_eps * fabsf(inv.x), s->box_eps * fabsf(inv.y), s->box_eps * fabsf(inv.z)};
+    const float e = s->box_eps;
+    const float olo[3] = {o.x + e, o.y + e, o.z + e}, ohi[3] = {o.x - e, o.y - e, o.z - e};
     int stack[128]; int sp = 0; stack[sp++] = 0;
     while (sp) {
         const or_node* n = &s->nodes[stack[--sp]];
         float te;
-        if (!box_hit(n, o, inv, tnear, h.t, &te, ew)) continue;
+        if (!box_hit(n, o, inv, tnear, h.t, &te, olo, ohi)) continue;
         if (n->count) {
             for (int i = n->first; i < n->first + n->count; ++i) {
                 uint32_t t = s->tri_index[i]; float tt, uu, vv;
@@ -658,7 +661,7 @@ static int any_hit(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
     while (sp) {
         const or_node* n = &s->nodes[stack[--sp]];
         float te;
-        if (!box_hit(n, o, inv, tnear, tfar, &te, NULL)) continue;
+        if (!box_hit(n, o, inv, tnear, tfar, &te, NULL, NULL)) continue;
         if (n->count) {
             for (int i = n->first; i < n->first + n->count; ++i) {
                 float tt, uu, vv;
@@ -720,17 +723,17 @@ int or_scene_set_wide(or_scene* s, int on) {
 }
 
 /* box_hit for the 8 children: bit c = child c accepted; tentry[c] = its entry t */
-__attribute__((target("avx2"))) static inline uint32_t box8(const or_wnode* w, const __m256* O, const __m256* I,
-                                                              float tnear, float tfar, float* tentry, const __m256* E) {
+/* OL / OH: the origins of the lo / hi planes (box_hit's olo / ohi; both O without the margin) */
+__attribute__((target("avx2"))) static inline uint32_t box8(const or_wnode* w, const __m256* OL, const __m256* OH,
+                                                              const __m256* I, float tnear, float tfar, float* tentry) {
     __m256 t0 = _mm256_set1_ps(tnear), t1 = _mm256_set1_ps(tfar);
     for (int a = 0; a < 3; ++a) {
-        const __m256 ta = _mm256_mul_ps(_mm256_sub_ps(_mm256_loadu_ps(w->lo[a]), O[a]), I[a]);
-        const __m256 tb = _mm256_mul_ps(_mm256_sub_ps(_mm256_loadu_ps(w->hi[a]), O[a]), I[a]);
+        const __m256 ta = _mm256_mul_ps(_mm256_sub_ps(_mm256_loadu_ps(w->lo[a]), OL[a]), I[a]);
+        const __m256 tb = _mm256_mul_ps(_mm256_sub_ps(_mm256_loadu_ps(w->hi[a]), OH[a]), I[a]);
         const __m256 nb = _mm256_cmp_ps(tb, tb, _CMP_UNORD_Q);
         /* fminf / fmaxf(ta, tb): the non-NaN operand if one is NaN (min_ps/max_ps return tb then) */
         __m256 mn = _mm256_blendv_ps(_mm256_min_ps(ta, tb), ta, nb);
         __m256 mx = _mm256_blendv_ps(_mm256_max_ps(ta, tb), ta, nb);
-        if (E) { mn = _mm256_sub_ps(mn, E[a]); mx = _mm256_add_ps(mx, E[a]); }   /* closest-hit margin */
         t0 = _mm256_max_ps(mn, t0);   /* fmaxf(t0, mn): t0 when mn is NaN */
         t1 = _mm256_min_ps(mx, t1);
     }
@@ -748,7 +751,7 @@ __attribute__((target("avx2"))) static int any_hit_wide(const or_scene* s, v3 o,
     float te[8];
     while (sp) {
         const or_wnode* w = &s->wn[stack[--sp]];
-        uint32_t m = box8(w, O, I, tnear, tfar, te, NULL);
+        uint32_t m = box8(w, O, O, I, tnear, tfar, te);
         while (m) {
             const int c = __builtin_ctz(m); m &= m - 1;
             const int32_t k = w->kid[c];
@@ -768,15 +771,15 @@ __attribute__((target("avx2"))) static int any_hit_wide(const or_scene* s, v3 o,
 __attribute__((target("avx2"))) static or_hit closest_hit_wide(const or_scene* s, v3 o, v3 d, float tnear, float tfar) {
     or_hit h = {0, tfar, 0, 0, 0xffffffffu};
     const v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const __m256 O[3] = {_mm256_set1_ps(o.x), _mm256_set1_ps(o.y), _mm256_set1_ps(o.z)};
     const __m256 I[3] = {_mm256_set1_ps(inv.x), _mm256_set1_ps(inv.y), _mm256_set1_ps(inv.z)};
-    const __m256 E[3] = {_mm256_set1_ps(s->box_eps * fabsf(inv.x)), _mm256_set1_ps(s->box_eps * fabsf(inv.y)),
-                         _mm256_set1_ps(s->box_eps * fabsf(inv.z))};
+    const float e = s->box_eps;
+    const __m256 OL[3] = {_mm256_set1_ps(o.x + e), _mm256_set1_ps(o.y + e), _mm256_set1_ps(o.z + e)};
+    const __m256 OH[3] = {_mm256_set1_ps(o.x - e), _mm256_set1_ps(o.y - e), _mm256_set1_ps(o.z - e)};
     int stack[OR_WSTACK]; int sp = 0; stack[sp++] = 0;
     float te[8];
     while (sp) {
         const or_wnode* w = &s->wn[stack[--sp]];
-        uint32_t m = box8(w, O, I, tnear, h.t, te, E);
+        uint32_t m = box8(w, OL, OH, I, tnear, h.t, te);
         int near[8]; int nn = 0;
         while (m) {
             const int c = __builtin_ctz(m); m &= m - 1;

@@ -2354,7 +2354,7 @@ __global__ void k_debug_trace(DevScene S, uint32_t n, const float* o, const floa
                         }
                 }
             } else {
-                closest_visit<false>(S, a, b, k, O, D, inv, box_margin(S, inv), tn[i], cur, h);
+                closest_visit<false>(S, a, b, k, O, D, inv, margin_origins(S, O), tn[i], cur, h);
             }
         }
         if (act) { prim_out[i] = (int32_t)((visits << 16) | (tris & 0xffff)); t_out[i] = occ ? 1.0f : 0.0f; }

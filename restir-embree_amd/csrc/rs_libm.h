@@ -11,8 +11,8 @@
  * case that the true value lies within ~1e-16 relative of a float rounding boundary (tests/test_oracle.py
  * checks them against numpy/glibc double precision on dense grids).
  *
- * Only +, -, *, /, conversions and bit moves are used (no fma, no hardware transcendental approximations,
- * no libm calls); both sides compile it with -ffp-contract=off, so the same operations round the same way.
+ * Only +, -, *, /, fma, conversions, bit moves and constant tables are used (no hardware transcendental
+ * approximations, no libm calls; fma is exactly rounded everywhere); both sides compile it with -ffp-contract=off, so the same operations round the same way.
  * Plain C99 (the oracle is C) and HIP (host + device).
  */
 #ifndef RS_LIBM_H
@@ -139,6 +139,161 @@ RS_LM double rs_lgamma_d(double x) {
 RS_LM float rs_expf(float x) { return (float)rs_exp_d((double)x); }
 RS_LM float rs_lgammaf(float x) { return (float)rs_lgamma_d((double)x); }
 
+/* powf's core, e^(y log x) for a positive finite float x and a finite float y, in double with table-driven
+ * reductions (the tables: scripts/gen_libm_tables.py).  log: x = 2^e m, m in [1, 2), c = the 21-bit reciprocal of
+ * m's 1/128-interval centre, r = m c - 1 exact (|r| < 2^-8), log1p(r) to r^6 (truncation < 2^-58 absolute);
+ * exp: t = k ln2/128 + r (|r| <= ln2/256), e^r - 1 to r^5 (truncation < 2^-60), 2^(k/128) from the table.
+ * Relative error of the double result below 2^-44 for every |y log x| <= 160, so the float result is the
+ * correctly rounded one unless the true value lies within that of a float rounding boundary.  fma is exactly
+ * rounded on both sides (v_fma_f64 on gfx950, the C library's fma on the host). */
+#define RS_LM_LOG_TAB_INIT { \
+    0x1.fe02000000000p-1, 0x1.fefeaa2b11bc0p-9, 0x1.fa11c00000000p-1, 0x1.7dc725f817e07p-7, \
+    0x1.f631000000000p-1, 0x1.3ceba4346e1f5p-6, 0x1.f25f600000000p-1, 0x1.b9fc8e7af9b2ap-6, \
+    0x1.ee9c800000000p-1, 0x1.1b0d90923d990p-5, 0x1.eae8000000000p-1, 0x1.58a63afc8f4d5p-5, \
+    0x1.e741a00000000p-1, 0x1.95c8deec9017cp-5, 0x1.e3a9200000000p-1, 0x1.d2762aadb1f03p-5, \
+    0x1.e01e000000000p-1, 0x1.075993598e4f1p-4, 0x1.dca0200000000p-1, 0x1.253f4ff0a14cbp-4, \
+    0x1.d92f200000000p-1, 0x1.42eddeea647a5p-4, 0x1.d5cac00000000p-1, 0x1.6065d09375a56p-4, \
+    0x1.d272c00000000p-1, 0x1.7da7c0d7b229fp-4, 0x1.cf26e00000000p-1, 0x1.9ab45762038c1p-4, \
+    0x1.cbe6e00000000p-1, 0x1.b78c47bb0f46ep-4, 0x1.c8b2600000000p-1, 0x1.d4317066cb872p-4, \
+    0x1.c589400000000p-1, 0x1.f0a3820117dd8p-4, 0x1.c26b600000000p-1, 0x1.067118aca65e6p-3, \
+    0x1.bf58400000000p-1, 0x1.14785346742c5p-3, 0x1.bc4fe00000000p-1, 0x1.2266c510a6288p-3, \
+    0x1.b951e00000000p-1, 0x1.303d7e0e4806fp-3, 0x1.b65e200000000p-1, 0x1.3dfc6d8ecd770p-3, \
+    0x1.b374800000000p-1, 0x1.4ba38539a57c9p-3, 0x1.b094c00000000p-1, 0x1.5933509982f0fp-3, \
+    0x1.adbe800000000p-1, 0x1.66acfa272b2f5p-3, 0x1.aaf1e00000000p-1, 0x1.740f50d4046e7p-3, \
+    0x1.a82e600000000p-1, 0x1.815c229435a43p-3, 0x1.a574200000000p-1, 0x1.8e92426888385p-3, \
+    0x1.a2c2a00000000p-1, 0x1.9bb38c67e023ep-3, 0x1.a01a000000000p-1, 0x1.a8bed7c882f59p-3, \
+    0x1.9d7a000000000p-1, 0x1.b5b4d1e8fc9e4p-3, 0x1.9ae2400000000p-1, 0x1.c296ce58c2d92p-3, \
+    0x1.9853000000000p-1, 0x1.cf6308e09dc6cp-3, 0x1.95cbc00000000p-1, 0x1.dc1b7d0ac03a6p-3, \
+    0x1.934c600000000p-1, 0x1.e8c04daaa60c8p-3, 0x1.90d5000000000p-1, 0x1.f5505964b91c7p-3, \
+    0x1.8e65200000000p-1, 0x1.00e6d81ad5329p-2, 0x1.8bfce00000000p-1, 0x1.071b9abcd5c6ap-2, \
+    0x1.899c000000000p-1, 0x1.0d46dd79ac3cbp-2, 0x1.8742800000000p-1, 0x1.136865293a9a2p-2, \
+    0x1.84f0000000000p-1, 0x1.1980f2dd42b6fp-2, 0x1.82a4a00000000p-1, 0x1.1f8ffa248a2f3p-2, \
+    0x1.8060200000000p-1, 0x1.2595ebcdf79c1p-2, 0x1.7e22600000000p-1, 0x1.2b92e66b8a3d4p-2, \
+    0x1.7beb400000000p-1, 0x1.31870a1544431p-2, 0x1.79baa00000000p-1, 0x1.3772786bfdaf5p-2, \
+    0x1.7790800000000p-1, 0x1.3d54fd5c1f722p-2, 0x1.756ca00000000p-1, 0x1.432f13e04f0b7p-2, \
+    0x1.734f000000000p-1, 0x1.49008a04012d9p-2, 0x1.7137800000000p-1, 0x1.4ec986260053cp-2, \
+    0x1.6f26000000000p-1, 0x1.548a303add283p-2, 0x1.6d1a600000000p-1, 0x1.5a42b1cf4d03dp-2, \
+    0x1.6b14a00000000p-1, 0x1.5ff2dbca7a271p-2, 0x1.6914800000000p-1, 0x1.659b34303eb85p-2, \
+    0x1.671a000000000p-1, 0x1.6b3b8e2359e5ep-2, 0x1.6525000000000p-1, 0x1.70d41827895fep-2, \
+    0x1.6335600000000p-1, 0x1.766502639e472p-2, 0x1.614b400000000p-1, 0x1.7bedc5237b5a8p-2, \
+    0x1.5f66400000000p-1, 0x1.816f4b5a0d54ap-2, 0x1.5d86800000000p-1, 0x1.86e90ea330c92p-2, \
+    0x1.5babc00000000p-1, 0x1.8c5ba1058bef3p-2, 0x1.59d6200000000p-1, 0x1.91c67bf45a84dp-2, \
+    0x1.5805600000000p-1, 0x1.972a345135159p-2, 0x1.5639800000000p-1, 0x1.9c86a32dc09b5p-2, \
+    0x1.5472600000000p-1, 0x1.a1dc018d5b9c3p-2, 0x1.52b0000000000p-1, 0x1.a72a2966be1eap-2, \
+    0x1.50f2200000000p-1, 0x1.ac71b6e58bf2bp-2, 0x1.4f39000000000p-1, 0x1.b1b1c2ebe0363p-2, \
+    0x1.4d84400000000p-1, 0x1.b6eb4d53cf496p-2, 0x1.4bd3e00000000p-1, 0x1.bc1e3370dbb51p-2, \
+    0x1.4a28000000000p-1, 0x1.c149ef115f227p-2, 0x1.4880600000000p-1, 0x1.c66f22fff7e95p-2, \
+    0x1.46dce00000000p-1, 0x1.cb8e1184d7b9cp-2, 0x1.453da00000000p-1, 0x1.d0a6352721ea6p-2, \
+    0x1.43a2800000000p-1, 0x1.d5b7d0ae2d3a6p-2, 0x1.420b600000000p-1, 0x1.dac328a2c67f1p-2, \
+    0x1.4078200000000p-1, 0x1.dfc883506e353p-2, 0x1.3ee9000000000p-1, 0x1.e4c6f4868824cp-2, \
+    0x1.3d5da00000000p-1, 0x1.e9bf9019865d4p-2, 0x1.3bd6000000000p-1, 0x1.eeb238640ed14p-2, \
+    0x1.3a52400000000p-1, 0x1.f39e674811f64p-2, 0x1.38d2200000000p-1, 0x1.f884ceafead5fp-2, \
+    0x1.3755c00000000p-1, 0x1.fd64e88f61626p-2, 0x1.35dce00000000p-1, 0x1.011fb4f260110p-1, \
+    0x1.3467a00000000p-1, 0x1.0389e65ce6465p-1, 0x1.32f5c00000000p-1, 0x1.05f1649264f2ep-1, \
+    0x1.3187800000000p-1, 0x1.0855b704b49d7p-1, 0x1.301c800000000p-1, 0x1.0ab7706ce1523p-1, \
+    0x1.2eb4e00000000p-1, 0x1.0d164deb9db4dp-1, 0x1.2d50a00000000p-1, 0x1.0f7241e9b497dp-1, \
+    0x1.2befa00000000p-1, 0x1.11cb75587cf44p-1, 0x1.2a91c00000000p-1, 0x1.1422121244125p-1, \
+    0x1.2937200000000p-1, 0x1.1675d49aba794p-1, 0x1.27dfa00000000p-1, 0x1.18c6e71f5cf9cp-1, \
+    0x1.268b400000000p-1, 0x1.1b153d17da5cbp-1, 0x1.2539e00000000p-1, 0x1.1d6101c677321p-1, \
+    0x1.23eb800000000p-1, 0x1.1faa293870b5dp-1, 0x1.22a0200000000p-1, 0x1.21f0a7665c834p-1, \
+    0x1.2157a00000000p-1, 0x1.2434a8d483c52p-1, 0x1.2012000000000p-1, 0x1.26762213430f0p-1, \
+    0x1.1ecf400000000p-1, 0x1.28b5079f60839p-1, 0x1.1d8f600000000p-1, 0x1.2af14de264542p-1, \
+    0x1.1c52200000000p-1, 0x1.2d2b5c72ee932p-1, 0x1.1b17c00000000p-1, 0x1.2f62b5550976ep-1, \
+    0x1.19e0200000000p-1, 0x1.319786da80914p-1, 0x1.18ab000000000p-1, 0x1.33ca3aa328d19p-1, \
+    0x1.1778a00000000p-1, 0x1.35fa51bd36ec1p-1, 0x1.1648e00000000p-1, 0x1.3827fbc587fd3p-1, \
+    0x1.151ba00000000p-1, 0x1.3a536947ebfbdp-1, 0x1.13f0e00000000p-1, 0x1.3c7c905f73636p-1, \
+    0x1.12c8c00000000p-1, 0x1.3ea32b76b3250p-1, 0x1.11a3000000000p-1, 0x1.40c7a7880dd0dp-1, \
+    0x1.107fc00000000p-1, 0x1.42e9bf1df81afp-1, 0x1.0f5ee00000000p-1, 0x1.4509a4733bb0cp-1, \
+    0x1.0e40600000000p-1, 0x1.47274e133ac47p-1, 0x1.0d24400000000p-1, 0x1.4942b27a2fdacp-1, \
+    0x1.0c0a800000000p-1, 0x1.4b5bc8156e5bdp-1, 0x1.0af3000000000p-1, 0x1.4d72c2a3a0184p-1, \
+    0x1.09ddc00000000p-1, 0x1.4f879935028b7p-1, 0x1.08cac00000000p-1, 0x1.519a42cba359dp-1, \
+    0x1.07ba000000000p-1, 0x1.53aab65b9a60dp-1, 0x1.06ab600000000p-1, 0x1.55b9292b40e19p-1, \
+    0x1.059ee00000000p-1, 0x1.57c592d36f795p-1, 0x1.0494a00000000p-1, 0x1.59cfabffae921p-1, \
+    0x1.038c600000000p-1, 0x1.5bd7e9ae72473p-1, 0x1.0286400000000p-1, 0x1.5dde04b14a866p-1, \
+    0x1.0182400000000p-1, 0x1.5fe1f46d189cfp-1, 0x1.0080400000000p-1, 0x1.61e3f01a46467p-1 }
+#define RS_LM_EXP2_TAB_INIT { \
+    0x1.0000000000000p+0, 0x1.0163da9fb3335p+0, 0x1.02c9a3e778061p+0, 0x1.04315e86e7f85p+0, \
+    0x1.059b0d3158574p+0, 0x1.0706b29ddf6dep+0, 0x1.0874518759bc8p+0, 0x1.09e3ecac6f383p+0, \
+    0x1.0b5586cf9890fp+0, 0x1.0cc922b7247f7p+0, 0x1.0e3ec32d3d1a2p+0, 0x1.0fb66affed31bp+0, \
+    0x1.11301d0125b51p+0, 0x1.12abdc06c31ccp+0, 0x1.1429aaea92de0p+0, 0x1.15a98c8a58e51p+0, \
+    0x1.172b83c7d517bp+0, 0x1.18af9388c8deap+0, 0x1.1a35beb6fcb75p+0, 0x1.1bbe084045cd4p+0, \
+    0x1.1d4873168b9aap+0, 0x1.1ed5022fcd91dp+0, 0x1.2063b88628cd6p+0, 0x1.21f49917ddc96p+0, \
+    0x1.2387a6e756238p+0, 0x1.251ce4fb2a63fp+0, 0x1.26b4565e27cddp+0, 0x1.284dfe1f56381p+0, \
+    0x1.29e9df51fdee1p+0, 0x1.2b87fd0dad990p+0, 0x1.2d285a6e4030bp+0, 0x1.2ecafa93e2f56p+0, \
+    0x1.306fe0a31b715p+0, 0x1.32170fc4cd831p+0, 0x1.33c08b26416ffp+0, 0x1.356c55f929ff1p+0, \
+    0x1.371a7373aa9cbp+0, 0x1.38cae6d05d866p+0, 0x1.3a7db34e59ff7p+0, 0x1.3c32dc313a8e5p+0, \
+    0x1.3dea64c123422p+0, 0x1.3fa4504ac801cp+0, 0x1.4160a21f72e2ap+0, 0x1.431f5d950a897p+0, \
+    0x1.44e086061892dp+0, 0x1.46a41ed1d0057p+0, 0x1.486a2b5c13cd0p+0, 0x1.4a32af0d7d3dep+0, \
+    0x1.4bfdad5362a27p+0, 0x1.4dcb299fddd0dp+0, 0x1.4f9b2769d2ca7p+0, 0x1.516daa2cf6642p+0, \
+    0x1.5342b569d4f82p+0, 0x1.551a4ca5d920fp+0, 0x1.56f4736b527dap+0, 0x1.58d12d497c7fdp+0, \
+    0x1.5ab07dd485429p+0, 0x1.5c9268a5946b7p+0, 0x1.5e76f15ad2148p+0, 0x1.605e1b976dc09p+0, \
+    0x1.6247eb03a5585p+0, 0x1.6434634ccc320p+0, 0x1.6623882552225p+0, 0x1.68155d44ca973p+0, \
+    0x1.6a09e667f3bcdp+0, 0x1.6c012750bdabfp+0, 0x1.6dfb23c651a2fp+0, 0x1.6ff7df9519484p+0, \
+    0x1.71f75e8ec5f74p+0, 0x1.73f9a48a58174p+0, 0x1.75feb564267c9p+0, 0x1.780694fde5d3fp+0, \
+    0x1.7a11473eb0187p+0, 0x1.7c1ed0130c132p+0, 0x1.7e2f336cf4e62p+0, 0x1.80427543e1a12p+0, \
+    0x1.82589994cce13p+0, 0x1.8471a4623c7adp+0, 0x1.868d99b4492edp+0, 0x1.88ac7d98a6699p+0, \
+    0x1.8ace5422aa0dbp+0, 0x1.8cf3216b5448cp+0, 0x1.8f1ae99157736p+0, 0x1.9145b0b91ffc6p+0, \
+    0x1.93737b0cdc5e5p+0, 0x1.95a44cbc8520fp+0, 0x1.97d829fde4e50p+0, 0x1.9a0f170ca07bap+0, \
+    0x1.9c49182a3f090p+0, 0x1.9e86319e32323p+0, 0x1.a0c667b5de565p+0, 0x1.a309bec4a2d33p+0, \
+    0x1.a5503b23e255dp+0, 0x1.a799e1330b358p+0, 0x1.a9e6b5579fdbfp+0, 0x1.ac36bbfd3f37ap+0, \
+    0x1.ae89f995ad3adp+0, 0x1.b0e07298db666p+0, 0x1.b33a2b84f15fbp+0, 0x1.b59728de5593ap+0, \
+    0x1.b7f76f2fb5e47p+0, 0x1.ba5b030a1064ap+0, 0x1.bcc1e904bc1d2p+0, 0x1.bf2c25bd71e09p+0, \
+    0x1.c199bdd85529cp+0, 0x1.c40ab5fffd07ap+0, 0x1.c67f12e57d14bp+0, 0x1.c8f6d9406e7b5p+0, \
+    0x1.cb720dcef9069p+0, 0x1.cdf0b555dc3fap+0, 0x1.d072d4a07897cp+0, 0x1.d2f87080d89f2p+0, \
+    0x1.d5818dcfba487p+0, 0x1.d80e316c98398p+0, 0x1.da9e603db3285p+0, 0x1.dd321f301b460p+0, \
+    0x1.dfc97337b9b5fp+0, 0x1.e264614f5a129p+0, 0x1.e502ee78b3ff6p+0, 0x1.e7a51fbc74c83p+0, \
+    0x1.ea4afa2a490dap+0, 0x1.ecf482d8e67f1p+0, 0x1.efa1bee615a27p+0, 0x1.f252b376bba97p+0, \
+    0x1.f50765b6e4540p+0, 0x1.f7bfdad9cbe14p+0, 0x1.fa7c1819e90d8p+0, 0x1.fd3c22b8f71f1p+0 }
+
+#if defined(__HIP__)
+static __constant__ const double rs_lm_log_tab_dev[256] = RS_LM_LOG_TAB_INIT;
+static __constant__ const double rs_lm_exp2_tab_dev[128] = RS_LM_EXP2_TAB_INIT;
+#endif
+static const double rs_lm_log_tab_host[256] = RS_LM_LOG_TAB_INIT;
+static const double rs_lm_exp2_tab_host[128] = RS_LM_EXP2_TAB_INIT;
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RS_LM_TAB(n) n##_dev
+#else
+#define RS_LM_TAB(n) n##_host
+#endif
+#define RS_LM_LN2_128_HI 0x1.62e42feep-8           /* ln2 / 128 to 33 significant bits: k hi exact */
+#define RS_LM_LN2_128_LO 1.4907929134926466e-12
+#define RS_LM_128_OVER_LN2 184.6649652337873
+
+RS_LM double rs_lm_pow_core(float ax, float y) {
+    uint32_t b = rs_lm_fbits(ax);
+    int e = -127;
+    if (b < 0x00800000u) { b = rs_lm_fbits(ax * 8388608.0f); e -= 23; }          /* subnormal: x 2^23 */
+    e += (int)(b >> 23);
+    const int i = (int)((b >> 16) & 127);
+    const double m = (double)rs_lm_flt((b & 0x007fffffu) | 0x3f800000u);
+    const double r = m * RS_LM_TAB(rs_lm_log_tab)[2 * i] - 1.0;                   /* exact */
+    double p = __builtin_fma(r, -1.0 / 6.0, 1.0 / 5.0);
+    p = __builtin_fma(r, p, -0.25);
+    p = __builtin_fma(r, p, 1.0 / 3.0);
+    p = __builtin_fma(r, p, -0.5);
+    const double l1p = __builtin_fma(r * r, p, r);
+    const double de = (double)e;
+    const double lx = __builtin_fma(de, RS_LM_LN2_HI, RS_LM_TAB(rs_lm_log_tab)[2 * i + 1]) +
+                      __builtin_fma(de, RS_LM_LN2_LO, l1p);
+    const double t = (double)y * lx;
+    if (t > 128.0) return RS_LM_DINF;
+    if (t < -160.0) return 0.0;
+    const double u = t * RS_LM_128_OVER_LN2;
+    const int k = (int)(u >= 0.0 ? u + 0.5 : u - 0.5);
+    const double dk = (double)k;
+    double rr = __builtin_fma(dk, -RS_LM_LN2_128_HI, t);
+    rr = __builtin_fma(dk, -RS_LM_LN2_128_LO, rr);
+    double q = __builtin_fma(rr, 1.0 / 120.0, 1.0 / 24.0);
+    q = __builtin_fma(rr, q, 1.0 / 6.0);
+    q = __builtin_fma(rr, q, 0.5);
+    const double em1 = __builtin_fma(rr * rr, q, rr);
+    const int j = k & 127;
+    const int64_t qk = (int64_t)((k - j) / 128);
+    const double s = rs_lm_dbl(rs_lm_bits(RS_LM_TAB(rs_lm_exp2_tab)[j]) + ((uint64_t)qk << 52));
+    return __builtin_fma(s, em1, s);
+}
+
 /* x^y (C99 special cases) */
 RS_LM float rs_powf(float x, float y) {
     if (y == 0.0f || x == 1.0f) return 1.0f;
@@ -161,11 +316,11 @@ RS_LM float rs_powf(float x, float y) {
         return ((ax < 1.0f) == (y > 0.0f)) ? 0.0f : RS_LM_FINF;
     }
     const int neg = (rs_lm_fbits(x) >> 31) && y_odd;   /* odd integer power of a negative (or -0) base */
-    if (x < 0.0f && !y_int) return RS_LM_FNAN;
     float r;
     if (ax == 0.0f) r = y > 0.0f ? 0.0f : RS_LM_FINF;
-    else if (rs_lm_fbits(ax) == 0x7f800000u) r = y > 0.0f ? ax : 0.0f;
-    else r = (float)rs_exp_d((double)y * rs_log_d((double)ax));
+    else if (rs_lm_fbits(ax) == 0x7f800000u) r = y > 0.0f ? ax : 0.0f;   /* (-inf)^y: sign by y_odd only */
+    else if (x < 0.0f && !y_int) return RS_LM_FNAN;
+    else r = (float)rs_lm_pow_core(ax, y);
     return neg ? -r : r;
 }
 

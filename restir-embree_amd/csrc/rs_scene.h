@@ -104,16 +104,26 @@ __device__ __forceinline__ bool box_test(float4 a, float4 b, vec3 o, vec3 inv, f
     return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
 }
 
-// the closest-hit walks' test: the box widened by `ew` = box_epsilon x |1/d| per axis in t (the margin in space
-// along each axis, rs_wide.h box_epsilon), so a triangle the test accepts is never culled with its box
-__device__ __forceinline__ bool box_test_m(float4 a, float4 b, vec3 o, vec3 inv, float tnear, float tfar, vec3 ew) {
-    float tx0 = (a.x - o.x) * inv.x, tx1 = (b.x - o.x) * inv.x;
-    float ty0 = (a.y - o.y) * inv.y, ty1 = (b.y - o.y) * inv.y;
-    float tz0 = (a.z - o.z) * inv.z, tz1 = (b.z - o.z) * inv.z;
-    float t0 = fmaxf(fmaxf(fmaxf(tnear, fminf(tx0, tx1) - ew.x), fminf(ty0, ty1) - ew.y), fminf(tz0, tz1) - ew.z);
-    float t1 = fminf(fminf(fminf(tfar, fmaxf(tx0, tx1) + ew.x), fmaxf(ty0, ty1) + ew.y), fmaxf(tz0, tz1) + ew.z);
+// the closest-hit walks' test: the box widened by the margin e (rs_wide.h box_epsilon) on every side, written as
+// box_test with the ray origin moved by -+e for the lo / hi planes (olo = o + e, ohi = o - e: (lo - e) - o and
+// (hi + e) - o up to rounding), so a triangle the test accepts is never culled with its box.  No per-box cost
+// over box_test, and a direction component of exactly 0 (1/d = inf) keeps the slab test exact: the widening
+// applied in t (e |1/d| added to the t interval) turned inf - inf into NaN there and dropped the axis --
+// C2's centre column and row (pixel-corner rays) then walked most of the tree (+27 % on the initial pass)
+__device__ __forceinline__ bool box_test_m(float4 a, float4 b, vec3 olo, vec3 ohi, vec3 inv, float tnear, float tfar) {
+    float tx0 = (a.x - olo.x) * inv.x, tx1 = (b.x - ohi.x) * inv.x;
+    float ty0 = (a.y - olo.y) * inv.y, ty1 = (b.y - ohi.y) * inv.y;
+    float tz0 = (a.z - olo.z) * inv.z, tz1 = (b.z - ohi.z) * inv.z;
+    float t0 = fmaxf(fmaxf(fmaxf(tnear, fminf(tx0, tx1)), fminf(ty0, ty1)), fminf(tz0, tz1));
+    float t1 = fminf(fminf(fminf(tfar, fmaxf(tx0, tx1)), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
     return t0 * (1.0f - 4.0f * FLT_EPSILON) <= t1 * (1.0f + 4.0f * FLT_EPSILON);
 }
+struct MarginO { vec3 lo, hi; };   // box_test_m's shifted origins
+__device__ __forceinline__ MarginO margin_origins(const DevScene& S, vec3 o) {
+    const float e = S.box_eps;
+    return MarginO{mk(o.x + e, o.y + e, o.z + e), mk(o.x - e, o.y - e, o.z - e)};
+}
+// the 8-wide walk's form of the margin: e |1/d| per axis in t (wide_hits widens its t bounds per axis already)
 __device__ __forceinline__ vec3 box_margin(const DevScene& S, vec3 inv) {
     return mk(S.box_eps * fabsf(inv.x), S.box_eps * fabsf(inv.y), S.box_eps * fabsf(inv.z));
 }
@@ -148,9 +158,9 @@ __device__ __forceinline__ float4 ld4(const float4* p, uint32_t i) {
 // result does not depend on the visit order.
 template <bool Uniform>
 __device__ __forceinline__ void closest_visit(const DevScene& S, float4 a, float4 b, uint32_t i, vec3 o, vec3 d,
-                                              vec3 inv, vec3 ew, float tnear, uint32_t& cur, Hit& h) {
+                                              vec3 inv, MarginO mo, float tnear, uint32_t& cur, Hit& h) {
     const uint32_t skip = (uint32_t)__float_as_int(a.w);
-    if (!box_test_m(a, b, o, inv, tnear, h.t, ew)) { cur = skip; return; }
+    if (!box_test_m(a, b, mo.lo, mo.hi, inv, tnear, h.t)) { cur = skip; return; }
     const int leaf = __float_as_int(b.w);
     if (leaf < 0) { cur = i + 1; return; }
     const int first = leaf >> 3, cnt = (leaf & 7) + 1;
@@ -202,14 +212,14 @@ __device__ __forceinline__ bool occluded_lane_from(const DevScene& S, uint32_t i
 __device__ __forceinline__ void closest_lane_from(const DevScene& S, uint32_t i, vec3 o, vec3 d, vec3 inv, float tnear,
                                                   Hit& h) {
     const uint32_t n = S.n_nodes;
-    const vec3 ew = box_margin(S, inv);
+    const MarginO mo = margin_origins(S, o);
     while (__ballot(i < n) != 0) {
         const bool live = i < n;
         const uint32_t ii = live ? i : 0u;
         const float4 a = S.nodes[2 * ii], b = S.nodes[2 * ii + 1];
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
-        const bool hit = live & box_test_m(a, b, o, inv, tnear, h.t, ew);
+        const bool hit = live & box_test_m(a, b, mo.lo, mo.hi, inv, tnear, h.t);
         const bool in_leaf = hit & (leaf >= 0);
         const int first = leaf >> 3, cnt = in_leaf ? (leaf & 7) + 1 : 0;
         for (int j = 0; j < 8; ++j) {
@@ -540,7 +550,7 @@ __device__ __forceinline__ bool occluded_wave(const DevScene& S, bool active, ve
 __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     const bool full = __ballot(1) == ~0ull;
     vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const vec3 ew = box_margin(S, inv);
+    const MarginO mo = margin_origins(S, o);
     Hit h; h.t = tfar; h.u = 0; h.v = 0; h.prim = -1;
     const uint32_t n = S.n_nodes;
     uint32_t i = active ? 0u : 0xffffffffu;
@@ -551,7 +561,7 @@ __device__ __forceinline__ Hit closest_wave(const DevScene& S, bool active, vec3
         const uint32_t skip = (uint32_t)__float_as_int(a.w);
         const int leaf = __float_as_int(b.w);
         const bool at = i == m;
-        const bool hb = at && box_test_m(a, b, o, inv, tnear, h.t, ew);
+        const bool hb = at && box_test_m(a, b, mo.lo, mo.hi, inv, tnear, h.t);
         if (leaf >= 0) {                                      // wave-uniform
             if (__ballot(hb) != 0) {
                 const int first = leaf >> 3, cnt = (leaf & 7) + 1;
