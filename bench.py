@@ -242,8 +242,8 @@ def cpu_baseline(name, W, H, threads, budget_s=12.0):
 
 # ---------------------------------------------------------------- PMC figures committed under profiles/
 def pmc_for(name, W, H):
-    """The newest committed PMC summary of this config (profiles/r05_pmc_<cfg>.json, else rounds 4 / 3 / 2)."""
-    for rnd in ("r05", "r04", "r03_v3", "r03", "r02"):
+    """The newest committed PMC summary of this config (profiles/r06_pmc_<cfg>.json, else rounds 5 / 4 / 3 / 2)."""
+    for rnd in ("r06", "r05", "r04", "r03_v3", "r03", "r02"):
         path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{name}.json")
         if not os.path.exists(path):
             continue

@@ -10,8 +10,8 @@
 #   bench   bench.py $BENCH_ARGS -> gpurun_out/bench${TAG}.json (+ .err)
 #   prof    rocprofv3 --kernel-trace --stats of bench.py per config (CFGS, default "C2 C3"), frames in flight and
 #           one frame in flight (RESTIR_RUNAHEAD=0) -> gpurun_out/prof{,0}_<cfg>/
-#   pmc     one rocprofv3 --pmc pass per counter group per config (one frame in flight) -> gpurun_out/pmc_<cfg>_<group>/
-#           (scripts/pmc_summary.py turns them into profiles/rNN_pmc_<cfg>.json)
+#   pmc     one rocprofv3 --pmc pass per counter group per config (one frame in flight) -> gpurun_out/pmc_<cfg>$PMC_TAG_<group>/
+#           (scripts/pmc_summary.py turns them into profiles/rNN_pmc_<cfg>$PMC_TAG.json); PMC_ENV: extra VAR=value settings
 #   ab      A/B of prebuilt libraries restir-embree_amd/_ab/lib_*.so: AB_TESTS against each non-base one, then
 #           bench.py (--steps STEPS, BENCH_ARGS) for each, REPS times interleaved
 #   band    scripts/band_probe.py $BAND_ARGS -> gpurun_out/band${TAG}.txt
@@ -55,14 +55,15 @@ step_prof() {
 step_pmc() {
   local TA="SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU SQ_WAVES TA_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES TD_TD_BUSY TD_TC_STALL GRBM_GUI_ACTIVE GRBM_COUNT TCP_TOTAL_CACHE_ACCESSES TCP_TCC_READ_REQ TCP_PENDING_STALL_CYCLES TCP_TCP_TA_DATA_STALL_CYCLES"
   ( cd /tmp && export TMPDIR=/tmp
+    [ -n "$PMC_ENV" ] && export $PMC_ENV
     for cfg in ${CFGS:-C2 C3}; do
       local trav=lockstep; [ $cfg = C3 ] && trav=lane
       for C in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY" "$TA"; do
         local D=${C%% *}
         RESTIR_RUNAHEAD=0 RESTIR_TRAVERSAL=$trav timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv \
-          -d "$R/gpurun_out/pmc_${cfg}_$D" -o run -- \
-          python3 "$R/bench.py" --scene $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-extras > "$R/gpurun_out/pmc_${cfg}_$D.log" 2>&1 \
-          || { echo "pmc $cfg $D failed"; tail -5 "$R/gpurun_out/pmc_${cfg}_$D.log"; exit 1; }
+          -d "$R/gpurun_out/pmc_${cfg}${PMC_TAG}_$D" -o run -- \
+          python3 "$R/bench.py" --scene $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-extras > "$R/gpurun_out/pmc_${cfg}${PMC_TAG}_$D.log" 2>&1 \
+          || { echo "pmc $cfg $D failed"; tail -5 "$R/gpurun_out/pmc_${cfg}${PMC_TAG}_$D.log"; exit 1; }
         echo "pmc $cfg $D ok"
       done
     done )

@@ -17,7 +17,8 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
 W, H = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (1920, 1080)
 src = os.path.join(ROOT, "gpurun_out")
 ROUND = os.environ.get("ROUND", "r03")
-out = os.path.join(ROOT, "profiles", f"{ROUND}_pmc_{cfg}.json")
+TAG = os.environ.get("PMC_TAG", "")            # gpu_session.sh pmc PMC_TAG (with its PMC_ENV)
+out = os.path.join(ROOT, "profiles", f"{ROUND}_pmc_{cfg}{TAG}.json")
 px = W * H
 PASS = ("k_gbuffer_initial", "k_visibility", "k_temporal", "k_spatial", "k_shade")
 
@@ -30,13 +31,14 @@ def kname(row):
 
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    with open(os.path.join(src, f"pmc_{cfg}_{c}", "run_counter_collection.csv")) as f:
+    with open(os.path.join(src, f"pmc_{cfg}{TAG}_{c}", "run_counter_collection.csv")) as f:
         for row in csv.DictReader(f):
             k = kname(row)
             if k in PASS:
                 vals[k][c].append(float(row["Counter_Value"]))
 res = {"config": f"{cfg}_{W}x{H}", "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE / --pmc SQ_* (separate "
-       f"runs), RESTIR_RUNAHEAD=0, bench.py --scene {cfg} --steps 3 --warmup 1 (scripts/gpu_profile_{ROUND}.sh)",
+       f"runs), RESTIR_RUNAHEAD=0 {os.environ.get('PMC_ENV', '')}, bench.py --scene {cfg} --steps 3 --warmup 1 "
+                 f"(scripts/gpu_session.sh pmc)",
        "kernels": {}}
 for k, d in vals.items():
     fe = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
@@ -45,7 +47,7 @@ for k, d in vals.items():
                          "hbm_bytes_corrected": int((2 * fe + wr) * 1024),
                          "hbm_bytes_uncorrected": int((fe + wr) * 1024),
                          "bytes_per_px_corrected": round((2 * fe + wr) * 1024 / px, 2)}
-sq_csv = os.path.join(src, f"pmc_{cfg}_SQ_WAVES", "run_counter_collection.csv")
+sq_csv = os.path.join(src, f"pmc_{cfg}{TAG}_SQ_WAVES", "run_counter_collection.csv")
 if os.path.exists(sq_csv):   # SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* / SQ_WAIT_* are quad-cycles
     sq = collections.defaultdict(lambda: collections.defaultdict(list))
     with open(sq_csv) as f:
@@ -54,7 +56,7 @@ if os.path.exists(sq_csv):   # SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* / SQ_WAIT_* are
     for k, d in sq.items():
         if k in res["kernels"]:
             res["kernels"][k]["sq"] = {c: round(sum(v) / len(v), 1) for c, v in d.items()}
-ta_csv = os.path.join(src, f"pmc_{cfg}_SQ_INSTS_VMEM_RD", "run_counter_collection.csv")
+ta_csv = os.path.join(src, f"pmc_{cfg}{TAG}_SQ_INSTS_VMEM_RD", "run_counter_collection.csv")
 if os.path.exists(ta_csv):   # vector-memory pipeline group: per-launch means, and derived ratios
     ta = collections.defaultdict(lambda: collections.defaultdict(list))
     with open(ta_csv) as f:
