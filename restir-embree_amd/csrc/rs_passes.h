@@ -850,6 +850,23 @@ __device__ __forceinline__ void sorted_tile(const DevScene& S, const FrameConst&
                     }
                 wave_lds_sync();
                 // ---- B: the chunk's shadow rays in bucket order (lane = ray)
+#if RS_SORT_STORE_RAY
+                if constexpr (trav_lane(T) && trav_wide(T)) {          // lanes refilled from the list (rs_scene.h)
+                    occluded_wide_list(S, n_rays, FLT_MIN + F.tnear_off,
+                        [&](uint32_t j, vec3& o, vec3& ld, float& tfar) {
+                            const uint32_t sl = L.e[j], src = sl & 63u;
+                            o = mk(L.px[src], L.py[src], L.pz[src]);
+                            const float4 dt = F.cand_ray[wtile * (size_t)(kSortChunk * 64) + sl];   // phase A's ray
+                            ld = xyz(dt);
+                            tfar = dt.w;
+                            rays += 1u;
+                        },
+                        [&](uint32_t j, bool occ) {
+                            const uint32_t sl = L.e[j];
+                            if (occ) atomicOr(&L.occ[sl & 63u], 1u << (sl >> 6));
+                        });
+                } else
+#endif
                 for (uint32_t j0 = 0; j0 < n_rays; j0 += 64u) {
                     const uint32_t j = j0 + (uint32_t)lane;
                     const bool act = j < n_rays;
@@ -1347,6 +1364,22 @@ __global__ void __launch_bounds__(256, RS_WAVES(T, RS_TEMPORAL_WAVES, RS_TEMPORA
                 if ((nd >> k) & 1u) L.e[L.cur[(bk >> (8 * k)) & 63u] + L.slot[k * 64 + lane]] = (uint16_t)(k * 64 + lane);
             wave_lds_sync();
             // ---- B: the rays in bucket order (lane = ray), re-formed from the pixel's LDS slot
+            if constexpr (trav_lane(T) && trav_wide(T)) {              // lanes refilled from the list (rs_scene.h)
+                occluded_wide_list(S, n_rays, FLT_MIN + F.tnear_off,
+                    [&](uint32_t j, vec3& o, vec3& d, float& tfar) {
+                        const uint32_t sl = L.e[j];
+                        const int k = (int)(sl >> 6), src = (int)(sl & 63u);
+                        const TemporalSlot tq{temporal_lds, wbase + src};
+                        o = tq.get3(3 * (k & 1));
+                        const vec3 ld = tq.get3(6 + 3 * (k >> 1)) - o;                   // evaluate_f_pre's ray
+                        d = normalize(ld);
+                        tfar = sqrtf(dot(ld, ld)) - F.tfar_off;
+                    },
+                    [&](uint32_t j, bool oc) {
+                        const uint32_t sl = L.e[j];
+                        if (oc) atomicOr(&L.occ[sl & 63u], 1u << (sl >> 6));
+                    });
+            } else
             for (uint32_t j0 = 0; j0 < n_rays; j0 += 64u) {
                 const uint32_t j = j0 + (uint32_t)lane;
                 const bool act = j < n_rays;
@@ -1728,6 +1761,26 @@ k_spatial_sorted(DevScene S, FrameConst F, GBuf G, ResBuf Rr, ResBuf Rw, int pas
             }
         wave_lds_sync();
         // ---- B: the rays in bucket order (lane = ray)
+        if constexpr (trav_lane(T) && trav_wide(T)) {                  // lanes refilled from the list (rs_scene.h)
+            occluded_wide_list(S, n_rays, FLT_MIN + F.tnear_off,
+                [&](uint32_t j, vec3& o, vec3& ld, float& tfar) {
+                    const uint32_t sl = L.e[j];
+                    const uint32_t i = sl >> 6, src = sl & 63u;
+                    const uint32_t psrc = tile_pixel(F, F.y0, F.y1, (int)src);
+                    const size_t q = i == 0 ? (size_t)psrc : (size_t)nbr[(i - 1) * 256 + wbase + src];
+                    o = xyz(G.g0[psrc]);
+                    const vec3 sp = xyz(Rr.r[3 * q]);
+                    ld = sp - o;                                        // evaluate_f_pre's ray
+                    const float r2 = dot(ld, ld);
+                    ld = normalize(ld);
+                    tfar = sqrtf(r2) - F.tfar_off;
+                    rays += 1u;
+                },
+                [&](uint32_t j, bool occ) {
+                    const uint32_t sl = L.e[j];
+                    if (occ) atomicOr(&L.occ[sl & 63u], 1u << (sl >> 6));
+                });
+        } else
         for (uint32_t j0 = 0; j0 < n_rays; j0 += 64u) {
             const uint32_t j = j0 + (uint32_t)lane;
             const bool act = j < n_rays;

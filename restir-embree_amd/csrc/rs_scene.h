@@ -388,6 +388,75 @@ __device__ __forceinline__ bool occluded_lane(const DevScene& S, bool active, ve
     wide_walk<true>(S, active, o, d, inv, tnear, tfar, h, occ, lost);   // lost == 0: depth <= kWideStack
     return occ != 0u;
 }
+// A list of n any-hit rays walked by one wave on the 8-wide tree, each lane taking the list's next ray when its own
+// walk ends (Aila & Laine's persistent "while-while" with dynamic fetch): the rays of a 64-ray batch differ in
+// walk length (C3 shadow rays: mean 12.8 node fetches, batch maximum 27; scripts/bvh_lab.cpp DUMP_ITERS), so a
+// batch-at-a-time loop idles half its lanes.  Lanes are refilled when at least RS_REFILL_IDLE of them are idle
+// (one round of ray loads serves them all; a refill per finished ray would add a load latency to most steps), or
+// when every lane is.  ray(j, o, d, tfar) loads ray j; done(j, occ) records its answer.  The box and triangle tests
+// are wide_walk<true>'s, so every ray's answer is the one wide_walk gives it -- only the lane and the time differ.
+#ifndef RS_REFILL_IDLE
+#define RS_REFILL_IDLE 8
+#endif
+template <class RayF, class DoneF>
+__device__ __forceinline__ void occluded_wide_list(const DevScene& S, uint32_t n, float tnear, RayF ray, DoneF done) {
+    const uint32_t lane = __lane_id();
+    uint32_t j = lane, next = 64u;                 // this lane's ray; the list's next unassigned ray (wave-uniform)
+    vec3 o = mk(0.0f, 0.0f, 0.0f), d = mk(1.0f, 1.0f, 1.0f), inv = mk(1.0f, 1.0f, 1.0f);
+    float tfar = 0.0f;
+    uint32_t gb = 0u, gm = 0u, occ = 0u;
+    WideStack st;
+    st.init();
+    if (j < n) {
+        ray(j, o, d, tfar);
+        inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        gm = 1u;
+    }
+    while (true) {
+        const uint64_t im = __ballot(gm == 0u);
+        const uint32_t nidle = (uint32_t)__popcll(im);
+        if (next < n && (nidle >= (uint32_t)RS_REFILL_IDLE || nidle == 64u)) {
+            const uint32_t nj = next + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+            next += nidle;
+            if (gm == 0u && nj < n) {
+                j = nj;
+                ray(j, o, d, tfar);
+                inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                gb = 0u; gm = 1u; occ = 0u;
+                st.n = 0;
+            }
+        }
+        if (__ballot(gm != 0u) == 0) break;        // every lane idle and the list drained
+        const bool live = gm != 0u;
+        const uint32_t slot = (uint32_t)__builtin_ctz(gm | 0x100u);
+        const uint32_t node = live ? gb + slot : 0u;
+        const uint32_t rest = gm & (gm - 1u);
+        st.push(live & (rest != 0u), (gb << 8) | rest);
+        const uint4* P = S.wnodes + 5 * (size_t)node;
+        const uint4 w0 = P[0], w1 = P[1], w2 = P[2], w3 = P[3], w4 = P[4];
+        const uint32_t hits = live ? wide_hits(w0, w1, w2, w3, w4, o, inv, tnear, tfar) : 0u;
+        const uint32_t ni = (w0.w >> 24) & 0xfu;
+        uint32_t tm = hits >> ni;                  // leaf slots ni.. -> triangles tri_base + (slot - ni)
+        const uint32_t tb = w1.y;
+        while (__ballot(tm != 0u && occ == 0u) != 0) {
+            const bool want = tm != 0u && occ == 0u;
+            const uint32_t jj = (uint32_t)__builtin_ctz(tm | 0x100u);
+            tm &= tm - 1u;
+            const float4* T = S.wtris + 3 * (size_t)(want ? tb + jj : 0u);
+            float t, u, v;
+            const bool hh = want & tri_test_nb(T[0], T[1], T[2], o, d, tnear, tfar, t, u, v);
+            occ = hh ? 1u : occ;
+        }
+        const uint32_t ngm = occ ? 0u : (hits & ((1u << ni) - 1u));
+        const bool pop = live & (ngm == 0u) & (st.n > 0) & (occ == 0u);
+        const uint32_t top = st.pop(pop);
+        gb = !live ? gb : (ngm ? w1.x : (pop ? top >> 8 : 0u));
+        gm = !live ? 0u : (ngm ? ngm : (pop ? top & 0xffu : 0u));
+        if (occ) st.n = 0;
+        if (live && gm == 0u) done(j, occ != 0u);
+    }
+}
 template <bool Wide>
 __device__ __forceinline__ Hit closest_lane(const DevScene& S, bool active, vec3 o, vec3 d, float tnear, float tfar) {
     const vec3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);

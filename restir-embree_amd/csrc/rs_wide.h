@@ -351,6 +351,23 @@ inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, 
     // (~1 GB of tables), or without a plan inside the depth, the greedy collapse
     if (collapse == 1 && (n > (1 << 21) || !sah.plan(nlo, nhi, n, root, c_node, c_tri, max_depth)))
         collapse = 0;
+    // triangles below every binary node (ids >= n; a primitive counts 1): a node's interior slots are ordered by it,
+    // most first, so the walks' lowest-slot-first order enters the fuller subtrees first -- an any-hit ray meets an
+    // occluder after fewer node fetches (scripts/bvh_lab.cpp ORDER: C3 shadow rays 13.86 -> 12.73 fetches)
+    std::vector<int> ntri(n > 1 ? (size_t)n - 1 : 0, 0);
+    if (n > 1) {
+        std::vector<std::pair<int, bool>> ps = {{root, false}};
+        while (!ps.empty()) {
+            auto [x, done] = ps.back();
+            ps.pop_back();
+            if (x < n) continue;
+            const int l = h_f2i(nlo[4 * (size_t)x + 3]), r = h_f2i(nhi[4 * (size_t)x + 3]);
+            if (l < 0 || r < 0 || l >= 2 * n - 1 || r >= 2 * n - 1) { err = "wide BVH: bad child id"; return -1; }
+            if (!done) { ps.push_back({x, true}); ps.push_back({l, false}); ps.push_back({r, false}); continue; }
+            ntri[x - n] = (l < n ? 1 : ntri[l - n]) + (r < n ? 1 : ntri[r - n]);
+        }
+    }
+    auto tri_count = [&](int c) { return c < n ? 1 : ntri[c - n]; };
     std::vector<int> queue = {root}, level = {0}, budget = {max_depth};   // wide node i = PLOC node queue[i]
     for (size_t qi = 0; qi < queue.size(); ++qi) {
         const int c = queue[qi];
@@ -381,6 +398,11 @@ inline int build_wide_host(const float* nlo, const float* nhi, int n, int root, 
         }
         int ni = 0;
         while (ni < (int)kids.size() && !is_prim(kids[ni])) ++ni;
+        for (int i = 1; i < ni; ++i)                   // interior slots: most triangles first, ties in expansion order
+            for (int j = i; j > 0 && tri_count(kids[j]) > tri_count(kids[j - 1]); --j) {
+                std::swap(kids[j], kids[j - 1]);
+                if (collapse == 1) std::swap(hb[j], hb[j - 1]);
+            }
         const int nv = (int)kids.size();
         const uint32_t child_base = (uint32_t)queue.size(), tri_base = (uint32_t)tri_prims.size();
         for (int i = 0; i < ni; ++i) {

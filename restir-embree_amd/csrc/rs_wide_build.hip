@@ -672,8 +672,9 @@ __global__ void k_depth_fill_flat(const int* __restrict__ depth, int m, int* fil
 // by shuffle).  One lane per node walking all ten rows serially took 25-130 us per level launch (23 launches
 // at C3), latency on the children's tables.
 constexpr int kDpLanes = 16;
+// (+ ntri: the node's triangle count, for build_wide_host's slot order; children are a deeper level, done already)
 __global__ void k_dp_level(const int* __restrict__ order, int b, int e, int n, const float4* __restrict__ nlo,
-                           const float4* __restrict__ nhi, float* S, uint8_t* open, uint8_t* split) {
+                           const float4* __restrict__ nhi, float* S, uint8_t* open, uint8_t* split, int* ntri) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int q = b + t / kDpLanes, gi = t % kDpLanes, g = gi - 1;
     const bool node = q < e, act = node && gi < kG;
@@ -688,6 +689,7 @@ __global__ void k_dp_level(const int* __restrict__ order, int b, int e, int n, c
         const float4 xl = nlo[x], xh = nhi[x];
         const int l = __float_as_int(xl.w), r = __float_as_int(xh.w);
         ax = area_f(xl, xh);
+        if (gi == 0) ntri[xi] = (l < n ? 1 : ntri[l - n]) + (r < n ? 1 : ntri[r - n]);
         float rl[8], rr[8];
         if (l < n) { const float al = area_f(nlo[l], nhi[l]) * kCtri; for (int k = 0; k < 8; ++k) rl[k] = al; }
         else {
@@ -763,16 +765,25 @@ __device__ int wide_kids(int c, int g, int n, const float4* __restrict__ nlo, co
 }
 __global__ void k_wide_kids(const WideQ* __restrict__ wq, int q0, int q1, int n, const float4* __restrict__ nlo,
                             const float4* __restrict__ nhi, const uint8_t* __restrict__ open,
-                            const uint8_t* __restrict__ split, int* kids, int* n_int, int* n_leaf, int* bad) {
+                            const uint8_t* __restrict__ split, const int* __restrict__ ntri, int* kids, int* n_int,
+                            int* n_leaf, int* bad) {
     const int i = q0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= q1) return;
     const WideQ Q = wq[i];
     int k[8];
     const int m = wide_kids(Q.node, Q.budget, n, nlo, nhi, open, split, k);
     if (m <= 0) { atomicOr(bad, 2); n_int[i - q0] = 0; n_leaf[i - q0] = 0; return; }
-    // interior slots first, each group in expansion order (build_wide_host's stable partition)
+    // interior slots first, each group in expansion order (build_wide_host's stable partition); the interior slots
+    // then by triangle count, most first, ties in expansion order (build_wide_host's insertion sort)
     int o = 0, ni = 0;
-    for (int j = 0; j < m; ++j) if (k[j] >= n) { kids[8 * (size_t)i + o++] = k[j]; ++ni; }
+    int ki[8], kc[8];
+    for (int j = 0; j < m; ++j)
+        if (k[j] >= n) {
+            int c = ntri[k[j] - n], p = ni++;
+            for (; p > 0 && c > kc[p - 1]; --p) { ki[p] = ki[p - 1]; kc[p] = kc[p - 1]; }
+            ki[p] = k[j]; kc[p] = c;
+        }
+    for (int j = 0; j < ni; ++j) kids[8 * (size_t)i + o++] = ki[j];
     for (int j = 0; j < m; ++j) if (k[j] < n) kids[8 * (size_t)i + o++] = k[j];
     for (int j = m; j < 8; ++j) kids[8 * (size_t)i + j] = -1;
     n_int[i - q0] = ni;
@@ -957,6 +968,8 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
     uint8_t *open = nullptr, *split = nullptr;
     WB_CHECK(X.get(&S, (size_t)std::max(1, m) * kG * 8) && X.get(&open, (size_t)std::max(1, m) * kG * 8) &&
              X.get(&split, (size_t)std::max(1, m) * kG * 8), "collapse tables: allocation failed");
+    int* ntri = nullptr;                             // triangles below each internal node (k_dp_level, k_wide_kids)
+    WB_CHECK(X.get(&ntri, std::max(1, m)), "scratch allocation failed");
     if (m > 0) {
         int *cnt = nullptr, *order = nullptr;
         const int nd = max_depth + 1;
@@ -974,7 +987,7 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
         else k_depth_fill_flat<<<(m + kB - 1) / kB, kB, 0, st>>>(depth, m, cnt, order);
         for (int d = nd - 1; d >= 0; --d) {
             const int b = off[d], e = off[d + 1];
-            if (e > b) k_dp_level<<<(unsigned)(((size_t)(e - b) * kDpLanes + 127) / 128), 128, 0, st>>>(order, b, e, n, nlo, nhi, S, open, split);
+            if (e > b) k_dp_level<<<(unsigned)(((size_t)(e - b) * kDpLanes + 127) / 128), 128, 0, st>>>(order, b, e, n, nlo, nhi, S, open, split, ntri);
         }
         WB_HIP(hipGetLastError());
         float s_root = 0.0f;
@@ -1007,7 +1020,7 @@ int build_wide_gpu(const float* d_pos, int n, hipStream_t st, WideBvh* w, std::s
     while (q0 < q1) {
         WB_CHECK(level < kWideLevels, "deeper than the walk's stack");
         const int cnt = q1 - q0;
-        k_wide_kids<<<(cnt + kB - 1) / kB, kB, 0, st>>>(wq, q0, q1, n, nlo, nhi, open, split, kidv, ni, nl, bad);
+        k_wide_kids<<<(cnt + kB - 1) / kB, kB, 0, st>>>(wq, q0, q1, n, nlo, nhi, open, split, ntri, kidv, ni, nl, bad);
         WB_HIP(hipGetLastError());
         WB_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ni, si, cnt, st));
         WB_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, nl, sl, cnt, st));

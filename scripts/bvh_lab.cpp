@@ -644,6 +644,80 @@ static WEmu emu_walk(const std::vector<uint32_t>& W, const std::vector<int>& pri
     return e;
 }
 
+
+// LAB (ORDER=1): any-hit walks that visit a node's hit interior children in another order than the slot order --
+// 1 nearest entry first, 2 farthest first, 3 largest (most slots below) first -- node fetches counted
+static uint32_t emu_hits_t(const uint32_t* w, V3 o, V3 inv, float tnear, float tfar, float* tent) {
+    const uint32_t eb = w[3];
+    const float s[3] = {u2f_((eb & 0xffu) << 23), u2f_(((eb >> 8) & 0xffu) << 23), u2f_(((eb >> 16) & 0xffu) << 23)};
+    const float iv[3] = {inv.x, inv.y, inv.z}, org[3] = {o.x, o.y, o.z};
+    float a[3], b[3];
+    for (int k = 0; k < 3; ++k) { a[k] = s[k] * iv[k]; b[k] = (u2f_(w[k]) - org[k]) * iv[k]; }
+    const uint32_t lo[3][2] = {{w[6], w[7]}, {w[8], w[9]}, {w[10], w[11]}};
+    const uint32_t hi[3][2] = {{w[12], w[13]}, {w[14], w[15]}, {w[16], w[17]}};
+    uint32_t hits = 0;
+    for (int c = 0; c < 8; ++c) {
+        float tn[3], tf[3];
+        for (int k = 0; k < 3; ++k) {
+            const bool pos = iv[k] >= 0.0f;
+            const uint32_t qn = pos ? lo[k][c >> 2] : hi[k][c >> 2], qf = pos ? hi[k][c >> 2] : lo[k][c >> 2];
+            tn[k] = std::fma((float)((qn >> (8 * (c & 3))) & 0xffu), a[k], b[k]);
+            tf[k] = std::fma((float)((qf >> (8 * (c & 3))) & 0xffu), a[k], b[k]);
+        }
+        const float t0 = std::fmax(std::fmax(std::fmax(tnear, tn[0]), tn[1]), tn[2]);
+        const float t1 = std::fmin(std::fmin(std::fmin(tfar, tf[0]), tf[1]), tf[2]);
+        tent[c] = t0;
+        if (t0 * 0.9999995f <= t1 * 1.0000005f) hits |= 1u << c;
+    }
+    return hits & ((1u << (w[3] >> 28)) - 1u);
+}
+static FILE* g_iters_dump = nullptr;           // DUMP_ITERS=path: each shadow ray's node fetches (int32, pixel order)
+static std::vector<int> g_subtree, g_subtri;     // per wide node: nodes / triangles below it (ORDER=3 / 5)
+static int emu_walk_order(const std::vector<uint32_t>& W, const std::vector<int>& prims, const Ray& r, int mode,
+                          bool any = true) {
+    V3 inv{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+    float tfar = r.tf;
+    std::vector<uint32_t> st{0u};
+    int iters = 0;
+    while (!st.empty()) {
+        const uint32_t node = st.back(); st.pop_back();
+        ++iters;
+        const uint32_t* w = &W[20 * (size_t)node];
+        float te[8];
+        const uint32_t hits = emu_hits_t(w, r.o, inv, r.tn, tfar, te);
+        const uint32_t ni = (w[3] >> 24) & 0xfu, tb = w[5];
+        for (uint32_t tm = hits >> ni; tm; tm &= tm - 1) {
+            float t;
+            if (tri_hit(prims[tb + __builtin_ctz(tm)], r.o, r.d, r.tn, tfar, t)) {
+                if (any) return iters;
+                tfar = std::min(tfar, t);
+            }
+        }
+        std::vector<std::pair<float, uint32_t>> kids;
+        for (uint32_t c = 0; c < ni; ++c)
+            if ((hits >> c) & 1u) {
+                const uint32_t k = w[4] + c;
+                float area = 0.0f;
+                if (mode == 4) {                         // the child's quantised box (surface area / 2)
+                    float e3[3];
+                    for (int a = 0; a < 3; ++a) {
+                        const float sc = u2f_(((w[3] >> (8 * a)) & 0xffu) << 23);
+                        const uint32_t ql = (w[6 + 2 * a + (c >> 2)] >> (8 * (c & 3))) & 0xffu;
+                        const uint32_t qh = (w[12 + 2 * a + (c >> 2)] >> (8 * (c & 3))) & 0xffu;
+                        e3[a] = (float)(qh - ql) * sc;
+                    }
+                    area = e3[0] * e3[1] + e3[1] * e3[2] + e3[2] * e3[0];
+                }
+                const float key = mode == 1 ? -te[c] : mode == 2 ? te[c] : mode == 3 ? (float)g_subtree[k] :
+                                  mode == 4 ? area : mode == 5 ? (float)g_subtri[k] : -(float)c;
+                kids.push_back({key, k});
+            }
+        std::sort(kids.begin(), kids.end());      // ascending key: the last pushed (popped first) has the largest key
+        for (auto& kv : kids) st.push_back(kv.second);
+    }
+    return iters;
+}
+
 int main(int argc, char** argv) {
     if (argc < 3) { fprintf(stderr, "usage: bvh_lab scene.bin which [W H]\n"); return 1; }
     FILE* f = fopen(argv[1], "rb");
@@ -732,6 +806,18 @@ int main(int argc, char** argv) {
         std::vector<size_t> lv_nodes(32, 0);
         for (size_t j = 0; j < NN; ++j) lv_nodes[lvl_of[j]]++;
         std::vector<uint32_t> lseq;
+        const bool order_lab = getenv("ORDER") != nullptr;
+        if (getenv("DUMP_ITERS")) g_iters_dump = fopen(getenv("DUMP_ITERS"), "wb");
+        double it_ord[6] = {0, 0, 0, 0, 0, 0}, it_ordp[6] = {0, 0, 0, 0, 0, 0};
+        if (order_lab) {
+            g_subtree.assign(NN, 1);
+            g_subtri.assign(NN, 0);
+            for (size_t j = NN; j-- > 0;) {              // children after parents (breadth-first ids)
+                const uint32_t ni = (WN[20 * j + 3] >> 24) & 0xfu, nv = WN[20 * j + 3] >> 28;
+                g_subtri[j] += (int)(nv - ni);
+                for (uint32_t i = 0; i < ni; ++i) { g_subtree[j] += g_subtree[WN[20 * j + 4] + i]; g_subtri[j] += g_subtri[WN[20 * j + 4] + i]; }
+            }
+        }
         auto lv_add = [&](int k) { for (uint32_t v : lseq) lv_hist[k][lvl_of[v]] += 1; lseq.clear(); };
         const bool levels = getenv("LEVELS") != nullptr;
         for (int y = 0; y < H; ++y)
@@ -745,6 +831,7 @@ int main(int argc, char** argv) {
                 Trace ref = walk(Fr, pr_, false);
                 mism += a.prim != ref.prim;
                 it_p += a.iters; tr_p += a.tris;
+                if (order_lab) for (int m = 0; m < 6; ++m) it_ordp[m] += emu_walk_order(WN, pr, pr_, m, false);
                 if (a.prim < 0) continue;
                 V3 o = eye + d * a.t;
                 {   // a cosine-distributed bounce off the hit triangle (the BRDF candidates' closest-hit rays)
@@ -777,8 +864,19 @@ int main(int argc, char** argv) {
                 Trace rs_ = walk(Fr, sh, true);
                 mism += b.occ != (int)rs_.occ;
                 it_s += b.iters; tr_s += b.tris; lost += b.lost; ++ns; maxsp = std::max(maxsp, b.maxsp);
+                if (g_iters_dump) fwrite(&b.iters, 4, 1, g_iters_dump);
+                if (order_lab) for (int m = 0; m < 6; ++m) it_ord[m] += emu_walk_order(WN, pr, sh, m);
                 if (y / 8 < H / 8 && x / 8 < W / 8) { int& wv = wave_it[(y / 8) * (W / 8) + x / 8]; wv = std::max(wv, b.iters); }
             }
+        if (g_iters_dump) fclose(g_iters_dump);
+        if (order_lab)
+            printf("ORDER shadow fetches/ray: slot order %.3f, nearest first %.3f, farthest first %.3f, most nodes first %.3f, "
+                   "largest area first %.3f, most triangles first %.3f\n",
+                   it_ord[0] / ns, it_ord[1] / ns, it_ord[2] / ns, it_ord[3] / ns, it_ord[4] / ns, it_ord[5] / ns);
+        if (order_lab)
+            printf("ORDER primary (closest hit) fetches/ray: slot %.3f, nearest %.3f, farthest %.3f, most nodes %.3f, "
+                   "largest area %.3f, most triangles %.3f\n", it_ordp[0] / (W * H), it_ordp[1] / (W * H), it_ordp[2] / (W * H),
+                   it_ordp[3] / (W * H), it_ordp[4] / (W * H), it_ordp[5] / (W * H));
         if (levels) {
             const char* nm[3] = {"primary", "bounce", "shadow"};
             for (int k = 0; k < 3; ++k) {
