@@ -14,6 +14,8 @@
 #           (scripts/pmc_summary.py turns them into profiles/rNN_pmc_<cfg>$PMC_TAG.json); PMC_ENV: extra VAR=value settings
 #   ab      A/B of prebuilt libraries restir-embree_amd/_ab/lib_*.so: AB_TESTS against each non-base one, then
 #           bench.py (--steps STEPS, BENCH_ARGS) for each, REPS times interleaved
+#   abenv   bench.py (--steps STEPS, BENCH_ARGS) under each environment of ENVS ("A=1 B=2;C=3;" -- ';'-separated
+#           sets, an empty set = the defaults), REPS times interleaved
 #   band    scripts/band_probe.py $BAND_ARGS -> gpurun_out/band${TAG}.txt
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -88,6 +90,24 @@ d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 kr = d.get('kernel_roofline', {})
 print(f"{sys.argv[1]:>14s} fps={d['value']:8.2f} {kr.get('kernel', '')}_ms={kr.get('kernel_ms', 0):.3f} " +
       " ".join(f"{k}={v:.3f}" for k, v in d.get('pass_ms_one_frame_in_flight', {}).items() if v > 0.01), flush=True)
+PY
+    done
+  done
+}
+step_abenv() {
+  local IFS_OLD="$IFS"
+  for rep in $(seq ${REPS:-2}); do
+    IFS=';'; local sets=($ENVS); IFS="$IFS_OLD"
+    for e in "${sets[@]}"; do
+      local tag=$(echo "${e:-default}" | tr ' =' '_-')
+      env $e timeout -k 10 240 python bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-extras ${BENCH_ARGS} \
+        > gpurun_out/abenv_$tag.log 2>&1; local rc=$?
+      [ $rc -ne 0 ] && { echo "$tag rc=$rc"; tail -3 gpurun_out/abenv_$tag.log; return $rc; }
+      python3 - "$tag" gpurun_out/abenv_$tag.log <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+kr = d.get('kernel_roofline', {})
+print(f"{sys.argv[1]:>40s} fps={d['value']:8.2f} {kr.get('kernel', '')}_ms={kr.get('kernel_ms', 0):.3f}", flush=True)
 PY
     done
   done
