@@ -26,7 +26,7 @@ PASS = ("k_gbuffer_initial", "k_visibility", "k_temporal", "k_spatial", "k_shade
 def kname(row):
     # "void rs::k_gbuffer_initial<0>(...)" -> "k_gbuffer_initial" (<0> lockstep / <1> lane kind)
     k = row["Kernel_Name"].split("(")[0].replace("rs::", "").replace("void ", "").split("<")[0]
-    return k.replace("_split", "").replace("_sorted", "")
+    return k.replace("_split", "").replace("_sorted", "").replace("_pq", "")
 
 
 vals = collections.defaultdict(lambda: collections.defaultdict(list))

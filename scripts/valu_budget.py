@@ -1,4 +1,4 @@
-"""Diagnostic (GPU box, 1 GPU): C2's initial pass broken into its parts by varying the workload -- the VALU
+"""Diagnostic (GPU box, 1 GPU): C2's (or C3's, --scene C3) initial pass broken into its parts by varying the workload -- the VALU
 budget of DESIGN §4.  Renders the C2 frame (1920x1080, lockstep walks, one frame in flight) for
 each variant in turn and prints the initial pass's mean time (HIP events, rs_get_timing_totals) and rays per frame:
 
@@ -32,10 +32,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scene", default="C2", help="C2 (lockstep walks) or C3 (per-lane walks, sorted pass)")
     a = ap.parse_args()
-    sc = scenes.cornell_many_lights(1024)
+    sc = scenes.cornell_many_lights(1024) if a.scene == "C2" else scenes.sponza_like()
     r = Renderer(1920, 1080)
-    r.set_traversal("lockstep")
+    r.set_traversal("lockstep" if a.scene == "C2" else "lane")
     r.set_run_ahead(0)
     gs = r.load_scene(sc)
     f = 0
