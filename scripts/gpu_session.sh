@@ -99,7 +99,7 @@ step_abenv() {
   for rep in $(seq ${REPS:-2}); do
     IFS=';'; local sets=($ENVS); IFS="$IFS_OLD"
     for e in "${sets[@]}"; do
-      local tag=$(echo "${e:-default}" | tr ' =' '_-')
+      local tag=$(echo "${e:-default}" | tr ' =/' '_-_' | cut -c1-80)
       env $e timeout -k 10 240 python bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-extras ${BENCH_ARGS} \
         > gpurun_out/abenv_$tag.log 2>&1; local rc=$?
       [ $rc -ne 0 ] && { echo "$tag rc=$rc"; tail -3 gpurun_out/abenv_$tag.log; return $rc; }
