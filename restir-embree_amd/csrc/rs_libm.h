@@ -329,29 +329,25 @@ RS_LM float rs_powf(float x, float y) {
 #define RS_LM_PIO2_HI 1.57079632673412561417e+00   /* 0x3ff921fb54400000: 33 significant bits */
 #define RS_LM_PIO2_LO 6.07710050650619224932e-11
 #define RS_LM_2_OVER_PI 6.36619772367581382433e-01
-RS_LM double rs_lm_sin_core(double r) {          /* |r| <= pi/4, to r^17 / 17! */
+RS_LM double rs_lm_sin_core(double r) {          /* |r| <= pi/4, to r^15 / 15! (truncation < 6e-17 relative) */
     const double z = r * r;
-    double p = 1.0 / 355687428096000.0;
-    p = -1.0 / 1307674368000.0 + z * p;
-    p = 1.0 / 6227020800.0 + z * p;
-    p = -1.0 / 39916800.0 + z * p;
-    p = 1.0 / 362880.0 + z * p;
-    p = -1.0 / 5040.0 + z * p;
-    p = 1.0 / 120.0 + z * p;
-    p = -1.0 / 6.0 + z * p;
-    return r + (r * z) * p;
+    double p = __builtin_fma(z, -1.0 / 1307674368000.0, 1.0 / 6227020800.0);
+    p = __builtin_fma(z, p, -1.0 / 39916800.0);
+    p = __builtin_fma(z, p, 1.0 / 362880.0);
+    p = __builtin_fma(z, p, -1.0 / 5040.0);
+    p = __builtin_fma(z, p, 1.0 / 120.0);
+    p = __builtin_fma(z, p, -1.0 / 6.0);
+    return __builtin_fma(r * z, p, r);
 }
-RS_LM double rs_lm_cos_core(double r) {          /* |r| <= pi/4, to r^18 / 18! */
+RS_LM double rs_lm_cos_core(double r) {          /* |r| <= pi/4, to r^16 / 16! (truncation < 3e-18) */
     const double z = r * r;
-    double p = -1.0 / 6402373705728000.0;
-    p = 1.0 / 20922789888000.0 + z * p;
-    p = -1.0 / 87178291200.0 + z * p;
-    p = 1.0 / 479001600.0 + z * p;
-    p = -1.0 / 3628800.0 + z * p;
-    p = 1.0 / 40320.0 + z * p;
-    p = -1.0 / 720.0 + z * p;
-    p = 1.0 / 24.0 + z * p;
-    return 1.0 + z * (-0.5 + z * p);
+    double p = __builtin_fma(z, 1.0 / 20922789888000.0, -1.0 / 87178291200.0);
+    p = __builtin_fma(z, p, 1.0 / 479001600.0);
+    p = __builtin_fma(z, p, -1.0 / 3628800.0);
+    p = __builtin_fma(z, p, 1.0 / 40320.0);
+    p = __builtin_fma(z, p, -1.0 / 720.0);
+    p = __builtin_fma(z, p, 1.0 / 24.0);
+    return __builtin_fma(z, __builtin_fma(z, p, -0.5), 1.0);
 }
 RS_LM void rs_sincosf(float a, float* s, float* c) {
     const double x = (double)a;
@@ -359,7 +355,7 @@ RS_LM void rs_sincosf(float a, float* s, float* c) {
     const double t = x * RS_LM_2_OVER_PI;
     const int64_t k = (int64_t)(t >= 0.0 ? t + 0.5 : t - 0.5);
     const double dk = (double)k;
-    const double r = (x - dk * RS_LM_PIO2_HI) - dk * RS_LM_PIO2_LO;
+    const double r = __builtin_fma(-dk, RS_LM_PIO2_LO, __builtin_fma(-dk, RS_LM_PIO2_HI, x));
     const double sr = rs_lm_sin_core(r), cr = rs_lm_cos_core(r);
     double sv, cv;
     switch ((int)(k & 3)) {

@@ -180,7 +180,8 @@ def load_library(path: str = LIB_PATH):
     L.rs_context_set_initial_split.argtypes = [vp, i32]
     L.rs_context_get_initial_split.argtypes = [vp, ip, ip]
     L.rs_context_set_frame_ring.argtypes = [vp, i32]
-    L.rs_context_handoff_bytes.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    if hasattr(L, "rs_context_handoff_bytes"):   # (absent from round-5 builds, which A/Bs load)
+        L.rs_context_handoff_bytes.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.rs_context_set_run_ahead.argtypes = [vp, i32]
     L.rs_max_run_ahead.argtypes = []
     L.rs_max_run_ahead.restype = i32
