@@ -720,12 +720,13 @@ __device__ __forceinline__ uint32_t tile_pixel(const FrameConst& F, int ya, int 
     const int x = bx * 16 + (wave & 1) * 8 + (l & 7), y = ya + by * 16 + (wave >> 1) * 8 + (l >> 3);
     return (uint32_t)y * (uint32_t)F.W + (uint32_t)x;
 }
-// the bucket of a shadow ray: RS_SORT_KEY 0 (default) = the light's Morton bucket alone; 1 = the direction's
-// octant x the top 3 bits of the light's Morton bucket (CPU lab, scripts/bvh_lab.cpp COHERENCE_WAVE, 32
+// the bucket of a shadow ray: RS_SORT_KEY 0 = the light's Morton bucket alone; 1 (default since round 6) = the
+// direction's octant x the top 3 bits of the light's Morton bucket (CPU lab, scripts/bvh_lab.cpp COHERENCE_WAVE, 32
 // candidates: light bucket alone -- C3 wide-walk distinct fetches -39 %, C2 binary lockstep union -6 %; octant x
-// light 3 bits -- C3 -30 %, C2 -45 %.  GPU, C3 1080p: initial pass 14.97 vs 15.14 ms, 58.6 vs 58.0 frames/s)
+// light 3 bits -- C3 -30 %, C2 -45 %.  GPU, C3 1080p, round 4: initial pass 14.97 vs 15.14 ms; round 6 with the
+// lane refill: 75.35-75.72 vs 75.11-75.39 frames/s, initial pass 11.88-11.94 vs 11.95-11.99 ms)
 #ifndef RS_SORT_KEY
-#define RS_SORT_KEY 0
+#define RS_SORT_KEY 1
 #endif
 __device__ __forceinline__ uint32_t ray_bucket(const DevScene& S, uint32_t pick, vec3 d) {
     const uint32_t eb = S.ebucket[pick];
