@@ -228,17 +228,20 @@ __device__ __forceinline__ bool is_phong(int type) { return type == MT_PHONG || 
 // pg/MaterialPhong.cpp:150-172)
 // Lambert surfaces (ks = 0: omp = 0) add the lobe term a * pow(..) * 0 = +0 exactly (a finite, the pow in
 // [0, 1]), so the powf is skipped for them -- the MIS pdf of every area candidate on a diffuse wall
+// (Call: the pow's core as a called function, rs_libm.h rs_powf_sel -- for the register-bound per-lane kernels)
+template <bool Call = false>
 __device__ __forceinline__ float phong_pdf(const ShadeFrame& s, vec3 wi) {
     float pdf = gmax(dot(s.nrm, wi), 0.0f) * kOneOverPi * s.pf;
-    pdf += (s.omp != 0.0f || !isfinite(s.a)) ? s.a * rs_powf(gmax(0.0f, dot(wi, s.wr)), s.shin) * s.omp : 0.0f;
+    pdf += (s.omp != 0.0f || !isfinite(s.a)) ? s.a * rs_powf_sel(gmax(0.0f, dot(wi, s.wr)), s.shin, Call) * s.omp : 0.0f;
     return pdf;
 }
 // BRDF eval dispatch (pg/ReSTIRIntegrator.h:32-41): Phong for PHONG/DIELECTRIC
 // (pg/MaterialPhong.cpp:122-148, with the cached 1/I_M), Lambert otherwise (pg/MaterialLambert.cpp:33-41)
+template <bool Call = false>
 __device__ __forceinline__ vec3 eval_brdf(const ShadeFrame& s, vec3 wi) {
     vec3 f = s.kd_pi;
     if (!is_phong(s.type)) return f;
-    float pw = rs_powf(gmax(dot(wi, s.wr), 0.0f), s.shin);
+    float pw = rs_powf_sel(gmax(dot(wi, s.wr), 0.0f), s.shin, Call);
     return f + s.ks_im * pw;
 }
 __device__ __forceinline__ float phong_pdf(const GElem& g, vec3 cam, vec3 wi) { return phong_pdf(make_frame(g, cam), wi); }

@@ -294,8 +294,15 @@ RS_LM double rs_lm_pow_core(float ax, float y) {
     return __builtin_fma(s, em1, s);
 }
 
-/* x^y (C99 special cases) */
-RS_LM float rs_powf(float x, float y) {
+#if defined(__HIP__)
+/* the core as a called function (rs_powf_sel's `call`): its constants and temporaries stay out of the calling
+   kernel's register allocation -- a gain in the register-bound per-lane kernels, a loss in the lockstep ones */
+__host__ __device__ static __attribute__((noinline)) double rs_lm_pow_core_call(float ax, float y) {
+    return rs_lm_pow_core(ax, y);
+}
+#endif
+/* x^y (C99 special cases); call != 0 (a constant at every call site): the core by rs_lm_pow_core_call */
+RS_LM float rs_powf_sel(float x, float y, int call) {
     if (y == 0.0f || x == 1.0f) return 1.0f;
     if (x != x || y != y) return x + y;
     const double ay = y < 0.0f ? -(double)y : (double)y;
@@ -320,9 +327,17 @@ RS_LM float rs_powf(float x, float y) {
     if (ax == 0.0f) r = y > 0.0f ? 0.0f : RS_LM_FINF;
     else if (rs_lm_fbits(ax) == 0x7f800000u) r = y > 0.0f ? ax : 0.0f;   /* (-inf)^y: sign by y_odd only */
     else if (x < 0.0f && !y_int) return RS_LM_FNAN;
-    else r = (float)rs_lm_pow_core(ax, y);
+    else {
+#if defined(__HIP_DEVICE_COMPILE__)
+        r = (float)(call ? rs_lm_pow_core_call(ax, y) : rs_lm_pow_core(ax, y));
+#else
+        (void)call;
+        r = (float)rs_lm_pow_core(ax, y);
+#endif
+    }
     return neg ? -r : r;
 }
+RS_LM float rs_powf(float x, float y) { return rs_powf_sel(x, y, 0); }
 
 /* sin and cos of a float angle (the path's angles are 2 pi U, U in [0, 1)): Cody-Waite reduction by pi/2 in
  * double, Taylor cores on |r| <= pi/4 */

@@ -224,6 +224,7 @@ __device__ __forceinline__ bool occluded(const DevScene& S, const FrameConst& F,
 // evaluate_f_pre computes the unoccluded L and the testOcclusion ray (dir = normalize(p - pos),
 // tfar = |p - pos| - tfarOffset, exactly as occluded<T>() forms them); evaluate_f_post applies V.
 struct FPre { vec3 L, dir; float tfar; bool ok, need; };
+template <bool Call = false>
 __device__ __forceinline__ FPre evaluate_f_pre(const FrameConst& F, const Sample& s, vec3 pos, bool emissive,
                                                const ShadeFrame& sf, bool test_vis, bool alive) {
     FPre r;
@@ -234,7 +235,7 @@ __device__ __forceinline__ FPre evaluate_f_pre(const FrameConst& F, const Sample
     float cI = gmax(dot(ld, sf.nrm), 0.0f);
     float cY = fabsf(dot(-ld, s.n));
     float G = cI * cY / r2;
-    r.L = (s.li * eval_brdf(sf, ld)) * G;
+    r.L = (s.li * eval_brdf<Call>(sf, ld)) * G;
     r.need = r.ok && test_vis && !(r.L.x == 0.0f && r.L.y == 0.0f && r.L.z == 0.0f);
     r.dir = ld;
     r.tfar = sqrtf(r2) - F.tfar_off;
@@ -368,6 +369,7 @@ __device__ __forceinline__ float emis_pdf_brdf(const DevScene& S, int id) { retu
 
 // areaSampleLight (pg/ReSTIRIntegrator.cpp:89-124), TriangleCDF::getTriangle (pg/TriangleCDF.cpp:36-54),
 // Sampling::sampleTriangle (pg/Sampling.cpp:63-76)
+template <bool Call = false>
 __device__ __forceinline__ Sample area_sample_at(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
                                                  Rng& rng, uint32_t idx, float& W_out, float& mis_out) {
     const EmisRec E = EmisRec::load(S.emis + 8 * idx);
@@ -382,7 +384,7 @@ __device__ __forceinline__ Sample area_sample_at(const DevScene& S, const FrameC
     ld = normalize(ld);
     float cY = gmax(dot(-ld, nn), 0.0f);
     float amf = cY / r2s;
-    float pba = phong_pdf(sf, ld) * amf;
+    float pba = phong_pdf<Call>(sf, ld) * amf;
     mis_out = m_area(F, pdf_area, pba);
     W_out = 1.0f / pdf_area;
     return Sample{pt, nn, E.le};
@@ -736,14 +738,18 @@ __device__ __forceinline__ uint32_t ray_bucket(const DevScene& S, uint32_t pick,
 }
 // candidate c of a pixel: area_batch's sample and unoccluded evaluation (pick, weights, shadow ray need)
 struct AreaCand { uint32_t pick, bucket; float wu; bool ok, need, wo_nan; vec3 dir; float tfar; };
+// (the sorted pass's candidates take the pow core by call: RS_SORT_POW_CALL, C3 +2 %)
+#ifndef RS_SORT_POW_CALL
+#define RS_SORT_POW_CALL 1
+#endif
 __device__ __forceinline__ AreaCand area_cand(const DevScene& S, const FrameConst& F, vec3 pos, const ShadeFrame& sf,
                                               Rng& rng, int c, bool tv, bool alive, float inv_ma) {
     AreaCand a;
     a.pick = area_pick(S, rng, c);
     float Wc, mis;
     rng.n = cand_slot(c) + 1u;
-    const Sample s = area_sample_at(S, F, pos, sf, rng, a.pick, Wc, mis);
-    const FPre pr = evaluate_f_pre(F, s, pos, false, sf, tv, alive);
+    const Sample s = area_sample_at<RS_SORT_POW_CALL>(S, F, pos, sf, rng, a.pick, Wc, mis);
+    const FPre pr = evaluate_f_pre<RS_SORT_POW_CALL>(F, s, pos, false, sf, tv, alive);
     a.bucket = ray_bucket(S, a.pick, pr.dir);
     const float m = F.m_brdf > 0 ? mis : inv_ma;
     a.wu = m * length(pr.L) * Wc;
